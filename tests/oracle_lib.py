@@ -1,0 +1,205 @@
+"""ctypes bindings for the oracle (test infrastructure: oracle/liboracle.so, oracle/_ref).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
+REF_PATH = os.path.join(ORACLE_DIR, "_ref", "libhkd_casadi_ref.so")
+
+DP = C.POINTER(C.c_double)
+IP = C.POINTER(C.c_int)
+
+
+class OrcOptions(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("alpha", "gamma", "update_penalty", "update_relax",
+                                          "update_regularization", "update_ReB")] + \
+               [(n, C.c_int) for n in ("max_DDP_iter", "max_AL_iter", "max_DDP_iter_runtime",
+                                       "max_AL_iter_runtime")] + \
+               [(n, C.c_double) for n in ("cost_thresh", "tconstr_thresh", "pconstr_thresh",
+                                          "dynamics_feas_thresh", "merit_rho", "merit_scale",
+                                          "merit_offset")] + \
+               [(n, C.c_int) for n in ("AL_active", "ReB_active", "smooth_active", "MS",
+                                       "nsteps_per_node", "no_early_exit")]
+
+
+class OrcWeights(C.Structure):
+    _fields_ = [("q_eul", C.c_double * 3), ("q_pos", C.c_double * 3), ("q_omega", C.c_double * 3),
+                ("q_v", C.c_double * 3), ("q_qJ", C.c_double), ("qf_scale", C.c_double * 24),
+                ("qf_gain", C.c_double), ("r_grf", C.c_double), ("r_qJd", C.c_double),
+                ("foot_w", C.c_double * 3), ("foot_gain", C.c_double),
+                ("foot_term_cost", C.c_double), ("foot_term_grad", C.c_double)]
+
+
+class OrcProblem(C.Structure):
+    _fields_ = [("n_phases", C.c_int), ("horizons", IP), ("dt", C.c_double), ("mu_fric", C.c_double),
+                ("grf_delta", C.c_double), ("grf_delta_min", C.c_double), ("grf_eps", C.c_double),
+                ("td_sigma", C.c_double), ("td_sigma_max", C.c_double), ("td_lambda", C.c_double),
+                ("ground_height", C.c_double), ("w", OrcWeights)]
+
+
+class OrcElement(C.Structure):
+    _fields_ = [("contacts", IP), ("x0", DP), ("ref_x", DP), ("ref_u", DP), ("ref_foot", DP),
+                ("Xbar", DP), ("X", DP), ("Defect", DP), ("Defect_bar", DP), ("dX", DP),
+                ("Ubar", DP), ("U", DP), ("dU", DP), ("K", DP),
+                ("reb_delta", DP), ("reb_eps", DP), ("al_sigma", DP), ("al_lambda", DP),
+                ("cost", C.c_double), ("feas", C.c_double), ("merit", C.c_double),
+                ("max_tconstr", C.c_double), ("max_pconstr", C.c_double),
+                ("iters", C.c_int), ("outer_iters", C.c_int), ("status", C.c_int),
+                ("n_ls_trials", C.c_int)]
+
+
+def build(quiet: bool = True) -> None:
+    """Compile oracle/liboracle.so (and oracle/_ref when /root/reference is present)."""
+    out = subprocess.run(["make", "-C", ORACLE_DIR, "all"], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + out.stdout + out.stderr)
+
+
+_lib = None
+_ref = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.orc_solve_batch.argtypes = [C.POINTER(OrcProblem), C.POINTER(OrcOptions),
+                                         C.POINTER(OrcElement), C.c_int, C.c_int]
+        _lib.orc_solve.argtypes = [C.POINTER(OrcProblem), C.POINTER(OrcOptions), C.POINTER(OrcElement)]
+        for f in ("orc_hkd_step",):
+            getattr(_lib, f).argtypes = [DP, DP, C.c_double, DP, DP]
+        _lib.orc_hkd_partial.argtypes = [DP, DP, C.c_double, DP, DP, DP]
+        _lib.orc_foot_position.argtypes = [C.c_int, DP, DP, DP, DP]
+        _lib.orc_foot_jacobian.argtypes = [C.c_int, DP, DP, DP, DP]
+        _lib.orc_resetmap.argtypes = [DP, IP, IP, DP]
+        _lib.orc_resetmap_partial.argtypes = [DP, IP, IP, DP]
+    return _lib
+
+
+def ref_lib():
+    """The reference's own CasADi kernels (oracle/_ref); None when not built."""
+    global _ref
+    if _ref is None and os.path.exists(REF_PATH):
+        _ref = C.CDLL(REF_PATH)
+        _ref.ref_hkinodyn.argtypes = [DP, DP, C.c_double, DP, DP]
+        _ref.ref_hkinodyn_par.argtypes = [DP, DP, C.c_double, DP, DP, DP]
+        _ref.ref_foot_position.argtypes = [DP, DP, DP, C.c_double, DP]
+        _ref.ref_foot_jacobian.argtypes = [C.c_int, DP, DP, DP, DP]
+    return _ref
+
+
+def dp(a):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(DP)
+
+
+def ip(a):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(IP)
+
+
+def default_options(**kw) -> OrcOptions:
+    o = OrcOptions()
+    lib().orc_default_options(C.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def default_problem(horizons, dt=0.01) -> tuple:
+    hz = np.asarray(horizons, dtype=np.int32)
+    p = OrcProblem()
+    p.n_phases = len(hz)
+    p.horizons = ip(hz)
+    p.dt = dt
+    p.mu_fric = 0.7
+    p.grf_delta, p.grf_delta_min, p.grf_eps = 0.1, 0.1, 0.1
+    p.td_sigma, p.td_sigma_max, p.td_lambda = 50.0, 1e4, 0.0
+    p.ground_height = 0.0
+    lib().orc_default_weights(C.byref(p.w))
+    return p, hz
+
+
+# ---- model wrappers ---------------------------------------------------------------------------
+def hkd_step(x, u, dt, c):
+    o = np.zeros(24)
+    lib().orc_hkd_step(dp(np.ascontiguousarray(x, float)), dp(np.ascontiguousarray(u, float)), dt,
+                       dp(np.ascontiguousarray(c, float)), dp(o))
+    return o
+
+
+def hkd_partial(x, u, dt, c):
+    A = np.zeros((24, 24)); B = np.zeros((24, 24))
+    lib().orc_hkd_partial(dp(np.ascontiguousarray(x, float)), dp(np.ascontiguousarray(u, float)), dt,
+                          dp(np.ascontiguousarray(c, float)), dp(A), dp(B))
+    return A, B
+
+
+def resetmap(x, c, cn):
+    o = np.zeros(24)
+    lib().orc_resetmap(dp(np.ascontiguousarray(x, float)), ip(np.asarray(c, np.int32)),
+                       ip(np.asarray(cn, np.int32)), dp(o))
+    return o
+
+
+def resetmap_partial(x, c, cn):
+    o = np.zeros((24, 24))
+    lib().orc_resetmap_partial(dp(np.ascontiguousarray(x, float)), ip(np.asarray(c, np.int32)),
+                               ip(np.asarray(cn, np.int32)), dp(o))
+    return o
+
+
+# ---- solver -----------------------------------------------------------------------------------
+def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 1,
+                elements=None) -> dict:
+    """Run the oracle solve on (a subset of) a synthetic batch; returns per-element outputs."""
+    options = options or default_options()
+    B = prob["batch"]
+    idx = list(range(B)) if elements is None else list(elements)
+    n = len(idx)
+    S, Kc, P = prob["S"], prob["Kc"], len(prob["horizons"])
+    p, hz = default_problem(prob["horizons"], prob["dt"])
+    st = {
+        "Xbar": np.ascontiguousarray(prob["Xbar"][idx]).copy(),
+        "X": np.ascontiguousarray(prob["Xbar"][idx]).copy(),
+        "Defect": np.zeros((n, S, 24)), "Defect_bar": np.zeros((n, S, 24)), "dX": np.zeros((n, S, 24)),
+        "Ubar": np.ascontiguousarray(prob["Ubar"][idx]).copy(),
+        "U": np.ascontiguousarray(prob["Ubar"][idx]).copy(), "dU": np.zeros((n, Kc, 24)),
+        "K": np.ascontiguousarray(prob["K"][idx]).copy(),
+        "reb_delta": np.zeros((n, Kc, 20)), "reb_eps": np.zeros((n, Kc, 20)),
+        "al_sigma": np.zeros((n, P, 4)), "al_lambda": np.zeros((n, P, 4)),
+    }
+    contacts = np.ascontiguousarray(prob["contacts"][idx])
+    x0 = np.ascontiguousarray(prob["x0"][idx])
+    shared = prob["ref_x"].shape[0] == 1
+    elems = (OrcElement * n)()
+    keep = [contacts, x0]
+    for j, b in enumerate(idx):
+        e = elems[j]
+        rb = 0 if shared else b
+        e.contacts = ip(contacts[j])
+        e.x0 = dp(x0[j])
+        rx = np.ascontiguousarray(prob["ref_x"][rb]); ru = np.ascontiguousarray(prob["ref_u"][rb])
+        rf = np.ascontiguousarray(prob["ref_foot"][rb])
+        keep += [rx, ru, rf]
+        e.ref_x, e.ref_u, e.ref_foot = dp(rx), dp(ru), dp(rf)
+        for k in st:
+            setattr(e, k, dp(st[k][j]))
+        lib().orc_init_element(C.byref(p), C.byref(e))
+    lib().orc_solve_batch(C.byref(p), C.byref(options), elems, n, n_threads)
+    out = dict(st)
+    for f in ("cost", "feas", "merit", "max_tconstr", "max_pconstr", "iters", "outer_iters", "status",
+              "n_ls_trials"):
+        out[f] = np.array([getattr(elems[j], f) for j in range(n)])
+    return out
