@@ -1,0 +1,662 @@
+// hsddp_api.cpp — C-ABI of the batched HS-DDP solver (include/hsddp.h): handle, device memory,
+// the per-element-masked solve loop (MultiPhaseDDP::solve, MultiPhaseDDP.cpp:232-428) and the
+// INFO-file loaders (loadHSDDPSetting, HSDDP_CompoundTypes.h:62-87; loadConstrintParameters,
+// HKDProblem.h:70-90).
+#include <hip/hip_runtime.h>
+
+#include <cctype>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/hsddp.h"
+#include "hsddp_internal.h"
+
+using namespace hsddp;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                                 \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess) return fail(HSDDP_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+extern "C" const char *hsddp_last_error(void) { return g_err.c_str(); }
+extern "C" const char *hsddp_version(void) { return "hsddp-mi355x 0.1 (gfx950, fp64)"; }
+
+// ---- options / parameters ----------------------------------------------------------------
+extern "C" void hsddp_default_options(hsddp_options *o)
+{
+    // HSDDP_OPTION in-class defaults (HSDDP_CompoundTypes.h:20-45)
+    o->alpha = 0.1; o->gamma = 0.1; o->update_penalty = 8; o->update_relax = 0.1;
+    o->update_regularization = 2; o->update_ReB = 7;
+    o->max_DDP_iter = 3; o->max_AL_iter = 2; o->max_DDP_iter_runtime = 1; o->max_AL_iter_runtime = 2;
+    o->cost_thresh = 1e-3; o->tconstr_thresh = 1e-3; o->pconstr_thresh = 1e-3; o->dynamics_feas_thresh = 1e-3;
+    o->merit_rho = 1e4; o->merit_scale = 0.2; o->merit_offset = 10;
+    o->AL_active = 1; o->ReB_active = 1; o->smooth_active = 0; o->MS = 1; o->nsteps_per_node = 1;
+    o->no_early_exit = 0;
+}
+
+extern "C" void hsddp_default_weights(hsddp_hkd_weights *w)
+{
+    const double qe[3] = {1, 4, 5}, qp[3] = {1, 1, 30}, qo[3] = {.2, .2, .2}, qv[3] = {4, 1, .5};
+    const double sc[24] = {1, 1, 2, 1, 1, 20, .3, .3, .3, 1, 3, 1, .01, .01, .01, .01, .01, .01, .01, .01, .01, .01, .01, .01};
+    for (int i = 0; i < 3; ++i) { w->q_eul[i] = qe[i]; w->q_pos[i] = qp[i]; w->q_omega[i] = qo[i]; w->q_v[i] = qv[i]; }
+    w->q_qJ = 0.2;
+    for (int i = 0; i < 24; ++i) w->qf_scale[i] = sc[i];
+    w->qf_gain = 20; w->r_grf = 0.2; w->r_qJd = 0.1;
+    w->foot_w[0] = 3; w->foot_w[1] = 1; w->foot_w[2] = 0; w->foot_gain = 20;
+    w->foot_term_cost = 10; w->foot_term_grad = 20;
+}
+
+extern "C" void hsddp_default_constraint_params(hsddp_constraint_params *cp)
+{
+    // settings/constraint_params.info values; mu = 0.7 (HKDConstraints.h:17); ground height 0
+    cp->grf_delta = 0.1; cp->grf_delta_min = 0.1; cp->grf_eps = 0.1;
+    cp->swing_delta = 1.0; cp->swing_delta_min = 0.5; cp->swing_eps = 0.01;
+    cp->td_sigma = 50; cp->td_sigma_max = 1e4; cp->td_lambda = 0;
+    cp->mu_fric = 0.7; cp->ground_height = 0.0;
+}
+
+// Minimal Boost.PropertyTree INFO reader: `key value` pairs, `key { ... }` children, ';' comments,
+// optional double quotes.  Produces dotted paths ("ddp.alpha").
+static int parse_info(const char *path, std::map<std::string, std::string> &out)
+{
+    std::ifstream f(path);
+    if (!f) return fail(HSDDP_ERR_IO, std::string("cannot open ") + path);
+    std::vector<std::string> stack;
+    std::string line, last_key;
+    while (std::getline(f, line)) {
+        // strip comment (outside quotes)
+        bool q = false;
+        for (size_t i = 0; i < line.size(); ++i) {
+            if (line[i] == '"') q = !q;
+            if (line[i] == ';' && !q) { line.resize(i); break; }
+        }
+        std::vector<std::string> tok;
+        std::string cur;
+        q = false;
+        for (char ch : line) {
+            if (ch == '"') { q = !q; continue; }
+            if (!q && (std::isspace((unsigned char)ch) || ch == '{' || ch == '}')) {
+                if (!cur.empty()) { tok.push_back(cur); cur.clear(); }
+                if (ch == '{' || ch == '}') tok.push_back(std::string(1, ch));
+                continue;
+            }
+            cur += ch;
+        }
+        if (!cur.empty()) tok.push_back(cur);
+        size_t i = 0;
+        while (i < tok.size()) {
+            if (tok[i] == "{") {
+                stack.push_back(last_key);
+                ++i;
+                continue;
+            }
+            if (tok[i] == "}") {
+                if (stack.empty()) return fail(HSDDP_ERR_IO, std::string("unbalanced '}' in ") + path);
+                stack.pop_back();
+                ++i;
+                continue;
+            }
+            std::string key = tok[i++];
+            std::string val;
+            if (i < tok.size() && tok[i] != "{" && tok[i] != "}") val = tok[i++];
+            std::string full;
+            for (auto &s : stack) full += s + ".";
+            full += key;
+            out[full] = val;
+            last_key = key;
+        }
+    }
+    if (!stack.empty()) return fail(HSDDP_ERR_IO, std::string("unbalanced '{' in ") + path);
+    return HSDDP_OK;
+}
+
+static int get_num(const std::map<std::string, std::string> &m, const std::string &k, double &v)
+{
+    auto it = m.find(k);
+    if (it == m.end()) return fail(HSDDP_ERR_IO, "No such node (" + k + ")"); // ptree_bad_path
+    char *end = nullptr;
+    v = std::strtod(it->second.c_str(), &end);
+    if (end == it->second.c_str() || *end) return fail(HSDDP_ERR_IO, "conversion of data failed (" + k + ")");
+    return HSDDP_OK;
+}
+static int get_int(const std::map<std::string, std::string> &m, const std::string &k, int &v)
+{
+    auto it = m.find(k);
+    if (it == m.end()) return fail(HSDDP_ERR_IO, "No such node (" + k + ")");
+    char *end = nullptr;
+    long x = std::strtol(it->second.c_str(), &end, 10);
+    if (end == it->second.c_str() || *end) return fail(HSDDP_ERR_IO, "conversion of data failed (" + k + ")");
+    v = (int)x;
+    return HSDDP_OK;
+}
+static int get_bool(const std::map<std::string, std::string> &m, const std::string &k, int &v)
+{
+    auto it = m.find(k);
+    if (it == m.end()) return fail(HSDDP_ERR_IO, "No such node (" + k + ")");
+    const std::string &s = it->second;
+    if (s == "true" || s == "1") v = 1;
+    else if (s == "false" || s == "0") v = 0;
+    else return fail(HSDDP_ERR_IO, "conversion of data failed (" + k + ")");
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_load_settings(const char *path, hsddp_options *o)
+{
+    if (!path || !o) return fail(HSDDP_ERR_ARG, "null argument");
+    std::map<std::string, std::string> m;
+    int rc = parse_info(path, m);
+    if (rc) return rc;
+    hsddp_options t = *o;
+    // exactly the keys loadHSDDPSetting reads (HSDDP_CompoundTypes.h:70-86); update_regularization and
+    // smooth_active are not read, so they keep the caller's values (quirk A1).
+#define N_(k) if ((rc = get_num(m, "ddp." #k, t.k))) return rc
+#define I_(k) if ((rc = get_int(m, "ddp." #k, t.k))) return rc
+#define B_(k) if ((rc = get_bool(m, "ddp." #k, t.k))) return rc
+    N_(alpha); N_(gamma); N_(update_penalty); N_(update_relax); N_(update_ReB);
+    I_(max_DDP_iter); I_(max_AL_iter); I_(max_DDP_iter_runtime); I_(max_AL_iter_runtime);
+    N_(cost_thresh); N_(tconstr_thresh); N_(pconstr_thresh); N_(dynamics_feas_thresh);
+    N_(merit_rho); N_(merit_scale); N_(merit_offset);
+    B_(AL_active); B_(ReB_active); B_(MS); I_(nsteps_per_node);
+#undef N_
+#undef I_
+#undef B_
+    *o = t;
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_load_constraint_params(const char *path, hsddp_constraint_params *cp)
+{
+    if (!path || !cp) return fail(HSDDP_ERR_ARG, "null argument");
+    std::map<std::string, std::string> m;
+    int rc = parse_info(path, m);
+    if (rc) return rc;
+    hsddp_constraint_params t = *cp;
+    if ((rc = get_num(m, "GRF_ReB.delta", t.grf_delta)) || (rc = get_num(m, "GRF_ReB.delta_min", t.grf_delta_min)) ||
+        (rc = get_num(m, "GRF_ReB.eps", t.grf_eps)) || (rc = get_num(m, "Swing_ReB.delta", t.swing_delta)) ||
+        (rc = get_num(m, "Swing_ReB.delta_min", t.swing_delta_min)) || (rc = get_num(m, "Swing_ReB.eps", t.swing_eps)) ||
+        (rc = get_num(m, "TD_AL.sigma", t.td_sigma)) || (rc = get_num(m, "TD_AL.lambda", t.td_lambda)) ||
+        (rc = get_num(m, "TD_AL.sigma_max", t.td_sigma_max)))
+        return rc;
+    *cp = t;
+    return HSDDP_OK;
+}
+
+// ---- handle ----------------------------------------------------------------------------------
+struct hsddp_handle_t {
+    hsddp_problem_desc desc;
+    hsddp_options opt;
+    Params p;
+    Bufs d;
+    hipStream_t stream = nullptr;
+    int *host_counter = nullptr;
+    std::vector<void *> allocs;
+    size_t bytes = 0;
+    int Bref = 1;
+    bool have_problem = false;
+};
+
+template <typename T>
+static int dalloc(hsddp_handle h, T *&ptr, size_t n)
+{
+    void *p = nullptr;
+    size_t sz = n * sizeof(T);
+    if (sz == 0) sz = 16;
+    hipError_t e = hipMalloc(&p, sz);
+    if (e != hipSuccess) return fail(HSDDP_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+    hipMemset(p, 0, sz);
+    h->allocs.push_back(p);
+    h->bytes += sz;
+    ptr = (T *)p;
+    return HSDDP_OK;
+}
+
+static void fill_params(hsddp_handle h)
+{
+    Params &p = h->p;
+    const hsddp_problem_desc &ds = h->desc;
+    const hsddp_options &o = h->opt;
+    p.dt = ds.dt;
+    p.mu = ds.cparams.mu_fric;
+    p.grf_delta = ds.cparams.grf_delta; p.grf_delta_min = ds.cparams.grf_delta_min; p.grf_eps = ds.cparams.grf_eps;
+    p.td_sigma = ds.cparams.td_sigma; p.td_sigma_max = ds.cparams.td_sigma_max; p.td_lambda = ds.cparams.td_lambda;
+    p.ground = ds.cparams.ground_height;
+    const hsddp_hkd_weights &w = ds.weights;
+    for (int j = 0; j < 3; ++j) { p.qbase[j] = w.q_eul[j]; p.qbase[3 + j] = w.q_pos[j]; p.qbase[6 + j] = w.q_omega[j]; p.qbase[9 + j] = w.q_v[j]; }
+    p.q_qJ = w.q_qJ;
+    for (int j = 0; j < 24; ++j) p.qf_scale[j] = w.qf_scale[j];
+    p.qf_gain = w.qf_gain; p.r_grf = w.r_grf; p.r_qJd = w.r_qJd;
+    for (int j = 0; j < 3; ++j) p.foot_w[j] = w.foot_w[j];
+    p.foot_gain = w.foot_gain; p.foot_term_cost = w.foot_term_cost; p.foot_term_grad = w.foot_term_grad;
+    p.alpha = o.alpha; p.gamma = o.gamma; p.update_penalty = o.update_penalty; p.update_relax = o.update_relax;
+    p.update_regularization = o.update_regularization; p.update_ReB = o.update_ReB;
+    p.cost_thresh = o.cost_thresh; p.tconstr_thresh = o.tconstr_thresh; p.pconstr_thresh = o.pconstr_thresh;
+    p.feas_thresh = o.dynamics_feas_thresh; p.merit_scale = o.merit_scale; p.merit_offset = o.merit_offset;
+    p.AL_active = o.AL_active; p.ReB_active = o.ReB_active; p.no_early_exit = o.no_early_exit;
+}
+
+extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
+{
+    if (!desc || !out) return fail(HSDDP_ERR_ARG, "null argument");
+    if (desc->batch < 1 || desc->n_phases < 1 || desc->n_phases > HSDDP_MAX_PHASES || !(desc->dt > 0))
+        return fail(HSDDP_ERR_ARG, "invalid batch / n_phases / dt");
+    for (int i = 0; i < desc->n_phases; ++i)
+        if (desc->horizons[i] < 1) return fail(HSDDP_ERR_ARG, "phase horizons must be >= 1");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+        return fail(HSDDP_ERR_DEVICE, "no HIP device available (the solver has no CPU fallback)");
+    if (desc->device < 0 || desc->device >= ndev) return fail(HSDDP_ERR_DEVICE, "device ordinal out of range");
+    HIPCHK(hipSetDevice(desc->device));
+    hsddp_handle h = new hsddp_handle_t();
+    h->desc = *desc;
+    hsddp_default_options(&h->opt);
+    Params &p = h->p;
+    p.B = desc->batch;
+    p.P = desc->n_phases;
+    int s = 0, k = 0;
+    for (int i = 0; i < p.P; ++i) {
+        p.N[i] = desc->horizons[i]; p.s0[i] = s; p.k0[i] = k;
+        s += p.N[i] + 1; k += p.N[i];
+    }
+    p.S = s; p.Kc = k;
+    p.ref_per_element = desc->ref_per_element ? 1 : 0;
+    h->Bref = p.ref_per_element ? p.B : 1;
+    fill_params(h);
+    const size_t B = p.B, S = p.S, Kc = p.Kc, P = p.P, Br = h->Bref;
+    Bufs &d = h->d;
+    int *contacts; double *x0, *rx, *ru, *rf;
+    int rc = 0;
+    if ((rc = dalloc(h, contacts, B * (P + 1) * 4)) || (rc = dalloc(h, x0, B * NX)) || (rc = dalloc(h, rx, Br * S * NX)) ||
+        (rc = dalloc(h, ru, Br * S * NX)) || (rc = dalloc(h, rf, Br * S * 12)) || (rc = dalloc(h, d.X, B * S * NX)) ||
+        (rc = dalloc(h, d.Xbar, B * S * NX)) || (rc = dalloc(h, d.Defect, B * S * NX)) ||
+        (rc = dalloc(h, d.Defect_bar, B * S * NX)) || (rc = dalloc(h, d.dX, B * S * NX)) ||
+        (rc = dalloc(h, d.U, B * Kc * NX)) || (rc = dalloc(h, d.Ubar, B * Kc * NX)) || (rc = dalloc(h, d.dU, B * Kc * NX)) ||
+        (rc = dalloc(h, d.du, B * Kc * NX)) || (rc = dalloc(h, d.K, B * Kc * NN)) || (rc = dalloc(h, d.lq, B * Kc * LQW)) ||
+        (rc = dalloc(h, d.term, B * P * TW)) || (rc = dalloc(h, d.reb_delta, B * Kc * 20)) ||
+        (rc = dalloc(h, d.reb_eps, B * Kc * 20)) || (rc = dalloc(h, d.al_sigma, B * P * 4)) ||
+        (rc = dalloc(h, d.al_lambda, B * P * 4)) || (rc = dalloc(h, d.term_h, B * P * 4)) ||
+        (rc = dalloc(h, d.slot_cost, B * S)) || (rc = dalloc(h, d.slot_feas, B * S)) || (rc = dalloc(h, d.slot_viol, B * S)) ||
+        (rc = dalloc(h, d.slot_div, B * S)) || (rc = dalloc(h, d.el, B)) || (rc = dalloc(h, d.counter, 4))) {
+        hsddp_destroy(h);
+        return rc;
+    }
+    d.contacts = contacts; d.x0 = x0; d.ref_x = rx; d.ref_u = ru; d.ref_foot = rf;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void **)&h->host_counter, 4 * sizeof(int), 0) != hipSuccess) {
+        hsddp_destroy(h);
+        return fail(HSDDP_ERR_DEVICE, "stream / pinned allocation failed");
+    }
+    launch_init_params(p, d, h->stream);
+    launch_reset_elements(p, d, h->stream);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) {
+        hsddp_destroy(h);
+        return fail(HSDDP_ERR_DEVICE, "kernel launch failed at create (is the library built for this GPU?)");
+    }
+    *out = h;
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_destroy(hsddp_handle h)
+{
+    if (!h) return HSDDP_OK;
+    hipSetDevice(h->desc.device);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    for (void *p : h->allocs) hipFree(p);
+    if (h->host_counter) hipHostFree(h->host_counter);
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_set_options(hsddp_handle h, const hsddp_options *o)
+{
+    if (!h || !o) return fail(HSDDP_ERR_ARG, "null argument");
+    if (!(o->alpha > 0 && o->alpha < 1)) return fail(HSDDP_ERR_ARG, "alpha must lie in (0, 1)");
+    if (o->max_AL_iter < 0 || o->max_DDP_iter < 0) return fail(HSDDP_ERR_ARG, "negative iteration budget");
+    h->opt = *o;
+    fill_params(h);
+    return HSDDP_OK;
+}
+
+static int h2d(void *dst, const void *src, size_t bytes, hipStream_t st)
+{
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_upload_problem(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
+                                    const double *ref_u, const double *ref_foot)
+{
+    if (!h || !contacts || !x0 || !ref_x || !ref_u || !ref_foot) return fail(HSDDP_ERR_ARG, "null argument");
+    HIPCHK(hipSetDevice(h->desc.device));
+    const Params &p = h->p;
+    const size_t B = p.B, S = p.S, P = p.P, Br = h->Bref;
+    for (size_t q = 0; q < B * (P + 1) * 4; ++q)
+        if (contacts[q] != 0 && contacts[q] != 1) return fail(HSDDP_ERR_ARG, "contacts must be 0/1");
+    int rc;
+    if ((rc = h2d((void *)h->d.contacts, contacts, B * (P + 1) * 4 * sizeof(int), h->stream)) ||
+        (rc = h2d((void *)h->d.x0, x0, B * NX * sizeof(double), h->stream)) ||
+        (rc = h2d((void *)h->d.ref_x, ref_x, Br * S * NX * sizeof(double), h->stream)) ||
+        (rc = h2d((void *)h->d.ref_u, ref_u, Br * S * NX * sizeof(double), h->stream)) ||
+        (rc = h2d((void *)h->d.ref_foot, ref_foot, Br * S * 12 * sizeof(double), h->stream)))
+        return rc;
+    // default warm start: Xbar = X = reference (HKDProblem.cpp:84-90), Ubar = U = 0, K = 0
+    for (size_t b = 0; b < B; ++b) {
+        const double *src = h->Bref == 1 ? h->d.ref_x : h->d.ref_x + b * S * NX;
+        HIPCHK(hipMemcpyAsync(h->d.Xbar + b * S * NX, src, S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    }
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->have_problem = true;
+    return hsddp_upload_warm_start(h, nullptr, nullptr, nullptr);
+}
+
+extern "C" int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const double *Ubar, const double *K)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
+    HIPCHK(hipSetDevice(h->desc.device));
+    const Params &p = h->p;
+    const size_t B = p.B, S = p.S, Kc = p.Kc;
+    Bufs &d = h->d;
+    int rc;
+    if (Xbar && (rc = h2d(d.Xbar, Xbar, B * S * NX * sizeof(double), h->stream))) return rc;
+    if (Ubar && (rc = h2d(d.Ubar, Ubar, B * Kc * NX * sizeof(double), h->stream))) return rc;
+    if (K && (rc = h2d(d.K, K, B * Kc * NN * sizeof(double), h->stream))) return rc;
+    HIPCHK(hipMemcpyAsync(d.X, d.Xbar, B * S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(d.U, d.Ubar, B * Kc * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipMemsetAsync(d.dX, 0, B * S * NX * sizeof(double), h->stream));
+    HIPCHK(hipMemsetAsync(d.du, 0, B * Kc * NX * sizeof(double), h->stream));
+    HIPCHK(hipMemsetAsync(d.dU, 0, B * Kc * NX * sizeof(double), h->stream));
+    HIPCHK(hipMemsetAsync(d.Defect, 0, B * S * NX * sizeof(double), h->stream));
+    launch_init_params(p, d, h->stream);
+    launch_reset_elements(p, d, h->stream);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return HSDDP_OK;
+}
+
+// ---- solve --------------------------------------------------------------------------------------
+namespace {
+struct Timer {
+    hipStream_t st;
+    bool on;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[4];
+    void begin(int cat, hipEvent_t &e0)
+    {
+        if (!on) return;
+        hipEventCreate(&e0);
+        hipEventRecord(e0, st);
+        (void)cat;
+    }
+    void end(int cat, hipEvent_t e0)
+    {
+        if (!on) return;
+        hipEvent_t e1;
+        hipEventCreate(&e1);
+        hipEventRecord(e1, st);
+        ev[cat].push_back({e0, e1});
+    }
+    double total(int cat)
+    {
+        double t = 0;
+        for (auto &pr : ev[cat]) {
+            float ms = 0;
+            hipEventElapsedTime(&ms, pr.first, pr.second);
+            t += ms;
+            hipEventDestroy(pr.first);
+            hipEventDestroy(pr.second);
+        }
+        ev[cat].clear();
+        return t;
+    }
+};
+}  // namespace
+
+static int count_active(hsddp_handle h, int which, int &n)
+{
+    HIPCHK(hipMemsetAsync(h->d.counter, 0, 4 * sizeof(int), h->stream));
+    launch_count(h->p, h->d, which, h->stream);
+    HIPCHK(hipMemcpyAsync(h->host_counter, h->d.counter, 4 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    n = h->host_counter[which];
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_solve(hsddp_handle h, hsddp_stats *stats)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
+    if (!h->opt.MS)
+        return fail(HSDDP_ERR_UNSUPPORTED, "single shooting (MS = false) is not supported by the knot-parallel rollout");
+    HIPCHK(hipSetDevice(h->desc.device));
+    const Params &p = h->p;
+    const Bufs &d = h->d;
+    hipStream_t st = h->stream;
+    Timer tm{st, stats != nullptr, {}};
+    hipEvent_t e_all0 = nullptr, e_all1 = nullptr;
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        hipEventCreate(&e_all0);
+        hipEventCreate(&e_all1);
+        hipEventRecord(e_all0, st);
+    }
+    // line-search step sizes exactly as `while (eps > 1e-3) { ...; eps *= alpha; }` evaluates them
+    std::vector<double> trials;
+    for (double eps = 1; eps > 1e-3; eps *= h->opt.alpha) trials.push_back(eps);
+
+    launch_reset_elements(p, d, st);
+    // initial rollout: hybrid_rollout(0), update_nominal_trajectory, compute_cost, feasibility
+    launch_rollout(p, d, 0.0, 1, st);
+    launch_decide(p, d, 0.0, 0, 1, st);
+    launch_update_nominal(p, d, 1, st);
+    int iters_launched = 0, outer_launched = 0, n_bwd = 0;
+    const bool checks = !h->opt.no_early_exit;
+    for (int ou = 0; ou < h->opt.max_AL_iter; ++ou) {
+        launch_outer_begin(p, d, st);
+        outer_launched++;
+        for (int in = 0; in < h->opt.max_DDP_iter; ++in) {
+            hipEvent_t e0;
+            tm.begin(0, e0);
+            launch_lq(p, d, st);
+            tm.end(0, e0);
+            tm.begin(1, e0);
+            launch_backward(p, d, st);
+            tm.end(1, e0);
+            n_bwd++;
+            tm.begin(2, e0);
+            for (size_t t = 0; t < trials.size(); ++t) {
+                launch_rollout(p, d, trials[t], 0, st);
+                launch_decide(p, d, trials[t], t + 1 == trials.size(), 0, st);
+            }
+            launch_update_nominal(p, d, 0, st);
+            tm.end(2, e0);
+            iters_launched++;
+            if (checks) {
+                int n = 0, rc = count_active(h, 1, n);
+                if (rc) return rc;
+                if (n == 0) break;
+            }
+        }
+        hipEvent_t e0;
+        tm.begin(3, e0);
+        if (h->opt.ReB_active) launch_reb_update(p, d, st);
+        launch_outer_end(p, d, st);
+        tm.end(3, e0);
+        if (checks) {
+            int n = 0, rc = count_active(h, 2, n);
+            if (rc) return rc;
+            if (n == 0) break;
+        }
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    if (stats) {
+        hipEventRecord(e_all1, st);
+        hipEventSynchronize(e_all1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e_all0, e_all1);
+        stats->ms_total = ms;
+        stats->ms_lq = tm.total(0);
+        stats->ms_backward = tm.total(1);
+        stats->ms_forward = tm.total(2);
+        stats->ms_other = tm.total(3);
+        stats->inner_iterations = iters_launched;
+        stats->outer_iterations = outer_launched;
+        stats->n_backward_launches = n_bwd;
+        hipEventDestroy(e_all0);
+        hipEventDestroy(e_all1);
+        std::vector<ElemState> el(p.B);
+        HIPCHK(hipMemcpy(el.data(), d.el, p.B * sizeof(ElemState), hipMemcpyDeviceToHost));
+        for (auto &e : el) { stats->ls_trials += e.n_ls; stats->element_iterations += e.iters; }
+    }
+    return HSDDP_OK;
+}
+
+static int d2h(void *dst, const void *src, size_t bytes)
+{
+    if (!dst) return HSDDP_OK;
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_download_trajectory(hsddp_handle h, double *Xbar, double *Ubar, double *K)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const size_t B = h->p.B, S = h->p.S, Kc = h->p.Kc;
+    int rc;
+    if ((rc = d2h(Xbar, h->d.Xbar, B * S * NX * 8)) || (rc = d2h(Ubar, h->d.Ubar, B * Kc * NX * 8)) ||
+        (rc = d2h(K, h->d.K, B * Kc * NN * 8)))
+        return rc;
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_download_working(hsddp_handle h, double *X, double *U, double *Defect, double *dX, double *dU)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const size_t B = h->p.B, S = h->p.S, Kc = h->p.Kc;
+    int rc;
+    if ((rc = d2h(X, h->d.X, B * S * NX * 8)) || (rc = d2h(U, h->d.U, B * Kc * NX * 8)) ||
+        (rc = d2h(Defect, h->d.Defect, B * S * NX * 8)) || (rc = d2h(dX, h->d.dX, B * S * NX * 8)) ||
+        (rc = d2h(dU, h->d.dU, B * Kc * NX * 8)))
+        return rc;
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_download_element_info(hsddp_handle h, hsddp_element_info *info)
+{
+    if (!h || !info) return fail(HSDDP_ERR_ARG, "null argument");
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    std::vector<ElemState> el(h->p.B);
+    HIPCHK(hipMemcpy(el.data(), h->d.el, h->p.B * sizeof(ElemState), hipMemcpyDeviceToHost));
+    for (int b = 0; b < h->p.B; ++b) {
+        const ElemState &e = el[b];
+        info[b].cost = e.cost; info[b].feas = e.feas; info[b].merit = e.merit;
+        info[b].max_tconstr = e.max_t; info[b].max_pconstr = e.max_p;
+        info[b].iters = e.iters; info[b].outer_iters = e.outer_iters; info[b].status = e.status;
+        info[b].n_ls_trials = e.n_ls;
+    }
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_synchronize(hsddp_handle h)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return HSDDP_OK;
+}
+
+extern "C" size_t hsddp_device_bytes(hsddp_handle h) { return h ? h->bytes : 0; }
+
+// ---- model primitives ------------------------------------------------------------------------
+static int check_launch()
+{
+    HIPCHK(hipGetLastError());
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_hkd_dynamics(const double *x, const double *u, const double *c, double dt, double *xn, int n,
+                                  void *stream)
+{
+    if (!x || !u || !c || !xn || n < 0) return fail(HSDDP_ERR_ARG, "bad argument");
+    if (n) launch_model_dynamics(x, u, c, dt, xn, n, (hipStream_t)stream);
+    return check_launch();
+}
+extern "C" int hsddp_hkd_dynamics_partial(const double *x, const double *u, const double *c, double dt, double *A,
+                                          double *B, int n, void *stream)
+{
+    if (!x || !u || !c || !A || !B || n < 0) return fail(HSDDP_ERR_ARG, "bad argument");
+    if (n) launch_model_partial(x, u, c, dt, A, B, n, (hipStream_t)stream);
+    return check_launch();
+}
+extern "C" int hsddp_hkd_foot_position(const double *x, const int *leg, double *p, int n, void *stream)
+{
+    if (!x || !leg || !p || n < 0) return fail(HSDDP_ERR_ARG, "bad argument");
+    if (n) launch_model_foot(x, leg, p, nullptr, n, (hipStream_t)stream);
+    return check_launch();
+}
+extern "C" int hsddp_hkd_foot_jacobian(const double *x, const int *leg, double *J, int n, void *stream)
+{
+    if (!x || !leg || !J || n < 0) return fail(HSDDP_ERR_ARG, "bad argument");
+    if (n) launch_model_foot(x, leg, nullptr, J, n, (hipStream_t)stream);
+    return check_launch();
+}
+extern "C" int hsddp_hkd_resetmap(const double *x, const int *c, const int *cn, double *xn, int n, void *stream)
+{
+    if (!x || !c || !cn || !xn || n < 0) return fail(HSDDP_ERR_ARG, "bad argument");
+    if (n) launch_model_reset(x, c, cn, xn, nullptr, n, (hipStream_t)stream);
+    return check_launch();
+}
+extern "C" int hsddp_hkd_resetmap_partial(const double *x, const int *c, const int *cn, double *Px, int n,
+                                          void *stream)
+{
+    if (!x || !c || !cn || !Px || n < 0) return fail(HSDDP_ERR_ARG, "bad argument");
+    if (n) launch_model_reset(x, c, cn, nullptr, Px, n, (hipStream_t)stream);
+    return check_launch();
+}
+
+extern "C" void *hsddp_device_alloc(size_t bytes, int device)
+{
+    if (hipSetDevice(device) != hipSuccess) { g_err = "hipSetDevice failed"; return nullptr; }
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) { g_err = "hipMalloc failed"; return nullptr; }
+    return p;
+}
+extern "C" int hsddp_device_free(void *p)
+{
+    HIPCHK(hipFree(p));
+    return HSDDP_OK;
+}
+extern "C" int hsddp_memcpy_h2d(void *dst, const void *src, size_t bytes)
+{
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return HSDDP_OK;
+}
+extern "C" int hsddp_memcpy_d2h(void *dst, const void *src, size_t bytes)
+{
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return HSDDP_OK;
+}
+extern "C" int hsddp_device_synchronize(int device)
+{
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipDeviceSynchronize());
+    return HSDDP_OK;
+}

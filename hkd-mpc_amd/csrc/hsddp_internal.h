@@ -1,0 +1,93 @@
+// hsddp_internal.h — device data layout and kernel interface of the batched HS-DDP solver.
+//
+// HBM layout (element-major, fp64; b = element, s = state slot, kc = control slot):
+//   X, Xbar, Defect, Defect_bar, dX   [B][S][24]
+//   U, Ubar, dU, du                   [B][Kc][24]     du = dU + K dX (linear-rollout control step)
+//   K                                 [B][Kc][24][24] row-major
+//   lq                                [B][Kc][LQW]    compact LQ model of one knot (below)
+//   term                              [B][P][TW]      Phix | Phixx | Px (reset-map Jacobian at X_i[N])
+//   reb_delta, reb_eps                [B][Kc][20]     ReB params, index leg*5 + row
+//   al_sigma, al_lambda, term_h       [B][P][4]
+//   slot_cost, slot_feas, slot_viol   [B][S]          per-slot partial sums for per-element reductions
+// One element's data is contiguous, so the per-element backward kernel streams it coalesced.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include "hkd_model.h"
+
+namespace hsddp {
+
+constexpr int NX = 24;
+constexpr int NN = 576;
+constexpr int MAXP = 16;
+
+// compact LQ record per control slot
+constexpr int LQ_SE = 0;                 // 15  A - I, eul rows
+constexpr int LQ_SW = LQ_SE + 15;        // 51  A - I, omega rows
+constexpr int LQ_BW = LQ_SW + 51;        // 36  B, omega rows x GRF cols
+constexpr int LQ_LX = LQ_BW + 36;        // 24
+constexpr int LQ_LU = LQ_LX + 24;        // 24
+constexpr int LQ_RB = LQ_LU + 24;        // 24  dt * ReB Hessian, 4 legs x sym 3x3 (00,01,02,11,12,22)
+constexpr int LQW = LQ_RB + 24;          // 174
+
+constexpr int TM_PHIX = 0;
+constexpr int TM_PHIXX = 24;
+constexpr int TM_PX = 24 + NN;
+constexpr int TW = 24 + 2 * NN;          // 1176
+
+struct Params {
+    int B, P, S, Kc;
+    int N[MAXP], s0[MAXP], k0[MAXP];
+    int ref_per_element;
+    double dt, mu, grf_delta, grf_delta_min, grf_eps, td_sigma, td_sigma_max, td_lambda, ground;
+    // HKD weights
+    double qbase[12], q_qJ, qf_scale[24], qf_gain, r_grf, r_qJd, foot_w[3], foot_gain, foot_term_cost, foot_term_grad;
+    // HSDDP_OPTION
+    double alpha, gamma, update_penalty, update_relax, update_regularization, update_ReB;
+    double cost_thresh, tconstr_thresh, pconstr_thresh, feas_thresh, merit_scale, merit_offset;
+    int AL_active, ReB_active, no_early_exit;
+};
+
+struct ElemState {
+    double cost, feas, merit, merit_rho, dV1, dV2, reg;
+    double max_t, max_p, max_t_prev, max_p_prev, cost_prev, merit_prev, feas_prev;
+    int done, inner_done, ls_active, accepted, status, iters, outer_iters, n_ls;
+};
+
+struct Bufs {
+    const int *contacts;                   // [B][P+1][4]
+    const double *x0;                      // [B][24]
+    const double *ref_x, *ref_u, *ref_foot; // [Bref][S][24|24|12]
+    double *X, *Xbar, *Defect, *Defect_bar, *dX;
+    double *U, *Ubar, *dU, *du;
+    double *K, *lq, *term;
+    double *reb_delta, *reb_eps, *al_sigma, *al_lambda, *term_h;
+    double *slot_cost, *slot_feas, *slot_viol;
+    int *slot_div;
+    ElemState *el;
+    int *counter;                          // [4] host-visible activity counters
+};
+
+// kernel launchers (hsddp_kernels.hip)
+void launch_rollout(const Params &p, const Bufs &d, double eps, int init, hipStream_t st);
+void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, hipStream_t st);
+void launch_update_nominal(const Params &p, const Bufs &d, int init, hipStream_t st);
+void launch_lq(const Params &p, const Bufs &d, hipStream_t st);
+void launch_backward(const Params &p, const Bufs &d, hipStream_t st);
+void launch_outer_begin(const Params &p, const Bufs &d, hipStream_t st);
+void launch_reb_update(const Params &p, const Bufs &d, hipStream_t st);
+void launch_outer_end(const Params &p, const Bufs &d, hipStream_t st);
+void launch_reset_elements(const Params &p, const Bufs &d, hipStream_t st);
+void launch_init_params(const Params &p, const Bufs &d, hipStream_t st);
+void launch_count(const Params &p, const Bufs &d, int which, hipStream_t st);
+
+// model primitives
+void launch_model_dynamics(const double *x, const double *u, const double *c, double dt, double *xn, int n,
+                           hipStream_t st);
+void launch_model_partial(const double *x, const double *u, const double *c, double dt, double *A, double *B,
+                          int n, hipStream_t st);
+void launch_model_foot(const double *x, const int *leg, double *p, double *J, int n, hipStream_t st);
+void launch_model_reset(const double *x, const int *c, const int *cn, double *xn, double *Px, int n,
+                        hipStream_t st);
+
+}  // namespace hsddp

@@ -1,0 +1,1117 @@
+// hsddp_kernels.hip — CDNA4 (gfx950) kernels of the batched HS-DDP solver, fp64.
+//
+// One DDP inner iteration of MultiPhaseDDP::solve (HSDDPSolver/source/MultiPhaseDDP.cpp:304-381)
+// for B trajectories is:
+//   k_lq        knot-parallel  cost at (X, U) + compact LQ model   SinglePhase::compute_cost/LQ_approximation
+//   k_terminal  (elem, phase)  Phix, Phixx (+AL), reset Jacobian   SinglePhase.cpp:286-295; HKDReset.h:78-136
+//   k_backward  one wave/elem  regularised Riccati sweep over all phases + MS linear rollout
+//                              MultiPhaseDDP.cpp:141-229, 20-50; SinglePhase.cpp:144-178, 298-367
+//   k_rollout   knot-parallel  one line-search trial (all knots are shooting states)  SinglePhase.cpp:181-233
+//   k_decide    per element    merit acceptance (MultiPhaseDDP.cpp:113-133) + inner-loop exit tests
+//   k_update_nominal           Trajectory::update_nominal_vals (TrajectoryManagement.cpp:110-115)
+// plus the outer AL/ReB updates (ConstraintsBase.h:168-183, 349-365; MultiPhaseDDP.cpp:383-408).
+//
+// Every element carries its own control-flow state (ElemState): regularisation retries, line-search
+// acceptance, early exits and AL/ReB updates are per-element masks, never lockstep.
+#include "hsddp_internal.h"
+
+namespace hsddp {
+
+using namespace hkd;
+
+#define DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------------------------------------
+// cost model helpers (HKDCost.h / HKDCost.cpp / SinglePhaseInterface.cpp:55-118)
+DEV double q_diag(const Params &p, const int *c, int j) { return j < 12 ? p.qbase[j] : p.q_qJ * (1 - c[(j - 12) / 3]); }
+DEV double r_diag(const Params &p, int j) { return j < 12 ? p.r_grf : p.r_qJd; }
+DEV double foot_weight(const Params &p, const int *c, int j) { return p.foot_gain * p.foot_w[j % 3] * c[j / 3]; }
+DEV bool touchdown(const int *c, const int *cn, int l) { return c[l] == 0 && cn[l] == 1; }
+
+DEV void slot_phase(const Params &p, int s, int &i, int &k)
+{
+    i = 0;
+    for (int j = 1; j < p.P; ++j)
+        if (s >= p.s0[j]) i = j;
+    k = s - p.s0[i];
+}
+
+DEV void load_contacts(const Bufs &d, const Params &p, int b, int i, int *c, int *cn)
+{
+    const int *cc = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) { c[l] = cc[l]; cn[l] = cc[4 + l]; }
+}
+
+DEV const double *ref_ptr(const Params &p, const double *base, int b, int s, int width)
+{
+    return base + ((size_t)(p.ref_per_element ? b : 0) * p.S + s) * width;
+}
+
+// ReB barrier (ConstraintsBase.h:204-263)
+DEV double reb_cost(double g, double delta)
+{
+    if (g > delta) return -log(g);
+    double t = (g - 2 * delta) / delta;
+    return .5 * (t * t - 1) - log(delta);
+}
+DEV void reb_derivs(double g, double delta, double &d1, double &d2)
+{
+    if (g > delta) { d1 = -1.0 / g; d2 = 1.0 / (g * g); }
+    else { d1 = (g - 2 * delta) / delta / delta; d2 = 1.0 / (delta * delta); }
+}
+
+// GRF friction pyramid (HKDConstraints.cpp:7-66): rows of A_leg applied to one leg's force
+DEV void grf_row(double mu, int r, double *row)
+{
+    row[0] = (r == 1) ? -1.0 : (r == 2) ? 1.0 : 0.0;
+    row[1] = (r == 3) ? -1.0 : (r == 4) ? 1.0 : 0.0;
+    row[2] = (r == 0) ? 1.0 : mu;
+}
+DEV double grf_value(double mu, int r, const double *f)
+{
+    double row[3];
+    grf_row(mu, r, row);
+    return row[0] * f[0] + row[1] * f[1] + row[2] * f[2];
+}
+
+// running cost l_k (tracking + foot regularisation + dt * ReB), and min(0, min g)
+DEV double running_cost(const Params &p, const int *c, const double *x, const double *u, const double *xr,
+                        const double *ur, const double *pf, const double *delta, const double *eps, double &viol)
+{
+    double lt = 0.0, lu = 0.0, lf = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) { double e = x[j] - xr[j]; lt += e * q_diag(p, c, j) * e; }
+    lt = 0.5 * lt;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) { double e = u[j] - ur[j]; lu += e * r_diag(p, j) * e; }
+    lt += 0.5 * lu;
+    lt *= p.dt;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        double e = (x[12 + j] - x[3 + j % 3]) - (pf[j] - xr[3 + j % 3]);
+        lf += e * foot_weight(p, c, j) * e;
+    }
+    lf = .5 * lf;
+    lf *= p.dt;
+    double l = lt + lf;
+    double rc = 0.0, mk = 0.0;
+    for (int lg = 0; lg < 4; ++lg) {
+        if (!c[lg]) continue;
+        for (int r = 0; r < 5; ++r) {
+            double g = grf_value(p.mu, r, u + 3 * lg);
+            mk = fmin(mk, g);
+            rc += eps[5 * lg + r] * reb_cost(g, delta[5 * lg + r]);
+        }
+    }
+    if (p.ReB_active && (c[0] + c[1] + c[2] + c[3]) > 0) l += p.dt * rc;
+    viol = mk;
+    return l;
+}
+
+// terminal cost Phi (tracking Qf + 10 * foot + AL), max |h| and h per touchdown leg
+DEV double terminal_cost(const Params &p, const int *c, const int *cn, const double *x, const double *xr,
+                         const double *pf, const double *sig, const double *lam, double &tviol, double *h_out)
+{
+    double phi = 0.0, fc = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+        double e = x[j] - xr[j];
+        phi += e * (p.qf_gain * p.qf_scale[j] * q_diag(p, c, j)) * e;
+    }
+    phi *= 0.5;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        double e = (x[12 + j] - x[3 + j % 3]) - (pf[j] - xr[3 + j % 3]);
+        fc += e * foot_weight(p, c, j) * e;
+    }
+    phi = phi + p.foot_term_cost * fc;
+    double al = 0.0, tv = 0.0;
+    for (int l = 0; l < 4; ++l) {
+        h_out[l] = 0.0;
+        if (!touchdown(c, cn, l)) continue;
+        double h = hkd_foot_height_grad(l, x, nullptr) - p.ground;
+        h_out[l] = h;
+        tv = fmax(tv, fabs(h));
+        al += 0.5 * sig[l] * h * h;
+        al += lam[l] * h;
+    }
+    if (p.AL_active) phi += al;
+    tviol = tv;
+    return phi;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_lq: per (element, state slot): cost and |Defect|^2 at the current (X, U); compact LQ model at
+// control slots (SinglePhase::compute_cost + LQ_approximation, SinglePhase.cpp:235-296).
+__global__ __launch_bounds__(256) void k_lq(Params p, Bufs d)
+{
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)p.B * p.S) return;
+    const int b = (int)(gid / p.S), s = (int)(gid % p.S);
+    const ElemState &E = d.el[b];
+    if (E.done || E.inner_done) return;
+    int i, k;
+    slot_phase(p, s, i, k);
+    int c[4], cn[4];
+    load_contacts(d, p, b, i, c, cn);
+    double x[NX];
+    const double *xg = d.X + ((size_t)b * p.S + s) * NX;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) x[j] = xg[j];
+    const double *dg = d.Defect + ((size_t)b * p.S + s) * NX;
+    double fs = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) fs += dg[j] * dg[j];
+    d.slot_feas[(size_t)b * p.S + s] = fs;
+    const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
+    if (k == p.N[i]) {
+        double tv, h[4];
+        const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
+        d.slot_cost[(size_t)b * p.S + s] = terminal_cost(p, c, cn, x, xr, pf, sg, lm, tv, h);
+        return;
+    }
+    const int kc = p.k0[i] + k;
+    double u[NU];
+    const double *ug = d.U + ((size_t)b * p.Kc + kc) * NU;
+#pragma unroll
+    for (int j = 0; j < NU; ++j) u[j] = ug[j];
+    const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
+    const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
+    double viol;
+    d.slot_cost[(size_t)b * p.S + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
+
+    double *rec = d.lq + ((size_t)b * p.Kc + kc) * LQW;
+    double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
+    double Se[SE_N], Sw[SW_N], Bw[BW_N];
+    hkd_partial_compact(x, u, cd, p.dt, Se, Sw, Bw);
+#pragma unroll
+    for (int j = 0; j < SE_N; ++j) rec[LQ_SE + j] = Se[j];
+#pragma unroll
+    for (int j = 0; j < SW_N; ++j) rec[LQ_SW + j] = Sw[j];
+#pragma unroll
+    for (int j = 0; j < BW_N; ++j) rec[LQ_BW + j] = Bw[j];
+    // lx: tracking + foot regularisation (HKDCost.cpp:22-37)
+    double lx[NX];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) lx[j] = p.dt * q_diag(p, c, j) * (x[j] - xr[j]);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        double e = (x[12 + j] - x[3 + j % 3]) - (pf[j] - xr[3 + j % 3]);
+        double v = p.dt * c[j / 3] * foot_weight(p, c, j) * e;
+        lx[3 + j % 3] += -v;
+        lx[12 + j] += v;
+    }
+#pragma unroll
+    for (int j = 0; j < NX; ++j) rec[LQ_LX + j] = lx[j];
+    // lu + ReB gradient / Hessian (SinglePhase.cpp:380-394)
+    double lu[NU], rb[24];
+#pragma unroll
+    for (int j = 0; j < NU; ++j) lu[j] = p.dt * r_diag(p, j) * (u[j] - ur[j]);
+#pragma unroll
+    for (int j = 0; j < 24; ++j) rb[j] = 0.0;
+    if (p.ReB_active) {
+        for (int lg = 0; lg < 4; ++lg) {
+            if (!c[lg]) continue;
+            double gu[3] = {0, 0, 0}, hu[6] = {0, 0, 0, 0, 0, 0};
+            for (int r = 0; r < 5; ++r) {
+                double row[3], d1, d2;
+                grf_row(p.mu, r, row);
+                double g = row[0] * u[3 * lg] + row[1] * u[3 * lg + 1] + row[2] * u[3 * lg + 2];
+                reb_derivs(g, dl[5 * lg + r], d1, d2);
+                double e = ep[5 * lg + r];
+                for (int a = 0; a < 3; ++a) gu[a] += e * d1 * row[a];
+                hu[0] += e * (d2 * row[0] * row[0]); hu[1] += e * (d2 * row[0] * row[1]);
+                hu[2] += e * (d2 * row[0] * row[2]); hu[3] += e * (d2 * row[1] * row[1]);
+                hu[4] += e * (d2 * row[1] * row[2]); hu[5] += e * (d2 * row[2] * row[2]);
+            }
+            for (int a = 0; a < 3; ++a) lu[3 * lg + a] += p.dt * gu[a];
+            for (int a = 0; a < 6; ++a) rb[6 * lg + a] = p.dt * hu[a];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NU; ++j) rec[LQ_LU + j] = lu[j];
+#pragma unroll
+    for (int j = 0; j < 24; ++j) rec[LQ_RB + j] = rb[j];
+}
+
+// k_terminal: one wave per (element, phase): Phix, Phixx (+AL, quirk A4) and reset-map Jacobian Px.
+__global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
+{
+    const int b = blockIdx.x / p.P, i = blockIdx.x % p.P, t = threadIdx.x;
+    const ElemState &E = d.el[b];
+    if (E.done || E.inner_done) return;
+    __shared__ double sx[NX], shx[4][NX], scoef[4][2];
+    __shared__ int sc[4], scn[4];
+    const int s = p.s0[i] + p.N[i];
+    if (t < NX) sx[t] = d.X[((size_t)b * p.S + s) * NX + t];
+    if (t < 4) {
+        const int *cc = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
+        sc[t] = cc[t]; scn[t] = cc[4 + t];
+    }
+    __syncthreads();
+    if (t < 4) {
+        const int l = t;
+        double hx[NX];
+        double h = 0.0;
+        bool td = touchdown(sc, scn, l);
+        if (td) h = hkd_foot_height_grad(l, sx, hx) - p.ground;
+        for (int j = 0; j < NX; ++j) shx[l][j] = td ? hx[j] : 0.0;
+        double sg = d.al_sigma[((size_t)b * p.P + i) * 4 + l], lm = d.al_lambda[((size_t)b * p.P + i) * 4 + l];
+        scoef[l][0] = (td && p.AL_active) ? sg * h + lm : 0.0;
+        scoef[l][1] = (td && p.AL_active) ? sg * (1 + h) + lm : 0.0;
+    }
+    __syncthreads();
+    double *rec = d.term + ((size_t)b * p.P + i) * TW;
+    const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
+    if (t < NX) { // Phix
+        const int j = t;
+        double v = p.qf_gain * p.qf_scale[j] * q_diag(p, sc, j) * (sx[j] - xr[j]);
+        if (j >= 3 && j < 6) {
+            for (int l = 0; l < 4; ++l) {
+                int m = 3 * l + (j - 3);
+                double e = (sx[12 + m] - sx[j]) - (pf[m] - xr[j]);
+                v += -(p.foot_term_grad * sc[l] * foot_weight(p, sc, m) * e);
+            }
+        } else if (j >= 12) {
+            int m = j - 12, l = m / 3;
+            double e = (sx[j] - sx[3 + m % 3]) - (pf[m] - xr[3 + m % 3]);
+            v += p.foot_term_grad * sc[l] * foot_weight(p, sc, m) * e;
+        }
+        for (int l = 0; l < 4; ++l) v += scoef[l][0] * shx[l][j];
+        rec[TM_PHIX + j] = v;
+    }
+    for (int e = t; e < NN; e += 64) { // Phixx
+        const int r = e / NX, cidx = e % NX;
+        double v = (r == cidx) ? p.qf_gain * p.qf_scale[r] * q_diag(p, sc, r) : 0.0;
+        // foot Hessian 20 D^T Qfoot D
+        for (int l = 0; l < 4; ++l)
+            for (int j = 0; j < 3; ++j) {
+                double w = p.foot_term_grad * sc[l] * sc[l] * foot_weight(p, sc, 3 * l + j);
+                int a = 3 + j, bb = 12 + 3 * l + j;
+                if ((r == a && cidx == a) || (r == bb && cidx == bb)) v += w;
+                if ((r == a && cidx == bb) || (r == bb && cidx == a)) v -= w;
+            }
+        for (int l = 0; l < 4; ++l) v += scoef[l][1] * (shx[l][r] * shx[l][cidx]);
+        rec[TM_PHIXX + e] = v;
+    }
+    if (i < p.P - 1 && t < NX) { // Px rows at X_i[N]
+        double row[NX];
+        hkd_resetmap_partial_row(sx, sc, scn, t, row);
+        for (int j = 0; j < NX; ++j) rec[TM_PX + t * NX + j] = row[j];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_backward: one 64-lane wave per element.  Regularised backward Riccati sweep over all phases
+// with impact-aware value transfer, then the multiple-shooting linear rollout.  24x24 blocks live
+// in LDS (row stride 25 doubles: column walks hit 32 distinct even banks).
+constexpr int LD = 25;
+constexpr int LDY = 26;
+
+struct BwdSmem {
+    double H[NX * LD], M[NX * LD], Q[NX * LD], Y[NX * LDY];
+    double G[NX], Gn[NX], Qx[NX], Qu[NX], dv[NX], lq[LQW + 2];
+    double red[64];
+    int contact[4];
+};
+
+DEV double S_at(const double *lq, double dt, int j, int c) // (A - I)[j][c]
+{
+    if (j < 3) { int q = se_index(c); return q >= 0 ? lq[LQ_SE + 5 * j + q] : 0.0; }
+    if (j < 6) return (c == j + 6) ? dt : 0.0;
+    if (j < 9) { int q = sw_index(c); return q >= 0 ? lq[LQ_SW + 17 * (j - 6) + q] : 0.0; }
+    return 0.0;
+}
+
+// (M)[r][c] = (H A)[r][c]
+DEV double HA_elem(const double *H, const double *lq, double dt, int r, int c)
+{
+    const double *h = H + r * LD;
+    double v = h[c];
+    int q = se_index(c);
+    if (q >= 0) v += h[0] * lq[LQ_SE + q] + h[1] * lq[LQ_SE + 5 + q] + h[2] * lq[LQ_SE + 10 + q];
+    if (c >= 9 && c < 12) v += h[c - 6] * dt;
+    q = sw_index(c);
+    if (q >= 0) v += h[6] * lq[LQ_SW + q] + h[7] * lq[LQ_SW + 17 + q] + h[8] * lq[LQ_SW + 34 + q];
+    return v;
+}
+
+// (S^T V)[r][c] for a row-major block V (stride ld): sum_j S[j][r] V[j][c]
+DEV double StV_elem(const double *V, int ld, const double *lq, double dt, int r, int c)
+{
+    double v = 0.0;
+    int q = se_index(r);
+    if (q >= 0) v += lq[LQ_SE + q] * V[c] + lq[LQ_SE + 5 + q] * V[ld + c] + lq[LQ_SE + 10 + q] * V[2 * ld + c];
+    if (r >= 9 && r < 12) v += dt * V[(r - 6) * ld + c];
+    q = sw_index(r);
+    if (q >= 0)
+        v += lq[LQ_SW + q] * V[6 * ld + c] + lq[LQ_SW + 17 + q] * V[7 * ld + c] + lq[LQ_SW + 34 + q] * V[8 * ld + c];
+    return v;
+}
+
+// (V B)[r][c] for row-major V: sum_j V[r][j] B[j][c]
+DEV double VB_elem(const double *V, int ld, const double *lq, const int *ct, double dt, int r, int c)
+{
+    const double *v = V + r * ld;
+    if (c < 12) {
+        int l = c / 3, m = c % 3;
+        return v[6] * lq[LQ_BW + c] + v[7] * lq[LQ_BW + 12 + c] + v[8] * lq[LQ_BW + 24 + c] +
+               v[9 + m] * (dt * ct[l] / kMass);
+    }
+    return v[c] * (dt * (1.0 - ct[(c - 12) / 3]));
+}
+
+// (B^T V)[r][c]: sum_j B[j][r] V[j][c]
+DEV double BtV_elem(const double *V, int ld, const double *lq, const int *ct, double dt, int r, int c)
+{
+    if (r < 12) {
+        int l = r / 3, m = r % 3;
+        return lq[LQ_BW + r] * V[6 * ld + c] + lq[LQ_BW + 12 + r] * V[7 * ld + c] + lq[LQ_BW + 24 + r] * V[8 * ld + c] +
+               (dt * ct[l] / kMass) * V[(9 + m) * ld + c];
+    }
+    return (dt * (1.0 - ct[(r - 12) / 3])) * V[r * ld + c];
+}
+
+DEV double lxx_elem(const Params &p, const int *ct, int r, int c)
+{
+    double v = 0.0;
+    if (r == c) v = p.dt * q_diag(p, ct, r);
+    // foot regularisation Hessian dt * D^T Qfoot D (HKDCost.cpp:32)
+    if (r >= 3 && r < 6 && c == r) {
+        for (int l = 0; l < 4; ++l) v += p.dt * ct[l] * ct[l] * foot_weight(p, ct, 3 * l + r - 3);
+    } else if (r >= 12 && c == r) {
+        int m = r - 12;
+        v += p.dt * ct[m / 3] * ct[m / 3] * foot_weight(p, ct, m);
+    } else if (r >= 3 && r < 6 && c >= 12 && (c - 12) % 3 == r - 3) {
+        int m = c - 12;
+        v -= p.dt * ct[m / 3] * ct[m / 3] * foot_weight(p, ct, m);
+    } else if (c >= 3 && c < 6 && r >= 12 && (r - 12) % 3 == c - 3) {
+        int m = r - 12;
+        v -= p.dt * ct[m / 3] * ct[m / 3] * foot_weight(p, ct, m);
+    }
+    return v;
+}
+
+DEV double luu_elem(const Params &p, const double *lq, int r, int c)
+{
+    double v = (r == c) ? p.dt * r_diag(p, r) : 0.0;
+    if (r < 12 && c < 12 && r / 3 == c / 3) {
+        int l = r / 3, a = r % 3, bb = c % 3;
+        if (a > bb) { int t = a; a = bb; bb = t; }
+        int idx = a == 0 ? bb : (a == 1 ? 2 + bb : 5);
+        v += lq[LQ_RB + 6 * l + idx];
+    }
+    return v;
+}
+
+DEV double wave_sum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// One knot of SinglePhase::backward_sweep.  Returns false when Quu fails the PSD test.
+DEV bool bwd_knot(const Params &p, const Bufs &d, BwdSmem &sm, int b, int s, int kc, double reg, double &dV1,
+                  double &dV2)
+{
+    const int t = threadIdx.x;
+    const double dt = p.dt;
+    const double *lqg = d.lq + ((size_t)b * p.Kc + kc) * LQW;
+    for (int j = t; j < LQW; j += 64) sm.lq[j] = lqg[j];
+    if (t < NX) sm.dv[t] = d.Defect[((size_t)b * p.S + s + 1) * NX + t];
+    __syncthreads();
+    // Gnext = G + H Defect[k+1]  (SinglePhase.cpp:317-320)
+    if (t < NX) {
+        double a = 0.0;
+        for (int c = 0; c < NX; ++c) a += sm.H[t * LD + c] * sm.dv[c];
+        sm.Gn[t] = sm.G[t] + a;
+    }
+    // M = H A, HB = H B (into Y)
+    for (int e = t; e < NN; e += 64) {
+        int r = e / NX, c = e % NX;
+        sm.M[r * LD + c] = HA_elem(sm.H, sm.lq, dt, r, c);
+        sm.Y[r * LDY + c] = VB_elem(sm.H, LD, sm.lq, sm.contact, dt, r, c);
+    }
+    __syncthreads();
+    // Qxx = lxx + A^T H A (into H), Quu = luu + B^T H B (into Q); Qx, Qu
+    for (int e = t; e < NN; e += 64) {
+        int r = e / NX, c = e % NX;
+        double qxx = lxx_elem(p, sm.contact, r, c) + (sm.M[r * LD + c] + StV_elem(sm.M, LD, sm.lq, dt, r, c));
+        sm.H[r * LD + c] = qxx + (r == c ? reg : 0.0);
+        double quu = luu_elem(p, sm.lq, r, c) + BtV_elem(sm.Y, LDY, sm.lq, sm.contact, dt, r, c);
+        sm.Q[r * LD + c] = quu + (r == c ? reg : 0.0);
+    }
+    if (t < NX) {
+        double a = 0.0;
+        int q = se_index(t);
+        if (q >= 0) a += sm.lq[LQ_SE + q] * sm.Gn[0] + sm.lq[LQ_SE + 5 + q] * sm.Gn[1] + sm.lq[LQ_SE + 10 + q] * sm.Gn[2];
+        if (t >= 9 && t < 12) a += dt * sm.Gn[t - 6];
+        q = sw_index(t);
+        if (q >= 0) a += sm.lq[LQ_SW + q] * sm.Gn[6] + sm.lq[LQ_SW + 17 + q] * sm.Gn[7] + sm.lq[LQ_SW + 34 + q] * sm.Gn[8];
+        sm.Qx[t] = sm.lq[LQ_LX + t] + (sm.Gn[t] + a);
+    } else if (t >= 32 && t < 32 + NX) {
+        int r = t - 32;
+        double a;
+        if (r < 12) {
+            int l = r / 3, m = r % 3;
+            a = sm.lq[LQ_BW + r] * sm.Gn[6] + sm.lq[LQ_BW + 12 + r] * sm.Gn[7] + sm.lq[LQ_BW + 24 + r] * sm.Gn[8] +
+                (dt * sm.contact[l] / kMass) * sm.Gn[9 + m];
+        } else {
+            a = (dt * (1.0 - sm.contact[(r - 12) / 3])) * sm.Gn[r];
+        }
+        sm.Qu[r] = sm.lq[LQ_LU + r] + a;
+    }
+    __syncthreads();
+    // Qux = B^T H A (into Y), Y[:,24] = Qu;  symmetrise Qxx (SinglePhase.cpp:352)
+    double qs[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+        int e = t + 64 * q, r = e / NX, c = e % NX;
+        sm.Y[r * LDY + c] = BtV_elem(sm.M, LD, sm.lq, sm.contact, dt, r, c);
+        qs[q] = (sm.H[r * LD + c] + sm.H[c * LD + r]) / 2;
+    }
+    if (t < NX) sm.Y[t * LDY + NX] = sm.Qu[t];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 9; ++q) { int e = t + 64 * q, r = e / NX, c = e % NX; sm.H[r * LD + c] = qs[q]; }
+    // Cholesky Quu = L L^T (lower, in Q).  PSD test of the reference: Eigen LDLT of Quu - 1e-9 I
+    // must show no negative pivot (SinglePhase.cpp:342-348); here every Cholesky pivot of Quu must
+    // exceed 1e-9 (pivots of Quu dominate those of Quu - eps I by eps, so every Quu the reference
+    // accepts passes).
+    for (int j = 0; j < NX; ++j) {
+        double piv = sm.Q[j * LD + j];
+        if (!(piv > 1e-9)) return false; // wave-uniform
+        double dj = sqrt(piv), inv = 1.0 / dj;
+        __syncthreads();
+        if (t > j && t < NX) sm.Q[t * LD + j] *= inv;
+        if (t == j) sm.Q[j * LD + j] = dj;
+        __syncthreads();
+        const int m = NX - 1 - j;               // trailing size
+        for (int e = t; e < m * m; e += 64) {
+            int r = j + 1 + e / m, c = j + 1 + e % m;
+            if (c <= r) sm.Q[r * LD + c] -= sm.Q[r * LD + j] * sm.Q[c * LD + j];
+        }
+        __syncthreads();
+    }
+    // forward solve L Y = [Qux | Qu]
+    for (int j = 0; j < NX; ++j) {
+        if (t <= NX) sm.Y[j * LDY + t] /= sm.Q[j * LD + j];
+        __syncthreads();
+        const int m = NX - 1 - j;
+        for (int e = t; e < m * (NX + 1); e += 64) {
+            int r = j + 1 + e / (NX + 1), c = e % (NX + 1);
+            sm.Y[r * LDY + c] -= sm.Q[r * LD + j] * sm.Y[j * LDY + c];
+        }
+        __syncthreads();
+    }
+    // H = Qxx - Y^T Y, G = Qx - Y^T y, dV_k = y^T y
+    for (int e = t; e < NN; e += 64) {
+        int r = e / NX, c = e % NX;
+        double a = 0.0;
+        for (int j = 0; j < NX; ++j) a += sm.Y[j * LDY + r] * sm.Y[j * LDY + c];
+        sm.H[r * LD + c] -= a;
+    }
+    double yy = (t < NX) ? sm.Y[t * LDY + NX] * sm.Y[t * LDY + NX] : 0.0;
+    if (t < NX) {
+        double a = 0.0;
+        for (int j = 0; j < NX; ++j) a += sm.Y[j * LDY + t] * sm.Y[j * LDY + NX];
+        sm.G[t] = sm.Qx[t] - a;
+    }
+    double dVk = wave_sum(yy);
+    dV1 -= dVk;
+    dV2 += dVk;
+    __syncthreads();
+    // back-substitution L^T Z = Y -> K = -Z[:, :24], dU = -Z[:, 24]
+    for (int j = NX - 1; j >= 0; --j) {
+        if (t <= NX) sm.Y[j * LDY + t] /= sm.Q[j * LD + j];
+        __syncthreads();
+        for (int e = t; e < j * (NX + 1); e += 64) {
+            int r = e / (NX + 1), c = e % (NX + 1);
+            sm.Y[r * LDY + c] -= sm.Q[j * LD + r] * sm.Y[j * LDY + c];
+        }
+        __syncthreads();
+    }
+    double *Kg = d.K + ((size_t)b * p.Kc + kc) * NN;
+    for (int e = t; e < NN; e += 64) Kg[e] = -sm.Y[(e / NX) * LDY + e % NX];
+    if (t < NX) d.dU[((size_t)b * p.Kc + kc) * NX + t] = -sm.Y[t * LDY + NX];
+    __syncthreads();
+    return true;
+}
+
+// G += H v  for the phase-initial defect (SinglePhase.cpp:365)
+DEV void add_Hv(BwdSmem &sm, const double *vg)
+{
+    const int t = threadIdx.x;
+    if (t < NX) sm.dv[t] = vg[t];
+    __syncthreads();
+    if (t < NX) {
+        double a = 0.0;
+        for (int c = 0; c < NX; ++c) a += sm.H[t * LD + c] * sm.dv[c];
+        sm.G[t] += a;
+    }
+    __syncthreads();
+}
+
+// MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229)
+DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdSmem &sm, int b, double reg, double &dV1, double &dV2)
+{
+    const int t = threadIdx.x;
+    dV1 = 0.0; dV2 = 0.0;
+    for (int i = p.P - 1; i >= 0; --i) {
+        const double *rec = d.term + ((size_t)b * p.P + i) * TW;
+        if (t < 4) sm.contact[t] = d.contacts[((size_t)b * (p.P + 1) + i) * 4 + t];
+        if (i == p.P - 1) {
+            for (int e = t; e < NN; e += 64) sm.H[(e / NX) * LD + e % NX] = rec[TM_PHIXX + e];
+            if (t < NX) sm.G[t] = rec[TM_PHIX + t];
+        } else {
+            // impact-aware step: G' = Px^T G0, H' = Px^T H0 Px (MultiPhaseDDP.cpp:480-484)
+            for (int e = t; e < NN; e += 64) sm.Q[(e / NX) * LD + e % NX] = rec[TM_PX + e];
+            __syncthreads();
+            for (int e = t; e < NN; e += 64) {
+                int r = e / NX, c = e % NX;
+                double a = 0.0;
+                for (int j = 0; j < NX; ++j) a += sm.H[r * LD + j] * sm.Q[j * LD + c];
+                sm.M[r * LD + c] = a;
+            }
+            double gp = 0.0;
+            if (t < NX)
+                for (int j = 0; j < NX; ++j) gp += sm.Q[j * LD + t] * sm.G[j];
+            __syncthreads();
+            for (int e = t; e < NN; e += 64) {
+                int r = e / NX, c = e % NX;
+                double a = 0.0;
+                for (int j = 0; j < NX; ++j) a += sm.Q[j * LD + r] * sm.M[j * LD + c];
+                sm.H[r * LD + c] = rec[TM_PHIXX + e] + a;
+            }
+            if (t < NX) sm.G[t] = rec[TM_PHIX + t] + gp;
+        }
+        __syncthreads();
+        const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
+        double v1 = 0.0, v2 = 0.0;
+        for (int k = N - 1; k >= 0; --k)
+            if (!bwd_knot(p, d, sm, b, s0 + k, k0 + k, reg, v1, v2)) return false;
+        add_Hv(sm, d.Defect + ((size_t)b * p.S + s0) * NX);
+        dV1 += v1;
+        dV2 += v2;
+    }
+    return true;
+}
+
+// MultiPhaseDDP::linear_rollout(1.0) (MultiPhaseDDP.cpp:20-50, SinglePhase.cpp:144-178): writes dX
+// and du = dU + K dX (the control step of every later line-search trial).
+DEV void linear_rollout(const Params &p, const Bufs &d, BwdSmem &sm, int b, double &dV1, double &dV2)
+{
+    const int t = threadIdx.x;
+    const double dt = p.dt;
+    double *dx = sm.G, *du = sm.Gn, *tmp = sm.Qx; // reuse vectors
+    double v1 = 0.0, v2 = 0.0;
+    if (t < NX) dx[t] = 0.0;
+    __syncthreads();
+    for (int i = 0; i < p.P; ++i) {
+        const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
+        if (t < 4) sm.contact[t] = d.contacts[((size_t)b * (p.P + 1) + i) * 4 + t];
+        if (i > 0) { // dx_init = Px dX_end
+            const double *Px = d.term + ((size_t)b * p.P + (i - 1)) * TW + TM_PX;
+            double a = 0.0;
+            if (t < NX)
+                for (int j = 0; j < NX; ++j) a += Px[t * NX + j] * dx[j];
+            __syncthreads();
+            if (t < NX) dx[t] = a;
+        }
+        __syncthreads();
+        if (t < NX) {
+            dx[t] = dx[t] + d.Defect[((size_t)b * p.S + s0) * NX + t];
+            d.dX[((size_t)b * p.S + s0) * NX + t] = dx[t];
+        }
+        __syncthreads();
+        for (int k = 0; k < N; ++k) {
+            const int s = s0 + k, kc = k0 + k;
+            const double *Kg = d.K + ((size_t)b * p.Kc + kc) * NN;
+            const double *lqg = d.lq + ((size_t)b * p.Kc + kc) * LQW;
+            for (int j = t; j < NN; j += 64) sm.M[(j / NX) * LD + j % NX] = Kg[j];
+            for (int j = t; j < LQW; j += 64) sm.lq[j] = lqg[j];
+            if (t < NX) sm.dv[t] = d.Defect[((size_t)b * p.S + s + 1) * NX + t];
+            __syncthreads();
+            if (t < NX) {
+                double a = 0.0;
+                for (int c = 0; c < NX; ++c) a += sm.M[t * LD + c] * dx[c];
+                du[t] = d.dU[((size_t)b * p.Kc + kc) * NX + t] + a;
+            }
+            __syncthreads();
+            double nx = 0.0, q1 = 0.0, q2 = 0.0;
+            if (t < NX) {
+                // A dx + B du + Defect
+                double sdx = 0.0;
+                for (int j = 0; j < 9; ++j) sdx += S_at(sm.lq, dt, t, j) * dx[j];
+                for (int j = 9; j < NX; ++j) sdx += S_at(sm.lq, dt, t, j) * dx[j];
+                double bdu = 0.0;
+                if (t >= 6 && t < 9)
+                    for (int c = 0; c < 12; ++c) bdu += sm.lq[LQ_BW + 12 * (t - 6) + c] * du[c];
+                else if (t >= 9 && t < 12)
+                    for (int l = 0; l < 4; ++l) bdu += (dt * sm.contact[l] / kMass) * du[3 * l + t - 9];
+                else if (t >= 12)
+                    bdu = (dt * (1.0 - sm.contact[(t - 12) / 3])) * du[t];
+                nx = (dx[t] + sdx) + bdu + sm.dv[t];
+                // dV terms (quirk A3: overwrite, no 1/2, cross term once)
+                q1 = sm.lq[LQ_LX + t] * dx[t] + sm.lq[LQ_LU + t] * du[t];
+                double a = 0.0, bq = 0.0;
+                for (int c = 0; c < NX; ++c) a += lxx_elem(p, sm.contact, t, c) * dx[c];
+                for (int c = 0; c < NX; ++c) bq += luu_elem(p, sm.lq, t, c) * du[c];
+                q2 = dx[t] * a + du[t] * bq;
+            }
+            v1 += wave_sum(q1);
+            v2 += wave_sum(q2);
+            __syncthreads();
+            if (t < NX) {
+                d.du[((size_t)b * p.Kc + kc) * NX + t] = du[t];
+                d.dX[((size_t)b * p.S + s + 1) * NX + t] = nx;
+                dx[t] = nx;
+            }
+            __syncthreads();
+        }
+        const double *rec = d.term + ((size_t)b * p.P + i) * TW;
+        double q1 = 0.0, q2 = 0.0;
+        if (t < NX) {
+            q1 = rec[TM_PHIX + t] * dx[t];
+            double a = 0.0;
+            for (int c = 0; c < NX; ++c) a += rec[TM_PHIXX + t * NX + c] * dx[c];
+            q2 = dx[t] * a;
+        }
+        v1 += wave_sum(q1);
+        v2 += wave_sum(q2);
+        __syncthreads();
+    }
+    (void)tmp;
+    dV1 = v1;
+    dV2 = v2;
+}
+
+__global__ __launch_bounds__(64) void k_backward(Params p, Bufs d)
+{
+    const int b = blockIdx.x, t = threadIdx.x;
+    ElemState &E = d.el[b];
+    if (E.done || E.inner_done) return;
+    __shared__ BwdSmem sm;
+    // compute_cost + measure_dynamics_feasibility at the start of the inner iteration
+    // (MultiPhaseDDP.cpp:306-307): per-phase sums in reference order
+    if (t == 0) {
+        double cost = 0.0, feas = 0.0;
+        for (int i = 0; i < p.P; ++i) {
+            double ci = 0.0, fi = 0.0;
+            for (int k = 0; k < p.N[i]; ++k) ci += d.slot_cost[(size_t)b * p.S + p.s0[i] + k];
+            ci += d.slot_cost[(size_t)b * p.S + p.s0[i] + p.N[i]];
+            for (int k = 0; k <= p.N[i]; ++k) fi += d.slot_feas[(size_t)b * p.S + p.s0[i] + k];
+            cost += ci;
+            feas += fi;
+        }
+        sm.red[0] = cost;
+        sm.red[1] = sqrt(feas);
+    }
+    __syncthreads();
+    const double cost = sm.red[0], feas = sm.red[1];
+    double reg = E.reg;
+    double dV1 = 0.0, dV2 = 0.0;
+    bool ok = false;
+    // backward_sweep_regularized (MultiPhaseDDP.cpp:141-181)
+    while (true) {
+        ok = bwd_sweep(p, d, sm, b, reg, dV1, dV2);
+        __syncthreads();
+        if (ok) break;
+        reg = fmax(reg * p.update_regularization, 1e-03);
+        if (reg > 1e2) break;
+    }
+    reg = reg / 20;
+    if (reg < 1e-06) reg = 0;
+    if (t == 0) {
+        E.iters += 1;
+        E.cost = cost;
+        E.feas = feas;
+        E.reg = reg;
+        E.accepted = 0;
+    }
+    if (!ok) { // goto bad_solve
+        if (t == 0) { E.status = 1; E.done = 1; E.ls_active = 0; }
+        return;
+    }
+    linear_rollout(p, d, sm, b, dV1, dV2);
+    if (t == 0) {
+        double dV_abs = fabs(dV1 + 0.5 * dV2);
+        double rho = (feas > p.feas_thresh) ? dV_abs / ((1 - p.merit_scale) * feas) + p.merit_offset : 0;
+        double merit = cost + rho * feas;
+        E.dV1 = dV1; E.dV2 = dV2; E.merit_rho = rho; E.merit = merit;
+        E.cost_prev = cost; E.merit_prev = merit; E.feas_prev = feas;
+        if (!p.no_early_exit && dV_abs < p.cost_thresh && feas <= p.feas_thresh) {
+            E.inner_done = 1;
+            E.ls_active = 0;
+        } else {
+            E.ls_active = 1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_rollout: one line-search trial (eps) per (element, state slot).  All knots are shooting states
+// (HKDProblem.cpp:104), so X[k] = Xbar[k] + eps dX[k] and the simulated state at k depends only on
+// knot k-1: the nonlinear rollout is knot-parallel.  U = Ubar + eps du with du = dU + K dX from the
+// linear rollout (equal to the reference's Ubar + eps dU + K (X - Xbar) up to rounding of X - Xbar).
+__global__ __launch_bounds__(256) void k_rollout(Params p, Bufs d, double eps, int init)
+{
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)p.B * p.S) return;
+    const int b = (int)(gid / p.S), s = (int)(gid % p.S);
+    const ElemState &E = d.el[b];
+    if (init ? E.done : !E.ls_active) return;
+    int i, k;
+    slot_phase(p, s, i, k);
+    int c[4], cn[4];
+    load_contacts(d, p, b, i, c, cn);
+    const size_t sb = (size_t)b * p.S;
+    double x[NX], xs[NX];
+    const double *xb = d.Xbar + (sb + s) * NX, *dxg = d.dX + (sb + s) * NX;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) x[j] = xb[j] + eps * dxg[j];
+    if (k == 0) {
+        if (i == 0) {
+#pragma unroll
+            for (int j = 0; j < NX; ++j) xs[j] = d.x0[(size_t)b * NX + j];
+        } else { // x_init = resetmap(X_{i-1}[N]) (MultiPhaseDDP.cpp:73-81)
+            int cp_[4], cpn[4];
+            load_contacts(d, p, b, i - 1, cp_, cpn);
+            double xe[NX];
+            const double *xbp = d.Xbar + (sb + s - 1) * NX, *dxp = d.dX + (sb + s - 1) * NX;
+#pragma unroll
+            for (int j = 0; j < NX; ++j) xe[j] = xbp[j] + eps * dxp[j];
+            hkd_resetmap(xe, cp_, cpn, xs);
+        }
+    } else {
+        const int kcp = p.k0[i] + k - 1;
+        double xp[NX], up[NU];
+        const double *xbp = d.Xbar + (sb + s - 1) * NX, *dxp = d.dX + (sb + s - 1) * NX;
+        const double *ubp = d.Ubar + ((size_t)b * p.Kc + kcp) * NU, *dup = d.du + ((size_t)b * p.Kc + kcp) * NU;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) xp[j] = xbp[j] + eps * dxp[j];
+#pragma unroll
+        for (int j = 0; j < NU; ++j) up[j] = ubp[j] + eps * dup[j];
+        double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
+        hkd_step(xp, up, cd, p.dt, xs);
+    }
+    double nrm = 0.0, fs = 0.0;
+    double *Xg = d.X + (sb + s) * NX, *Dg = d.Defect + (sb + s) * NX;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+        nrm += xs[j] * xs[j];
+        double df = xs[j] - x[j];
+        fs += df * df;
+        Xg[j] = x[j];
+        Dg[j] = df;
+    }
+    d.slot_feas[sb + s] = fs;
+    d.slot_div[sb + s] = (k > 0 && sqrt(nrm) > 1e6) ? 1 : 0;
+    const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
+    if (k == p.N[i]) {
+        double tv, h[4];
+        const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
+        d.slot_cost[sb + s] = terminal_cost(p, c, cn, x, xr, pf, sg, lm, tv, h);
+        d.slot_viol[sb + s] = tv;
+        for (int l = 0; l < 4; ++l) d.term_h[((size_t)b * p.P + i) * 4 + l] = h[l];
+    } else {
+        const int kc = p.k0[i] + k;
+        double u[NU];
+        const double *ub = d.Ubar + ((size_t)b * p.Kc + kc) * NU, *dug = d.du + ((size_t)b * p.Kc + kc) * NU;
+        double *Ug = d.U + ((size_t)b * p.Kc + kc) * NU;
+#pragma unroll
+        for (int j = 0; j < NU; ++j) { u[j] = ub[j] + eps * dug[j]; Ug[j] = u[j]; }
+        const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
+        const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
+        double viol;
+        d.slot_cost[sb + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
+        d.slot_viol[sb + s] = viol;
+    }
+}
+
+// k_decide: reductions of one trial + merit acceptance (MultiPhaseDDP.cpp:113-133) + the
+// later-termination test (:358).  One thread per element, reference summation order.
+__global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int last, int init)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.B) return;
+    ElemState &E = d.el[b];
+    if (init ? E.done : !E.ls_active) return;
+    const size_t sb = (size_t)b * p.S;
+    double cost = 0.0, feas = 0.0, max_p = 0.0, max_t = 0.0;
+    int div = 0;
+    for (int i = 0; i < p.P; ++i) {
+        double ci = 0.0, fi = 0.0, pv = 0.0;
+        const int s0 = p.s0[i];
+        for (int k = 0; k < p.N[i]; ++k) {
+            ci += d.slot_cost[sb + s0 + k];
+            pv = fmin(pv, d.slot_viol[sb + s0 + k]);
+        }
+        ci += d.slot_cost[sb + s0 + p.N[i]];
+        for (int k = 0; k <= p.N[i]; ++k) { fi += d.slot_feas[sb + s0 + k]; div |= d.slot_div[sb + s0 + k]; }
+        cost += ci;
+        feas += fi;
+        max_p = fmin(max_p, pv);
+        max_t = fmax(max_t, d.slot_viol[sb + s0 + p.N[i]]);
+    }
+    feas = sqrt(feas);
+    E.max_p = max_p;
+    E.max_t = max_t;
+    if (init) {
+        E.cost = cost; E.feas = feas; E.accepted = 1;
+        return;
+    }
+    E.n_ls += 1;
+    const double merit = cost + E.merit_rho * feas;
+    const double exp_cost = eps * E.dV1 + 0.5 * eps * eps * E.dV2;
+    const double exp_merit = exp_cost - eps * E.merit_rho * E.feas_prev;
+    E.cost = cost; E.feas = feas; E.merit = merit;
+    bool fin = false;
+    if ((merit <= E.merit_prev + p.gamma * exp_merit) && !div) {
+        E.accepted = 1; E.ls_active = 0; fin = true;
+    } else if (last) {
+        E.accepted = 0; E.ls_active = 0; E.cost = E.cost_prev; E.merit = E.merit_prev; fin = true;
+    }
+    if (fin && !p.no_early_exit && fabs((E.cost_prev - E.cost) / E.cost_prev) < p.cost_thresh &&
+        E.feas <= p.feas_thresh)
+        E.inner_done = 1;
+}
+
+// Trajectory::update_nominal_vals for accepted elements (copy X->Xbar, U->Ubar, Defect->Defect_bar)
+__global__ __launch_bounds__(256) void k_update_nominal(Params p, Bufs d, int init)
+{
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long per = (long)p.S * NX;
+    if (gid >= (long)p.B * per) return;
+    const int b = (int)(gid / per);
+    const ElemState &E = d.el[b];
+    if (!E.accepted || (init && E.done)) return;
+    d.Xbar[gid] = d.X[gid];
+    d.Defect_bar[gid] = d.Defect[gid];
+    const long r = gid % per;
+    if (r < (long)p.Kc * NU) {
+        const long ug = (long)b * p.Kc * NU + r;
+        d.Ubar[ug] = d.U[ug];
+    }
+}
+
+__global__ void k_outer_begin(Params p, Bufs d)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.B) return;
+    ElemState &E = d.el[b];
+    if (E.done) return;
+    E.outer_iters += 1;
+    E.max_t_prev = E.max_t;
+    E.max_p_prev = E.max_p;
+    E.reg = 0.0;
+    E.inner_done = 0;
+}
+
+// update_REB_params (ConstraintsBase.h:168-183) per (element, control slot)
+__global__ __launch_bounds__(256) void k_reb_update(Params p, Bufs d)
+{
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)p.B * p.Kc) return;
+    const int b = (int)(gid / p.Kc), kc = (int)(gid % p.Kc);
+    if (d.el[b].done) return;
+    int i = 0;
+    for (int j = 1; j < p.P; ++j)
+        if (kc >= p.k0[j]) i = j;
+    int c[4], cn[4];
+    load_contacts(d, p, b, i, c, cn);
+    const double *u = d.U + gid * NU;
+    double *dl = d.reb_delta + gid * 20, *ep = d.reb_eps + gid * 20;
+    for (int l = 0; l < 4; ++l) {
+        if (!c[l]) continue;
+        for (int r = 0; r < 5; ++r) {
+            double g = grf_value(p.mu, r, u + 3 * l);
+            if (g > -p.pconstr_thresh) continue;
+            ep[5 * l + r] *= p.update_ReB;
+            dl[5 * l + r] *= p.update_relax;
+            dl[5 * l + r] = fmax(dl[5 * l + r], p.grf_delta_min);
+        }
+    }
+}
+
+// update_AL_params (ConstraintsBase.h:349-365) + outer convergence tests (MultiPhaseDDP.cpp:397-408)
+__global__ void k_outer_end(Params p, Bufs d)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.B) return;
+    ElemState &E = d.el[b];
+    if (E.done) return;
+    if (p.AL_active) {
+        for (int i = 0; i < p.P; ++i) {
+            int c[4], cn[4];
+            load_contacts(d, p, b, i, c, cn);
+            for (int l = 0; l < 4; ++l) {
+                if (!touchdown(c, cn, l)) continue;
+                const size_t q = ((size_t)b * p.P + i) * 4 + l;
+                double h = d.term_h[q];
+                if (fabs(h) < p.tconstr_thresh) continue;
+                if (fabs(h) > 0.005) {
+                    d.al_sigma[q] *= p.update_penalty;
+                    d.al_sigma[q] = fmin(d.al_sigma[q], p.td_sigma_max);
+                } else {
+                    d.al_lambda[q] += h * d.al_sigma[q];
+                }
+            }
+        }
+    }
+    if (p.no_early_exit) return;
+    if (E.max_t < p.tconstr_thresh && fabs(E.max_p) < p.pconstr_thresh && E.feas <= p.feas_thresh) E.done = 1;
+    else if (fabs(E.max_t - E.max_t_prev) < 0.0001 && fabs(E.max_p - E.max_p_prev) < 0.0001 &&
+             E.feas <= p.feas_thresh)
+        E.done = 1;
+}
+
+__global__ void k_reset_elements(Params p, Bufs d)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.B) return;
+    ElemState &E = d.el[b];
+    E = ElemState{};
+}
+
+__global__ __launch_bounds__(256) void k_init_params(Params p, Bufs d)
+{
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid < (long)p.B * p.Kc * 20) { d.reb_delta[gid] = p.grf_delta; d.reb_eps[gid] = p.grf_eps; }
+    if (gid < (long)p.B * p.P * 4) { d.al_sigma[gid] = p.td_sigma; d.al_lambda[gid] = p.td_lambda; }
+}
+
+// which: 0 = elements with ls_active, 1 = elements still iterating (!done && !inner_done), 2 = !done
+__global__ void k_count(Params p, Bufs d, int which)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    int v = 0;
+    if (b < p.B) {
+        const ElemState &E = d.el[b];
+        v = which == 0 ? E.ls_active : which == 1 ? (!E.done && !E.inner_done) : !E.done;
+    }
+    unsigned long long m = __ballot(v);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&d.counter[which], __popcll(m));
+}
+
+// ---------------------------------------------------------------------------------------------
+// model primitives
+__global__ void k_model_dynamics(const double *x, const double *u, const double *c, double dt, double *xn, int n)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    hkd_step(x + (size_t)q * NX, u + (size_t)q * NU, c + (size_t)q * 4, dt, xn + (size_t)q * NX);
+}
+
+__global__ void k_model_partial(const double *x, const double *u, const double *c, double dt, double *A, double *B,
+                                int n)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    double Se[SE_N], Sw[SW_N], Bw[BW_N];
+    hkd_partial_compact(x + (size_t)q * NX, u + (size_t)q * NU, c + (size_t)q * 4, dt, Se, Sw, Bw);
+    hkd_expand_colmajor(Se, Sw, Bw, c + (size_t)q * 4, dt, A + (size_t)q * NN, B + (size_t)q * NN);
+}
+
+__global__ void k_model_foot(const double *x, const int *leg, double *p, double *J, int n)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const double *xx = x + (size_t)q * NX;
+    const int l = leg[q];
+    if (p) hkd_foot_position(l, xx + 3, xx, xx + 12 + 3 * l, p + (size_t)q * 3);
+    if (J) {
+        double Jr[54];
+        hkd_foot_jacobian(l, xx, xx + 12 + 3 * l, Jr);
+        for (int r = 0; r < 3; ++r)
+            for (int cc = 0; cc < 18; ++cc) J[(size_t)q * 54 + r + 3 * cc] = Jr[18 * r + cc];
+    }
+}
+
+__global__ void k_model_reset(const double *x, const int *c, const int *cn, double *xn, double *Px, int n)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const double *xx = x + (size_t)q * NX;
+    if (xn) hkd_resetmap(xx, c + (size_t)q * 4, cn + (size_t)q * 4, xn + (size_t)q * NX);
+    if (Px)
+        for (int r = 0; r < NX; ++r) {
+            double row[NX];
+            hkd_resetmap_partial_row(xx, c + (size_t)q * 4, cn + (size_t)q * 4, r, row);
+            for (int cc = 0; cc < NX; ++cc) Px[(size_t)q * NN + r + NX * cc] = row[cc];
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
+static inline unsigned blocks_for(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+void launch_rollout(const Params &p, const Bufs &d, double eps, int init, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_rollout, dim3(blocks_for((long)p.B * p.S, 256)), dim3(256), 0, st, p, d, eps, init);
+}
+void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_decide, dim3(blocks_for(p.B, 64)), dim3(64), 0, st, p, d, eps, last, init);
+}
+void launch_update_nominal(const Params &p, const Bufs &d, int init, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_update_nominal, dim3(blocks_for((long)p.B * p.S * NX, 256)), dim3(256), 0, st, p, d, init);
+}
+void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_lq, dim3(blocks_for((long)p.B * p.S, 256)), dim3(256), 0, st, p, d);
+    hipLaunchKernelGGL(k_terminal, dim3(p.B * p.P), dim3(64), 0, st, p, d);
+}
+void launch_backward(const Params &p, const Bufs &d, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_backward, dim3(p.B), dim3(64), 0, st, p, d);
+}
+void launch_outer_begin(const Params &p, const Bufs &d, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_outer_begin, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);
+}
+void launch_reb_update(const Params &p, const Bufs &d, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_reb_update, dim3(blocks_for((long)p.B * p.Kc, 256)), dim3(256), 0, st, p, d);
+}
+void launch_outer_end(const Params &p, const Bufs &d, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_outer_end, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);
+}
+void launch_reset_elements(const Params &p, const Bufs &d, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_reset_elements, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);
+}
+void launch_init_params(const Params &p, const Bufs &d, hipStream_t st)
+{
+    long n = (long)p.B * p.Kc * 20;
+    if ((long)p.B * p.P * 4 > n) n = (long)p.B * p.P * 4;
+    hipLaunchKernelGGL(k_init_params, dim3(blocks_for(n, 256)), dim3(256), 0, st, p, d);
+}
+void launch_count(const Params &p, const Bufs &d, int which, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_count, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d, which);
+}
+void launch_model_dynamics(const double *x, const double *u, const double *c, double dt, double *xn, int n,
+                           hipStream_t st)
+{
+    hipLaunchKernelGGL(k_model_dynamics, dim3(blocks_for(n, 128)), dim3(128), 0, st, x, u, c, dt, xn, n);
+}
+void launch_model_partial(const double *x, const double *u, const double *c, double dt, double *A, double *B,
+                          int n, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_model_partial, dim3(blocks_for(n, 64)), dim3(64), 0, st, x, u, c, dt, A, B, n);
+}
+void launch_model_foot(const double *x, const int *leg, double *p, double *J, int n, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_model_foot, dim3(blocks_for(n, 64)), dim3(64), 0, st, x, leg, p, J, n);
+}
+void launch_model_reset(const double *x, const int *c, const int *cn, double *xn, double *Px, int n,
+                        hipStream_t st)
+{
+    hipLaunchKernelGGL(k_model_reset, dim3(blocks_for(n, 64)), dim3(64), 0, st, x, c, cn, xn, Px, n);
+}
+
+}  // namespace hsddp

@@ -1,0 +1,141 @@
+"""hsddp — MI355X-native batched Hybrid-Systems DDP for the HKD quadruped model.
+
+Python mirror of the reference's solver surface (HSDDPSolver/header/MultiPhaseDDP.h:19-122):
+``Solver`` wraps one C-ABI handle (include/hsddp.h) holding B independent multi-phase problems on
+one GPU; ``solve()`` runs MultiPhaseDDP::solve for all of them.  ``load_settings`` reads the
+reference's ``ddp_setting.info`` surface (loadHSDDPSetting, HSDDP_CompoundTypes.h:62-87).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import model, synthetic  # noqa: F401
+from ._lib import (ConstraintParams, ElementInfo, HSDDPError, Options, ProblemDesc, Stats, Weights,
+                   check, dp, ip, lib)
+
+SETTINGS_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "settings")
+
+__all__ = ["Solver", "Options", "default_options", "load_settings", "load_constraint_params",
+           "HSDDPError", "model"]
+
+
+def default_options(**overrides) -> Options:
+    """HSDDP_OPTION in-class defaults (HSDDP_CompoundTypes.h:20-45)."""
+    o = Options()
+    lib().hsddp_default_options(C.byref(o))
+    for k, v in overrides.items():
+        setattr(o, k, v)
+    return o
+
+
+def load_settings(path: str | None = None, base: Options | None = None, **overrides) -> Options:
+    """loadHSDDPSetting: start from HSDDP_OPTION defaults, overlay the INFO file's keys."""
+    o = base if base is not None else default_options()
+    path = path or os.path.join(SETTINGS_DIR, "ddp_setting.info")
+    check(lib().hsddp_load_settings(path.encode(), C.byref(o)))
+    for k, v in overrides.items():
+        setattr(o, k, v)
+    return o
+
+
+def load_constraint_params(path: str | None = None) -> ConstraintParams:
+    cp = ConstraintParams()
+    lib().hsddp_default_constraint_params(C.byref(cp))
+    path = path or os.path.join(SETTINGS_DIR, "constraint_params.info")
+    check(lib().hsddp_load_constraint_params(path.encode(), C.byref(cp)))
+    return cp
+
+
+class Solver:
+    """B independent HKD trajectory optimisations on one GPU (one C-ABI handle)."""
+
+    def __init__(self, prob: dict, options: Options | None = None, device: int = 0,
+                 cparams: ConstraintParams | None = None, weights: Weights | None = None):
+        L = lib()
+        self.prob = prob
+        self.B = int(prob["batch"])
+        self.S, self.Kc = int(prob["S"]), int(prob["Kc"])
+        self.P = len(prob["horizons"])
+        desc = ProblemDesc()
+        desc.device = device
+        desc.batch = self.B
+        desc.n_phases = self.P
+        for i, n in enumerate(prob["horizons"]):
+            desc.horizons[i] = int(n)
+        desc.dt = float(prob["dt"])
+        desc.ref_per_element = 0 if prob["ref_x"].shape[0] == 1 else 1
+        if weights is None:
+            L.hsddp_default_weights(C.byref(desc.weights))
+        else:
+            desc.weights = weights
+        if cparams is None:
+            L.hsddp_default_constraint_params(C.byref(desc.cparams))
+        else:
+            desc.cparams = cparams
+        h = C.c_void_p()
+        check(L.hsddp_create(C.byref(desc), C.byref(h)))
+        self._h = h
+        self.options = options if options is not None else load_settings()
+        check(L.hsddp_set_options(h, C.byref(self.options)))
+        self._contacts = np.ascontiguousarray(prob["contacts"], dtype=np.int32)
+        check(L.hsddp_upload_problem(h, ip(self._contacts), dp(np.ascontiguousarray(prob["x0"])),
+                                     dp(np.ascontiguousarray(prob["ref_x"])),
+                                     dp(np.ascontiguousarray(prob["ref_u"])),
+                                     dp(np.ascontiguousarray(prob["ref_foot"]))))
+        self.warm_start(prob.get("Xbar"), prob.get("Ubar"), prob.get("K"))
+
+    # -- MultiPhaseDDP surface ---------------------------------------------------------------
+    def set_options(self, options: Options) -> None:
+        self.options = options
+        check(lib().hsddp_set_options(self._h, C.byref(options)))
+
+    def warm_start(self, Xbar=None, Ubar=None, K=None) -> None:
+        cv = lambda a: None if a is None else dp(np.ascontiguousarray(a, dtype=np.float64))
+        keep = [np.ascontiguousarray(a, dtype=np.float64) if a is not None else None for a in (Xbar, Ubar, K)]
+        check(lib().hsddp_upload_warm_start(self._h, *(None if a is None else dp(a) for a in keep)))
+        del cv
+
+    def solve(self) -> Stats:
+        st = Stats()
+        check(lib().hsddp_solve(self._h, C.byref(st)))
+        return st
+
+    def trajectory(self) -> dict:
+        Xbar = np.empty((self.B, self.S, 24)); Ubar = np.empty((self.B, self.Kc, 24))
+        K = np.empty((self.B, self.Kc, 24, 24))
+        check(lib().hsddp_download_trajectory(self._h, dp(Xbar), dp(Ubar), dp(K)))
+        return {"Xbar": Xbar, "Ubar": Ubar, "K": K}
+
+    def working(self) -> dict:
+        X = np.empty((self.B, self.S, 24)); U = np.empty((self.B, self.Kc, 24))
+        D = np.empty((self.B, self.S, 24)); dX = np.empty((self.B, self.S, 24)); dU = np.empty((self.B, self.Kc, 24))
+        check(lib().hsddp_download_working(self._h, dp(X), dp(U), dp(D), dp(dX), dp(dU)))
+        return {"X": X, "U": U, "Defect": D, "dX": dX, "dU": dU}
+
+    def element_info(self) -> dict:
+        info = (ElementInfo * self.B)()
+        check(lib().hsddp_download_element_info(self._h, info))
+        out = {}
+        for f, _ in ElementInfo._fields_:
+            out[f] = np.array([getattr(info[b], f) for b in range(self.B)])
+        return out
+
+    def synchronize(self) -> None:
+        check(lib().hsddp_synchronize(self._h))
+
+    def device_bytes(self) -> int:
+        return int(lib().hsddp_device_bytes(self._h))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().hsddp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,141 @@
+"""ctypes binding of the C-ABI in include/hsddp.h (libhsddp_amd.so, built in-tree).
+
+The product path has no fallback: if the shared library is missing or no HIP device is present,
+every entry point raises.  Import torch (if at all) before this module so the library binds to
+the same HIP runtime instance torch loaded.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libhsddp_amd.so")
+
+DP = C.POINTER(C.c_double)
+IP = C.POINTER(C.c_int)
+MAX_PHASES = 16
+
+
+class Options(C.Structure):
+    """Mirror of hsddp_options / HSDDP_OPTION (HSDDP_CompoundTypes.h:18-60)."""
+    _fields_ = [(n, C.c_double) for n in ("alpha", "gamma", "update_penalty", "update_relax",
+                                          "update_regularization", "update_ReB")] + \
+               [(n, C.c_int) for n in ("max_DDP_iter", "max_AL_iter", "max_DDP_iter_runtime",
+                                       "max_AL_iter_runtime")] + \
+               [(n, C.c_double) for n in ("cost_thresh", "tconstr_thresh", "pconstr_thresh",
+                                          "dynamics_feas_thresh", "merit_rho", "merit_scale",
+                                          "merit_offset")] + \
+               [(n, C.c_int) for n in ("AL_active", "ReB_active", "smooth_active", "MS",
+                                       "nsteps_per_node", "no_early_exit")]
+
+
+class Weights(C.Structure):
+    _fields_ = [("q_eul", C.c_double * 3), ("q_pos", C.c_double * 3), ("q_omega", C.c_double * 3),
+                ("q_v", C.c_double * 3), ("q_qJ", C.c_double), ("qf_scale", C.c_double * 24),
+                ("qf_gain", C.c_double), ("r_grf", C.c_double), ("r_qJd", C.c_double),
+                ("foot_w", C.c_double * 3), ("foot_gain", C.c_double),
+                ("foot_term_cost", C.c_double), ("foot_term_grad", C.c_double)]
+
+
+class ConstraintParams(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("grf_delta", "grf_delta_min", "grf_eps", "swing_delta",
+                                          "swing_delta_min", "swing_eps", "td_sigma", "td_sigma_max",
+                                          "td_lambda", "mu_fric", "ground_height")]
+
+
+class ProblemDesc(C.Structure):
+    _fields_ = [("device", C.c_int), ("batch", C.c_int), ("n_phases", C.c_int),
+                ("horizons", C.c_int * MAX_PHASES), ("dt", C.c_double), ("ref_per_element", C.c_int),
+                ("weights", Weights), ("cparams", ConstraintParams)]
+
+
+class ElementInfo(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("cost", "feas", "merit", "max_tconstr", "max_pconstr")] + \
+               [(n, C.c_int) for n in ("iters", "outer_iters", "status", "n_ls_trials")]
+
+
+class Stats(C.Structure):
+    _fields_ = [("inner_iterations", C.c_int), ("outer_iterations", C.c_int), ("ls_trials", C.c_longlong),
+                ("element_iterations", C.c_longlong), ("ms_total", C.c_double), ("ms_backward", C.c_double),
+                ("ms_lq", C.c_double), ("ms_forward", C.c_double), ("ms_other", C.c_double),
+                ("n_backward_launches", C.c_int)]
+
+
+class HSDDPError(RuntimeError):
+    pass
+
+
+_lib = None
+
+# every symbol include/hsddp.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "hsddp_last_error", "hsddp_version", "hsddp_default_options", "hsddp_default_weights",
+    "hsddp_default_constraint_params", "hsddp_load_settings", "hsddp_load_constraint_params",
+    "hsddp_create", "hsddp_destroy", "hsddp_set_options", "hsddp_upload_problem",
+    "hsddp_upload_warm_start", "hsddp_solve", "hsddp_download_trajectory", "hsddp_download_working",
+    "hsddp_download_element_info", "hsddp_synchronize", "hsddp_device_bytes", "hsddp_hkd_dynamics",
+    "hsddp_hkd_dynamics_partial", "hsddp_hkd_foot_position", "hsddp_hkd_foot_jacobian",
+    "hsddp_hkd_resetmap", "hsddp_hkd_resetmap_partial", "hsddp_device_alloc", "hsddp_device_free",
+    "hsddp_memcpy_h2d", "hsddp_memcpy_d2h", "hsddp_device_synchronize",
+]
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HSDDPError(f"{LIB_PATH} not built: run __graft_entry__.build() (or make -C hkd-mpc_amd/csrc)")
+    L = C.CDLL(LIB_PATH)
+    L.hsddp_last_error.restype = C.c_char_p
+    L.hsddp_version.restype = C.c_char_p
+    L.hsddp_device_bytes.restype = C.c_size_t
+    L.hsddp_device_bytes.argtypes = [C.c_void_p]
+    L.hsddp_create.argtypes = [C.POINTER(ProblemDesc), C.POINTER(C.c_void_p)]
+    L.hsddp_destroy.argtypes = [C.c_void_p]
+    L.hsddp_set_options.argtypes = [C.c_void_p, C.POINTER(Options)]
+    L.hsddp_upload_problem.argtypes = [C.c_void_p, IP, DP, DP, DP, DP]
+    L.hsddp_upload_warm_start.argtypes = [C.c_void_p, DP, DP, DP]
+    L.hsddp_solve.argtypes = [C.c_void_p, C.POINTER(Stats)]
+    L.hsddp_download_trajectory.argtypes = [C.c_void_p, DP, DP, DP]
+    L.hsddp_download_working.argtypes = [C.c_void_p, DP, DP, DP, DP, DP]
+    L.hsddp_download_element_info.argtypes = [C.c_void_p, C.POINTER(ElementInfo)]
+    L.hsddp_synchronize.argtypes = [C.c_void_p]
+    L.hsddp_load_settings.argtypes = [C.c_char_p, C.POINTER(Options)]
+    L.hsddp_load_constraint_params.argtypes = [C.c_char_p, C.POINTER(ConstraintParams)]
+    for f in ("hsddp_hkd_dynamics",):
+        getattr(L, f).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_double, C.c_void_p, C.c_int, C.c_void_p]
+    L.hsddp_hkd_dynamics_partial.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_double, C.c_void_p,
+                                             C.c_void_p, C.c_int, C.c_void_p]
+    L.hsddp_hkd_foot_position.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    L.hsddp_hkd_foot_jacobian.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    L.hsddp_hkd_resetmap.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    L.hsddp_hkd_resetmap_partial.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    L.hsddp_device_alloc.restype = C.c_void_p
+    L.hsddp_device_alloc.argtypes = [C.c_size_t, C.c_int]
+    L.hsddp_device_free.argtypes = [C.c_void_p]
+    L.hsddp_memcpy_h2d.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    L.hsddp_memcpy_d2h.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    L.hsddp_device_synchronize.argtypes = [C.c_int]
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise HSDDPError(f"hsddp error {rc}: {lib().hsddp_last_error().decode()}")
+
+
+def dp(a: np.ndarray):
+    if a.dtype != np.float64 or not a.flags.c_contiguous:
+        raise TypeError("expected a C-contiguous float64 array")
+    return a.ctypes.data_as(DP)
+
+
+def ip(a: np.ndarray):
+    if a.dtype != np.int32 or not a.flags.c_contiguous:
+        raise TypeError("expected a C-contiguous int32 array")
+    return a.ctypes.data_as(IP)

@@ -1,0 +1,186 @@
+/*
+ * hsddp.h — C-ABI of the MI355X-native batched HS-DDP solver for the HKD quadruped model.
+ *
+ * Drop-in boundary for the hot path of heli-sudoo/HKD-MPC: one host call runs the reference's
+ * MultiPhaseDDP::solve (HSDDPSolver/source/MultiPhaseDDP.cpp:232-428) for B independent
+ * trajectories at once on one GPU.  Plain pointers and sizes only; no torch or Eigen types.
+ *
+ * Reference interfaces replaced (file:line in /root/reference):
+ *   hsddp_default_options / hsddp_options     HSDDP_OPTION            HSDDPSolver/common/HSDDP_CompoundTypes.h:18-60
+ *   hsddp_load_settings                       loadHSDDPSetting        HSDDPSolver/common/HSDDP_CompoundTypes.h:62-87
+ *   hsddp_load_constraint_params              loadConstrintParameters HKDMPC/HKD-TrajOpt/HKDProblem.h:70-90
+ *   hsddp_create (+ problem descriptor)       HKDProblem::initialization/create_problem_one_phase/
+ *                                             add_tconstr_one_phase   HKDMPC/HKD-TrajOpt/HKDProblem.cpp:15-111,225-310
+ *                                             MultiPhaseDDP::set_multiPhaseProblem  MultiPhaseDDP.h:374-382
+ *   hsddp_upload_problem (x0, references)     MultiPhaseDDP::set_initial_condition  MultiPhaseDDP.h:384;
+ *                                             HKDSinglePhaseReference::get_reference_at_t HKDReference.cpp:8-57
+ *   hsddp_upload_warm_start                   Trajectory::Xbar/Ubar/K warm start    TrajectoryManagement.h:54-77
+ *   hsddp_solve                               MultiPhaseDDP::solve                  MultiPhaseDDP.cpp:232-428
+ *   hsddp_download_trajectory                 Trajectory fields read by the caller  HKDMPC.cpp:243-298
+ *   hsddp_download_element_info               get_actual_cost / get_solver_info     MultiPhaseDDP.h:416; .cpp:532-541
+ *   hsddp_hkd_dynamics                        HKD::Model::dynamics (hkinodyn)       HKDModel.h:33-45
+ *   hsddp_hkd_dynamics_partial                HKD::Model::dynamics_partial          HKDModel.h:46-61
+ *   hsddp_hkd_resetmap(_partial)              HKDReset::resetmap(_partial)          HKDReset.h:41-136
+ *   hsddp_hkd_foot_position / _jacobian       compute_foot_position / comp_foot_jacob_{1..4}
+ *                                             (CasadiGen/header/comp_foot_*.h via casadi_interface.cpp:5-80)
+ *
+ * Conventions
+ *   - Return 0 on success, < 0 on error (hsddp_last_error() gives a message).  The reference
+ *     reports failures with bool returns and printf (MultiPhaseDDP.cpp:421-427); here the per-
+ *     element outcome is hsddp_element_info.status.
+ *   - Caller owns host buffers; the library owns device buffers.  One HIP stream per handle.
+ *     Not thread-safe per handle (the reference's solve is single-threaded per instance).
+ *   - Arrays are element-major, fp64.  State slots: phase i owns N_i + 1 states (S = sum(N_i+1));
+ *     control slots: N_i per phase (Kc = sum N_i).  Matrices in the solver API are row-major
+ *     [row][col]; the model primitives write Eigen's column-major layout (as the reference's
+ *     StateMap/ContrlMap buffers) — see each function.
+ *   - Every path runs on the GPU.  A handle created without a usable device fails with
+ *     HSDDP_ERR_DEVICE; there is no CPU fallback.
+ */
+#ifndef HSDDP_H
+#define HSDDP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HSDDP_NX 24
+#define HSDDP_NU 24
+#define HSDDP_MAX_PHASES 16
+
+enum {
+    HSDDP_OK = 0,
+    HSDDP_ERR_ARG = -1,
+    HSDDP_ERR_DEVICE = -2,
+    HSDDP_ERR_ALLOC = -3,
+    HSDDP_ERR_IO = -4,
+    HSDDP_ERR_UNSUPPORTED = -5,
+};
+
+/* Per-element solve outcome (replaces the reference's printf + `goto bad_solve`). */
+enum {
+    HSDDP_STATUS_OK = 0,            /* finished: converged or iteration budget spent */
+    HSDDP_STATUS_REG_OVERFLOW = 1,  /* regularization exceeded 1e2 (MultiPhaseDDP.cpp:162-167) */
+};
+
+/* POD mirror of HSDDP_OPTION (HSDDP_CompoundTypes.h:18-60), same field names and meaning. */
+typedef struct hsddp_options {
+    double alpha, gamma, update_penalty, update_relax, update_regularization, update_ReB;
+    int max_DDP_iter, max_AL_iter, max_DDP_iter_runtime, max_AL_iter_runtime;
+    double cost_thresh, tconstr_thresh, pconstr_thresh, dynamics_feas_thresh;
+    double merit_rho, merit_scale, merit_offset;
+    int AL_active, ReB_active, smooth_active, MS, nsteps_per_node;
+    /* extension: throughput mode — disable the inner/outer early-termination tests so every
+       element runs exactly max_AL_iter * max_DDP_iter inner iterations. */
+    int no_early_exit;
+} hsddp_options;
+
+/* HKD cost weights (HKDCost.h:14-36, 56-69; HKDCost.cpp:49,63). */
+typedef struct hsddp_hkd_weights {
+    double q_eul[3], q_pos[3], q_omega[3], q_v[3], q_qJ;
+    double qf_scale[24], qf_gain;
+    double r_grf, r_qJd;
+    double foot_w[3], foot_gain;
+    double foot_term_cost, foot_term_grad;
+} hsddp_hkd_weights;
+
+/* ReB / AL initial parameters (settings/constraint_params.info:1-19, HKDConstraints.h:17). */
+typedef struct hsddp_constraint_params {
+    double grf_delta, grf_delta_min, grf_eps;   /* GRF_ReB */
+    double swing_delta, swing_delta_min, swing_eps; /* Swing_ReB (read, unused by HKD: SwingConstraint is never added) */
+    double td_sigma, td_sigma_max, td_lambda;   /* TD_AL */
+    double mu_fric;                             /* GRFConstraint mu (0.7) */
+    double ground_height;                       /* TouchDownConstraint ground height (0) */
+} hsddp_constraint_params;
+
+typedef struct hsddp_problem_desc {
+    int device;                          /* HIP device ordinal */
+    int batch;                           /* B independent trajectories */
+    int n_phases;                        /* P <= HSDDP_MAX_PHASES */
+    int horizons[HSDDP_MAX_PHASES];      /* N_i knots per phase (same for every element) */
+    double dt;                           /* integration step (HKDMPC.cpp:28) */
+    int ref_per_element;                 /* 0: one reference shared by the batch; 1: per element */
+    hsddp_hkd_weights weights;
+    hsddp_constraint_params cparams;
+} hsddp_problem_desc;
+
+typedef struct hsddp_element_info {
+    double cost, feas, merit, max_tconstr, max_pconstr;
+    int iters, outer_iters, status, n_ls_trials;
+} hsddp_element_info;
+
+typedef struct hsddp_stats {
+    int inner_iterations;      /* inner-loop iterations launched (max over elements) */
+    int outer_iterations;
+    long long ls_trials;       /* line-search rollouts summed over elements */
+    long long element_iterations; /* sum over elements of inner iterations (trajectory-iterations) */
+    double ms_total;           /* device time of the solve (HIP events) */
+    double ms_backward;        /* device time in the backward Riccati + linear rollout kernel */
+    double ms_lq, ms_forward, ms_other;
+    int n_backward_launches;
+} hsddp_stats;
+
+typedef struct hsddp_handle_t *hsddp_handle;
+
+const char *hsddp_last_error(void);
+const char *hsddp_version(void);
+
+void hsddp_default_options(hsddp_options *opt);
+void hsddp_default_weights(hsddp_hkd_weights *w);
+void hsddp_default_constraint_params(hsddp_constraint_params *cp);
+/* INFO-file loaders with the reference loaders' exact key sets (Boost INFO subset parser). */
+int hsddp_load_settings(const char *path, hsddp_options *opt);
+int hsddp_load_constraint_params(const char *path, hsddp_constraint_params *cp);
+
+int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out);
+int hsddp_destroy(hsddp_handle h);
+int hsddp_set_options(hsddp_handle h, const hsddp_options *opt);
+
+/* contacts int32 [B][P+1][4] (row P: contact after the horizon, for the last phase's touchdown
+ * constraint); x0 [B][24]; ref_x, ref_u [Bref][S][24]; ref_foot [Bref][S][12]. */
+int hsddp_upload_problem(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
+                         const double *ref_u, const double *ref_foot);
+/* Xbar [B][S][24], Ubar [B][Kc][24], K [B][Kc][24][24]; NULL keeps the current value (initially
+ * Xbar = ref_x, Ubar = 0, K = 0 as HKDProblem.cpp:84-90 / TrajectoryManagement.cpp:5-35).  Also
+ * resets X = Xbar, U = Ubar, dX = 0 and the ReB/AL parameters to their initial values. */
+int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const double *Ubar, const double *K);
+
+int hsddp_solve(hsddp_handle h, hsddp_stats *stats);
+
+int hsddp_download_trajectory(hsddp_handle h, double *Xbar, double *Ubar, double *K);
+/* X, U, Defect, dX, dU (any may be NULL) — the working trajectory (quirk A2 state). */
+int hsddp_download_working(hsddp_handle h, double *X, double *U, double *Defect, double *dX, double *dU);
+int hsddp_download_element_info(hsddp_handle h, hsddp_element_info *info);
+int hsddp_synchronize(hsddp_handle h);
+size_t hsddp_device_bytes(hsddp_handle h);
+
+/* ---- batched model primitives (device pointers, n points, async on `stream` (NULL = default)) */
+/* xn[n][24] = hkinodyn(x[n][24], u[n][24], dt, c[n][4]) */
+int hsddp_hkd_dynamics(const double *x, const double *u, const double *c, double dt, double *xn,
+                       int n, void *stream);
+/* A[n][24*24], B[n][24*24] column-major (Eigen StateMap/ContrlMap memory layout) */
+int hsddp_hkd_dynamics_partial(const double *x, const double *u, const double *c, double dt,
+                               double *A, double *B, int n, void *stream);
+/* p[n][3] = compute_foot_position(pos, eul, qleg, leg+1) with q = x[12+3leg..], pos = x[3..5], eul = x[0..2]; leg[n] */
+int hsddp_hkd_foot_position(const double *x, const int *leg, double *p, int n, void *stream);
+/* J[n][3*18] column-major, columns [pos(3) | eul(3) | qJ(12)] as comp_foot_jacob_{leg+1} */
+int hsddp_hkd_foot_jacobian(const double *x, const int *leg, double *J, int n, void *stream);
+/* c, cn int32 [n][4] */
+int hsddp_hkd_resetmap(const double *x, const int *c, const int *cn, double *xn, int n, void *stream);
+/* Px[n][24*24] column-major */
+int hsddp_hkd_resetmap_partial(const double *x, const int *c, const int *cn, double *Px, int n,
+                               void *stream);
+
+/* device memory helpers for the primitives (so callers without a HIP runtime binding can use them) */
+void *hsddp_device_alloc(size_t bytes, int device);
+int hsddp_device_free(void *p);
+int hsddp_memcpy_h2d(void *dst, const void *src, size_t bytes);
+int hsddp_memcpy_d2h(void *dst, const void *src, size_t bytes);
+int hsddp_device_synchronize(int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HSDDP_H */
