@@ -435,93 +435,168 @@ static int count_active(hsddp_handle h, int which, int &n)
     return HSDDP_OK;
 }
 
-extern "C" int hsddp_solve(hsddp_handle h, hsddp_stats *stats)
+// The solve is split so a caller can time a fixed number of inner iterations:
+//   hsddp_solve_begin  = initial hybrid_rollout(0) + update_nominal + compute_cost (MultiPhaseDDP.cpp:257-260)
+//                        and the first outer-iteration prologue (:284-303)
+//   hsddp_iterate      = n inner iterations (:304-381) for every still-active element
+//   hsddp_solve_end    = outer epilogue: AL / ReB updates and tests (:383-408)
+// hsddp_solve runs the complete reference loop with per-element early exits.
+static int solve_check(hsddp_handle h)
 {
     if (!h) return fail(HSDDP_ERR_ARG, "null handle");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     if (!h->opt.MS)
         return fail(HSDDP_ERR_UNSUPPORTED, "single shooting (MS = false) is not supported by the knot-parallel rollout");
     HIPCHK(hipSetDevice(h->desc.device));
+    return HSDDP_OK;
+}
+
+static std::vector<double> ls_steps(double alpha)
+{
+    // line-search step sizes exactly as `while (eps > 1e-3) { ...; eps *= alpha; }` evaluates them
+    std::vector<double> trials;
+    for (double eps = 1; eps > 1e-3; eps *= alpha) trials.push_back(eps);
+    return trials;
+}
+
+static void begin_launches(hsddp_handle h)
+{
+    launch_reset_elements(h->p, h->d, h->stream);
+    launch_rollout(h->p, h->d, 0.0, 1, h->stream);
+    launch_decide(h->p, h->d, 0.0, 0, 1, h->stream);
+    launch_update_nominal(h->p, h->d, 1, h->stream);
+}
+
+static void iteration_launches(hsddp_handle h, const std::vector<double> &trials, Timer &tm)
+{
     const Params &p = h->p;
     const Bufs &d = h->d;
     hipStream_t st = h->stream;
-    Timer tm{st, stats != nullptr, {}};
-    hipEvent_t e_all0 = nullptr, e_all1 = nullptr;
-    if (stats) {
-        memset(stats, 0, sizeof(*stats));
-        hipEventCreate(&e_all0);
-        hipEventCreate(&e_all1);
-        hipEventRecord(e_all0, st);
+    hipEvent_t e0;
+    tm.begin(0, e0);
+    launch_lq(p, d, st);
+    tm.end(0, e0);
+    tm.begin(1, e0);
+    launch_backward(p, d, st);
+    tm.end(1, e0);
+    tm.begin(2, e0);
+    for (size_t t = 0; t < trials.size(); ++t) {
+        launch_rollout(p, d, trials[t], 0, st);
+        launch_decide(p, d, trials[t], t + 1 == trials.size(), 0, st);
     }
-    // line-search step sizes exactly as `while (eps > 1e-3) { ...; eps *= alpha; }` evaluates them
-    std::vector<double> trials;
-    for (double eps = 1; eps > 1e-3; eps *= h->opt.alpha) trials.push_back(eps);
+    launch_update_nominal(p, d, 0, st);
+    tm.end(2, e0);
+}
 
-    launch_reset_elements(p, d, st);
-    // initial rollout: hybrid_rollout(0), update_nominal_trajectory, compute_cost, feasibility
-    launch_rollout(p, d, 0.0, 1, st);
-    launch_decide(p, d, 0.0, 0, 1, st);
-    launch_update_nominal(p, d, 1, st);
-    int iters_launched = 0, outer_launched = 0, n_bwd = 0;
+static void outer_end_launches(hsddp_handle h, Timer &tm)
+{
+    hipEvent_t e0;
+    tm.begin(3, e0);
+    if (h->opt.ReB_active) launch_reb_update(h->p, h->d, h->stream);
+    launch_outer_end(h->p, h->d, h->stream);
+    tm.end(3, e0);
+}
+
+static int finish_stats(hsddp_handle h, Timer &tm, hipEvent_t e0, hsddp_stats *stats, int iters, int outers, int nbwd)
+{
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (!stats) return HSDDP_OK;
+    hipEvent_t e1;
+    hipEventCreate(&e1);
+    hipEventRecord(e1, h->stream);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    stats->ms_total = ms;
+    stats->ms_lq = tm.total(0);
+    stats->ms_backward = tm.total(1);
+    stats->ms_forward = tm.total(2);
+    stats->ms_other = tm.total(3);
+    stats->inner_iterations = iters;
+    stats->outer_iterations = outers;
+    stats->n_backward_launches = nbwd;
+    std::vector<ElemState> el(h->p.B);
+    HIPCHK(hipMemcpy(el.data(), h->d.el, h->p.B * sizeof(ElemState), hipMemcpyDeviceToHost));
+    for (auto &e : el) { stats->ls_trials += e.n_ls; stats->element_iterations += e.iters; }
+    return HSDDP_OK;
+}
+
+static hipEvent_t start_stats(hsddp_handle h, hsddp_stats *stats)
+{
+    if (!stats) return nullptr;
+    memset(stats, 0, sizeof(*stats));
+    hipEvent_t e0;
+    hipEventCreate(&e0);
+    hipEventRecord(e0, h->stream);
+    return e0;
+}
+
+extern "C" int hsddp_solve(hsddp_handle h, hsddp_stats *stats)
+{
+    int rc = solve_check(h);
+    if (rc) return rc;
+    Timer tm{h->stream, stats != nullptr, {}};
+    hipEvent_t e0 = start_stats(h, stats);
+    const std::vector<double> trials = ls_steps(h->opt.alpha);
+    begin_launches(h);
+    int iters = 0, outers = 0, nbwd = 0;
     const bool checks = !h->opt.no_early_exit;
     for (int ou = 0; ou < h->opt.max_AL_iter; ++ou) {
-        launch_outer_begin(p, d, st);
-        outer_launched++;
+        launch_outer_begin(h->p, h->d, h->stream);
+        outers++;
         for (int in = 0; in < h->opt.max_DDP_iter; ++in) {
-            hipEvent_t e0;
-            tm.begin(0, e0);
-            launch_lq(p, d, st);
-            tm.end(0, e0);
-            tm.begin(1, e0);
-            launch_backward(p, d, st);
-            tm.end(1, e0);
-            n_bwd++;
-            tm.begin(2, e0);
-            for (size_t t = 0; t < trials.size(); ++t) {
-                launch_rollout(p, d, trials[t], 0, st);
-                launch_decide(p, d, trials[t], t + 1 == trials.size(), 0, st);
-            }
-            launch_update_nominal(p, d, 0, st);
-            tm.end(2, e0);
-            iters_launched++;
+            iteration_launches(h, trials, tm);
+            iters++;
+            nbwd++;
             if (checks) {
-                int n = 0, rc = count_active(h, 1, n);
-                if (rc) return rc;
+                int n = 0;
+                if ((rc = count_active(h, 1, n))) return rc;
                 if (n == 0) break;
             }
         }
-        hipEvent_t e0;
-        tm.begin(3, e0);
-        if (h->opt.ReB_active) launch_reb_update(p, d, st);
-        launch_outer_end(p, d, st);
-        tm.end(3, e0);
+        outer_end_launches(h, tm);
         if (checks) {
-            int n = 0, rc = count_active(h, 2, n);
-            if (rc) return rc;
+            int n = 0;
+            if ((rc = count_active(h, 2, n))) return rc;
             if (n == 0) break;
         }
     }
+    return finish_stats(h, tm, e0, stats, iters, outers, nbwd);
+}
+
+extern "C" int hsddp_solve_begin(hsddp_handle h)
+{
+    int rc = solve_check(h);
+    if (rc) return rc;
+    begin_launches(h);
+    launch_outer_begin(h->p, h->d, h->stream);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(st));
-    if (stats) {
-        hipEventRecord(e_all1, st);
-        hipEventSynchronize(e_all1);
-        float ms = 0;
-        hipEventElapsedTime(&ms, e_all0, e_all1);
-        stats->ms_total = ms;
-        stats->ms_lq = tm.total(0);
-        stats->ms_backward = tm.total(1);
-        stats->ms_forward = tm.total(2);
-        stats->ms_other = tm.total(3);
-        stats->inner_iterations = iters_launched;
-        stats->outer_iterations = outer_launched;
-        stats->n_backward_launches = n_bwd;
-        hipEventDestroy(e_all0);
-        hipEventDestroy(e_all1);
-        std::vector<ElemState> el(p.B);
-        HIPCHK(hipMemcpy(el.data(), d.el, p.B * sizeof(ElemState), hipMemcpyDeviceToHost));
-        for (auto &e : el) { stats->ls_trials += e.n_ls; stats->element_iterations += e.iters; }
-    }
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_iterate(hsddp_handle h, int n, hsddp_stats *stats)
+{
+    int rc = solve_check(h);
+    if (rc) return rc;
+    if (n < 0) return fail(HSDDP_ERR_ARG, "negative iteration count");
+    Timer tm{h->stream, stats != nullptr, {}};
+    hipEvent_t e0 = start_stats(h, stats);
+    const std::vector<double> trials = ls_steps(h->opt.alpha);
+    for (int i = 0; i < n; ++i) iteration_launches(h, trials, tm);
+    return finish_stats(h, tm, e0, stats, n, 0, n);
+}
+
+extern "C" int hsddp_solve_end(hsddp_handle h)
+{
+    int rc = solve_check(h);
+    if (rc) return rc;
+    Timer tm{h->stream, false, {}};
+    outer_end_launches(h, tm);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(h->stream));
     return HSDDP_OK;
 }
 

@@ -93,15 +93,26 @@ class Solver:
         check(lib().hsddp_set_options(self._h, C.byref(options)))
 
     def warm_start(self, Xbar=None, Ubar=None, K=None) -> None:
-        cv = lambda a: None if a is None else dp(np.ascontiguousarray(a, dtype=np.float64))
         keep = [np.ascontiguousarray(a, dtype=np.float64) if a is not None else None for a in (Xbar, Ubar, K)]
         check(lib().hsddp_upload_warm_start(self._h, *(None if a is None else dp(a) for a in keep)))
-        del cv
 
     def solve(self) -> Stats:
+        """MultiPhaseDDP::solve for every element (MultiPhaseDDP.cpp:232-428)."""
         st = Stats()
         check(lib().hsddp_solve(self._h, C.byref(st)))
         return st
+
+    def begin(self) -> None:
+        check(lib().hsddp_solve_begin(self._h))
+
+    def iterate(self, n: int) -> Stats:
+        """n inner DDP iterations of every active element (throughput mode)."""
+        st = Stats()
+        check(lib().hsddp_iterate(self._h, int(n), C.byref(st)))
+        return st
+
+    def end(self) -> None:
+        check(lib().hsddp_solve_end(self._h))
 
     def trajectory(self) -> dict:
         Xbar = np.empty((self.B, self.S, 24)); Ubar = np.empty((self.B, self.Kc, 24))

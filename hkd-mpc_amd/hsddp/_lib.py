@@ -75,7 +75,7 @@ EXPORTS = [
     "hsddp_last_error", "hsddp_version", "hsddp_default_options", "hsddp_default_weights",
     "hsddp_default_constraint_params", "hsddp_load_settings", "hsddp_load_constraint_params",
     "hsddp_create", "hsddp_destroy", "hsddp_set_options", "hsddp_upload_problem",
-    "hsddp_upload_warm_start", "hsddp_solve", "hsddp_download_trajectory", "hsddp_download_working",
+    "hsddp_upload_warm_start", "hsddp_solve", "hsddp_solve_begin", "hsddp_iterate", "hsddp_solve_end", "hsddp_download_trajectory", "hsddp_download_working",
     "hsddp_download_element_info", "hsddp_synchronize", "hsddp_device_bytes", "hsddp_hkd_dynamics",
     "hsddp_hkd_dynamics_partial", "hsddp_hkd_foot_position", "hsddp_hkd_foot_jacobian",
     "hsddp_hkd_resetmap", "hsddp_hkd_resetmap_partial", "hsddp_device_alloc", "hsddp_device_free",
@@ -100,6 +100,9 @@ def lib():
     L.hsddp_upload_problem.argtypes = [C.c_void_p, IP, DP, DP, DP, DP]
     L.hsddp_upload_warm_start.argtypes = [C.c_void_p, DP, DP, DP]
     L.hsddp_solve.argtypes = [C.c_void_p, C.POINTER(Stats)]
+    L.hsddp_solve_begin.argtypes = [C.c_void_p]
+    L.hsddp_iterate.argtypes = [C.c_void_p, C.c_int, C.POINTER(Stats)]
+    L.hsddp_solve_end.argtypes = [C.c_void_p]
     L.hsddp_download_trajectory.argtypes = [C.c_void_p, DP, DP, DP]
     L.hsddp_download_working.argtypes = [C.c_void_p, DP, DP, DP, DP, DP]
     L.hsddp_download_element_info.argtypes = [C.c_void_p, C.POINTER(ElementInfo)]

@@ -12,7 +12,8 @@ batch of independent trajectories with closed-form gait references instead of CS
 * x0[b] = nominal stance (HKDMPC.cpp:44-54: z = 0.2486, qJ = (0, -0.8, 1.6), stance qdummy =
   forward kinematics) + uniform perturbation (eul ±0.1, pos ±0.03, omega ±0.3, v ±0.3), drawn
   by splitmix64 seeded with 20240807 + b;
-* Xbar = reference (HKDProblem.cpp:84-90), Ubar = 0, K = 0 (TrajectoryManagement.cpp:5-35).
+* Xbar = reference (HKDProblem.cpp:84-90), Ubar = 0, K = 0 (TrajectoryManagement.cpp:5-35; K is
+  returned as None = zero).
 
 Layout (element-major, fp64): contacts [B][P+1][4] (row P = contact after the horizon, which
 defines the last phase's touchdown constraint, HKDProblem.cpp:268-310); ref_x/ref_u [Bref][S][24];
@@ -143,14 +144,17 @@ def initial_state(b: int, contact0, seed: int = SEED) -> np.ndarray:
 
 
 def make_batch(batch: int, n_phases: int = 4, knots: int = 50, gait: str = "trot",
-               mixed: bool = False, seed: int = SEED, dt: float = DT) -> dict:
-    """Build a synthetic batch.  mixed=True draws a per-element gait."""
+               mixed: bool = False, seed: int = SEED, dt: float = DT, first_element: int = 0) -> dict:
+    """Build a synthetic batch.  mixed=True draws a per-element gait.
+
+    Element b of this batch is global element first_element + b (seed SEED + global index), so
+    shards of one global batch built on different ranks are disjoint and reproducible."""
     horizons = [knots] * n_phases
     S = sum(n + 1 for n in horizons)
     Kc = sum(horizons)
     if mixed:
         names = ["trot", "pace", "bound", "pronk"]
-        pick = (uniform_stream(seed ^ 0x5A5A, batch) * len(names)).astype(int)
+        pick = (uniform_stream(seed ^ 0x5A5A, first_element + batch)[first_element:] * len(names)).astype(int)
         gaits = [names[i] for i in pick]
     else:
         gaits = [gait] * batch
@@ -166,7 +170,7 @@ def make_batch(batch: int, n_phases: int = 4, knots: int = 50, gait: str = "trot
     for b in range(batch):
         sched = phase_schedule(gaits[b], n_phases)
         contacts[b] = np.array(sched, dtype=np.int32)
-        x0[b] = initial_state(b, sched[0], seed)
+        x0[b] = initial_state(first_element + b, sched[0], seed)
         rx, ru, rf = refs[gaits[b]]
         if len(uniq) > 1:
             ref_x[b], ref_u[b], ref_f[b] = rx, ru, rf
@@ -175,5 +179,6 @@ def make_batch(batch: int, n_phases: int = 4, knots: int = 50, gait: str = "trot
         "batch": batch, "horizons": horizons, "dt": dt, "S": S, "Kc": Kc, "gaits": gaits,
         "contacts": contacts, "x0": x0, "ref_x": np.ascontiguousarray(ref_x),
         "ref_u": np.ascontiguousarray(ref_u), "ref_foot": np.ascontiguousarray(ref_f),
-        "Xbar": Xbar, "Ubar": np.zeros((batch, Kc, 24)), "K": np.zeros((batch, Kc, 24, 24)),
+        "Xbar": Xbar, "Ubar": np.zeros((batch, Kc, 24)),
+        "K": None,  # feedback gains default to zero on the device (3.8 GB as a host array at B=4096)
     }

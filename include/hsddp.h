@@ -16,6 +16,7 @@
  *                                             HKDSinglePhaseReference::get_reference_at_t HKDReference.cpp:8-57
  *   hsddp_upload_warm_start                   Trajectory::Xbar/Ubar/K warm start    TrajectoryManagement.h:54-77
  *   hsddp_solve                               MultiPhaseDDP::solve                  MultiPhaseDDP.cpp:232-428
+ *   hsddp_solve_begin/_iterate/_end           the same loop split at its inner iterations (:257-303 / :304-381 / :383-408)
  *   hsddp_download_trajectory                 Trajectory fields read by the caller  HKDMPC.cpp:243-298
  *   hsddp_download_element_info               get_actual_cost / get_solver_info     MultiPhaseDDP.h:416; .cpp:532-541
  *   hsddp_hkd_dynamics                        HKD::Model::dynamics (hkinodyn)       HKDModel.h:33-45
@@ -148,6 +149,12 @@ int hsddp_upload_problem(hsddp_handle h, const int *contacts, const double *x0, 
 int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const double *Ubar, const double *K);
 
 int hsddp_solve(hsddp_handle h, hsddp_stats *stats);
+/* Split form of hsddp_solve for timing a fixed number of inner iterations (throughput mode):
+ * begin = initial rollout + first outer prologue; iterate = n inner iterations of every active
+ * element (MultiPhaseDDP.cpp:304-381); end = AL/ReB updates + outer tests. */
+int hsddp_solve_begin(hsddp_handle h);
+int hsddp_iterate(hsddp_handle h, int n, hsddp_stats *stats);
+int hsddp_solve_end(hsddp_handle h);
 
 int hsddp_download_trajectory(hsddp_handle h, double *Xbar, double *Ubar, double *K);
 /* X, U, Defect, dX, dU (any may be NULL) — the working trajectory (quirk A2 state). */

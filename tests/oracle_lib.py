@@ -176,7 +176,7 @@ def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 
         "Defect": np.zeros((n, S, 24)), "Defect_bar": np.zeros((n, S, 24)), "dX": np.zeros((n, S, 24)),
         "Ubar": np.ascontiguousarray(prob["Ubar"][idx]).copy(),
         "U": np.ascontiguousarray(prob["Ubar"][idx]).copy(), "dU": np.zeros((n, Kc, 24)),
-        "K": np.ascontiguousarray(prob["K"][idx]).copy(),
+        "K": (np.zeros((n, Kc, 24, 24)) if prob.get("K") is None else np.ascontiguousarray(prob["K"][idx]).copy()),
         "reb_delta": np.zeros((n, Kc, 20)), "reb_eps": np.zeros((n, Kc, 20)),
         "al_sigma": np.zeros((n, P, 4)), "al_lambda": np.zeros((n, P, 4)),
     }

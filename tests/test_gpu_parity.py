@@ -1,0 +1,178 @@
+"""GPU parity tests: the HIP product path (through the C-ABI) against the oracle.
+
+Tolerances (fp64): model primitives 1e-12 relative to the largest entry (different operation
+order than the CasADi graph); one/three inner iterations 1e-9 relative on K, dU, dX, X, U, Xbar,
+Ubar and exact equality of every branch decision (line-search trial counts, iteration counts,
+statuses); full solves 1e-7 relative on elements whose own oracle solution is insensitive to a
+1e-15 relative perturbation of x0 (the "chaos screen": a few jump elements wander for 50
+iterations and flip line-search decisions on rounding alone — the oracle disagrees with itself
+there).  Full-size (B = 4096) runs are checked through size-independent properties.
+"""
+import numpy as np
+import pytest
+
+import hsddp
+import oracle_lib as O
+from hsddp import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b))) / max(1e-300, np.max(np.abs(b))))
+
+
+# ---- model primitives ------------------------------------------------------------------------
+def test_model_matches_golden(golden):
+    xn = hsddp.model.dynamics(golden["x"], golden["u"], golden["c"], float(golden["dt"]))
+    A, B = hsddp.model.dynamics_partial(golden["x"], golden["u"], golden["c"], float(golden["dt"]))
+    assert rel(xn, golden["xn"]) < 1e-12
+    for q in range(A.shape[0]):
+        assert rel(A[q], golden["A"][q]) < 1e-12
+        assert rel(B[q], golden["B"][q]) < 1e-12
+        # compact device representation: every reference structural zero of B stays zero
+        assert np.all(B[q][golden["B"][q] == 0] == 0)
+
+
+def test_kinematics_and_reset_match_golden(golden):
+    m = golden["fx"].shape[0]
+    for leg in range(4):
+        p = hsddp.model.foot_position(golden["fx"], np.full(m, leg))
+        J = hsddp.model.foot_jacobian(golden["fx"], np.full(m, leg))
+        assert rel(p, golden["fp"][:, leg]) < 1e-12
+        assert rel(J, golden["fJ"][:, leg]) < 1e-12
+    xn = hsddp.model.resetmap(golden["rx"], golden["rc"], golden["rcn"])
+    Px = hsddp.model.resetmap_partial(golden["rx"], golden["rc"], golden["rcn"])
+    assert rel(xn, golden["rxn"]) < 1e-12
+    assert rel(Px, golden["rPx"]) < 1e-12
+
+
+def test_model_edge_cases():
+    # flight (no stance) and all-stance, zero batch
+    x = np.zeros((2, 24)); x[:, 5] = 0.25
+    u = np.ones((2, 24))
+    c = np.array([[0, 0, 0, 0], [1, 1, 1, 1]], float)
+    xn = hsddp.model.dynamics(x, u, c)
+    for q in range(2):
+        assert rel(xn[q], O.hkd_step(x[q], u[q], 0.01, c[q])) < 1e-14
+    hsddp.model.dynamics(np.zeros((0, 24)), np.zeros((0, 24)), np.zeros((0, 4)))
+
+
+# ---- solver ----------------------------------------------------------------------------------
+def _run(prob, **kw):
+    s = hsddp.Solver(prob, hsddp.load_settings(**kw))
+    s.solve()
+    out = {**s.trajectory(), **s.working(), **s.element_info()}
+    s.close()
+    return out
+
+
+def _chaotic(prob, kw, elems):
+    """Elements whose oracle solution changes under a 1e-15 relative x0 perturbation."""
+    a = O.solve_batch(prob, O.default_options(**kw), n_threads=8, elements=elems)
+    p2 = dict(prob); p2["x0"] = prob["x0"] * (1 + 1e-15)
+    b = O.solve_batch(p2, O.default_options(**kw), n_threads=8, elements=elems)
+    bad = set()
+    for j, e in enumerate(elems):
+        if a["n_ls_trials"][j] != b["n_ls_trials"][j] or abs(a["cost"][j] - b["cost"][j]) > 1e-8 * abs(a["cost"][j]):
+            bad.add(e)
+    return a, bad
+
+
+@pytest.mark.parametrize("n_iter", [1, 3])
+@pytest.mark.parametrize("gait,P,N", [("trot", 4, 50), ("jump", 8, 25), ("pronk", 4, 20)])
+def test_fixed_iterations_match_oracle(gait, P, N, n_iter):
+    prob = syn.make_batch(8, P, N, gait)
+    kw = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=n_iter)
+    g = _run(prob, **kw)
+    r = O.solve_batch(prob, O.default_options(**kw), n_threads=8)
+    for f in ("Xbar", "Ubar", "K", "X", "U", "dX", "dU"):
+        assert rel(g[f], r[f]) < 1e-9, f
+    for f in ("cost", "feas", "max_tconstr"):
+        assert rel(g[f], r[f]) < 1e-9, f
+    for f in ("iters", "outer_iters", "status", "n_ls_trials"):
+        assert np.array_equal(g[f], r[f]), f
+
+
+@pytest.mark.parametrize("gait,P,N,mixed", [("trot", 4, 50, False), ("jump", 8, 25, False),
+                                              ("trot", 4, 50, True)])
+def test_full_solve_matches_oracle(gait, P, N, mixed):
+    prob = syn.make_batch(16, P, N, gait, mixed=mixed)
+    g = _run(prob)
+    r, chaotic = _chaotic(prob, {}, list(range(16)))
+    ok = [b for b in range(16) if b not in chaotic]
+    assert len(ok) >= 12
+    for f in ("iters", "outer_iters", "status", "n_ls_trials"):
+        assert np.array_equal(g[f][ok], r[f][ok]), f
+    for f in ("Xbar", "Ubar"):
+        assert rel(g[f][ok], r[f][ok]) < 1e-7, f
+    assert rel(g["cost"][ok], r["cost"][ok]) < 1e-9
+
+
+def test_regularization_overflow_status():
+    """Negative control weights make Quu indefinite for every mu <= 1e2: the element must stop
+    with the reference's bad_solve outcome (MultiPhaseDDP.cpp:162-167, :421-427)."""
+    prob = syn.make_batch(2, 2, 10, "trot")
+    w = hsddp.Weights()
+    hsddp._lib.lib().hsddp_default_weights(__import__("ctypes").byref(w))
+    w.r_qJd = -1e5
+    s = hsddp.Solver(prob, hsddp.load_settings(), weights=w)
+    s.solve()
+    info = s.element_info()
+    s.close()
+    assert np.all(info["status"] == 1)
+    assert np.all(info["iters"] == 1)
+
+
+def test_repeat_solve_is_deterministic():
+    prob = syn.make_batch(64, 4, 50, "trot")
+    a = _run(prob, no_early_exit=1, max_AL_iter=1, max_DDP_iter=3)
+    b = _run(prob, no_early_exit=1, max_AL_iter=1, max_DDP_iter=3)
+    for f in ("Xbar", "Ubar", "K", "cost"):
+        assert np.array_equal(a[f], b[f]), f
+
+
+def test_full_batch_properties():
+    """B = 4096 (the metric config): every element runs, costs fall, gathered sample matches."""
+    B = 4096
+    prob = syn.make_batch(B, 4, 50, "trot")
+    s = hsddp.Solver(prob, hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=3))
+    s.begin()
+    c0 = s.element_info()["cost"].copy()
+    st = s.iterate(3)
+    info = s.element_info()
+    tr = s.trajectory()
+    s.close()
+    assert np.all(np.isfinite(info["cost"])) and np.all(info["status"] == 0)
+    assert np.all(info["iters"] == 3)
+    assert np.mean(info["cost"] < c0) > 0.99
+    assert st.n_backward_launches == 3
+    # spot-check a strided sample of elements against the oracle
+    sample = list(range(0, B, 512))
+    r = O.solve_batch(prob, O.default_options(no_early_exit=1, max_AL_iter=1, max_DDP_iter=3),
+                      n_threads=8, elements=sample)
+    assert rel(tr["Xbar"][sample], r["Xbar"]) < 1e-9
+    assert rel(tr["K"][sample], r["K"]) < 1e-9
+
+
+def test_warm_start_round_trip():
+    """Warm start from a previous solution (the MPC update's reuse of Xbar/Ubar/K)."""
+    prob = syn.make_batch(4, 4, 20, "trot")
+    s = hsddp.Solver(prob, hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=2))
+    s.solve()
+    tr = s.trajectory()
+    s.warm_start(tr["Xbar"], tr["Ubar"], tr["K"])
+    s.solve()
+    g = {**s.trajectory(), **s.element_info()}
+    s.close()
+    p2 = dict(prob); p2["Xbar"], p2["Ubar"], p2["K"] = tr["Xbar"], tr["Ubar"], tr["K"]
+    r = O.solve_batch(p2, O.default_options(no_early_exit=1, max_AL_iter=1, max_DDP_iter=2))
+    assert rel(g["Xbar"], r["Xbar"]) < 1e-9 and rel(g["K"], r["K"]) < 1e-9
+
+
+def test_single_shooting_rejected():
+    prob = syn.make_batch(2, 2, 5, "trot")
+    s = hsddp.Solver(prob, hsddp.load_settings(MS=0))
+    with pytest.raises(hsddp.HSDDPError, match="single shooting"):
+        s.solve()
+    s.close()
