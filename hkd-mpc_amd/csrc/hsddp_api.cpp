@@ -208,6 +208,7 @@ struct hsddp_handle_t {
     size_t bytes = 0;
     int Bref = 1;
     bool have_problem = false;
+    bool backward_v1 = false;  // HSDDP_BACKWARD=1 selects the first-generation kernel (A/B runs)
 };
 
 template <typename T>
@@ -231,6 +232,7 @@ static void fill_params(hsddp_handle h)
     const hsddp_problem_desc &ds = h->desc;
     const hsddp_options &o = h->opt;
     p.dt = ds.dt;
+    p.dt_m = ds.dt / hkd::kMass;
     p.mu = ds.cparams.mu_fric;
     p.grf_delta = ds.cparams.grf_delta; p.grf_delta_min = ds.cparams.grf_delta_min; p.grf_eps = ds.cparams.grf_eps;
     p.td_sigma = ds.cparams.td_sigma; p.td_sigma_max = ds.cparams.td_sigma_max; p.td_lambda = ds.cparams.td_lambda;
@@ -263,6 +265,7 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
     HIPCHK(hipSetDevice(desc->device));
     hsddp_handle h = new hsddp_handle_t();
     h->desc = *desc;
+    if (const char *e = std::getenv("HSDDP_BACKWARD")) h->backward_v1 = std::atoi(e) == 1;
     hsddp_default_options(&h->opt);
     Params &p = h->p;
     p.B = desc->batch;
@@ -477,7 +480,8 @@ static void iteration_launches(hsddp_handle h, const std::vector<double> &trials
     launch_lq(p, d, st);
     tm.end(0, e0);
     tm.begin(1, e0);
-    launch_backward(p, d, st);
+    if (h->backward_v1) launch_backward_v1(p, d, st);
+    else launch_backward(p, d, st);
     tm.end(1, e0);
     tm.begin(2, e0);
     for (size_t t = 0; t < trials.size(); ++t) {

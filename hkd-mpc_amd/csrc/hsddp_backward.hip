@@ -1,0 +1,720 @@
+// hsddp_backward.hip — regularised backward Riccati sweep + multiple-shooting linear rollout.
+//
+// MultiPhaseDDP::backward_sweep_regularized / backward_sweep / linear_rollout
+//   (HSDDPSolver/source/MultiPhaseDDP.cpp:20-50, 141-229) over SinglePhase::backward_sweep /
+//   linear_rollout (SinglePhase.cpp:144-178, 298-367), for B independent elements.
+//
+// k_riccati (gfx950): one 64-lane wave per element.  Lane L has row r = L & 31 and half
+// hf = L >> 5; a row lane (r < 24) owns columns 12 hf .. 12 hf + 11 of row r of the value
+// Hessian H, of Qxx, of Quu and of Qux^T — 12-double register arrays, so 4 waves/SIMD fit in
+// the register file and the 4096 elements of the metric batch are all resident at once.
+// Lane 24 of each half ("vector lane") owns that half of Qu.  The halves exchange values with
+// v_permlane32_swap (VALU, no LDS round trip).  Values every lane reads at the same address
+// (the knot's LQ record, phase constants) come through the scalar cache into SGPRs.
+// Products with the sparse A = I + S and B read only rows 0..11 of T = H B and rows 0..8 of
+// M = H A, broadcast through LDS (7.6 KB per element).
+// Quu^-1 [Qux | Qu] is formed by Gauss-Jordan elimination without pivoting on the 24 x 49 block
+// matrix whose columns live one per row lane (rows split across the halves): 24 dependent steps
+// per knot (vs 72 for Cholesky + two triangular solves), each broadcasting one pivot column.
+// This is the reference's explicit inverse formulation (Quu.inverse(), SinglePhase.cpp:351)
+// computed as a solve; Quu is SPD whenever it passes the PSD test, so no pivoting is needed.
+// PSD test: every elimination pivot (= the LDL^T pivot of Quu) must exceed 1e-9; pivots of Quu
+// dominate those of the reference's Quu - 1e-9 I by 1e-9, so every Quu the reference's LDLT
+// accepts passes here too.
+//
+// k_lin_rollout: the linear rollout that follows a successful sweep, one wave per element.
+#include <utility>
+
+#include "hsddp_device.h"
+
+namespace hsddp {
+
+using namespace hkd;
+
+constexpr int HC = 12;   // columns per half-wave
+constexpr int XS = 25;   // padded row stride of the LDS matrix (row-per-lane writes without conflicts)
+constexpr int M9R = 12;  // LDS row of M = H A row 0
+constexpr int NTRI = NX * (NX + 1) / 2;
+
+struct BwdElem {
+    double X[NX * XS];  // T rows 0..11 | M rows 0..8 -> Qxx (symmetrisation) -> Qux, row-major
+    union {
+        struct {
+            double lq[LQW + 2];
+            double Gn[NX], d[NX];
+        } k;               // knot inputs, dead after Qx / Qu are formed
+        double qp[NTRI];   // then: symmetric Qxx, packed upper triangle
+    } u;
+    double col[NX];        // Gauss-Jordan pivot column
+    double Qu[NX];
+    double red[4];
+};
+
+// packed upper-triangle index of (a, b), a <= b
+DEV int tri(int a, int b) { return a * (2 * NX - a + 1) / 2 + (b - a); }
+
+// A 64-thread workgroup is one wave, so __syncthreads() lowers to no instruction and stops no
+// code motion; the memory clobber keeps each phase's LDS loads in their phase.
+#define HSYNC()                        \
+    do {                               \
+        __syncthreads();               \
+        asm volatile("" ::: "memory"); \
+    } while (0)
+// scheduling fence between the stages of a knot: keeps the scheduler from hoisting a later
+// stage's loads (and their registers) into an earlier one
+#define SFENCE() __builtin_amdgcn_sched_barrier(0)
+
+// Compile-time loop: the body sees its index as a constant, so per-lane register arrays indexed
+// by it stay in VGPRs (a runtime index would demote them to scratch).
+template <typename F, int... I>
+DEV void static_for_impl(F &&f, std::integer_sequence<int, I...>)
+{
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+DEV void static_for(F &&f)
+{
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Register pin: the values must exist in VGPRs at this point.  Placed at the end of each stage
+// of a knot, it stops LLVM from sinking a stage's arithmetic into a later one, which would keep
+// that stage's LDS operands live (the unpinned Gauss-Jordan deferred its Qux updates to the end
+// and spilled every pivot column).
+template <int N>
+DEV void pin(double (&a)[N])
+{
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(a[i]));
+}
+
+// read-only, wave-uniform data: the constant address space lets the compiler use scalar loads
+typedef const __attribute__((address_space(4))) double cdouble;
+DEV cdouble *uniform_ptr(const double *p) { return (cdouble *)p; }
+
+// a value known to be equal on all lanes, moved to SGPRs
+DEV double uniform(double v)
+{
+    const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+    const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+
+// value held by the same lane of the other half-wave (call with all 64 lanes active)
+DEV double other_half(double v)
+{
+    const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return threadIdx.x < 32 ? __hiloint2double(b[1], a[1]) : __hiloint2double(b[0], a[0]);
+}
+
+// per-phase constants of one element
+struct PhaseConst {
+    int c[4];
+    double bv[4];  // dt c_l / m     (B rows 9..11)
+    double bq[4];  // dt (1 - c_l)   (B rows 12..23)
+};
+
+// Wave-uniform: contacts through the scalar cache, and selects instead of arithmetic so the
+// constants stay in SGPRs (dt * c / m is dt / m or 0 exactly for c in {0, 1}).
+DEV void load_phase(const Params &p, const Bufs &d, size_t b, int i, PhaseConst &pc)
+{
+    typedef const __attribute__((address_space(4))) int cint;
+    cint *cs = (cint *)(d.contacts + (b * (p.P + 1) + i) * 4);
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        pc.c[l] = cs[l];
+        pc.bv[l] = pc.c[l] ? p.dt_m : 0.0;
+        pc.bq[l] = pc.c[l] ? 0.0 : p.dt;
+    }
+}
+
+// lxx (dt Q + dt D^T Qfoot D, HKDCost.cpp:32) row r as: diagonal + cross terms with the foot columns
+struct LxxRow {
+    double diag, xq[4], xp;  // xq[l]: (r in pos) x (col 12+3l+(r-3)); xp: (r in q) x (col 3+(r-12)%3)
+};
+
+// a[i] for a runtime i, as selects (a runtime index would put the array in scratch)
+template <typename T>
+DEV T pick4(const T (&a)[4], int i)
+{
+    return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
+}
+
+// q_diag / foot_weight (hsddp_device.h) with the contact index resolved by selects
+DEV void lxx_row(const Params &p, const PhaseConst &pc, int r, LxxRow &L)
+{
+    L.diag = 0.0; L.xp = 0.0;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) L.xq[l] = 0.0;
+    if (r >= NX) return;
+    L.diag = p.dt * (r < 12 ? p.qbase[r] : p.q_qJ * (1 - pick4(pc.c, (r - 12) / 3)));
+    if (r >= 3 && r < 6) {
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const int cl = pc.c[l];
+            double w = p.dt * cl * cl * (p.foot_gain * p.foot_w[r - 3] * cl);
+            L.diag += w;
+            L.xq[l] = -w;
+        }
+    } else if (r >= 12) {
+        const int m = r - 12, cl = pick4(pc.c, m / 3);
+        double w = p.dt * cl * cl * (p.foot_gain * p.foot_w[m % 3] * cl);
+        L.diag += w;
+        L.xp = -w;
+    }
+}
+
+// lxx(r, 12 hf + i) for a compile-time i
+template <int i>
+DEV double lxx_half(const LxxRow &L, int r, int hf)
+{
+    const double dg = (HC * hf + i == r) ? L.diag : 0.0;
+    const double x1 = (r == 3 + i % 3) ? L.xq[i / 3] : 0.0;  // hf = 1
+    double x0 = 0.0;                                         // hf = 0
+    if constexpr (i >= 3 && i < 6) x0 = (r >= 12 && r < NX && (r - 12) % 3 == i - 3) ? L.xp : 0.0;
+    return dg + (hf ? x1 : x0);
+}
+
+// luu row r: dt R(r) on the diagonal + the ReB 3x3 block of r's leg (row r of it)
+struct LuuRow {
+    double diag, blk[3];
+};
+
+DEV void luu_row(const Params &p, const double *lq, int r, LuuRow &L)
+{
+    L.diag = (r < NX) ? p.dt * r_diag(p, r) : 0.0;
+    L.blk[0] = L.blk[1] = L.blk[2] = 0.0;
+    if (r < 12) {
+        const double *rb = lq + LQ_RB + 6 * (r / 3);
+        int a = r % 3;
+        // symmetric 3x3 stored (00,01,02,11,12,22)
+        L.blk[0] = a == 0 ? rb[0] : a == 1 ? rb[1] : rb[2];
+        L.blk[1] = a == 0 ? rb[1] : a == 1 ? rb[3] : rb[4];
+        L.blk[2] = a == 0 ? rb[2] : a == 1 ? rb[4] : rb[5];
+    }
+}
+
+// luu(r, 12 hf + i) for a compile-time i
+template <int i>
+DEV double luu_half(const LuuRow &L, int r, int hf)
+{
+    const double dg = (HC * hf + i == r) ? L.diag : 0.0;
+    const double b0 = (r < 12 && r / 3 == i / 3) ? L.blk[i % 3] : 0.0;
+    return dg + (hf ? 0.0 : b0);
+}
+
+// Column r of S (= A - I): coefficients S[j][r], j = 0..8
+DEV void s_column(const double *lq, double dt, int r, double *sc)
+{
+    int q = (r < NX) ? se_index(r) : -1;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sc[j] = q >= 0 ? lq[LQ_SE + 5 * j + q] : 0.0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sc[3 + j] = (r == j + 9) ? dt : 0.0;
+    q = (r < NX) ? sw_index(r) : -1;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sc[6 + j] = q >= 0 ? lq[LQ_SW + 17 * j + q] : 0.0;
+}
+
+DEV double half_sum(double v)
+{
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// One knot of SinglePhase::backward_sweep (SinglePhase.cpp:298-362).  h/g hold this lane's
+// columns of H[k+1] row r and G[k+1][r] on entry, H[k] and G[k] on exit.  `live` turns false
+// when Quu fails the PSD test (wave-uniform).
+DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &pc, size_t b, int s, int kc,
+                  double reg, bool &live, double (&h)[HC], double &g, double &dV1, double &dV2)
+{
+    // opaque per knot: keeps LICM from hoisting ~50 lane-dependent constants of the knot body
+    // (regularised diagonals, lxx / luu entries) out of the knot loop into long-lived VGPRs
+    int lane = threadIdx.x;
+    asm volatile("" : "+v"(lane));
+    asm volatile("" : "+v"(reg));
+    const int r = lane & 31, hf = lane >> 5, cb = HC * hf;
+    const bool rowl = r < NX, vecl = r == NX;
+    const double dt = p.dt;
+    const size_t kq = b * p.Kc + kc;
+    cdouble *lqs = uniform_ptr(d.lq + kq * LQW);
+    for (int q = lane; q < LQW; q += 64) S.u.k.lq[q] = d.lq[kq * LQW + q];
+    if (lane < NX) S.u.k.d[lane] = d.Defect[(b * p.S + s + 1) * NX + lane];
+    HSYNC();
+    // Gnext = G + H Defect[k+1] (SinglePhase.cpp:320)
+    double part = 0.0;
+#pragma unroll
+    for (int i = 0; i < HC; ++i) part += h[i] * S.u.k.d[cb + i];
+    const double gn = g + (part + other_half(part));
+    // T = H B, M = H A on this half's columns; the second half needs H[r][6..8] from the first
+    double h68[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) h68[j] = other_half(h[6 + j]);
+    double t[HC], m[HC];
+    if (hf == 0) {
+        static_for<HC>([&](auto I) {
+            constexpr int c = I;
+            t[c] = h[6] * lqs[LQ_BW + c] + h[7] * lqs[LQ_BW + 12 + c] + h[8] * lqs[LQ_BW + 24 + c] +
+                   h[9 + c % 3] * pc.bv[c / 3];
+            double v = h[c];
+            constexpr int qe = se_index(c), qw = sw_index(c);
+            if constexpr (qe >= 0)
+                v += h[0] * lqs[LQ_SE + qe] + h[1] * lqs[LQ_SE + 5 + qe] + h[2] * lqs[LQ_SE + 10 + qe];
+            if constexpr (c >= 9) v += h[c - 6] * dt;
+            if constexpr (qw >= 0)
+                v += h[6] * lqs[LQ_SW + qw] + h[7] * lqs[LQ_SW + 17 + qw] + h[8] * lqs[LQ_SW + 34 + qw];
+            m[c] = v;
+        });
+    } else {
+        static_for<HC>([&](auto I) {
+            constexpr int i = I;
+            t[i] = h[i] * pc.bq[i / 3];
+            double v = h[i];
+            constexpr int qw = sw_index(HC + i);
+            if constexpr (qw >= 0)
+                v += h68[0] * lqs[LQ_SW + qw] + h68[1] * lqs[LQ_SW + 17 + qw] + h68[2] * lqs[LQ_SW + 34 + qw];
+            m[i] = v;
+        });
+    }
+    pin(t);
+    pin(m);
+    if (r < 12)
+#pragma unroll
+        for (int i = 0; i < HC; ++i) S.X[r * XS + cb + i] = t[i];
+    if (r < 9)
+#pragma unroll
+        for (int i = 0; i < HC; ++i) S.X[(M9R + r) * XS + cb + i] = m[i];
+    if (lane < NX) S.u.k.Gn[lane] = gn;
+    HSYNC();
+    SFENCE();
+    // Qx, Qxx = lxx + A^T H A, Qux^T row = (A^T H B) row, Quu row = luu + B^T H B
+    // (SinglePhase.cpp:323-327; regularisation on both diagonals, MultiPhaseDDP.cpp:160)
+    double sc[9];
+    s_column(S.u.k.lq, dt, r, sc);
+    double qx = 0.0;
+    if (rowl) {
+        double a = 0.0;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) a += sc[j] * S.u.k.Gn[j];
+        qx = S.u.k.lq[LQ_LX + r] + (gn + a);
+    }
+    double qxx[HC], wa[HC], wb[HC];
+    {
+        LxxRow lx_;
+        lxx_row(p, pc, r, lx_);
+        static_for<HC>([&](auto I) {
+            constexpr int i = I;
+            double a = 0.0;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) a += sc[j] * S.X[(M9R + j) * XS + cb + i];
+            qxx[i] = lxx_half<i>(lx_, r, hf) + (m[i] + a) + (cb + i == r ? reg : 0.0);
+        });
+    }
+    pin(qxx);
+    SFENCE();
+    {
+        LuuRow lu_;
+        luu_row(p, S.u.k.lq, r, lu_);
+        double bc[6] = {0, 0, 0, 0, 0, 0};
+        double bqr = 0.0;
+        if (r < 12) {
+            bc[0] = S.u.k.lq[LQ_BW + r]; bc[1] = S.u.k.lq[LQ_BW + 12 + r]; bc[2] = S.u.k.lq[LQ_BW + 24 + r];
+            const int l = r / 3, mm = r % 3;
+            const double bvl = l == 0 ? pc.bv[0] : l == 1 ? pc.bv[1] : l == 2 ? pc.bv[2] : pc.bv[3];
+            bc[3] = mm == 0 ? bvl : 0.0;
+            bc[4] = mm == 1 ? bvl : 0.0;
+            bc[5] = mm == 2 ? bvl : 0.0;
+        } else if (rowl) {
+            bqr = pick4(pc.bq, (r - 12) / 3);
+        }
+        static_for<HC>([&](auto I) {
+            constexpr int i = I;
+            double a = 0.0;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) a += sc[j] * S.X[j * XS + cb + i];
+            wb[i] = t[i] + a;
+            double q = bqr * t[i];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) q += bc[j] * S.X[(6 + j) * XS + cb + i];
+            wa[i] = luu_half<i>(lu_, r, hf) + q + (cb + i == r ? reg : 0.0);
+        });
+    }
+    if (vecl) { // Qu = lu + B^T Gnext
+        if (hf == 0) {
+#pragma unroll
+            for (int c = 0; c < HC; ++c)
+                wb[c] = lqs[LQ_LU + c] + (lqs[LQ_BW + c] * S.u.k.Gn[6] + lqs[LQ_BW + 12 + c] * S.u.k.Gn[7] +
+                                          lqs[LQ_BW + 24 + c] * S.u.k.Gn[8] + pc.bv[c / 3] * S.u.k.Gn[9 + c % 3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < HC; ++i) wb[i] = lqs[LQ_LU + HC + i] + pc.bq[i / 3] * S.u.k.Gn[HC + i];
+        }
+#pragma unroll
+        for (int i = 0; i < HC; ++i) wa[i] = 0.0;
+    }
+    pin(wa);
+    pin(wb);
+    HSYNC();
+    SFENCE();
+    // Qxx = (Qxx + Qxx^T) / 2 (SinglePhase.cpp:352), kept in LDS as a packed upper triangle
+    if (rowl)
+#pragma unroll
+        for (int i = 0; i < HC; ++i) S.X[r * XS + cb + i] = qxx[i];
+    HSYNC();
+    if (rowl)
+#pragma unroll
+        for (int i = 0; i < HC; ++i) {
+            const int c = cb + i;
+            const double q = (qxx[i] + S.X[c * XS + r]) / 2;
+            if (r <= c) S.u.qp[tri(r, c)] = q;
+        }
+    HSYNC();
+    // Qux[j][r] (rows j of this half) and Qu into LDS for the value update
+    if (rowl)
+#pragma unroll
+        for (int i = 0; i < HC; ++i) S.X[(cb + i) * XS + r] = wb[i];
+    if (vecl)
+#pragma unroll
+        for (int i = 0; i < HC; ++i) S.Qu[cb + i] = wb[i];
+    SFENCE();
+    // Gauss-Jordan: [Quu | Qux | Qu] -> [I | Quu^-1 Qux | Quu^-1 Qu]
+    unsigned long long bad = 0;  // ballot: convergent, so the PSD test stays in its step
+    static_for<NX>([&](auto J) {
+        constexpr int j = J, hj = j / HC, ij = j % HC;
+        if (r == j)
+#pragma unroll
+            for (int i = 0; i < HC; ++i) S.col[cb + i] = wa[i];
+        const double xa = other_half(wa[ij]), xb = other_half(wb[ij]);
+        HSYNC();
+        const bool own = hf == hj;
+        const double piv = S.col[j];
+        bad |= __builtin_amdgcn_ballot_w64(!(piv > 1e-9)); // PSD test
+        const double inv = 1.0 / piv;
+        const double fa = (own ? wa[ij] : xa) * inv, fb = (own ? wb[ij] : xb) * inv;
+        static_for<HC>([&](auto I) {
+            constexpr int i = I;
+            const double cq = S.col[cb + i];
+            const double na = wa[i] - cq * fa, nb = wb[i] - cq * fb;
+            if constexpr (i == ij) {
+                wa[i] = own ? fa : na;
+                wb[i] = own ? fb : nb;
+            } else {
+                wa[i] = na;
+                wb[i] = nb;
+            }
+        });
+        pin(wa);
+        pin(wb);
+        HSYNC();
+        SFENCE();
+    });
+    live = live && bad == 0;
+    if (!live) return;
+    // K = -Quu^-1 Qux, dU = -Quu^-1 Qu, G = Qx - Qux^T Quu^-1 Qu (wb = this half's rows of
+    // column r of Quu^-1 Qux, or of Quu^-1 Qu on the vector lane)
+    double gp = 0.0, dvp = 0.0;
+#pragma unroll
+    for (int i = 0; i < HC; ++i) {
+        const double qu = S.Qu[cb + i];
+        gp += wb[i] * qu;
+        dvp += qu * wb[i];
+    }
+    gp += other_half(gp);
+    dvp += other_half(dvp);
+    if (rowl) {
+        double *Kg = d.K + kq * NN;
+#pragma unroll
+        for (int i = 0; i < HC; ++i) Kg[(cb + i) * NX + r] = -wb[i];
+    }
+    if (vecl) {
+        double *dUg = d.dU + kq * NX;
+#pragma unroll
+        for (int i = 0; i < HC; ++i) dUg[cb + i] = -wb[i];
+    }
+    const double dvk = __shfl(dvp, NX);
+    dV1 -= dvk;
+    dV2 += dvk;
+    g = rowl ? qx - gp : 0.0;
+    SFENCE();
+    // H = Qxx - Qux^T Quu^-1 Qux: rows j of this half use wb, rows of the other half its copy
+    double acc[HC];
+#pragma unroll
+    for (int i = 0; i < HC; ++i) acc[i] = 0.0;
+    const int ob = HC - cb;
+    static_for<HC>([&](auto J) {
+        constexpr int jj = J;
+        const double ko = other_half(wb[jj]);
+#pragma unroll
+        for (int i = 0; i < HC; ++i) acc[i] += wb[jj] * S.X[(cb + jj) * XS + cb + i];
+#pragma unroll
+        for (int i = 0; i < HC; ++i) acc[i] += ko * S.X[(ob + jj) * XS + cb + i];
+        pin(acc);
+        SFENCE();
+    });
+#pragma unroll
+    for (int i = 0; i < HC; ++i) {
+        const int c = cb + i;
+        h[i] = rowl ? S.u.qp[r <= c ? tri(r, c) : tri(c, r)] - acc[i] : 0.0;
+    }
+    HSYNC();
+}
+
+// MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229) with one regularisation value.
+// Returns false (and stops) at the first knot whose Quu fails the PSD test.
+DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double reg, double &dV1, double &dV2)
+{
+    const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5, cb = HC * hf;
+    const bool rowl = r < NX;
+    double h[HC], g = 0.0;
+    bool live = true;
+    dV1 = 0.0; dV2 = 0.0;
+    for (int i = p.P - 1; i >= 0; --i) {
+        PhaseConst pc;
+        load_phase(p, d, b, i, pc);
+        const double *rec = d.term + (b * p.P + i) * TW;
+        if (i == p.P - 1) {
+#pragma unroll
+            for (int c = 0; c < HC; ++c) h[c] = rowl ? rec[TM_PHIXX + r * NX + cb + c] : 0.0;
+            g = rowl ? rec[TM_PHIX + r] : 0.0;
+        } else {
+            // impact-aware step G' = Phix + Px^T G0, H' = Phixx + Px^T H0 Px
+            // (MultiPhaseDDP.cpp:480-484): W = H0 Px in place of H0 in LDS, then Px^T W.
+            const double *Px = rec + TM_PX;
+            if (rowl)
+#pragma unroll
+                for (int c = 0; c < HC; ++c) S.X[r * XS + cb + c] = h[c];
+            if (lane < NX) S.col[lane] = g;
+            HSYNC();
+            double w[HC];
+#pragma unroll
+            for (int c = 0; c < HC; ++c) w[c] = 0.0;
+            if (rowl)
+                for (int k = 0; k < NX; ++k) {
+                    const double hk = S.X[r * XS + k];
+#pragma unroll
+                    for (int c = 0; c < HC; ++c) w[c] += hk * Px[k * NX + cb + c];
+                }
+            HSYNC();
+            if (rowl)
+#pragma unroll
+                for (int c = 0; c < HC; ++c) S.X[r * XS + cb + c] = w[c];
+            HSYNC();
+            double gp = 0.0;
+#pragma unroll
+            for (int c = 0; c < HC; ++c) w[c] = 0.0;
+            if (rowl)
+                for (int j = 0; j < NX; ++j) {
+                    const double pj = Px[j * NX + r];
+                    gp += pj * S.col[j];
+#pragma unroll
+                    for (int c = 0; c < HC; ++c) w[c] += pj * S.X[j * XS + cb + c];
+                }
+#pragma unroll
+            for (int c = 0; c < HC; ++c) h[c] = rowl ? rec[TM_PHIXX + r * NX + cb + c] + w[c] : 0.0;
+            g = rowl ? rec[TM_PHIX + r] + gp : 0.0;
+            HSYNC();
+        }
+        const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
+#pragma unroll 1
+        for (int k = N - 1; k >= 0 && live; --k)
+            bwd_knot(p, d, S, pc, b, s0 + k, k0 + k, reg, live, h, g, dV1, dV2);
+        if (!live) return false;
+        // G[0] += H[0] Defect[0] (SinglePhase.cpp:365)
+        if (lane < NX) S.col[lane] = d.Defect[(b * p.S + s0) * NX + lane];
+        HSYNC();
+        double a = 0.0;
+#pragma unroll
+        for (int c = 0; c < HC; ++c) a += h[c] * S.col[cb + c];
+        a += other_half(a);
+        if (rowl) g += a;
+        HSYNC();
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(64, 4) void k_riccati(Params p, Bufs d)
+{
+    __shared__ BwdElem S;
+    const int lane = threadIdx.x;
+    const size_t b = blockIdx.x;
+    ElemState &E = d.el[b];
+    if (E.done || E.inner_done) return;
+    // compute_cost + feasibility at the start of the inner iteration (MultiPhaseDDP.cpp:306-307)
+    if (lane == 0) {
+        double cost = 0.0, feas = 0.0;
+        for (int i = 0; i < p.P; ++i) {
+            double ci = 0.0, fi = 0.0;
+            for (int k = 0; k < p.N[i]; ++k) ci += d.slot_cost[b * p.S + p.s0[i] + k];
+            ci += d.slot_cost[b * p.S + p.s0[i] + p.N[i]];
+            for (int k = 0; k <= p.N[i]; ++k) fi += d.slot_feas[b * p.S + p.s0[i] + k];
+            cost += ci;
+            feas += fi;
+        }
+        S.red[0] = cost;
+        S.red[1] = sqrt(feas);
+    }
+    HSYNC();
+    const double cost = uniform(S.red[0]), feas = uniform(S.red[1]);
+    double reg = uniform(E.reg);
+    bool ok = false;
+    double dV1 = 0.0, dV2 = 0.0;
+    // backward_sweep_regularized (MultiPhaseDDP.cpp:141-181)
+    for (;;) {
+        if (bwd_sweep(p, d, S, b, reg, dV1, dV2)) { ok = true; break; }
+        reg = fmax(reg * p.update_regularization, 1e-03);
+        if (reg > 1e2) break;
+    }
+    reg = reg / 20;
+    if (reg < 1e-06) reg = 0;
+    if (lane == 0) {
+        E.iters += 1; E.cost = cost; E.feas = feas; E.reg = reg; E.accepted = 0;
+        if (!ok) { E.status = 1; E.done = 1; E.ls_active = 0; } // goto bad_solve
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// MultiPhaseDDP::linear_rollout(1.0): dX, du = dU + K dX, and the expected cost change (quirk
+// A3: it replaces the sweep's dV), then the merit function (MultiPhaseDDP.cpp:309-318).
+// Lanes r < 24 of each half compute row r of the same vectors; the first half stores them.
+struct LinElem {
+    double lq[LQW + 2];
+    double dx[NX], du[NX], d[NX];
+};
+
+__global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
+{
+    __shared__ LinElem S;
+    const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5, cb = HC * hf;
+    const size_t b = blockIdx.x;
+    ElemState &E = d.el[b];
+    if (E.done || E.inner_done) return;
+    const bool rowl = r < NX, st = rowl && hf == 0;
+    const int rr = rowl ? r : 0;
+    const double dt = p.dt;
+    double v1 = 0.0, v2 = 0.0, dx = 0.0;
+    for (int i = 0; i < p.P; ++i) {
+        PhaseConst pc;
+        load_phase(p, d, b, i, pc);
+        const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
+        if (i > 0) { // dx_init = Px dX_end
+            const double *Px = d.term + (b * p.P + (i - 1)) * TW + TM_PX;
+            if (lane < NX) S.dx[lane] = dx;
+            HSYNC();
+            double a = 0.0;
+            if (rowl)
+                for (int j = 0; j < NX; ++j) a += Px[r * NX + j] * S.dx[j];
+            dx = a;
+            HSYNC();
+        } else {
+            dx = 0.0;
+        }
+        if (rowl) {
+            dx = dx + d.Defect[(b * p.S + s0) * NX + r];
+            if (st) d.dX[(b * p.S + s0) * NX + r] = dx;
+        }
+        // lxx row r (HKDCost.cpp:32): diagonal + foot cross terms
+        LxxRow lx_;
+        lxx_row(p, pc, r, lx_);
+        const double ru = rowl ? p.dt * r_diag(p, r) : 0.0;
+        for (int k = 0; k < N; ++k) {
+            const int s = s0 + k, kc = k0 + k;
+            const size_t kq = b * p.Kc + kc;
+            double krow[HC];
+#pragma unroll
+            for (int c = 0; c < HC; ++c) krow[c] = d.K[kq * NN + rr * NX + cb + c];
+            const double dUr = d.dU[kq * NX + rr];
+            for (int q = lane; q < LQW; q += 64) S.lq[q] = d.lq[kq * LQW + q];
+            if (lane < NX) { S.d[lane] = d.Defect[(b * p.S + s + 1) * NX + lane]; S.dx[lane] = dx; }
+            HSYNC();
+            double kd = 0.0;
+#pragma unroll
+            for (int c = 0; c < HC; ++c) kd += krow[c] * S.dx[cb + c];
+            kd += other_half(kd);
+            const double du = dUr + kd;
+            if (lane < NX) S.du[lane] = du;
+            HSYNC();
+            double nx = 0.0, q1 = 0.0, q2 = 0.0;
+            if (rowl) {
+                double sdx = 0.0;
+                if (r < 3) {
+#pragma unroll
+                    for (int q = 0; q < 5; ++q) sdx += S.lq[LQ_SE + 5 * r + q] * S.dx[se_col(q)];
+                } else if (r < 6) {
+                    sdx = dt * S.dx[r + 6];
+                } else if (r < 9) {
+#pragma unroll
+                    for (int q = 0; q < 17; ++q) sdx += S.lq[LQ_SW + 17 * (r - 6) + q] * S.dx[sw_col(q)];
+                }
+                double bdu = 0.0, lxd = lx_.diag * dx, lud = ru * du;
+                if (r < 6) {
+                    if (r >= 3) {
+#pragma unroll
+                        for (int l = 0; l < 4; ++l) lxd += lx_.xq[l] * S.dx[12 + 3 * l + r - 3];
+                    }
+                } else if (r < 9) {
+#pragma unroll
+                    for (int c = 0; c < 12; ++c) bdu += S.lq[LQ_BW + 12 * (r - 6) + c] * S.du[c];
+                } else if (r < 12) {
+#pragma unroll
+                    for (int l = 0; l < 4; ++l) bdu += pc.bv[l] * S.du[3 * l + r - 9];
+                } else {
+                    bdu = pick4(pc.bq, (r - 12) / 3) * S.du[r];
+                    lxd += lx_.xp * S.dx[3 + (r - 12) % 3];
+                }
+                if (r < 12) {
+                    const double *rb = S.lq + LQ_RB + 6 * (r / 3);
+                    const int a = r % 3, u0 = 3 * (r / 3);
+                    const double b0 = a == 0 ? rb[0] : a == 1 ? rb[1] : rb[2];
+                    const double b1 = a == 0 ? rb[1] : a == 1 ? rb[3] : rb[4];
+                    const double b2 = a == 0 ? rb[2] : a == 1 ? rb[4] : rb[5];
+                    lud += b0 * S.du[u0] + b1 * S.du[u0 + 1] + b2 * S.du[u0 + 2];
+                }
+                nx = (dx + sdx) + bdu + S.d[r];
+                q1 = S.lq[LQ_LX + r] * dx + S.lq[LQ_LU + r] * du;
+                q2 = dx * lxd + du * lud;
+                if (st) {
+                    d.du[kq * NX + r] = du;
+                    d.dX[(b * p.S + s + 1) * NX + r] = nx;
+                }
+            }
+            v1 += half_sum(q1);
+            v2 += half_sum(q2);
+            dx = nx;
+            HSYNC();
+        }
+        const double *rec = d.term + (b * p.P + i) * TW;
+        if (lane < NX) S.dx[lane] = dx;
+        HSYNC();
+        double q1 = 0.0, q2 = 0.0;
+        if (rowl) {
+            q1 = rec[TM_PHIX + r] * dx;
+            double a = 0.0;
+            for (int c = 0; c < NX; ++c) a += rec[TM_PHIXX + r * NX + c] * S.dx[c];
+            q2 = dx * a;
+        }
+        v1 += half_sum(q1);
+        v2 += half_sum(q2);
+        HSYNC();
+    }
+    if (lane == 0) {
+        const double cost = E.cost, feas = E.feas;
+        const double dV_abs = fabs(v1 + 0.5 * v2);
+        const double rho = (feas > p.feas_thresh) ? dV_abs / ((1 - p.merit_scale) * feas) + p.merit_offset : 0;
+        const double merit = cost + rho * feas;
+        E.dV1 = v1; E.dV2 = v2; E.merit_rho = rho; E.merit = merit;
+        E.cost_prev = cost; E.merit_prev = merit; E.feas_prev = feas;
+        if (!p.no_early_exit && dV_abs < p.cost_thresh && feas <= p.feas_thresh) { E.inner_done = 1; E.ls_active = 0; }
+        else E.ls_active = 1;
+    }
+}
+
+void launch_backward(const Params &p, const Bufs &d, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_riccati, dim3(p.B), dim3(64), 0, st, p, d);
+    hipLaunchKernelGGL(k_lin_rollout, dim3(p.B), dim3(64), 0, st, p, d);
+}
+
+}  // namespace hsddp

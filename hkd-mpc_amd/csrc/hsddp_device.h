@@ -1,0 +1,134 @@
+// hsddp_device.h — device-side cost/constraint helpers shared by the solver kernels.
+// HKD costs: HKDCost.h:8-99, HKDCost.cpp:5-63; SinglePhaseInterface.cpp:55-118.
+// ReB / GRF: ConstraintsBase.h:204-263, HKDConstraints.cpp:7-66.  AL / touchdown: ConstraintsBase.h:374-399,
+// HKDConstraints.cpp:69-171.
+#pragma once
+#include "hsddp_internal.h"
+
+namespace hsddp {
+using namespace hkd;
+
+#define DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------------------------------------
+// cost model helpers (HKDCost.h / HKDCost.cpp / SinglePhaseInterface.cpp:55-118)
+DEV double q_diag(const Params &p, const int *c, int j) { return j < 12 ? p.qbase[j] : p.q_qJ * (1 - c[(j - 12) / 3]); }
+DEV double r_diag(const Params &p, int j) { return j < 12 ? p.r_grf : p.r_qJd; }
+DEV double foot_weight(const Params &p, const int *c, int j) { return p.foot_gain * p.foot_w[j % 3] * c[j / 3]; }
+DEV bool touchdown(const int *c, const int *cn, int l) { return c[l] == 0 && cn[l] == 1; }
+
+DEV void slot_phase(const Params &p, int s, int &i, int &k)
+{
+    i = 0;
+    for (int j = 1; j < p.P; ++j)
+        if (s >= p.s0[j]) i = j;
+    k = s - p.s0[i];
+}
+
+DEV void load_contacts(const Bufs &d, const Params &p, int b, int i, int *c, int *cn)
+{
+    const int *cc = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) { c[l] = cc[l]; cn[l] = cc[4 + l]; }
+}
+
+DEV const double *ref_ptr(const Params &p, const double *base, int b, int s, int width)
+{
+    return base + ((size_t)(p.ref_per_element ? b : 0) * p.S + s) * width;
+}
+
+// ReB barrier (ConstraintsBase.h:204-263)
+DEV double reb_cost(double g, double delta)
+{
+    if (g > delta) return -log(g);
+    double t = (g - 2 * delta) / delta;
+    return .5 * (t * t - 1) - log(delta);
+}
+DEV void reb_derivs(double g, double delta, double &d1, double &d2)
+{
+    if (g > delta) { d1 = -1.0 / g; d2 = 1.0 / (g * g); }
+    else { d1 = (g - 2 * delta) / delta / delta; d2 = 1.0 / (delta * delta); }
+}
+
+// GRF friction pyramid (HKDConstraints.cpp:7-66): rows of A_leg applied to one leg's force
+DEV void grf_row(double mu, int r, double *row)
+{
+    row[0] = (r == 1) ? -1.0 : (r == 2) ? 1.0 : 0.0;
+    row[1] = (r == 3) ? -1.0 : (r == 4) ? 1.0 : 0.0;
+    row[2] = (r == 0) ? 1.0 : mu;
+}
+DEV double grf_value(double mu, int r, const double *f)
+{
+    double row[3];
+    grf_row(mu, r, row);
+    return row[0] * f[0] + row[1] * f[1] + row[2] * f[2];
+}
+
+// running cost l_k (tracking + foot regularisation + dt * ReB), and min(0, min g)
+DEV double running_cost(const Params &p, const int *c, const double *x, const double *u, const double *xr,
+                        const double *ur, const double *pf, const double *delta, const double *eps, double &viol)
+{
+    double lt = 0.0, lu = 0.0, lf = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) { double e = x[j] - xr[j]; lt += e * q_diag(p, c, j) * e; }
+    lt = 0.5 * lt;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) { double e = u[j] - ur[j]; lu += e * r_diag(p, j) * e; }
+    lt += 0.5 * lu;
+    lt *= p.dt;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        double e = (x[12 + j] - x[3 + j % 3]) - (pf[j] - xr[3 + j % 3]);
+        lf += e * foot_weight(p, c, j) * e;
+    }
+    lf = .5 * lf;
+    lf *= p.dt;
+    double l = lt + lf;
+    double rc = 0.0, mk = 0.0;
+    for (int lg = 0; lg < 4; ++lg) {
+        if (!c[lg]) continue;
+        for (int r = 0; r < 5; ++r) {
+            double g = grf_value(p.mu, r, u + 3 * lg);
+            mk = fmin(mk, g);
+            rc += eps[5 * lg + r] * reb_cost(g, delta[5 * lg + r]);
+        }
+    }
+    if (p.ReB_active && (c[0] + c[1] + c[2] + c[3]) > 0) l += p.dt * rc;
+    viol = mk;
+    return l;
+}
+
+// terminal cost Phi (tracking Qf + 10 * foot + AL), max |h| and h per touchdown leg
+DEV double terminal_cost(const Params &p, const int *c, const int *cn, const double *x, const double *xr,
+                         const double *pf, const double *sig, const double *lam, double &tviol, double *h_out)
+{
+    double phi = 0.0, fc = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+        double e = x[j] - xr[j];
+        phi += e * (p.qf_gain * p.qf_scale[j] * q_diag(p, c, j)) * e;
+    }
+    phi *= 0.5;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        double e = (x[12 + j] - x[3 + j % 3]) - (pf[j] - xr[3 + j % 3]);
+        fc += e * foot_weight(p, c, j) * e;
+    }
+    phi = phi + p.foot_term_cost * fc;
+    double al = 0.0, tv = 0.0;
+    for (int l = 0; l < 4; ++l) {
+        h_out[l] = 0.0;
+        if (!touchdown(c, cn, l)) continue;
+        double h = hkd_foot_height_grad(l, x, nullptr) - p.ground;
+        h_out[l] = h;
+        tv = fmax(tv, fabs(h));
+        al += 0.5 * sig[l] * h * h;
+        al += lam[l] * h;
+    }
+    if (p.AL_active) phi += al;
+    tviol = tv;
+    return phi;
+}
+
+
+}  // namespace hsddp

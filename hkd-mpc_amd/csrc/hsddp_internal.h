@@ -39,7 +39,7 @@ struct Params {
     int B, P, S, Kc;
     int N[MAXP], s0[MAXP], k0[MAXP];
     int ref_per_element;
-    double dt, mu, grf_delta, grf_delta_min, grf_eps, td_sigma, td_sigma_max, td_lambda, ground;
+    double dt, dt_m /* dt / mass, = dt * c / mass for c = 1 */, mu, grf_delta, grf_delta_min, grf_eps, td_sigma, td_sigma_max, td_lambda, ground;
     // HKD weights
     double qbase[12], q_qJ, qf_scale[24], qf_gain, r_grf, r_qJd, foot_w[3], foot_gain, foot_term_cost, foot_term_grad;
     // HSDDP_OPTION
@@ -74,6 +74,7 @@ void launch_decide(const Params &p, const Bufs &d, double eps, int last, int ini
 void launch_update_nominal(const Params &p, const Bufs &d, int init, hipStream_t st);
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st);
 void launch_backward(const Params &p, const Bufs &d, hipStream_t st);
+void launch_backward_v1(const Params &p, const Bufs &d, hipStream_t st);
 void launch_outer_begin(const Params &p, const Bufs &d, hipStream_t st);
 void launch_reb_update(const Params &p, const Bufs &d, hipStream_t st);
 void launch_outer_end(const Params &p, const Bufs &d, hipStream_t st);
