@@ -31,22 +31,15 @@ namespace hsddp {
 
 using namespace hkd;
 
-constexpr int HC = 12;   // columns per half-wave
-constexpr int XS = 25;   // padded row stride of the LDS matrix (row-per-lane writes without conflicts)
-constexpr int M9R = 12;  // LDS row of M = H A row 0
-constexpr int NTRI = NX * (NX + 1) / 2;
+constexpr int HC = 12;      // columns per half-wave; coupled controls per knot
+constexpr int XS = 25;      // padded row stride of the LDS matrix (row-per-lane writes without conflicts)
+constexpr int OFF_M9 = NX * HC;  // M rows 0..8 after T_c in Bm
+constexpr int OFF_KP = HC * NX;  // Quu_cc^-1 Qux_c after Qux_c in A
 
 struct BwdElem {
-    double X[NX * XS];  // T rows 0..11 | M rows 0..8 -> Qxx (symmetrisation) -> Qux, row-major
-    union {
-        struct {
-            double lq[LQW + 2];
-            double Gn[NX], d[NX];
-        } k;               // knot inputs, dead after Qx / Qu are formed
-        double qp[NTRI];   // then: symmetric Qxx, packed upper triangle
-    } u;
-    double col[NX];        // Gauss-Jordan pivot column
-    double Qu[NX];
+    double A[NX * XS];             // LQ record copy -> Qxx rows (symmetrisation) -> Qux_c [12][24] | Kp [12][24]
+    double Bm[NX * HC + 9 * NX];   // T_c = H B_c [24][12] | M rows 0..8 [9][24] -> packed symmetric Qxx
+    double Gn[NX], d[NX], wqu[HC];
     double red[4];
 };
 
@@ -97,6 +90,14 @@ DEV double uniform(double v)
 {
     const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
     const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+
+// v on lane `src` (a constant), broadcast to every lane through SGPRs
+DEV double lane_value(double v, int src)
+{
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
     return __hiloint2double(hi, lo);
 }
 
@@ -177,34 +178,6 @@ DEV double lxx_half(const LxxRow &L, int r, int hf)
     return dg + (hf ? x1 : x0);
 }
 
-// luu row r: dt R(r) on the diagonal + the ReB 3x3 block of r's leg (row r of it)
-struct LuuRow {
-    double diag, blk[3];
-};
-
-DEV void luu_row(const Params &p, const double *lq, int r, LuuRow &L)
-{
-    L.diag = (r < NX) ? p.dt * r_diag(p, r) : 0.0;
-    L.blk[0] = L.blk[1] = L.blk[2] = 0.0;
-    if (r < 12) {
-        const double *rb = lq + LQ_RB + 6 * (r / 3);
-        int a = r % 3;
-        // symmetric 3x3 stored (00,01,02,11,12,22)
-        L.blk[0] = a == 0 ? rb[0] : a == 1 ? rb[1] : rb[2];
-        L.blk[1] = a == 0 ? rb[1] : a == 1 ? rb[3] : rb[4];
-        L.blk[2] = a == 0 ? rb[2] : a == 1 ? rb[4] : rb[5];
-    }
-}
-
-// luu(r, 12 hf + i) for a compile-time i
-template <int i>
-DEV double luu_half(const LuuRow &L, int r, int hf)
-{
-    const double dg = (HC * hf + i == r) ? L.diag : 0.0;
-    const double b0 = (r < 12 && r / 3 == i / 3) ? L.blk[i % 3] : 0.0;
-    return dg + (hf ? 0.0 : b0);
-}
-
 // Column r of S (= A - I): coefficients S[j][r], j = 0..8
 DEV void s_column(const double *lq, double dt, int r, double *sc)
 {
@@ -228,37 +201,51 @@ DEV double half_sum(double v)
 // One knot of SinglePhase::backward_sweep (SinglePhase.cpp:298-362).  h/g hold this lane's
 // columns of H[k+1] row r and G[k+1][r] on entry, H[k] and G[k] on exit.  `live` turns false
 // when Quu fails the PSD test (wave-uniform).
+//
+// Coupled controls: for leg l the three GRF columns of B carry a factor c_l and the three
+// joint-velocity columns a factor (1 - c_l) (HKDDynamics: contact_moment, B rows 9..23), so
+// exactly 12 columns of B are nonzero — control q (0..11) is u = q for a stance leg and
+// u = 12 + q for a swing leg.  The other 12 controls z have B[:, z] = 0 exactly, hence
+// Qux[z, :] = 0, Quu[z, :] = Quu[:, z] = 0 off the diagonal and Quu[z][z] = dt R_z + reg
+// (the ReB Hessian only touches stance GRFs).  Quu is block diagonal under this permutation,
+// so Quu^-1 [Qux | Qu] = [Quu_cc^-1 [Qux_c | Qu_c] ; 0 | Qu_z / Quu_zz] exactly, and the
+// reference's 24-control solve reduces to a 12 x 12 one plus 12 divisions.
 DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &pc, size_t b, int s, int kc,
                   double reg, bool &live, double (&h)[HC], double &g, double &dV1, double &dV2)
 {
-    // opaque per knot: keeps LICM from hoisting ~50 lane-dependent constants of the knot body
-    // (regularised diagonals, lxx / luu entries) out of the knot loop into long-lived VGPRs
+    // opaque per knot: keeps LICM from hoisting lane-dependent constants of the knot body
+    // (regularised diagonals, lxx entries) out of the knot loop into long-lived VGPRs
     int lane = threadIdx.x;
     asm volatile("" : "+v"(lane));
     asm volatile("" : "+v"(reg));
     const int r = lane & 31, hf = lane >> 5, cb = HC * hf;
-    const bool rowl = r < NX, vecl = r == NX;
+    const bool rowl = r < NX;
+    const bool xl = hf == 0 && r < NX;  // lanes holding column r of Qux_c^T ... (A^T H B_c) row r
+    const bool ql = hf == 1 && r < HC;  // lanes holding column r of Quu_cc, and decoupled control z(r)
+    const bool ul = hf == 1 && r == HC; // lane holding Qu_c
     const double dt = p.dt;
     const size_t kq = b * p.Kc + kc;
     cdouble *lqs = uniform_ptr(d.lq + kq * LQW);
-    for (int q = lane; q < LQW; q += 64) S.u.k.lq[q] = d.lq[kq * LQW + q];
-    if (lane < NX) S.u.k.d[lane] = d.Defect[(b * p.S + s + 1) * NX + lane];
+    double *lq = S.A;  // LDS copy for lane-indexed reads
+    for (int q = lane; q < LQW; q += 64) lq[q] = d.lq[kq * LQW + q];
+    if (lane < NX) S.d[lane] = d.Defect[(b * p.S + s + 1) * NX + lane];
     HSYNC();
     // Gnext = G + H Defect[k+1] (SinglePhase.cpp:320)
     double part = 0.0;
 #pragma unroll
-    for (int i = 0; i < HC; ++i) part += h[i] * S.u.k.d[cb + i];
+    for (int i = 0; i < HC; ++i) part += h[i] * S.d[cb + i];
     const double gn = g + (part + other_half(part));
-    // T = H B, M = H A on this half's columns; the second half needs H[r][6..8] from the first
+    // M = H A on this half's columns (the second half needs H[r][6..8] from the first);
+    // T_c = H B_c, each coupled column written by the half that holds its H entries
     double h68[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) h68[j] = other_half(h[6 + j]);
-    double t[HC], m[HC];
+    // (for a swing leg the first half's GRF column value is exactly 0, for a stance leg the second
+    // half's joint-velocity value is: each half stores only the columns it owns)
+    double m[HC], tc[HC];
     if (hf == 0) {
         static_for<HC>([&](auto I) {
             constexpr int c = I;
-            t[c] = h[6] * lqs[LQ_BW + c] + h[7] * lqs[LQ_BW + 12 + c] + h[8] * lqs[LQ_BW + 24 + c] +
-                   h[9 + c % 3] * pc.bv[c / 3];
             double v = h[c];
             constexpr int qe = se_index(c), qw = sw_index(c);
             if constexpr (qe >= 0)
@@ -267,41 +254,45 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
             if constexpr (qw >= 0)
                 v += h[6] * lqs[LQ_SW + qw] + h[7] * lqs[LQ_SW + 17 + qw] + h[8] * lqs[LQ_SW + 34 + qw];
             m[c] = v;
+            tc[c] = h[6] * lqs[LQ_BW + c] + h[7] * lqs[LQ_BW + 12 + c] + h[8] * lqs[LQ_BW + 24 + c] +
+                    h[9 + c % 3] * pc.bv[c / 3];
         });
     } else {
         static_for<HC>([&](auto I) {
             constexpr int i = I;
-            t[i] = h[i] * pc.bq[i / 3];
             double v = h[i];
             constexpr int qw = sw_index(HC + i);
             if constexpr (qw >= 0)
                 v += h68[0] * lqs[LQ_SW + qw] + h68[1] * lqs[LQ_SW + 17 + qw] + h68[2] * lqs[LQ_SW + 34 + qw];
             m[i] = v;
+            tc[i] = h[i] * pc.bq[i / 3];
         });
     }
-    pin(t);
     pin(m);
-    if (r < 12)
-#pragma unroll
-        for (int i = 0; i < HC; ++i) S.X[r * XS + cb + i] = t[i];
+    pin(tc);
+    if (rowl)
+        static_for<HC>([&](auto I) {
+            constexpr int q = I;
+            if ((hf == 0) == (pc.c[q / 3] != 0)) S.Bm[r * HC + q] = tc[q];
+        });
     if (r < 9)
 #pragma unroll
-        for (int i = 0; i < HC; ++i) S.X[(M9R + r) * XS + cb + i] = m[i];
-    if (lane < NX) S.u.k.Gn[lane] = gn;
+        for (int i = 0; i < HC; ++i) S.Bm[OFF_M9 + r * NX + cb + i] = m[i];
+    if (lane < NX) S.Gn[lane] = gn;
     HSYNC();
     SFENCE();
-    // Qx, Qxx = lxx + A^T H A, Qux^T row = (A^T H B) row, Quu row = luu + B^T H B
+    // Qx, Qxx = lxx + A^T M, and the coupled blocks Qux_c, Quu_cc, Qu_c
     // (SinglePhase.cpp:323-327; regularisation on both diagonals, MultiPhaseDDP.cpp:160)
     double sc[9];
-    s_column(S.u.k.lq, dt, r, sc);
+    s_column(lq, dt, r, sc);
     double qx = 0.0;
     if (rowl) {
         double a = 0.0;
 #pragma unroll
-        for (int j = 0; j < 9; ++j) a += sc[j] * S.u.k.Gn[j];
-        qx = S.u.k.lq[LQ_LX + r] + (gn + a);
+        for (int j = 0; j < 9; ++j) a += sc[j] * S.Gn[j];
+        qx = lq[LQ_LX + r] + (gn + a);
     }
-    double qxx[HC], wa[HC], wb[HC];
+    double qxx[HC];
     {
         LxxRow lx_;
         lxx_row(p, pc, r, lx_);
@@ -309,155 +300,164 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
             constexpr int i = I;
             double a = 0.0;
 #pragma unroll
-            for (int j = 0; j < 9; ++j) a += sc[j] * S.X[(M9R + j) * XS + cb + i];
+            for (int j = 0; j < 9; ++j) a += sc[j] * S.Bm[OFF_M9 + j * NX + cb + i];
             qxx[i] = lxx_half<i>(lx_, r, hf) + (m[i] + a) + (cb + i == r ? reg : 0.0);
         });
     }
     pin(qxx);
     SFENCE();
-    {
-        LuuRow lu_;
-        luu_row(p, S.u.k.lq, r, lu_);
-        double bc[6] = {0, 0, 0, 0, 0, 0};
-        double bqr = 0.0;
-        if (r < 12) {
-            bc[0] = S.u.k.lq[LQ_BW + r]; bc[1] = S.u.k.lq[LQ_BW + 12 + r]; bc[2] = S.u.k.lq[LQ_BW + 24 + r];
-            const int l = r / 3, mm = r % 3;
-            const double bvl = l == 0 ? pc.bv[0] : l == 1 ? pc.bv[1] : l == 2 ? pc.bv[2] : pc.bv[3];
-            bc[3] = mm == 0 ? bvl : 0.0;
-            bc[4] = mm == 1 ? bvl : 0.0;
-            bc[5] = mm == 2 ? bvl : 0.0;
-        } else if (rowl) {
-            bqr = pick4(pc.bq, (r - 12) / 3);
-        }
+    double w[HC];
+    double quz = 0.0, qzz = 1.0;  // decoupled control z(r) on the ql lanes: Qu_z, Quu_zz
+    if (hf == 0) {
+        // (A^T T_c)[r][q] = T_c[r][q] + sum_j S[j][r] T_c[j][q]: row r of Qux_c^T
+        const int rr = xl ? r : 0;
         static_for<HC>([&](auto I) {
-            constexpr int i = I;
+            constexpr int q = I;
             double a = 0.0;
 #pragma unroll
-            for (int j = 0; j < 9; ++j) a += sc[j] * S.X[j * XS + cb + i];
-            wb[i] = t[i] + a;
-            double q = bqr * t[i];
-#pragma unroll
-            for (int j = 0; j < 6; ++j) q += bc[j] * S.X[(6 + j) * XS + cb + i];
-            wa[i] = luu_half<i>(lu_, r, hf) + q + (cb + i == r ? reg : 0.0);
+            for (int j = 0; j < 9; ++j) a += sc[j] * S.Bm[j * HC + q];
+            w[q] = xl ? S.Bm[rr * HC + q] + a : 0.0;
         });
+    } else if (ql) {
+        // column r of Quu_cc = luu + B_c^T T_c + reg I
+        const int lr = r / 3, ar = r % 3;
+        static_for<HC>([&](auto I) {
+            constexpr int q = I, l = q / 3, a = q % 3;
+            double v, lu;
+            if (pc.c[l]) {
+                v = lqs[LQ_BW + q] * S.Bm[6 * HC + r] + lqs[LQ_BW + 12 + q] * S.Bm[7 * HC + r] +
+                    lqs[LQ_BW + 24 + q] * S.Bm[8 * HC + r] + pc.bv[l] * S.Bm[(9 + a) * HC + r];
+                // ReB Hessian block of leg l, stored (00,01,02,11,12,22)
+                const int lo = a < ar ? a : ar, hi = a < ar ? ar : a;
+                const double rb = lq[LQ_RB + 6 * l + (lo == 0 ? hi : lo == 1 ? 2 + hi : 5)];
+                lu = (q == r ? dt * p.r_grf : 0.0) + (lr == l ? rb : 0.0);
+            } else {
+                v = pc.bq[l] * S.Bm[(HC + q) * HC + r];
+                lu = q == r ? dt * p.r_qJd : 0.0;
+            }
+            w[q] = lu + v + (q == r ? reg : 0.0);
+        });
+        const bool st = pick4(pc.c, lr) != 0;
+        qzz = dt * (st ? p.r_qJd : p.r_grf) + reg;
+        quz = lq[LQ_LU + (st ? HC + r : r)];
+    } else if (ul) {
+        // Qu_c = lu_c + B_c^T Gnext
+        static_for<HC>([&](auto I) {
+            constexpr int q = I, l = q / 3, a = q % 3;
+            if (pc.c[l])
+                w[q] = lqs[LQ_LU + q] + (lqs[LQ_BW + q] * S.Gn[6] + lqs[LQ_BW + 12 + q] * S.Gn[7] +
+                                         lqs[LQ_BW + 24 + q] * S.Gn[8] + pc.bv[l] * S.Gn[9 + a]);
+            else
+                w[q] = lqs[LQ_LU + HC + q] + pc.bq[l] * S.Gn[HC + q];
+        });
+    } else {
+#pragma unroll
+        for (int q = 0; q < HC; ++q) w[q] = 0.0;
     }
-    if (vecl) { // Qu = lu + B^T Gnext
-        if (hf == 0) {
-#pragma unroll
-            for (int c = 0; c < HC; ++c)
-                wb[c] = lqs[LQ_LU + c] + (lqs[LQ_BW + c] * S.u.k.Gn[6] + lqs[LQ_BW + 12 + c] * S.u.k.Gn[7] +
-                                          lqs[LQ_BW + 24 + c] * S.u.k.Gn[8] + pc.bv[c / 3] * S.u.k.Gn[9 + c % 3]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < HC; ++i) wb[i] = lqs[LQ_LU + HC + i] + pc.bq[i / 3] * S.u.k.Gn[HC + i];
-        }
-#pragma unroll
-        for (int i = 0; i < HC; ++i) wa[i] = 0.0;
-    }
-    pin(wa);
-    pin(wb);
+    pin(w);
     HSYNC();
     SFENCE();
     // Qxx = (Qxx + Qxx^T) / 2 (SinglePhase.cpp:352), kept in LDS as a packed upper triangle
     if (rowl)
 #pragma unroll
-        for (int i = 0; i < HC; ++i) S.X[r * XS + cb + i] = qxx[i];
+        for (int i = 0; i < HC; ++i) S.A[r * XS + cb + i] = qxx[i];
     HSYNC();
     if (rowl)
 #pragma unroll
         for (int i = 0; i < HC; ++i) {
             const int c = cb + i;
-            const double q = (qxx[i] + S.X[c * XS + r]) / 2;
-            if (r <= c) S.u.qp[tri(r, c)] = q;
+            const double q = (qxx[i] + S.A[c * XS + r]) / 2;
+            if (r <= c) S.Bm[tri(r, c)] = q;
         }
     HSYNC();
-    // Qux[j][r] (rows j of this half) and Qu into LDS for the value update
-    if (rowl)
+    // pre-elimination Qux_c (rows q) and Qu_c for the value update
+    if (xl)
 #pragma unroll
-        for (int i = 0; i < HC; ++i) S.X[(cb + i) * XS + r] = wb[i];
-    if (vecl)
+        for (int q = 0; q < HC; ++q) S.A[q * NX + r] = w[q];
+    if (ul)
 #pragma unroll
-        for (int i = 0; i < HC; ++i) S.Qu[cb + i] = wb[i];
+        for (int q = 0; q < HC; ++q) S.d[q] = w[q];
     SFENCE();
-    // Gauss-Jordan: [Quu | Qux | Qu] -> [I | Quu^-1 Qux | Quu^-1 Qu]
-    unsigned long long bad = 0;  // ballot: convergent, so the PSD test stays in its step
-    static_for<NX>([&](auto J) {
-        constexpr int j = J, hj = j / HC, ij = j % HC;
-        if (r == j)
+    // PSD test (LDLT of Quu - 1e-9 I, SinglePhase.cpp:342-348): the decoupled diagonal, then
+    // every Gauss-Jordan pivot of the coupled block.  ballot is convergent, so each test stays
+    // in its step.
+    unsigned long long bad = __builtin_amdgcn_ballot_w64(ql && !(qzz > 1e-9));
+    // Gauss-Jordan on [Quu_cc | Qux_c | Qu_c] (one column per lane): pivot column j comes from
+    // lane 32 + j through SGPRs
+    static_for<HC>([&](auto J) {
+        constexpr int j = J;
+        double col[HC];
 #pragma unroll
-            for (int i = 0; i < HC; ++i) S.col[cb + i] = wa[i];
-        const double xa = other_half(wa[ij]), xb = other_half(wb[ij]);
-        HSYNC();
-        const bool own = hf == hj;
-        const double piv = S.col[j];
-        bad |= __builtin_amdgcn_ballot_w64(!(piv > 1e-9)); // PSD test
-        const double inv = 1.0 / piv;
-        const double fa = (own ? wa[ij] : xa) * inv, fb = (own ? wb[ij] : xb) * inv;
-        static_for<HC>([&](auto I) {
-            constexpr int i = I;
-            const double cq = S.col[cb + i];
-            const double na = wa[i] - cq * fa, nb = wb[i] - cq * fb;
-            if constexpr (i == ij) {
-                wa[i] = own ? fa : na;
-                wb[i] = own ? fb : nb;
-            } else {
-                wa[i] = na;
-                wb[i] = nb;
-            }
-        });
-        pin(wa);
-        pin(wb);
-        HSYNC();
+        for (int i = 0; i < HC; ++i) col[i] = lane_value(w[i], 32 + j);
+        const double piv = col[j];
+        bad |= __builtin_amdgcn_ballot_w64(!(piv > 1e-9));
+        const double f = w[j] * (1.0 / piv);
+#pragma unroll
+        for (int i = 0; i < HC; ++i)
+            if (i != j) w[i] -= col[i] * f;
+        w[j] = f;
+        pin(w);
         SFENCE();
     });
     live = live && bad == 0;
     if (!live) return;
-    // K = -Quu^-1 Qux, dU = -Quu^-1 Qu, G = Qx - Qux^T Quu^-1 Qu (wb = this half's rows of
-    // column r of Quu^-1 Qux, or of Quu^-1 Qu on the vector lane)
-    double gp = 0.0, dvp = 0.0;
+    // K = -Quu^-1 Qux, dU = -Quu^-1 Qu; K rows of decoupled controls are zero
+    if (xl)
 #pragma unroll
-    for (int i = 0; i < HC; ++i) {
-        const double qu = S.Qu[cb + i];
-        gp += wb[i] * qu;
-        dvp += qu * wb[i];
-    }
-    gp += other_half(gp);
-    dvp += other_half(dvp);
-    if (rowl) {
-        double *Kg = d.K + kq * NN;
+        for (int q = 0; q < HC; ++q) S.A[OFF_KP + q * NX + r] = w[q];
+    if (ul)
 #pragma unroll
-        for (int i = 0; i < HC; ++i) Kg[(cb + i) * NX + r] = -wb[i];
+        for (int q = 0; q < HC; ++q) S.wqu[q] = w[q];
+    double *dUg = d.dU + kq * NX;
+    if (xl) {
+        double *Kg = d.K + kq * NN + r;
+        static_for<HC>([&](auto I) {
+            constexpr int q = I;
+            const bool st = pc.c[q / 3] != 0;
+            Kg[(st ? q : HC + q) * NX] = -w[q];
+            Kg[(st ? HC + q : q) * NX] = 0.0;
+        });
     }
-    if (vecl) {
-        double *dUg = d.dU + kq * NX;
+    if (ul)
+        static_for<HC>([&](auto I) {
+            constexpr int q = I;
+            dUg[pc.c[q / 3] ? q : HC + q] = -w[q];
+        });
+    double dvp = 0.0;
+    if (ql) {
+        const double duz = quz / qzz;
+        dUg[pick4(pc.c, r / 3) ? HC + r : r] = -duz;
+        dvp = quz * duz;
+    }
+    HSYNC();
+    if (ul)
 #pragma unroll
-        for (int i = 0; i < HC; ++i) dUg[cb + i] = -wb[i];
-    }
-    const double dvk = __shfl(dvp, NX);
+        for (int q = 0; q < HC; ++q) dvp += S.d[q] * w[q];
+    // expected cost change Qu^T Quu^-1 Qu (SinglePhase.cpp:357-358): half 1 holds every term
+    const double dvk = lane_value(half_sum(dvp), 32);
     dV1 -= dvk;
     dV2 += dvk;
+    // G = Qx - Qux_c^T Quu_cc^-1 Qu_c, H = Qxx - Qux_c^T Quu_cc^-1 Qux_c (SinglePhase.cpp:359-361)
+    const int rr = rowl ? r : 0;
+    double gp = 0.0;
+#pragma unroll
+    for (int q = 0; q < HC; ++q) gp += S.A[q * NX + rr] * S.wqu[q];
     g = rowl ? qx - gp : 0.0;
-    SFENCE();
-    // H = Qxx - Qux^T Quu^-1 Qux: rows j of this half use wb, rows of the other half its copy
     double acc[HC];
 #pragma unroll
     for (int i = 0; i < HC; ++i) acc[i] = 0.0;
-    const int ob = HC - cb;
-    static_for<HC>([&](auto J) {
-        constexpr int jj = J;
-        const double ko = other_half(wb[jj]);
+    static_for<HC>([&](auto Q) {
+        constexpr int q = Q;
+        const double qr = S.A[q * NX + rr];
 #pragma unroll
-        for (int i = 0; i < HC; ++i) acc[i] += wb[jj] * S.X[(cb + jj) * XS + cb + i];
-#pragma unroll
-        for (int i = 0; i < HC; ++i) acc[i] += ko * S.X[(ob + jj) * XS + cb + i];
+        for (int i = 0; i < HC; ++i) acc[i] += qr * S.A[OFF_KP + q * NX + cb + i];
         pin(acc);
         SFENCE();
     });
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
         const int c = cb + i;
-        h[i] = rowl ? S.u.qp[r <= c ? tri(r, c) : tri(c, r)] - acc[i] : 0.0;
+        h[i] = rowl ? S.Bm[r <= c ? tri(r, c) : tri(c, r)] - acc[i] : 0.0;
     }
     HSYNC();
 }
@@ -485,22 +485,22 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double 
             const double *Px = rec + TM_PX;
             if (rowl)
 #pragma unroll
-                for (int c = 0; c < HC; ++c) S.X[r * XS + cb + c] = h[c];
-            if (lane < NX) S.col[lane] = g;
+                for (int c = 0; c < HC; ++c) S.A[r * XS + cb + c] = h[c];
+            if (lane < NX) S.Gn[lane] = g;
             HSYNC();
             double w[HC];
 #pragma unroll
             for (int c = 0; c < HC; ++c) w[c] = 0.0;
             if (rowl)
                 for (int k = 0; k < NX; ++k) {
-                    const double hk = S.X[r * XS + k];
+                    const double hk = S.A[r * XS + k];
 #pragma unroll
                     for (int c = 0; c < HC; ++c) w[c] += hk * Px[k * NX + cb + c];
                 }
             HSYNC();
             if (rowl)
 #pragma unroll
-                for (int c = 0; c < HC; ++c) S.X[r * XS + cb + c] = w[c];
+                for (int c = 0; c < HC; ++c) S.A[r * XS + cb + c] = w[c];
             HSYNC();
             double gp = 0.0;
 #pragma unroll
@@ -508,9 +508,9 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double 
             if (rowl)
                 for (int j = 0; j < NX; ++j) {
                     const double pj = Px[j * NX + r];
-                    gp += pj * S.col[j];
+                    gp += pj * S.Gn[j];
 #pragma unroll
-                    for (int c = 0; c < HC; ++c) w[c] += pj * S.X[j * XS + cb + c];
+                    for (int c = 0; c < HC; ++c) w[c] += pj * S.A[j * XS + cb + c];
                 }
 #pragma unroll
             for (int c = 0; c < HC; ++c) h[c] = rowl ? rec[TM_PHIXX + r * NX + cb + c] + w[c] : 0.0;
@@ -523,11 +523,11 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double 
             bwd_knot(p, d, S, pc, b, s0 + k, k0 + k, reg, live, h, g, dV1, dV2);
         if (!live) return false;
         // G[0] += H[0] Defect[0] (SinglePhase.cpp:365)
-        if (lane < NX) S.col[lane] = d.Defect[(b * p.S + s0) * NX + lane];
+        if (lane < NX) S.d[lane] = d.Defect[(b * p.S + s0) * NX + lane];
         HSYNC();
         double a = 0.0;
 #pragma unroll
-        for (int c = 0; c < HC; ++c) a += h[c] * S.col[cb + c];
+        for (int c = 0; c < HC; ++c) a += h[c] * S.d[cb + c];
         a += other_half(a);
         if (rowl) g += a;
         HSYNC();
