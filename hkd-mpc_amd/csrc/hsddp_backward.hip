@@ -306,54 +306,41 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     }
     pin(qxx);
     SFENCE();
+    // Every lane evaluates all three column roles and selects its own: the two halves would run
+    // both sides of a divergent branch anyway, and straight-line code keeps the register
+    // allocator from spilling live values around the branches.
     double w[HC];
-    double quz = 0.0, qzz = 1.0;  // decoupled control z(r) on the ql lanes: Qu_z, Quu_zz
-    if (hf == 0) {
+    const int rx = xl ? r : 0;  // row of T_c on the Qux lanes
+    const int rq = ql ? r : 0;  // column of T_c on the Quu lanes
+    const int lr = rq / 3, ar = rq % 3;
+    static_for<HC>([&](auto I) {
+        constexpr int q = I, l = q / 3, a = q % 3;
+        const bool st = pc.c[l] != 0;
         // (A^T T_c)[r][q] = T_c[r][q] + sum_j S[j][r] T_c[j][q]: row r of Qux_c^T
-        const int rr = xl ? r : 0;
-        static_for<HC>([&](auto I) {
-            constexpr int q = I;
-            double a = 0.0;
+        double ax = 0.0;
 #pragma unroll
-            for (int j = 0; j < 9; ++j) a += sc[j] * S.Bm[j * HC + q];
-            w[q] = xl ? S.Bm[rr * HC + q] + a : 0.0;
-        });
-    } else if (ql) {
-        // column r of Quu_cc = luu + B_c^T T_c + reg I
-        const int lr = r / 3, ar = r % 3;
-        static_for<HC>([&](auto I) {
-            constexpr int q = I, l = q / 3, a = q % 3;
-            double v, lu;
-            if (pc.c[l]) {
-                v = lqs[LQ_BW + q] * S.Bm[6 * HC + r] + lqs[LQ_BW + 12 + q] * S.Bm[7 * HC + r] +
-                    lqs[LQ_BW + 24 + q] * S.Bm[8 * HC + r] + pc.bv[l] * S.Bm[(9 + a) * HC + r];
-                // ReB Hessian block of leg l, stored (00,01,02,11,12,22)
-                const int lo = a < ar ? a : ar, hi = a < ar ? ar : a;
-                const double rb = lq[LQ_RB + 6 * l + (lo == 0 ? hi : lo == 1 ? 2 + hi : 5)];
-                lu = (q == r ? dt * p.r_grf : 0.0) + (lr == l ? rb : 0.0);
-            } else {
-                v = pc.bq[l] * S.Bm[(HC + q) * HC + r];
-                lu = q == r ? dt * p.r_qJd : 0.0;
-            }
-            w[q] = lu + v + (q == r ? reg : 0.0);
-        });
-        const bool st = pick4(pc.c, lr) != 0;
-        qzz = dt * (st ? p.r_qJd : p.r_grf) + reg;
-        quz = lq[LQ_LU + (st ? HC + r : r)];
-    } else if (ul) {
+        for (int j = 0; j < 9; ++j) ax += sc[j] * S.Bm[j * HC + q];
+        const double vx = S.Bm[rx * HC + q] + ax;
+        // column r of Quu_cc = luu + B_c^T T_c + reg I (ReB block stored (00,01,02,11,12,22))
+        const double vs = lqs[LQ_BW + q] * S.Bm[6 * HC + rq] + lqs[LQ_BW + 12 + q] * S.Bm[7 * HC + rq] +
+                          lqs[LQ_BW + 24 + q] * S.Bm[8 * HC + rq] + pc.bv[l] * S.Bm[(9 + a) * HC + rq];
+        const double vw = pc.bq[l] * S.Bm[(HC + q) * HC + rq];
+        const int lo = min(a, ar), hi = max(a, ar);
+        const double rb = lq[LQ_RB + 6 * l + (lo == 0 ? hi : lo == 1 ? 2 + hi : 5)];
+        const double lu = st ? (q == rq ? dt * p.r_grf : 0.0) + (lr == l ? rb : 0.0) : (q == rq ? dt * p.r_qJd : 0.0);
+        const double vu = lu + (st ? vs : vw) + (q == rq ? reg : 0.0);
         // Qu_c = lu_c + B_c^T Gnext
-        static_for<HC>([&](auto I) {
-            constexpr int q = I, l = q / 3, a = q % 3;
-            if (pc.c[l])
-                w[q] = lqs[LQ_LU + q] + (lqs[LQ_BW + q] * S.Gn[6] + lqs[LQ_BW + 12 + q] * S.Gn[7] +
-                                         lqs[LQ_BW + 24 + q] * S.Gn[8] + pc.bv[l] * S.Gn[9 + a]);
-            else
-                w[q] = lqs[LQ_LU + HC + q] + pc.bq[l] * S.Gn[HC + q];
-        });
-    } else {
-#pragma unroll
-        for (int q = 0; q < HC; ++q) w[q] = 0.0;
-    }
+        const double vg = st ? lqs[LQ_LU + q] + (lqs[LQ_BW + q] * S.Gn[6] + lqs[LQ_BW + 12 + q] * S.Gn[7] +
+                                                 lqs[LQ_BW + 24 + q] * S.Gn[8] + pc.bv[l] * S.Gn[9 + a])
+                             : lqs[LQ_LU + HC + q] + pc.bq[l] * S.Gn[HC + q];
+        w[q] = xl ? vx : ql ? vu : ul ? vg : 0.0;
+        asm volatile("" : "+v"(w[q]));
+        SFENCE();
+    });
+    // decoupled control z(r) on the ql lanes: Qu_z, Quu_zz
+    const bool stz = pick4(pc.c, lr) != 0;
+    const double qzz = dt * (stz ? p.r_qJd : p.r_grf) + reg;
+    const double quz = lq[LQ_LU + (stz ? HC + rq : rq)];
     pin(w);
     HSYNC();
     SFENCE();
@@ -457,7 +444,8 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
         const int c = cb + i;
-        h[i] = rowl ? S.Bm[r <= c ? tri(r, c) : tri(c, r)] - acc[i] : 0.0;
+        const double q = S.Bm[tri(min(rr, c), max(rr, c))];
+        h[i] = rowl ? q - acc[i] : 0.0;
     }
     HSYNC();
 }
