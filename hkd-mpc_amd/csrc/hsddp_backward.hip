@@ -191,6 +191,20 @@ DEV void s_column(const double *lq, double dt, int r, double *sc)
     for (int j = 0; j < 3; ++j) sc[6 + j] = q >= 0 ? lq[LQ_SW + 17 * j + q] : 0.0;
 }
 
+// one knot's LQ record (LQW doubles) and a 24-vector from global memory into LDS: every load is
+// issued before the first store, so the wave waits for one memory round trip, not four
+DEV void stage_knot_inputs(double *lq_lds, const double *lq_g, double *v_lds, const double *v_g, int lane)
+{
+    static_assert(LQW > 128 && LQW <= 192, "three loads per lane");
+    const double a0 = lq_g[lane], a1 = lq_g[64 + lane];
+    const double a2 = lane < LQW - 128 ? lq_g[128 + lane] : 0.0;
+    const double v = lane < NX ? v_g[lane] : 0.0;
+    lq_lds[lane] = a0;
+    lq_lds[64 + lane] = a1;
+    if (lane < LQW - 128) lq_lds[128 + lane] = a2;
+    if (lane < NX) v_lds[lane] = v;
+}
+
 DEV double half_sum(double v)
 {
 #pragma unroll
@@ -227,8 +241,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     const size_t kq = b * p.Kc + kc;
     cdouble *lqs = uniform_ptr(d.lq + kq * LQW);
     double *lq = S.A;  // LDS copy for lane-indexed reads
-    for (int q = lane; q < LQW; q += 64) lq[q] = d.lq[kq * LQW + q];
-    if (lane < NX) S.d[lane] = d.Defect[(b * p.S + s + 1) * NX + lane];
+    stage_knot_inputs(lq, d.lq + kq * LQW, S.d, d.Defect + (b * p.S + s + 1) * NX, lane);
     HSYNC();
     // Gnext = G + H Defect[k+1] (SinglePhase.cpp:320)
     double part = 0.0;
@@ -282,7 +295,9 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     HSYNC();
     SFENCE();
     // Qx, Qxx = lxx + A^T M, and the coupled blocks Qux_c, Quu_cc, Qu_c
-    // (SinglePhase.cpp:323-327; regularisation on both diagonals, MultiPhaseDDP.cpp:160)
+    // (SinglePhase.cpp:323-327; regularisation on both diagonals, MultiPhaseDDP.cpp:160).
+    // The lane-indexed LQ entries are read first; the LQ copy's LDS then takes the Qxx rows,
+    // so Qxx never occupies registers.
     double sc[9];
     s_column(lq, dt, r, sc);
     double qx = 0.0;
@@ -292,7 +307,20 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         for (int j = 0; j < 9; ++j) a += sc[j] * S.Gn[j];
         qx = lq[LQ_LX + r] + (gn + a);
     }
-    double qxx[HC];
+    const int rx = xl ? r : 0;  // row of T_c on the Qux lanes
+    const int rq = ql ? r : 0;  // column of T_c on the Quu lanes
+    const int lr = rq / 3, ar = rq % 3;
+    double rb3[3];              // row ar of leg lr's ReB Hessian block, stored (00,01,02,11,12,22)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const int lo = min(a, ar), hi = max(a, ar);
+        rb3[a] = lq[LQ_RB + 6 * lr + (lo == 0 ? hi : lo == 1 ? 2 + hi : 5)];
+    }
+    // decoupled control z(r) on the ql lanes: Qu_z, Quu_zz
+    const bool stz = pick4(pc.c, lr) != 0;
+    const double qzz = dt * (stz ? p.r_qJd : p.r_grf) + reg;
+    const double quz = lq[LQ_LU + (stz ? HC + rq : rq)];
+    HSYNC();
     {
         LxxRow lx_;
         lxx_row(p, pc, r, lx_);
@@ -301,18 +329,15 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
             double a = 0.0;
 #pragma unroll
             for (int j = 0; j < 9; ++j) a += sc[j] * S.Bm[OFF_M9 + j * NX + cb + i];
-            qxx[i] = lxx_half<i>(lx_, r, hf) + (m[i] + a) + (cb + i == r ? reg : 0.0);
+            const double v = lxx_half<i>(lx_, r, hf) + (m[i] + a) + (cb + i == r ? reg : 0.0);
+            if (rowl) S.A[r * XS + cb + i] = v;
         });
     }
-    pin(qxx);
     SFENCE();
     // Every lane evaluates all three column roles and selects its own: the two halves would run
     // both sides of a divergent branch anyway, and straight-line code keeps the register
     // allocator from spilling live values around the branches.
     double w[HC];
-    const int rx = xl ? r : 0;  // row of T_c on the Qux lanes
-    const int rq = ql ? r : 0;  // column of T_c on the Quu lanes
-    const int lr = rq / 3, ar = rq % 3;
     static_for<HC>([&](auto I) {
         constexpr int q = I, l = q / 3, a = q % 3;
         const bool st = pc.c[l] != 0;
@@ -321,13 +346,12 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
 #pragma unroll
         for (int j = 0; j < 9; ++j) ax += sc[j] * S.Bm[j * HC + q];
         const double vx = S.Bm[rx * HC + q] + ax;
-        // column r of Quu_cc = luu + B_c^T T_c + reg I (ReB block stored (00,01,02,11,12,22))
+        // column r of Quu_cc = luu + B_c^T T_c + reg I
         const double vs = lqs[LQ_BW + q] * S.Bm[6 * HC + rq] + lqs[LQ_BW + 12 + q] * S.Bm[7 * HC + rq] +
                           lqs[LQ_BW + 24 + q] * S.Bm[8 * HC + rq] + pc.bv[l] * S.Bm[(9 + a) * HC + rq];
         const double vw = pc.bq[l] * S.Bm[(HC + q) * HC + rq];
-        const int lo = min(a, ar), hi = max(a, ar);
-        const double rb = lq[LQ_RB + 6 * l + (lo == 0 ? hi : lo == 1 ? 2 + hi : 5)];
-        const double lu = st ? (q == rq ? dt * p.r_grf : 0.0) + (lr == l ? rb : 0.0) : (q == rq ? dt * p.r_qJd : 0.0);
+        const double lu =
+            st ? (q == rq ? dt * p.r_grf : 0.0) + (lr == l ? rb3[a] : 0.0) : (q == rq ? dt * p.r_qJd : 0.0);
         const double vu = lu + (st ? vs : vw) + (q == rq ? reg : 0.0);
         // Qu_c = lu_c + B_c^T Gnext
         const double vg = st ? lqs[LQ_LU + q] + (lqs[LQ_BW + q] * S.Gn[6] + lqs[LQ_BW + 12 + q] * S.Gn[7] +
@@ -337,23 +361,13 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         asm volatile("" : "+v"(w[q]));
         SFENCE();
     });
-    // decoupled control z(r) on the ql lanes: Qu_z, Quu_zz
-    const bool stz = pick4(pc.c, lr) != 0;
-    const double qzz = dt * (stz ? p.r_qJd : p.r_grf) + reg;
-    const double quz = lq[LQ_LU + (stz ? HC + rq : rq)];
-    pin(w);
     HSYNC();
-    SFENCE();
     // Qxx = (Qxx + Qxx^T) / 2 (SinglePhase.cpp:352), kept in LDS as a packed upper triangle
-    if (rowl)
-#pragma unroll
-        for (int i = 0; i < HC; ++i) S.A[r * XS + cb + i] = qxx[i];
-    HSYNC();
     if (rowl)
 #pragma unroll
         for (int i = 0; i < HC; ++i) {
             const int c = cb + i;
-            const double q = (qxx[i] + S.A[c * XS + r]) / 2;
+            const double q = (S.A[r * XS + c] + S.A[c * XS + r]) / 2;
             if (r <= c) S.Bm[tri(r, c)] = q;
         }
     HSYNC();
@@ -614,8 +628,8 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
 #pragma unroll
             for (int c = 0; c < HC; ++c) krow[c] = d.K[kq * NN + rr * NX + cb + c];
             const double dUr = d.dU[kq * NX + rr];
-            for (int q = lane; q < LQW; q += 64) S.lq[q] = d.lq[kq * LQW + q];
-            if (lane < NX) { S.d[lane] = d.Defect[(b * p.S + s + 1) * NX + lane]; S.dx[lane] = dx; }
+            stage_knot_inputs(S.lq, d.lq + kq * LQW, S.d, d.Defect + (b * p.S + s + 1) * NX, lane);
+            if (lane < NX) S.dx[lane] = dx;
             HSYNC();
             double kd = 0.0;
 #pragma unroll
