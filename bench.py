@@ -31,29 +31,19 @@ UNIT = "trajectory-iterations/s"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
-def backward_bytes_per_element(S: int, Kc: int, P: int) -> int:
-    """Algorithmic HBM bytes k_backward moves per element per launch (one successful sweep).
-
-    per control knot: backward r lq 174 + Defect 24, w K 576 + dU 24;
-                      linear rollout r K 576 + lq 174 + Defect 24 + dU 24, w du 24 + dX 24
-                      -> 1644 doubles;
-    per phase:        r Phix 24 + Phixx 576 (twice: sweep and rollout), Defect[s0] 24 (twice),
-                      r Px 576 (twice) for phases with a successor, w dX[s0] 24;
-    per element:      r slot_cost + slot_feas (2 S).
-    """
-    per_knot = 1644
-    per_phase = 2 * (24 + 576) + 2 * 24 + 24
-    per_boundary = 2 * 576
-    return 8 * (Kc * per_knot + P * per_phase + (P - 1) * per_boundary + 2 * S)
+# algorithmic bytes per knot per DDP iteration of the BWD pass (r A, B, l*, Defect
+# 2952 fp64; w K, dU 600 fp64) — the per-unit figure the roofline is quoted on.  One k_riccati
+# launch processes every control knot of every element once.
+BWD_BYTES_PER_KNOT = 8 * (2952 + 600)
 
 
 def load_traffic(cfg_key: str):
-    """HBM bytes per k_backward launch from the committed rocprofv3 PMC summary (or None)."""
-    path = os.path.join(ROOT, "profiles", "pmc_k_backward.json")
+    """Measured HBM bytes per k_riccati launch from the committed rocprofv3 PMC summary (or None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             data = json.load(f)
-        return data.get(cfg_key, {}).get("hbm_bytes_per_launch")
+        return data.get(cfg_key, {}).get("k_riccati", {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
 
@@ -135,8 +125,9 @@ def main():
 
     if rank == 0:
         S, Kc, P = prob["S"], prob["Kc"], len(prob["horizons"])
+        # k_riccati time from HIP events recorded around its launches on the solver's stream
         avg_bwd_ms = st.ms_backward / max(1, st.n_backward_launches)
-        bytes_launch = backward_bytes_per_element(S, Kc, P) * B
+        bytes_launch = BWD_BYTES_PER_KNOT * Kc * B
         achieved = bytes_launch / (avg_bwd_ms * 1e-3) / 1e9
         cfg_key = f"{args.gait}_{args.phases}x{args.knots}_b{B}"
         traffic = load_traffic(cfg_key)
@@ -150,7 +141,7 @@ def main():
                                    f"batch={B} per GPU (BASELINE metric config)",
                        "global_batch": B * world, "batch_per_gpu": B, "phases": args.phases,
                        "knots_per_phase": args.knots, "nx": 24, "nu": 24, "parallelism": f"shard{world}"},
-            "roofline": {"bound": "hbm", "kernel": "k_backward", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": "k_riccati", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch,
                          "avg_launch_ms": avg_bwd_ms},
@@ -158,6 +149,7 @@ def main():
                       "mean_ls_trials": total_ls / max(1.0, total_iters),
                       "device_ms_per_step": {"total": st.ms_total / args.steps, "lq": st.ms_lq / args.steps,
                                              "backward": st.ms_backward / args.steps,
+                                             "linear_rollout": st.ms_linear / args.steps,
                                              "forward_ls": st.ms_forward / args.steps},
                       "all_costs_finite": finite, "device_bytes": solver.device_bytes()},
         }

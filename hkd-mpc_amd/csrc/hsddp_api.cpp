@@ -396,7 +396,7 @@ namespace {
 struct Timer {
     hipStream_t st;
     bool on;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[4];
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[5];  // lq, riccati, forward, other, linear
     void begin(int cat, hipEvent_t &e0)
     {
         if (!on) return;
@@ -481,8 +481,13 @@ static void iteration_launches(hsddp_handle h, const std::vector<double> &trials
     tm.end(0, e0);
     tm.begin(1, e0);
     if (h->backward_v1) launch_backward_v1(p, d, st);
-    else launch_backward(p, d, st);
+    else launch_riccati(p, d, st);
     tm.end(1, e0);
+    if (!h->backward_v1) {
+        tm.begin(4, e0);
+        launch_lin_rollout(p, d, st);
+        tm.end(4, e0);
+    }
     tm.begin(2, e0);
     for (size_t t = 0; t < trials.size(); ++t) {
         launch_rollout(p, d, trials[t], 0, st);
@@ -519,6 +524,7 @@ static int finish_stats(hsddp_handle h, Timer &tm, hipEvent_t e0, hsddp_stats *s
     stats->ms_backward = tm.total(1);
     stats->ms_forward = tm.total(2);
     stats->ms_other = tm.total(3);
+    stats->ms_linear = tm.total(4);
     stats->inner_iterations = iters;
     stats->outer_iterations = outers;
     stats->n_backward_launches = nbwd;

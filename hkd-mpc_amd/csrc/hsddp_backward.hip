@@ -713,9 +713,13 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
     }
 }
 
-void launch_backward(const Params &p, const Bufs &d, hipStream_t st)
+void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
 {
     hipLaunchKernelGGL(k_riccati, dim3(p.B), dim3(64), 0, st, p, d);
+}
+
+void launch_lin_rollout(const Params &p, const Bufs &d, hipStream_t st)
+{
     hipLaunchKernelGGL(k_lin_rollout, dim3(p.B), dim3(64), 0, st, p, d);
 }
 

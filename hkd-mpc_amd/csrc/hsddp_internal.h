@@ -73,7 +73,8 @@ void launch_rollout(const Params &p, const Bufs &d, double eps, int init, hipStr
 void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, hipStream_t st);
 void launch_update_nominal(const Params &p, const Bufs &d, int init, hipStream_t st);
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st);
-void launch_backward(const Params &p, const Bufs &d, hipStream_t st);
+void launch_riccati(const Params &p, const Bufs &d, hipStream_t st);
+void launch_lin_rollout(const Params &p, const Bufs &d, hipStream_t st);
 void launch_backward_v1(const Params &p, const Bufs &d, hipStream_t st);
 void launch_outer_begin(const Params &p, const Bufs &d, hipStream_t st);
 void launch_reb_update(const Params &p, const Bufs &d, hipStream_t st);

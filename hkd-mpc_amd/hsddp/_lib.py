@@ -61,7 +61,7 @@ class Stats(C.Structure):
     _fields_ = [("inner_iterations", C.c_int), ("outer_iterations", C.c_int), ("ls_trials", C.c_longlong),
                 ("element_iterations", C.c_longlong), ("ms_total", C.c_double), ("ms_backward", C.c_double),
                 ("ms_lq", C.c_double), ("ms_forward", C.c_double), ("ms_other", C.c_double),
-                ("n_backward_launches", C.c_int)]
+                ("n_backward_launches", C.c_int), ("ms_linear", C.c_double)]
 
 
 class HSDDPError(RuntimeError):

@@ -118,9 +118,10 @@ typedef struct hsddp_stats {
     long long ls_trials;       /* line-search rollouts summed over elements */
     long long element_iterations; /* sum over elements of inner iterations (trajectory-iterations) */
     double ms_total;           /* device time of the solve (HIP events) */
-    double ms_backward;        /* device time in the backward Riccati + linear rollout kernel */
+    double ms_backward;        /* device time in the backward Riccati kernel (k_riccati) */
     double ms_lq, ms_forward, ms_other;
     int n_backward_launches;
+    double ms_linear;          /* device time in the linear rollout kernel (k_lin_rollout) */
 } hsddp_stats;
 
 typedef struct hsddp_handle_t *hsddp_handle;

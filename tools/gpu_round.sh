@@ -28,5 +28,9 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     cd /tmp && export TMPDIR=/tmp
     step rocprof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_trace" -o run -- \
         python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline
+    cd "$R"
+fi
+if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
+    bash "$R/tools/pmc.sh" || exit $?
 fi
 exit 0
