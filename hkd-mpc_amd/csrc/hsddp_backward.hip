@@ -101,6 +101,17 @@ DEV double lane_value(double v, int src)
     return __hiloint2double(hi, lo);
 }
 
+// 1 / x from the hardware reciprocal refined by two Newton steps (within an ulp of the IEEE
+// quotient; 5 VALU operations instead of the ~10 of a correctly rounded division)
+DEV double recip(double x)
+{
+    double r = __builtin_amdgcn_rcp(x);
+    double e = __builtin_fma(-x, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-x, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
 // value held by the same lane of the other half-wave (call with all 64 lanes active)
 DEV double other_half(double v)
 {
@@ -392,7 +403,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         for (int i = 0; i < HC; ++i) col[i] = lane_value(w[i], 32 + j);
         const double piv = col[j];
         bad |= __builtin_amdgcn_ballot_w64(!(piv > 1e-9));
-        const double f = w[j] * (1.0 / piv);
+        const double f = w[j] * recip(piv);
 #pragma unroll
         for (int i = 0; i < HC; ++i)
             if (i != j) w[i] -= col[i] * f;
