@@ -208,8 +208,18 @@ struct hsddp_handle_t {
     size_t bytes = 0;
     int Bref = 1;
     bool have_problem = false;
-    bool backward_v1 = false;  // HSDDP_BACKWARD=1 selects the first-generation kernel (A/B runs)
+    std::vector<int> contacts;  // host copy [B][P+1][4]: maps the compact K rows to controls
 };
+
+// control u of compact gain row q at control slot k of element b (KCW layout, hsddp_internal.h)
+static int coupled_control(hsddp_handle h, size_t b, size_t k, int q)
+{
+    const Params &p = h->p;
+    int i = 0;
+    while (i + 1 < p.P && (int)k >= p.k0[i + 1]) ++i;
+    const int c = h->contacts[(b * (p.P + 1) + i) * 4 + q / 3];
+    return c ? q : 12 + q;
+}
 
 template <typename T>
 static int dalloc(hsddp_handle h, T *&ptr, size_t n)
@@ -265,7 +275,6 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
     HIPCHK(hipSetDevice(desc->device));
     hsddp_handle h = new hsddp_handle_t();
     h->desc = *desc;
-    if (const char *e = std::getenv("HSDDP_BACKWARD")) h->backward_v1 = std::atoi(e) == 1;
     hsddp_default_options(&h->opt);
     Params &p = h->p;
     p.B = desc->batch;
@@ -288,7 +297,7 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         (rc = dalloc(h, d.Xbar, B * S * NX)) || (rc = dalloc(h, d.Defect, B * S * NX)) ||
         (rc = dalloc(h, d.Defect_bar, B * S * NX)) || (rc = dalloc(h, d.dX, B * S * NX)) ||
         (rc = dalloc(h, d.U, B * Kc * NX)) || (rc = dalloc(h, d.Ubar, B * Kc * NX)) || (rc = dalloc(h, d.dU, B * Kc * NX)) ||
-        (rc = dalloc(h, d.du, B * Kc * NX)) || (rc = dalloc(h, d.K, B * Kc * NN)) || (rc = dalloc(h, d.lq, B * Kc * LQW)) ||
+        (rc = dalloc(h, d.du, B * Kc * NX)) || (rc = dalloc(h, d.K, B * Kc * KCW)) || (rc = dalloc(h, d.lq, B * Kc * LQW)) ||
         (rc = dalloc(h, d.term, B * P * TW)) || (rc = dalloc(h, d.reb_delta, B * Kc * 20)) ||
         (rc = dalloc(h, d.reb_eps, B * Kc * 20)) || (rc = dalloc(h, d.al_sigma, B * P * 4)) ||
         (rc = dalloc(h, d.al_lambda, B * P * 4)) || (rc = dalloc(h, d.term_h, B * P * 4)) ||
@@ -357,11 +366,12 @@ extern "C" int hsddp_upload_problem(hsddp_handle h, const int *contacts, const d
         (rc = h2d((void *)h->d.ref_u, ref_u, Br * S * NX * sizeof(double), h->stream)) ||
         (rc = h2d((void *)h->d.ref_foot, ref_foot, Br * S * 12 * sizeof(double), h->stream)))
         return rc;
+    h->contacts.assign(contacts, contacts + B * (P + 1) * 4);
     // default warm start: Xbar = X = reference (HKDProblem.cpp:84-90), Ubar = U = 0, K = 0
-    for (size_t b = 0; b < B; ++b) {
-        const double *src = h->Bref == 1 ? h->d.ref_x : h->d.ref_x + b * S * NX;
-        HIPCHK(hipMemcpyAsync(h->d.Xbar + b * S * NX, src, S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
-    }
+    if (Br == 1) launch_broadcast(h->d.Xbar, h->d.ref_x, S * NX, B, h->stream);
+    else HIPCHK(hipMemcpyAsync(h->d.Xbar, h->d.ref_x, B * S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipMemsetAsync(h->d.Ubar, 0, B * p.Kc * NX * sizeof(double), h->stream));
+    HIPCHK(hipMemsetAsync(h->d.K, 0, B * p.Kc * KCW * sizeof(double), h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     h->have_problem = true;
     return hsddp_upload_warm_start(h, nullptr, nullptr, nullptr);
@@ -378,7 +388,17 @@ extern "C" int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const
     int rc;
     if (Xbar && (rc = h2d(d.Xbar, Xbar, B * S * NX * sizeof(double), h->stream))) return rc;
     if (Ubar && (rc = h2d(d.Ubar, Ubar, B * Kc * NX * sizeof(double), h->stream))) return rc;
-    if (K && (rc = h2d(d.K, K, B * Kc * NN * sizeof(double), h->stream))) return rc;
+    if (K) { // keep the 12 coupled rows of each knot's gain (KCW layout, hsddp_internal.h)
+        std::vector<double> kc(B * Kc * KCW);
+        for (size_t b = 0; b < B; ++b)
+            for (size_t k = 0; k < Kc; ++k)
+                for (int q = 0; q < 12; ++q) {
+                    const int u = coupled_control(h, b, k, q);
+                    std::memcpy(&kc[((b * Kc + k) * 12 + q) * NX], K + ((b * Kc + k) * NX + u) * NX, NX * sizeof(double));
+                }
+        if ((rc = h2d(d.K, kc.data(), B * Kc * KCW * sizeof(double), h->stream))) return rc;
+        HIPCHK(hipStreamSynchronize(h->stream));
+    }
     HIPCHK(hipMemcpyAsync(d.X, d.Xbar, B * S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(d.U, d.Ubar, B * Kc * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
     HIPCHK(hipMemsetAsync(d.dX, 0, B * S * NX * sizeof(double), h->stream));
@@ -480,14 +500,11 @@ static void iteration_launches(hsddp_handle h, const std::vector<double> &trials
     launch_lq(p, d, st);
     tm.end(0, e0);
     tm.begin(1, e0);
-    if (h->backward_v1) launch_backward_v1(p, d, st);
-    else launch_riccati(p, d, st);
+    launch_riccati(p, d, st);
     tm.end(1, e0);
-    if (!h->backward_v1) {
-        tm.begin(4, e0);
-        launch_lin_rollout(p, d, st);
-        tm.end(4, e0);
-    }
+    tm.begin(4, e0);
+    launch_lin_rollout(p, d, st);
+    tm.end(4, e0);
     tm.begin(2, e0);
     for (size_t t = 0; t < trials.size(); ++t) {
         launch_rollout(p, d, trials[t], 0, st);
@@ -624,9 +641,19 @@ extern "C" int hsddp_download_trajectory(hsddp_handle h, double *Xbar, double *U
     HIPCHK(hipStreamSynchronize(h->stream));
     const size_t B = h->p.B, S = h->p.S, Kc = h->p.Kc;
     int rc;
-    if ((rc = d2h(Xbar, h->d.Xbar, B * S * NX * 8)) || (rc = d2h(Ubar, h->d.Ubar, B * Kc * NX * 8)) ||
-        (rc = d2h(K, h->d.K, B * Kc * NN * 8)))
+    if ((rc = d2h(Xbar, h->d.Xbar, B * S * NX * 8)) || (rc = d2h(Ubar, h->d.Ubar, B * Kc * NX * 8)))
         return rc;
+    if (K) { // expand the coupled rows; the decoupled controls' rows are exactly zero
+        std::vector<double> kc(B * Kc * KCW);
+        if ((rc = d2h(kc.data(), h->d.K, B * Kc * KCW * 8))) return rc;
+        std::memset(K, 0, B * Kc * NN * sizeof(double));
+        for (size_t b = 0; b < B; ++b)
+            for (size_t k = 0; k < Kc; ++k)
+                for (int q = 0; q < 12; ++q) {
+                    const int u = coupled_control(h, b, k, q);
+                    std::memcpy(K + ((b * Kc + k) * NX + u) * NX, &kc[((b * Kc + k) * 12 + q) * NX], NX * sizeof(double));
+                }
+    }
     return HSDDP_OK;
 }
 

@@ -421,14 +421,10 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
 #pragma unroll
         for (int q = 0; q < HC; ++q) S.wqu[q] = w[q];
     double *dUg = d.dU + kq * NX;
-    if (xl) {
-        double *Kg = d.K + kq * NN + r;
-        static_for<HC>([&](auto I) {
-            constexpr int q = I;
-            const bool st = pc.c[q / 3] != 0;
-            Kg[(st ? q : HC + q) * NX] = -w[q];
-            Kg[(st ? HC + q : q) * NX] = 0.0;
-        });
+    if (xl) { // compact gain rows (KCW layout)
+        double *Kg = d.K + kq * KCW + r;
+#pragma unroll
+        for (int q = 0; q < HC; ++q) Kg[q * NX] = -w[q];
     }
     if (ul)
         static_for<HC>([&](auto I) {
@@ -632,12 +628,19 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
         LxxRow lx_;
         lxx_row(p, pc, r, lx_);
         const double ru = rowl ? p.dt * r_diag(p, r) : 0.0;
+        // control r has a gain row only when its B column is non-zero (KCW layout)
+        const bool stl = pick4(pc.c, (rr % HC) / 3) != 0;
+        const bool cpl = rowl && (rr < HC ? stl : !stl);
+        const size_t krow0 = (size_t)(rr % HC) * NX + cb;
         for (int k = 0; k < N; ++k) {
             const int s = s0 + k, kc = k0 + k;
             const size_t kq = b * p.Kc + kc;
             double krow[HC];
 #pragma unroll
-            for (int c = 0; c < HC; ++c) krow[c] = d.K[kq * NN + rr * NX + cb + c];
+            for (int c = 0; c < HC; ++c) krow[c] = 0.0;
+            if (cpl)
+#pragma unroll
+                for (int c = 0; c < HC; ++c) krow[c] = d.K[kq * KCW + krow0 + c];
             const double dUr = d.dU[kq * NX + rr];
             stage_knot_inputs(S.lq, d.lq + kq * LQW, S.d, d.Defect + (b * p.S + s + 1) * NX, lane);
             if (lane < NX) S.dx[lane] = dx;

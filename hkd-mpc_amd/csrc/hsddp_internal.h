@@ -3,7 +3,7 @@
 // HBM layout (element-major, fp64; b = element, s = state slot, kc = control slot):
 //   X, Xbar, Defect, Defect_bar, dX   [B][S][24]
 //   U, Ubar, dU, du                   [B][Kc][24]     du = dU + K dX (linear-rollout control step)
-//   K                                 [B][Kc][24][24] row-major
+//   K                                 [B][Kc][12][24] row-major, coupled controls only (below)
 //   lq                                [B][Kc][LQW]    compact LQ model of one knot (below)
 //   term                              [B][P][TW]      Phix | Phixx | Px (reset-map Jacobian at X_i[N])
 //   reb_delta, reb_eps                [B][Kc][20]     ReB params, index leg*5 + row
@@ -20,6 +20,11 @@ namespace hsddp {
 constexpr int NX = 24;
 constexpr int NN = 576;
 constexpr int MAXP = 16;
+// Gains are stored for the 12 controls whose B column is non-zero: row q (0..11) is control
+// u = q when leg q/3 is in stance, u = 12 + q when it swings.  The other 12 rows of the
+// reference's 24 x 24 K are exactly zero (hsddp_backward.hip, bwd_knot) and are expanded on
+// download.
+constexpr int KCW = 12 * 24;
 
 // compact LQ record per control slot
 constexpr int LQ_SE = 0;                 // 15  A - I, eul rows
@@ -75,13 +80,14 @@ void launch_update_nominal(const Params &p, const Bufs &d, int init, hipStream_t
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st);
 void launch_riccati(const Params &p, const Bufs &d, hipStream_t st);
 void launch_lin_rollout(const Params &p, const Bufs &d, hipStream_t st);
-void launch_backward_v1(const Params &p, const Bufs &d, hipStream_t st);
 void launch_outer_begin(const Params &p, const Bufs &d, hipStream_t st);
 void launch_reb_update(const Params &p, const Bufs &d, hipStream_t st);
 void launch_outer_end(const Params &p, const Bufs &d, hipStream_t st);
 void launch_reset_elements(const Params &p, const Bufs &d, hipStream_t st);
 void launch_init_params(const Params &p, const Bufs &d, hipStream_t st);
 void launch_count(const Params &p, const Bufs &d, int which, hipStream_t st);
+// dst[c][n] = src[n] for c < copies
+void launch_broadcast(double *dst, const double *src, size_t n, size_t copies, hipStream_t st);
 
 // model primitives
 void launch_model_dynamics(const double *x, const double *u, const double *c, double dt, double *xn, int n,

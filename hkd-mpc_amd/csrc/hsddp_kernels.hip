@@ -4,8 +4,10 @@
 // for B trajectories is:
 //   k_lq        knot-parallel  cost at (X, U) + compact LQ model   SinglePhase::compute_cost/LQ_approximation
 //   k_terminal  (elem, phase)  Phix, Phixx (+AL), reset Jacobian   SinglePhase.cpp:286-295; HKDReset.h:78-136
-//   k_backward  one wave/elem  regularised Riccati sweep over all phases + MS linear rollout
-//                              MultiPhaseDDP.cpp:141-229, 20-50; SinglePhase.cpp:144-178, 298-367
+//   k_riccati   one wave/elem  regularised Riccati sweep over all phases     (hsddp_backward.hip)
+//                              MultiPhaseDDP.cpp:141-229; SinglePhase.cpp:298-367
+//   k_lin_rollout one wave/elem  MS linear rollout + merit                    (hsddp_backward.hip)
+//                              MultiPhaseDDP.cpp:20-50, 309-318; SinglePhase.cpp:144-178
 //   k_rollout   knot-parallel  one line-search trial (all knots are shooting states)  SinglePhase.cpp:181-233
 //   k_decide    per element    merit acceptance (MultiPhaseDDP.cpp:113-133) + inner-loop exit tests
 //   k_update_nominal           Trajectory::update_nominal_vals (TrajectoryManagement.cpp:110-115)
@@ -177,455 +179,6 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
         double row[NX];
         hkd_resetmap_partial_row(sx, sc, scn, t, row);
         for (int j = 0; j < NX; ++j) rec[TM_PX + t * NX + j] = row[j];
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// k_backward: one 64-lane wave per element.  Regularised backward Riccati sweep over all phases
-// with impact-aware value transfer, then the multiple-shooting linear rollout.  24x24 blocks live
-// in LDS (row stride 25 doubles: column walks hit 32 distinct even banks).
-constexpr int LD = 25;
-constexpr int LDY = 26;
-
-struct BwdSmem {
-    double H[NX * LD], M[NX * LD], Q[NX * LD], Y[NX * LDY];
-    double G[NX], Gn[NX], Qx[NX], Qu[NX], dv[NX], lq[LQW + 2];
-    double red[64];
-    int contact[4];
-};
-
-DEV double S_at(const double *lq, double dt, int j, int c) // (A - I)[j][c]
-{
-    if (j < 3) { int q = se_index(c); return q >= 0 ? lq[LQ_SE + 5 * j + q] : 0.0; }
-    if (j < 6) return (c == j + 6) ? dt : 0.0;
-    if (j < 9) { int q = sw_index(c); return q >= 0 ? lq[LQ_SW + 17 * (j - 6) + q] : 0.0; }
-    return 0.0;
-}
-
-// (M)[r][c] = (H A)[r][c]
-DEV double HA_elem(const double *H, const double *lq, double dt, int r, int c)
-{
-    const double *h = H + r * LD;
-    double v = h[c];
-    int q = se_index(c);
-    if (q >= 0) v += h[0] * lq[LQ_SE + q] + h[1] * lq[LQ_SE + 5 + q] + h[2] * lq[LQ_SE + 10 + q];
-    if (c >= 9 && c < 12) v += h[c - 6] * dt;
-    q = sw_index(c);
-    if (q >= 0) v += h[6] * lq[LQ_SW + q] + h[7] * lq[LQ_SW + 17 + q] + h[8] * lq[LQ_SW + 34 + q];
-    return v;
-}
-
-// (S^T V)[r][c] for a row-major block V (stride ld): sum_j S[j][r] V[j][c]
-DEV double StV_elem(const double *V, int ld, const double *lq, double dt, int r, int c)
-{
-    double v = 0.0;
-    int q = se_index(r);
-    if (q >= 0) v += lq[LQ_SE + q] * V[c] + lq[LQ_SE + 5 + q] * V[ld + c] + lq[LQ_SE + 10 + q] * V[2 * ld + c];
-    if (r >= 9 && r < 12) v += dt * V[(r - 6) * ld + c];
-    q = sw_index(r);
-    if (q >= 0)
-        v += lq[LQ_SW + q] * V[6 * ld + c] + lq[LQ_SW + 17 + q] * V[7 * ld + c] + lq[LQ_SW + 34 + q] * V[8 * ld + c];
-    return v;
-}
-
-// (V B)[r][c] for row-major V: sum_j V[r][j] B[j][c]
-DEV double VB_elem(const double *V, int ld, const double *lq, const int *ct, double dt, int r, int c)
-{
-    const double *v = V + r * ld;
-    if (c < 12) {
-        int l = c / 3, m = c % 3;
-        return v[6] * lq[LQ_BW + c] + v[7] * lq[LQ_BW + 12 + c] + v[8] * lq[LQ_BW + 24 + c] +
-               v[9 + m] * (dt * ct[l] / kMass);
-    }
-    return v[c] * (dt * (1.0 - ct[(c - 12) / 3]));
-}
-
-// (B^T V)[r][c]: sum_j B[j][r] V[j][c]
-DEV double BtV_elem(const double *V, int ld, const double *lq, const int *ct, double dt, int r, int c)
-{
-    if (r < 12) {
-        int l = r / 3, m = r % 3;
-        return lq[LQ_BW + r] * V[6 * ld + c] + lq[LQ_BW + 12 + r] * V[7 * ld + c] + lq[LQ_BW + 24 + r] * V[8 * ld + c] +
-               (dt * ct[l] / kMass) * V[(9 + m) * ld + c];
-    }
-    return (dt * (1.0 - ct[(r - 12) / 3])) * V[r * ld + c];
-}
-
-DEV double lxx_elem(const Params &p, const int *ct, int r, int c)
-{
-    double v = 0.0;
-    if (r == c) v = p.dt * q_diag(p, ct, r);
-    // foot regularisation Hessian dt * D^T Qfoot D (HKDCost.cpp:32)
-    if (r >= 3 && r < 6 && c == r) {
-        for (int l = 0; l < 4; ++l) v += p.dt * ct[l] * ct[l] * foot_weight(p, ct, 3 * l + r - 3);
-    } else if (r >= 12 && c == r) {
-        int m = r - 12;
-        v += p.dt * ct[m / 3] * ct[m / 3] * foot_weight(p, ct, m);
-    } else if (r >= 3 && r < 6 && c >= 12 && (c - 12) % 3 == r - 3) {
-        int m = c - 12;
-        v -= p.dt * ct[m / 3] * ct[m / 3] * foot_weight(p, ct, m);
-    } else if (c >= 3 && c < 6 && r >= 12 && (r - 12) % 3 == c - 3) {
-        int m = r - 12;
-        v -= p.dt * ct[m / 3] * ct[m / 3] * foot_weight(p, ct, m);
-    }
-    return v;
-}
-
-DEV double luu_elem(const Params &p, const double *lq, int r, int c)
-{
-    double v = (r == c) ? p.dt * r_diag(p, r) : 0.0;
-    if (r < 12 && c < 12 && r / 3 == c / 3) {
-        int l = r / 3, a = r % 3, bb = c % 3;
-        if (a > bb) { int t = a; a = bb; bb = t; }
-        int idx = a == 0 ? bb : (a == 1 ? 2 + bb : 5);
-        v += lq[LQ_RB + 6 * l + idx];
-    }
-    return v;
-}
-
-DEV double wave_sum(double v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-// One knot of SinglePhase::backward_sweep.  Returns false when Quu fails the PSD test.
-DEV bool bwd_knot(const Params &p, const Bufs &d, BwdSmem &sm, int b, int s, int kc, double reg, double &dV1,
-                  double &dV2)
-{
-    const int t = threadIdx.x;
-    const double dt = p.dt;
-    const double *lqg = d.lq + ((size_t)b * p.Kc + kc) * LQW;
-    for (int j = t; j < LQW; j += 64) sm.lq[j] = lqg[j];
-    if (t < NX) sm.dv[t] = d.Defect[((size_t)b * p.S + s + 1) * NX + t];
-    __syncthreads();
-    // Gnext = G + H Defect[k+1]  (SinglePhase.cpp:317-320)
-    if (t < NX) {
-        double a = 0.0;
-        for (int c = 0; c < NX; ++c) a += sm.H[t * LD + c] * sm.dv[c];
-        sm.Gn[t] = sm.G[t] + a;
-    }
-    // M = H A, HB = H B (into Y)
-    for (int e = t; e < NN; e += 64) {
-        int r = e / NX, c = e % NX;
-        sm.M[r * LD + c] = HA_elem(sm.H, sm.lq, dt, r, c);
-        sm.Y[r * LDY + c] = VB_elem(sm.H, LD, sm.lq, sm.contact, dt, r, c);
-    }
-    __syncthreads();
-    // Qxx = lxx + A^T H A (into H), Quu = luu + B^T H B (into Q); Qx, Qu
-    for (int e = t; e < NN; e += 64) {
-        int r = e / NX, c = e % NX;
-        double qxx = lxx_elem(p, sm.contact, r, c) + (sm.M[r * LD + c] + StV_elem(sm.M, LD, sm.lq, dt, r, c));
-        sm.H[r * LD + c] = qxx + (r == c ? reg : 0.0);
-        double quu = luu_elem(p, sm.lq, r, c) + BtV_elem(sm.Y, LDY, sm.lq, sm.contact, dt, r, c);
-        sm.Q[r * LD + c] = quu + (r == c ? reg : 0.0);
-    }
-    if (t < NX) {
-        double a = 0.0;
-        int q = se_index(t);
-        if (q >= 0) a += sm.lq[LQ_SE + q] * sm.Gn[0] + sm.lq[LQ_SE + 5 + q] * sm.Gn[1] + sm.lq[LQ_SE + 10 + q] * sm.Gn[2];
-        if (t >= 9 && t < 12) a += dt * sm.Gn[t - 6];
-        q = sw_index(t);
-        if (q >= 0) a += sm.lq[LQ_SW + q] * sm.Gn[6] + sm.lq[LQ_SW + 17 + q] * sm.Gn[7] + sm.lq[LQ_SW + 34 + q] * sm.Gn[8];
-        sm.Qx[t] = sm.lq[LQ_LX + t] + (sm.Gn[t] + a);
-    } else if (t >= 32 && t < 32 + NX) {
-        int r = t - 32;
-        double a;
-        if (r < 12) {
-            int l = r / 3, m = r % 3;
-            a = sm.lq[LQ_BW + r] * sm.Gn[6] + sm.lq[LQ_BW + 12 + r] * sm.Gn[7] + sm.lq[LQ_BW + 24 + r] * sm.Gn[8] +
-                (dt * sm.contact[l] / kMass) * sm.Gn[9 + m];
-        } else {
-            a = (dt * (1.0 - sm.contact[(r - 12) / 3])) * sm.Gn[r];
-        }
-        sm.Qu[r] = sm.lq[LQ_LU + r] + a;
-    }
-    __syncthreads();
-    // Qux = B^T H A (into Y), Y[:,24] = Qu;  symmetrise Qxx (SinglePhase.cpp:352)
-    double qs[9];
-#pragma unroll
-    for (int q = 0; q < 9; ++q) {
-        int e = t + 64 * q, r = e / NX, c = e % NX;
-        sm.Y[r * LDY + c] = BtV_elem(sm.M, LD, sm.lq, sm.contact, dt, r, c);
-        qs[q] = (sm.H[r * LD + c] + sm.H[c * LD + r]) / 2;
-    }
-    if (t < NX) sm.Y[t * LDY + NX] = sm.Qu[t];
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 9; ++q) { int e = t + 64 * q, r = e / NX, c = e % NX; sm.H[r * LD + c] = qs[q]; }
-    // Cholesky Quu = L L^T (lower, in Q).  PSD test of the reference: Eigen LDLT of Quu - 1e-9 I
-    // must show no negative pivot (SinglePhase.cpp:342-348); here every Cholesky pivot of Quu must
-    // exceed 1e-9 (pivots of Quu dominate those of Quu - eps I by eps, so every Quu the reference
-    // accepts passes).
-    for (int j = 0; j < NX; ++j) {
-        double piv = sm.Q[j * LD + j];
-        if (!(piv > 1e-9)) return false; // wave-uniform
-        double dj = sqrt(piv), inv = 1.0 / dj;
-        __syncthreads();
-        if (t > j && t < NX) sm.Q[t * LD + j] *= inv;
-        if (t == j) sm.Q[j * LD + j] = dj;
-        __syncthreads();
-        const int m = NX - 1 - j;               // trailing size
-        for (int e = t; e < m * m; e += 64) {
-            int r = j + 1 + e / m, c = j + 1 + e % m;
-            if (c <= r) sm.Q[r * LD + c] -= sm.Q[r * LD + j] * sm.Q[c * LD + j];
-        }
-        __syncthreads();
-    }
-    // forward solve L Y = [Qux | Qu]
-    for (int j = 0; j < NX; ++j) {
-        if (t <= NX) sm.Y[j * LDY + t] /= sm.Q[j * LD + j];
-        __syncthreads();
-        const int m = NX - 1 - j;
-        for (int e = t; e < m * (NX + 1); e += 64) {
-            int r = j + 1 + e / (NX + 1), c = e % (NX + 1);
-            sm.Y[r * LDY + c] -= sm.Q[r * LD + j] * sm.Y[j * LDY + c];
-        }
-        __syncthreads();
-    }
-    // H = Qxx - Y^T Y, G = Qx - Y^T y, dV_k = y^T y
-    for (int e = t; e < NN; e += 64) {
-        int r = e / NX, c = e % NX;
-        double a = 0.0;
-        for (int j = 0; j < NX; ++j) a += sm.Y[j * LDY + r] * sm.Y[j * LDY + c];
-        sm.H[r * LD + c] -= a;
-    }
-    double yy = (t < NX) ? sm.Y[t * LDY + NX] * sm.Y[t * LDY + NX] : 0.0;
-    if (t < NX) {
-        double a = 0.0;
-        for (int j = 0; j < NX; ++j) a += sm.Y[j * LDY + t] * sm.Y[j * LDY + NX];
-        sm.G[t] = sm.Qx[t] - a;
-    }
-    double dVk = wave_sum(yy);
-    dV1 -= dVk;
-    dV2 += dVk;
-    __syncthreads();
-    // back-substitution L^T Z = Y -> K = -Z[:, :24], dU = -Z[:, 24]
-    for (int j = NX - 1; j >= 0; --j) {
-        if (t <= NX) sm.Y[j * LDY + t] /= sm.Q[j * LD + j];
-        __syncthreads();
-        for (int e = t; e < j * (NX + 1); e += 64) {
-            int r = e / (NX + 1), c = e % (NX + 1);
-            sm.Y[r * LDY + c] -= sm.Q[j * LD + r] * sm.Y[j * LDY + c];
-        }
-        __syncthreads();
-    }
-    double *Kg = d.K + ((size_t)b * p.Kc + kc) * NN;
-    for (int e = t; e < NN; e += 64) Kg[e] = -sm.Y[(e / NX) * LDY + e % NX];
-    if (t < NX) d.dU[((size_t)b * p.Kc + kc) * NX + t] = -sm.Y[t * LDY + NX];
-    __syncthreads();
-    return true;
-}
-
-// G += H v  for the phase-initial defect (SinglePhase.cpp:365)
-DEV void add_Hv(BwdSmem &sm, const double *vg)
-{
-    const int t = threadIdx.x;
-    if (t < NX) sm.dv[t] = vg[t];
-    __syncthreads();
-    if (t < NX) {
-        double a = 0.0;
-        for (int c = 0; c < NX; ++c) a += sm.H[t * LD + c] * sm.dv[c];
-        sm.G[t] += a;
-    }
-    __syncthreads();
-}
-
-// MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229)
-DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdSmem &sm, int b, double reg, double &dV1, double &dV2)
-{
-    const int t = threadIdx.x;
-    dV1 = 0.0; dV2 = 0.0;
-    for (int i = p.P - 1; i >= 0; --i) {
-        const double *rec = d.term + ((size_t)b * p.P + i) * TW;
-        if (t < 4) sm.contact[t] = d.contacts[((size_t)b * (p.P + 1) + i) * 4 + t];
-        if (i == p.P - 1) {
-            for (int e = t; e < NN; e += 64) sm.H[(e / NX) * LD + e % NX] = rec[TM_PHIXX + e];
-            if (t < NX) sm.G[t] = rec[TM_PHIX + t];
-        } else {
-            // impact-aware step: G' = Px^T G0, H' = Px^T H0 Px (MultiPhaseDDP.cpp:480-484)
-            for (int e = t; e < NN; e += 64) sm.Q[(e / NX) * LD + e % NX] = rec[TM_PX + e];
-            __syncthreads();
-            for (int e = t; e < NN; e += 64) {
-                int r = e / NX, c = e % NX;
-                double a = 0.0;
-                for (int j = 0; j < NX; ++j) a += sm.H[r * LD + j] * sm.Q[j * LD + c];
-                sm.M[r * LD + c] = a;
-            }
-            double gp = 0.0;
-            if (t < NX)
-                for (int j = 0; j < NX; ++j) gp += sm.Q[j * LD + t] * sm.G[j];
-            __syncthreads();
-            for (int e = t; e < NN; e += 64) {
-                int r = e / NX, c = e % NX;
-                double a = 0.0;
-                for (int j = 0; j < NX; ++j) a += sm.Q[j * LD + r] * sm.M[j * LD + c];
-                sm.H[r * LD + c] = rec[TM_PHIXX + e] + a;
-            }
-            if (t < NX) sm.G[t] = rec[TM_PHIX + t] + gp;
-        }
-        __syncthreads();
-        const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
-        double v1 = 0.0, v2 = 0.0;
-        for (int k = N - 1; k >= 0; --k)
-            if (!bwd_knot(p, d, sm, b, s0 + k, k0 + k, reg, v1, v2)) return false;
-        add_Hv(sm, d.Defect + ((size_t)b * p.S + s0) * NX);
-        dV1 += v1;
-        dV2 += v2;
-    }
-    return true;
-}
-
-// MultiPhaseDDP::linear_rollout(1.0) (MultiPhaseDDP.cpp:20-50, SinglePhase.cpp:144-178): writes dX
-// and du = dU + K dX (the control step of every later line-search trial).
-DEV void linear_rollout(const Params &p, const Bufs &d, BwdSmem &sm, int b, double &dV1, double &dV2)
-{
-    const int t = threadIdx.x;
-    const double dt = p.dt;
-    double *dx = sm.G, *du = sm.Gn, *tmp = sm.Qx; // reuse vectors
-    double v1 = 0.0, v2 = 0.0;
-    if (t < NX) dx[t] = 0.0;
-    __syncthreads();
-    for (int i = 0; i < p.P; ++i) {
-        const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
-        if (t < 4) sm.contact[t] = d.contacts[((size_t)b * (p.P + 1) + i) * 4 + t];
-        if (i > 0) { // dx_init = Px dX_end
-            const double *Px = d.term + ((size_t)b * p.P + (i - 1)) * TW + TM_PX;
-            double a = 0.0;
-            if (t < NX)
-                for (int j = 0; j < NX; ++j) a += Px[t * NX + j] * dx[j];
-            __syncthreads();
-            if (t < NX) dx[t] = a;
-        }
-        __syncthreads();
-        if (t < NX) {
-            dx[t] = dx[t] + d.Defect[((size_t)b * p.S + s0) * NX + t];
-            d.dX[((size_t)b * p.S + s0) * NX + t] = dx[t];
-        }
-        __syncthreads();
-        for (int k = 0; k < N; ++k) {
-            const int s = s0 + k, kc = k0 + k;
-            const double *Kg = d.K + ((size_t)b * p.Kc + kc) * NN;
-            const double *lqg = d.lq + ((size_t)b * p.Kc + kc) * LQW;
-            for (int j = t; j < NN; j += 64) sm.M[(j / NX) * LD + j % NX] = Kg[j];
-            for (int j = t; j < LQW; j += 64) sm.lq[j] = lqg[j];
-            if (t < NX) sm.dv[t] = d.Defect[((size_t)b * p.S + s + 1) * NX + t];
-            __syncthreads();
-            if (t < NX) {
-                double a = 0.0;
-                for (int c = 0; c < NX; ++c) a += sm.M[t * LD + c] * dx[c];
-                du[t] = d.dU[((size_t)b * p.Kc + kc) * NX + t] + a;
-            }
-            __syncthreads();
-            double nx = 0.0, q1 = 0.0, q2 = 0.0;
-            if (t < NX) {
-                // A dx + B du + Defect
-                double sdx = 0.0;
-                for (int j = 0; j < 9; ++j) sdx += S_at(sm.lq, dt, t, j) * dx[j];
-                for (int j = 9; j < NX; ++j) sdx += S_at(sm.lq, dt, t, j) * dx[j];
-                double bdu = 0.0;
-                if (t >= 6 && t < 9)
-                    for (int c = 0; c < 12; ++c) bdu += sm.lq[LQ_BW + 12 * (t - 6) + c] * du[c];
-                else if (t >= 9 && t < 12)
-                    for (int l = 0; l < 4; ++l) bdu += (dt * sm.contact[l] / kMass) * du[3 * l + t - 9];
-                else if (t >= 12)
-                    bdu = (dt * (1.0 - sm.contact[(t - 12) / 3])) * du[t];
-                nx = (dx[t] + sdx) + bdu + sm.dv[t];
-                // dV terms (quirk A3: overwrite, no 1/2, cross term once)
-                q1 = sm.lq[LQ_LX + t] * dx[t] + sm.lq[LQ_LU + t] * du[t];
-                double a = 0.0, bq = 0.0;
-                for (int c = 0; c < NX; ++c) a += lxx_elem(p, sm.contact, t, c) * dx[c];
-                for (int c = 0; c < NX; ++c) bq += luu_elem(p, sm.lq, t, c) * du[c];
-                q2 = dx[t] * a + du[t] * bq;
-            }
-            v1 += wave_sum(q1);
-            v2 += wave_sum(q2);
-            __syncthreads();
-            if (t < NX) {
-                d.du[((size_t)b * p.Kc + kc) * NX + t] = du[t];
-                d.dX[((size_t)b * p.S + s + 1) * NX + t] = nx;
-                dx[t] = nx;
-            }
-            __syncthreads();
-        }
-        const double *rec = d.term + ((size_t)b * p.P + i) * TW;
-        double q1 = 0.0, q2 = 0.0;
-        if (t < NX) {
-            q1 = rec[TM_PHIX + t] * dx[t];
-            double a = 0.0;
-            for (int c = 0; c < NX; ++c) a += rec[TM_PHIXX + t * NX + c] * dx[c];
-            q2 = dx[t] * a;
-        }
-        v1 += wave_sum(q1);
-        v2 += wave_sum(q2);
-        __syncthreads();
-    }
-    (void)tmp;
-    dV1 = v1;
-    dV2 = v2;
-}
-
-__global__ __launch_bounds__(64) void k_backward(Params p, Bufs d)
-{
-    const int b = blockIdx.x, t = threadIdx.x;
-    ElemState &E = d.el[b];
-    if (E.done || E.inner_done) return;
-    __shared__ BwdSmem sm;
-    // compute_cost + measure_dynamics_feasibility at the start of the inner iteration
-    // (MultiPhaseDDP.cpp:306-307): per-phase sums in reference order
-    if (t == 0) {
-        double cost = 0.0, feas = 0.0;
-        for (int i = 0; i < p.P; ++i) {
-            double ci = 0.0, fi = 0.0;
-            for (int k = 0; k < p.N[i]; ++k) ci += d.slot_cost[(size_t)b * p.S + p.s0[i] + k];
-            ci += d.slot_cost[(size_t)b * p.S + p.s0[i] + p.N[i]];
-            for (int k = 0; k <= p.N[i]; ++k) fi += d.slot_feas[(size_t)b * p.S + p.s0[i] + k];
-            cost += ci;
-            feas += fi;
-        }
-        sm.red[0] = cost;
-        sm.red[1] = sqrt(feas);
-    }
-    __syncthreads();
-    const double cost = sm.red[0], feas = sm.red[1];
-    double reg = E.reg;
-    double dV1 = 0.0, dV2 = 0.0;
-    bool ok = false;
-    // backward_sweep_regularized (MultiPhaseDDP.cpp:141-181)
-    while (true) {
-        ok = bwd_sweep(p, d, sm, b, reg, dV1, dV2);
-        __syncthreads();
-        if (ok) break;
-        reg = fmax(reg * p.update_regularization, 1e-03);
-        if (reg > 1e2) break;
-    }
-    reg = reg / 20;
-    if (reg < 1e-06) reg = 0;
-    if (t == 0) {
-        E.iters += 1;
-        E.cost = cost;
-        E.feas = feas;
-        E.reg = reg;
-        E.accepted = 0;
-    }
-    if (!ok) { // goto bad_solve
-        if (t == 0) { E.status = 1; E.done = 1; E.ls_active = 0; }
-        return;
-    }
-    linear_rollout(p, d, sm, b, dV1, dV2);
-    if (t == 0) {
-        double dV_abs = fabs(dV1 + 0.5 * dV2);
-        double rho = (feas > p.feas_thresh) ? dV_abs / ((1 - p.merit_scale) * feas) + p.merit_offset : 0;
-        double merit = cost + rho * feas;
-        E.dV1 = dV1; E.dV2 = dV2; E.merit_rho = rho; E.merit = merit;
-        E.cost_prev = cost; E.merit_prev = merit; E.feas_prev = feas;
-        if (!p.no_early_exit && dV_abs < p.cost_thresh && feas <= p.feas_thresh) {
-            E.inner_done = 1;
-            E.ls_active = 0;
-        } else {
-            E.ls_active = 1;
-        }
     }
 }
 
@@ -942,12 +495,18 @@ void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
     hipLaunchKernelGGL(k_lq, dim3(blocks_for((long)p.B * p.S, 256)), dim3(256), 0, st, p, d);
     hipLaunchKernelGGL(k_terminal, dim3(p.B * p.P), dim3(64), 0, st, p, d);
 }
-// first-generation backward kernel (one element per wave, Cholesky + triangular solves in LDS);
-// kept for A/B measurement against k_backward2 (hsddp_backward.hip), selected by HSDDP_BACKWARD=1
-void launch_backward_v1(const Params &p, const Bufs &d, hipStream_t st)
+
+__global__ __launch_bounds__(256) void k_broadcast(double *dst, const double *src, size_t n, size_t total)
 {
-    hipLaunchKernelGGL(k_backward, dim3(p.B), dim3(64), 0, st, p, d);
+    const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid < total) dst[gid] = src[gid % n];
 }
+void launch_broadcast(double *dst, const double *src, size_t n, size_t copies, hipStream_t st)
+{
+    const size_t total = n * copies;
+    if (total) hipLaunchKernelGGL(k_broadcast, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dst, src, n, total);
+}
+
 void launch_outer_begin(const Params &p, const Bufs &d, hipStream_t st)
 {
     hipLaunchKernelGGL(k_outer_begin, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);
