@@ -315,6 +315,7 @@ HKD_FN double hkd_foot_height_grad(int l, const double *x, double *hx)
 HKD_FN void hkd_resetmap(const double *x, const int *c, const int *cn, double *xn)
 {
     for (int j = 0; j < NX; ++j) xn[j] = x[j];
+#pragma unroll  // compile-time leg index keeps xn in registers on the device
     for (int l = 0; l < 4; ++l) {
         if (c[l] && !cn[l]) { xn[12 + 3 * l] = 0.0; xn[13 + 3 * l] = -0.8; xn[14 + 3 * l] = 1.7; }
         if (!c[l] && cn[l]) {

@@ -259,6 +259,10 @@ static void fill_params(hsddp_handle h)
     p.cost_thresh = o.cost_thresh; p.tconstr_thresh = o.tconstr_thresh; p.pconstr_thresh = o.pconstr_thresh;
     p.feas_thresh = o.dynamics_feas_thresh; p.merit_scale = o.merit_scale; p.merit_offset = o.merit_offset;
     p.AL_active = o.AL_active; p.ReB_active = o.ReB_active; p.no_early_exit = o.no_early_exit;
+    // With update_ReB = update_relax = 1 (the shipped settings) update_REB_params leaves every
+    // (delta, eps) at its initial value (ConstraintsBase.h:168-183): the kernels then read the two
+    // scalars instead of the per-knot arrays.
+    p.reb_uniform = o.update_ReB == 1.0 && o.update_relax == 1.0 && p.grf_delta >= p.grf_delta_min;
 }
 
 extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)

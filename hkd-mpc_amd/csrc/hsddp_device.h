@@ -85,12 +85,16 @@ DEV double running_cost(const Params &p, const int *c, const double *x, const do
     lf *= p.dt;
     double l = lt + lf;
     double rc = 0.0, mk = 0.0;
+    // unrolled: a runtime leg index into u would put the control vector in scratch
+#pragma unroll
     for (int lg = 0; lg < 4; ++lg) {
         if (!c[lg]) continue;
+#pragma unroll
         for (int r = 0; r < 5; ++r) {
             double g = grf_value(p.mu, r, u + 3 * lg);
             mk = fmin(mk, g);
-            rc += eps[5 * lg + r] * reb_cost(g, delta[5 * lg + r]);
+            const double e = p.reb_uniform ? p.grf_eps : eps[5 * lg + r];
+            rc += e * reb_cost(g, p.reb_uniform ? p.grf_delta : delta[5 * lg + r]);
         }
     }
     if (p.ReB_active && (c[0] + c[1] + c[2] + c[3]) > 0) l += p.dt * rc;
@@ -116,6 +120,7 @@ DEV double terminal_cost(const Params &p, const int *c, const int *cn, const dou
     }
     phi = phi + p.foot_term_cost * fc;
     double al = 0.0, tv = 0.0;
+#pragma unroll
     for (int l = 0; l < 4; ++l) {
         h_out[l] = 0.0;
         if (!touchdown(c, cn, l)) continue;

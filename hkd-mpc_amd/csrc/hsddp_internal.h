@@ -51,6 +51,7 @@ struct Params {
     double alpha, gamma, update_penalty, update_relax, update_regularization, update_ReB;
     double cost_thresh, tconstr_thresh, pconstr_thresh, feas_thresh, merit_scale, merit_offset;
     int AL_active, ReB_active, no_early_exit;
+    int reb_uniform;  // every ReB (delta, eps) equals (grf_delta, grf_eps): per-knot arrays not read
 };
 
 struct ElemState {

@@ -24,7 +24,7 @@ using namespace hkd;
 // ---------------------------------------------------------------------------------------------
 // k_lq: per (element, state slot): cost and |Defect|^2 at the current (X, U); compact LQ model at
 // control slots (SinglePhase::compute_cost + LQ_approximation, SinglePhase.cpp:235-296).
-__global__ __launch_bounds__(256) void k_lq(Params p, Bufs d)
+__global__ __launch_bounds__(256, 2) void k_lq(Params p, Bufs d)
 {
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long)p.B * p.S) return;
@@ -91,15 +91,17 @@ __global__ __launch_bounds__(256) void k_lq(Params p, Bufs d)
 #pragma unroll
     for (int j = 0; j < 24; ++j) rb[j] = 0.0;
     if (p.ReB_active) {
+#pragma unroll
         for (int lg = 0; lg < 4; ++lg) {
             if (!c[lg]) continue;
             double gu[3] = {0, 0, 0}, hu[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
             for (int r = 0; r < 5; ++r) {
                 double row[3], d1, d2;
                 grf_row(p.mu, r, row);
                 double g = row[0] * u[3 * lg] + row[1] * u[3 * lg + 1] + row[2] * u[3 * lg + 2];
-                reb_derivs(g, dl[5 * lg + r], d1, d2);
-                double e = ep[5 * lg + r];
+                reb_derivs(g, p.reb_uniform ? p.grf_delta : dl[5 * lg + r], d1, d2);
+                double e = p.reb_uniform ? p.grf_eps : ep[5 * lg + r];
                 for (int a = 0; a < 3; ++a) gu[a] += e * d1 * row[a];
                 hu[0] += e * (d2 * row[0] * row[0]); hu[1] += e * (d2 * row[0] * row[1]);
                 hu[2] += e * (d2 * row[0] * row[2]); hu[3] += e * (d2 * row[1] * row[1]);
@@ -246,6 +248,7 @@ __global__ __launch_bounds__(256) void k_rollout(Params p, Bufs d, double eps, i
         const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
         d.slot_cost[sb + s] = terminal_cost(p, c, cn, x, xr, pf, sg, lm, tv, h);
         d.slot_viol[sb + s] = tv;
+#pragma unroll
         for (int l = 0; l < 4; ++l) d.term_h[((size_t)b * p.P + i) * 4 + l] = h[l];
     } else {
         const int kc = p.k0[i] + k;
@@ -263,30 +266,40 @@ __global__ __launch_bounds__(256) void k_rollout(Params p, Bufs d, double eps, i
 }
 
 // k_decide: reductions of one trial + merit acceptance (MultiPhaseDDP.cpp:113-133) + the
-// later-termination test (:358).  One thread per element, reference summation order.
+// later-termination test (:358).  16 lanes per element, one per phase: each lane sums its phase's
+// slots in order, and the phase sums are added in phase order — the reference's summation order
+// (compute_cost, MultiPhaseDDP.cpp:431-440; SinglePhase.cpp:235-262).
 __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int last, int init)
 {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= p.B) return;
-    ElemState &E = d.el[b];
-    if (init ? E.done : !E.ls_active) return;
-    const size_t sb = (size_t)b * p.S;
-    double cost = 0.0, feas = 0.0, max_p = 0.0, max_t = 0.0;
+    const int lane = threadIdx.x, g = lane & 15, base = lane & ~15;
+    const int b = blockIdx.x * 4 + (lane >> 4);
+    const bool valid = b < p.B;
+    const ElemState *Ep = valid ? &d.el[b] : nullptr;
+    const bool act = valid && (init ? !Ep->done : Ep->ls_active);
+    double ci = 0.0, fi = 0.0, pv = 0.0, tv = 0.0;
     int div = 0;
-    for (int i = 0; i < p.P; ++i) {
-        double ci = 0.0, fi = 0.0, pv = 0.0;
-        const int s0 = p.s0[i];
-        for (int k = 0; k < p.N[i]; ++k) {
-            ci += d.slot_cost[sb + s0 + k];
-            pv = fmin(pv, d.slot_viol[sb + s0 + k]);
+    if (act && g < p.P) {
+        const size_t sb = (size_t)b * p.S + p.s0[g];
+        const int N = p.N[g];
+        for (int k = 0; k < N; ++k) {
+            ci += d.slot_cost[sb + k];
+            pv = fmin(pv, d.slot_viol[sb + k]);
         }
-        ci += d.slot_cost[sb + s0 + p.N[i]];
-        for (int k = 0; k <= p.N[i]; ++k) { fi += d.slot_feas[sb + s0 + k]; div |= d.slot_div[sb + s0 + k]; }
-        cost += ci;
-        feas += fi;
-        max_p = fmin(max_p, pv);
-        max_t = fmax(max_t, d.slot_viol[sb + s0 + p.N[i]]);
+        ci += d.slot_cost[sb + N];
+        for (int k = 0; k <= N; ++k) { fi += d.slot_feas[sb + k]; div |= d.slot_div[sb + k]; }
+        tv = d.slot_viol[sb + N];
     }
+    double cost = 0.0, feas = 0.0, max_p = 0.0, max_t = 0.0;
+    int dv = 0;
+    for (int i = 0; i < p.P; ++i) {
+        cost += __shfl(ci, base + i);
+        feas += __shfl(fi, base + i);
+        max_p = fmin(max_p, __shfl(pv, base + i));
+        max_t = fmax(max_t, __shfl(tv, base + i));
+        dv |= __shfl(div, base + i);
+    }
+    if (!act || g != 0) return;
+    ElemState &E = d.el[b];
     feas = sqrt(feas);
     E.max_p = max_p;
     E.max_t = max_t;
@@ -300,7 +313,7 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
     const double exp_merit = exp_cost - eps * E.merit_rho * E.feas_prev;
     E.cost = cost; E.feas = feas; E.merit = merit;
     bool fin = false;
-    if ((merit <= E.merit_prev + p.gamma * exp_merit) && !div) {
+    if ((merit <= E.merit_prev + p.gamma * exp_merit) && !dv) {
         E.accepted = 1; E.ls_active = 0; fin = true;
     } else if (last) {
         E.accepted = 0; E.ls_active = 0; E.cost = E.cost_prev; E.merit = E.merit_prev; fin = true;
@@ -484,7 +497,7 @@ void launch_rollout(const Params &p, const Bufs &d, double eps, int init, hipStr
 }
 void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_decide, dim3(blocks_for(p.B, 64)), dim3(64), 0, st, p, d, eps, last, init);
+    hipLaunchKernelGGL(k_decide, dim3((p.B + 3) / 4), dim3(64), 0, st, p, d, eps, last, init);
 }
 void launch_update_nominal(const Params &p, const Bufs &d, int init, hipStream_t st)
 {
