@@ -53,9 +53,6 @@ DEV int tri(int a, int b) { return a * (2 * NX - a + 1) / 2 + (b - a); }
         __syncthreads();               \
         asm volatile("" ::: "memory"); \
     } while (0)
-// scheduling fence between the stages of a knot: keeps the scheduler from hoisting a later
-// stage's loads (and their registers) into an earlier one
-#define SFENCE() __builtin_amdgcn_sched_barrier(0)
 
 // Compile-time loop: the body sees its index as a constant, so per-lane register arrays indexed
 // by it stay in VGPRs (a runtime index would demote them to scratch).
@@ -68,17 +65,6 @@ template <int N, typename F>
 DEV void static_for(F &&f)
 {
     static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// Register pin: the values must exist in VGPRs at this point.  Placed at the end of each stage
-// of a knot, it stops LLVM from sinking a stage's arithmetic into a later one, which would keep
-// that stage's LDS operands live (the unpinned Gauss-Jordan deferred its Qux updates to the end
-// and spilled every pivot column).
-template <int N>
-DEV void pin(double (&a)[N])
-{
-#pragma unroll
-    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(a[i]));
 }
 
 // read-only, wave-uniform data: the constant address space lets the compiler use scalar loads

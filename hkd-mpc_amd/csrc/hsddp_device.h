@@ -10,6 +10,19 @@ using namespace hkd;
 
 #define DEV __device__ __forceinline__
 
+// Register pin: the values must exist in VGPRs at this point.  Placed at the end of a stage, it
+// stops LLVM from sinking the stage's arithmetic into a later one (which keeps the stage's
+// operands live and spills).
+template <int N>
+DEV void pin(double (&a)[N])
+{
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(a[i]));
+}
+// scheduling fence between stages: keeps the scheduler from hoisting a later stage's loads (and
+// their registers) into an earlier one
+#define SFENCE() __builtin_amdgcn_sched_barrier(0)
+
 // ---------------------------------------------------------------------------------------------
 // cost model helpers (HKDCost.h / HKDCost.cpp / SinglePhaseInterface.cpp:55-118)
 DEV double q_diag(const Params &p, const int *c, int j) { return j < 12 ? p.qbase[j] : p.q_qJ * (1 - c[(j - 12) / 3]); }

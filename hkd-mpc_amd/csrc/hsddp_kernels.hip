@@ -189,7 +189,7 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
 // (HKDProblem.cpp:104), so X[k] = Xbar[k] + eps dX[k] and the simulated state at k depends only on
 // knot k-1: the nonlinear rollout is knot-parallel.  U = Ubar + eps du with du = dU + K dX from the
 // linear rollout (equal to the reference's Ubar + eps dU + K (X - Xbar) up to rounding of X - Xbar).
-__global__ __launch_bounds__(256) void k_rollout(Params p, Bufs d, double eps, int init)
+__global__ __launch_bounds__(256, 2) void k_rollout(Params p, Bufs d, double eps, int init)
 {
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long)p.B * p.S) return;
@@ -201,10 +201,9 @@ __global__ __launch_bounds__(256) void k_rollout(Params p, Bufs d, double eps, i
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     const size_t sb = (size_t)b * p.S;
-    double x[NX], xs[NX];
-    const double *xb = d.Xbar + (sb + s) * NX, *dxg = d.dX + (sb + s) * NX;
-#pragma unroll
-    for (int j = 0; j < NX; ++j) x[j] = xb[j] + eps * dxg[j];
+    // simulated state first, then the shooting state: the inputs of one are dead before the
+    // other's are loaded (register pressure sets this kernel's occupancy)
+    double xs[NX];
     if (k == 0) {
         if (i == 0) {
 #pragma unroll
@@ -230,6 +229,12 @@ __global__ __launch_bounds__(256) void k_rollout(Params p, Bufs d, double eps, i
         double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
         hkd_step(xp, up, cd, p.dt, xs);
     }
+    pin(xs);
+    SFENCE();
+    double x[NX];
+    const double *xb = d.Xbar + (sb + s) * NX, *dxg = d.dX + (sb + s) * NX;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) x[j] = xb[j] + eps * dxg[j];
     double nrm = 0.0, fs = 0.0;
     double *Xg = d.X + (sb + s) * NX, *Dg = d.Defect + (sb + s) * NX;
 #pragma unroll
@@ -242,6 +247,8 @@ __global__ __launch_bounds__(256) void k_rollout(Params p, Bufs d, double eps, i
     }
     d.slot_feas[sb + s] = fs;
     d.slot_div[sb + s] = (k > 0 && sqrt(nrm) > 1e6) ? 1 : 0;
+    pin(x);
+    SFENCE();
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
     if (k == p.N[i]) {
         double tv, h[4];
