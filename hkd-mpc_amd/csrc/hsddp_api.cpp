@@ -301,7 +301,7 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         (rc = dalloc(h, d.Xbar, B * S * NX)) || (rc = dalloc(h, d.Defect, B * S * NX)) ||
         (rc = dalloc(h, d.Defect_bar, B * S * NX)) || (rc = dalloc(h, d.dX, B * S * NX)) ||
         (rc = dalloc(h, d.U, B * Kc * NX)) || (rc = dalloc(h, d.Ubar, B * Kc * NX)) || (rc = dalloc(h, d.dU, B * Kc * NX)) ||
-        (rc = dalloc(h, d.du, B * Kc * NX)) || (rc = dalloc(h, d.K, B * Kc * KCW)) || (rc = dalloc(h, d.lq, B * Kc * LQW)) ||
+        (rc = dalloc(h, d.du, B * Kc * NX)) || (rc = dalloc(h, d.K, B * Kc * KCW)) || (rc = dalloc(h, d.dbg, B * 16)) || (rc = dalloc(h, d.lq, B * Kc * LQW)) ||
         (rc = dalloc(h, d.term, B * P * TW)) || (rc = dalloc(h, d.reb_delta, B * Kc * 20)) ||
         (rc = dalloc(h, d.reb_eps, B * Kc * 20)) || (rc = dalloc(h, d.al_sigma, B * P * 4)) ||
         (rc = dalloc(h, d.al_lambda, B * P * 4)) || (rc = dalloc(h, d.term_h, B * P * 4)) ||
@@ -658,6 +658,16 @@ extern "C" int hsddp_download_trajectory(hsddp_handle h, double *Xbar, double *U
                     std::memcpy(K + ((b * Kc + k) * NX + u) * NX, &kc[((b * Kc + k) * 12 + q) * NX], NX * sizeof(double));
                 }
     }
+    return HSDDP_OK;
+}
+
+// diagnostic builds (-DHSDDP_STAMPS=1): per-element in-kernel stamp sums [B][16]; not in hsddp.h
+extern "C" int hsddp_debug_stamps(hsddp_handle h, unsigned long long *out)
+{
+    if (!h || !out) return fail(HSDDP_ERR_ARG, "null argument");
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipMemcpy(out, h->d.dbg, h->p.B * 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return HSDDP_OK;
 }
 

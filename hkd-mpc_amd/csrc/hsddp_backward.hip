@@ -36,12 +36,39 @@ constexpr int XS = 25;      // padded row stride of the LDS matrix (row-per-lane
 constexpr int OFF_M9 = NX * HC;  // M rows 0..8 after T_c in Bm
 constexpr int OFF_KP = HC * NX;  // Quu_cc^-1 Qux_c after Qux_c in A
 
+#ifndef HSDDP_STAMPS
+#define HSDDP_STAMPS 0
+#endif
+
 struct BwdElem {
+#if HSDDP_STAMPS
+    unsigned long long st[10], tprev;  // diagnostic build: cycles per knot stage (lane 0)
+#endif
     double A[NX * XS];             // LQ record copy -> Qxx rows (symmetrisation) -> Qux_c [12][24] | Kp [12][24]
     double Bm[NX * HC + 9 * NX];   // T_c = H B_c [24][12] | M rows 0..8 [9][24] -> packed symmetric Qxx
     double Gn[NX], d[NX], wqu[HC];
     double red[4];
 };
+
+// In-kernel stamps (diagnostic build only, -DHSDDP_STAMPS=1): s_memtime at the stage boundaries
+// of a knot, the differences summed per stage by lane 0 into LDS and written to Bufs::dbg.
+#if HSDDP_STAMPS
+#define STAMP(n)                                                                              \
+    do {                                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        unsigned long long t_;                                                                \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        if (threadIdx.x == 0) {                                                               \
+            if ((n) > 0) S.st[n] += t_ - S.tprev;                                             \
+            S.tprev = t_;                                                                     \
+        }                                                                                     \
+    } while (0)
+#else
+#define STAMP(n) \
+    do {         \
+    } while (0)
+#endif
 
 // packed upper-triangle index of (a, b), a <= b
 DEV int tri(int a, int b) { return a * (2 * NX - a + 1) / 2 + (b - a); }
@@ -175,6 +202,34 @@ DEV double lxx_half(const LxxRow &L, int r, int hf)
     return dg + (hf ? x1 : x0);
 }
 
+// out[i] = sum_j S[j][12 hf + i] col[j] for this half's 12 columns of S (= A - I; rows 0..2:
+// eul, cols {1,2,6,7,8}; rows 3..5: dt at cols 9..11; rows 6..8: omega, cols {0..8, 12, 13, 15,
+// 16, 18, 19, 21, 22}), S values wave-uniform from the LQ record
+DEV void st_apply(cdouble *lqs, double dt, int hf, const double (&col)[9], double (&out)[12])
+{
+    if (hf == 0) {
+        static_for<12>([&](auto I) {
+            constexpr int c = I;
+            constexpr int qe = se_index(c), qw = sw_index(c);
+            double v = 0.0;
+            if constexpr (qe >= 0)
+                v += lqs[LQ_SE + qe] * col[0] + lqs[LQ_SE + 5 + qe] * col[1] + lqs[LQ_SE + 10 + qe] * col[2];
+            if constexpr (c >= 9) v += dt * col[c - 6];
+            if constexpr (qw >= 0)
+                v += lqs[LQ_SW + qw] * col[6] + lqs[LQ_SW + 17 + qw] * col[7] + lqs[LQ_SW + 34 + qw] * col[8];
+            out[c] = v;
+        });
+    } else {
+        static_for<12>([&](auto I) {
+            constexpr int i = I, qw = sw_index(12 + i);
+            if constexpr (qw >= 0)
+                out[i] = lqs[LQ_SW + qw] * col[6] + lqs[LQ_SW + 17 + qw] * col[7] + lqs[LQ_SW + 34 + qw] * col[8];
+            else
+                out[i] = 0.0;
+        });
+    }
+}
+
 // Column r of S (= A - I): coefficients S[j][r], j = 0..8
 DEV void s_column(const double *lq, double dt, int r, double *sc)
 {
@@ -236,10 +291,12 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     const bool ul = hf == 1 && r == HC; // lane holding Qu_c
     const double dt = p.dt;
     const size_t kq = b * p.Kc + kc;
+    STAMP(0);
     cdouble *lqs = uniform_ptr(d.lq + kq * LQW);
     double *lq = S.A;  // LDS copy for lane-indexed reads
     stage_knot_inputs(lq, d.lq + kq * LQW, S.d, d.Defect + (b * p.S + s + 1) * NX, lane);
     HSYNC();
+    STAMP(1);
     // Gnext = G + H Defect[k+1] (SinglePhase.cpp:320)
     double part = 0.0;
 #pragma unroll
@@ -291,10 +348,12 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     if (lane < NX) S.Gn[lane] = gn;
     HSYNC();
     SFENCE();
+    STAMP(2);
     // Qx, Qxx = lxx + A^T M, and the coupled blocks Qux_c, Quu_cc, Qu_c
     // (SinglePhase.cpp:323-327; regularisation on both diagonals, MultiPhaseDDP.cpp:160).
-    // The lane-indexed LQ entries are read first; the LQ copy's LDS then takes the Qxx rows,
-    // so Qxx never occupies registers.
+    // The S^T X products (S = A - I) are evaluated transposed: a lane gathers one column of X
+    // and applies S, whose sparsity is known at compile time and whose values are wave-uniform
+    // (SGPRs) — 9 LDS reads per product instead of one broadcast read per multiply.
     double sc[9];
     s_column(lq, dt, r, sc);
     double qx = 0.0;
@@ -317,20 +376,28 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     const bool stz = pick4(pc.c, lr) != 0;
     const double qzz = dt * (stz ? p.r_qJd : p.r_grf) + reg;
     const double quz = lq[LQ_LU + (stz ? HC + rq : rq)];
-    HSYNC();
+    HSYNC();  // the LQ copy is dead from here; S.A takes Y2, then the Z rows
+    double z[HC];
     {
-        LxxRow lx_;
-        lxx_row(p, pc, r, lx_);
-        static_for<HC>([&](auto I) {
-            constexpr int i = I;
-            double a = 0.0;
+        const int rr = rowl ? r : 0, rt = r < HC ? r : 0;
+        double col[9], y[HC];
+        // Y2 = S^T T_c: column r (< 12) of it, this half's rows -> S.A row-major [24][12]
 #pragma unroll
-            for (int j = 0; j < 9; ++j) a += sc[j] * S.Bm[OFF_M9 + j * NX + cb + i];
-            const double v = lxx_half<i>(lx_, r, hf) + (m[i] + a) + (cb + i == r ? reg : 0.0);
-            if (rowl) S.A[r * XS + cb + i] = v;
-        });
+        for (int j = 0; j < 9; ++j) col[j] = S.Bm[j * HC + rt];
+        st_apply(lqs, dt, hf, col, y);
+        if (r < HC)
+#pragma unroll
+            for (int i = 0; i < HC; ++i) S.A[(cb + i) * HC + r] = y[i];
+        // Z = M + (S^T M9)^T on this lane's row: Qxx = lxx + Z^T-symmetric part (below)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) col[j] = S.Bm[OFF_M9 + j * NX + rr];
+        st_apply(lqs, dt, hf, col, y);
+#pragma unroll
+        for (int i = 0; i < HC; ++i) z[i] = m[i] + y[i];
     }
-    SFENCE();
+    pin(z);
+    HSYNC();
+    STAMP(3);
     // Every lane evaluates all three column roles and selects its own: the two halves would run
     // both sides of a divergent branch anyway, and straight-line code keeps the register
     // allocator from spilling live values around the branches.
@@ -338,11 +405,8 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     static_for<HC>([&](auto I) {
         constexpr int q = I, l = q / 3, a = q % 3;
         const bool st = pc.c[l] != 0;
-        // (A^T T_c)[r][q] = T_c[r][q] + sum_j S[j][r] T_c[j][q]: row r of Qux_c^T
-        double ax = 0.0;
-#pragma unroll
-        for (int j = 0; j < 9; ++j) ax += sc[j] * S.Bm[j * HC + q];
-        const double vx = S.Bm[rx * HC + q] + ax;
+        // (A^T T_c)[r][q] = T_c[r][q] + (S^T T_c)[r][q]: row r of Qux_c^T
+        const double vx = S.Bm[rx * HC + q] + S.A[rx * HC + q];
         // column r of Quu_cc = luu + B_c^T T_c + reg I
         const double vs = lqs[LQ_BW + q] * S.Bm[6 * HC + rq] + lqs[LQ_BW + 12 + q] * S.Bm[7 * HC + rq] +
                           lqs[LQ_BW + 24 + q] * S.Bm[8 * HC + rq] + pc.bv[l] * S.Bm[(9 + a) * HC + rq];
@@ -359,15 +423,25 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         SFENCE();
     });
     HSYNC();
-    // Qxx = (Qxx + Qxx^T) / 2 (SinglePhase.cpp:352), kept in LDS as a packed upper triangle
+    // Qxx = lxx + M + S^T M9 and lxx is symmetric, so (Qxx + Qxx^T) / 2 (SinglePhase.cpp:352)
+    // = lxx + (Z + Z^T) / 2 with Z = M + (S^T M9)^T; kept in LDS as a packed upper triangle
     if (rowl)
 #pragma unroll
-        for (int i = 0; i < HC; ++i) {
-            const int c = cb + i;
-            const double q = (S.A[r * XS + c] + S.A[c * XS + r]) / 2;
-            if (r <= c) S.Bm[tri(r, c)] = q;
-        }
+        for (int i = 0; i < HC; ++i) S.A[r * XS + cb + i] = z[i];
     HSYNC();
+    STAMP(4);
+    if (rowl) {
+        LxxRow lx_;
+        lxx_row(p, pc, r, lx_);
+        static_for<HC>([&](auto I) {
+            constexpr int i = I;
+            const int c = cb + i;
+            const double q = lxx_half<i>(lx_, r, hf) + (c == r ? reg : 0.0) + (S.A[r * XS + c] + S.A[c * XS + r]) / 2;
+            if (r <= c) S.Bm[tri(r, c)] = q;
+        });
+    }
+    HSYNC();
+    STAMP(5);
     // pre-elimination Qux_c (rows q) and Qu_c for the value update
     if (xl)
 #pragma unroll
@@ -381,12 +455,52 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     // in its step.
     unsigned long long bad = __builtin_amdgcn_ballot_w64(ql && !(qzz > 1e-9));
     // Gauss-Jordan on [Quu_cc | Qux_c | Qu_c] (one column per lane): pivot column j comes from
-    // lane 32 + j through SGPRs
+    // lane 32 + j (GJ_BCAST 0: v_readlane through SGPRs; 1: LDS store + broadcast read;
+    // 2: ds_bpermute)
+#ifndef GJ_BCAST
+#define GJ_BCAST 0
+#endif
+    double *pcol = S.Bm + NX * (NX + 1) / 2;  // free during the elimination: Bm past the packed Qxx
+#if GJ_PIPE
+    // pivot reciprocal one step ahead: row j+1 is updated first, its value on lane 32 + j + 1 is
+    // the next pivot, and its reciprocal is formed while the other rows are updated
+    double inv = recip(lane_value(w[0], 32));
     static_for<HC>([&](auto J) {
         constexpr int j = J;
         double col[HC];
 #pragma unroll
+        for (int i = 0; i < HC; ++i) col[i] = (i == j) ? 0.0 : lane_value(w[i], 32 + j);
+        const double piv = lane_value(w[j], 32 + j);
+        bad |= __builtin_amdgcn_ballot_w64(!(piv > 1e-9));
+        const double f = w[j] * inv;
+        if constexpr (j + 1 < HC) {
+            w[j + 1] -= col[j + 1] * f;
+            inv = recip(lane_value(w[j + 1], 32 + j + 1));
+        }
+#pragma unroll
+        for (int i = 0; i < HC; ++i)
+            if (i != j && i != j + 1) w[i] -= col[i] * f;
+        w[j] = f;
+        pin(w);
+    });
+#else
+    static_for<HC>([&](auto J) {
+        constexpr int j = J;
+        double col[HC];
+#if GJ_BCAST == 0
+#pragma unroll
         for (int i = 0; i < HC; ++i) col[i] = lane_value(w[i], 32 + j);
+#elif GJ_BCAST == 1
+        if (lane == 32 + j)
+#pragma unroll
+            for (int i = 0; i < HC; ++i) pcol[i] = w[i];
+        HSYNC();
+#pragma unroll
+        for (int i = 0; i < HC; ++i) col[i] = pcol[i];
+#else
+#pragma unroll
+        for (int i = 0; i < HC; ++i) col[i] = __shfl(w[i], 32 + j);
+#endif
         const double piv = col[j];
         bad |= __builtin_amdgcn_ballot_w64(!(piv > 1e-9));
         const double f = w[j] * recip(piv);
@@ -395,8 +509,13 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
             if (i != j) w[i] -= col[i] * f;
         w[j] = f;
         pin(w);
+#if GJ_BCAST == 1
+        HSYNC();
+#endif
         SFENCE();
     });
+#endif
+    STAMP(6);
     live = live && bad == 0;
     if (!live) return;
     // K = -Quu^-1 Qux, dU = -Quu^-1 Qu; K rows of decoupled controls are zero
@@ -424,6 +543,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         dvp = quz * duz;
     }
     HSYNC();
+    STAMP(7);
     if (ul)
 #pragma unroll
         for (int q = 0; q < HC; ++q) dvp += S.d[q] * w[q];
@@ -455,6 +575,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         h[i] = rowl ? q - acc[i] : 0.0;
     }
     HSYNC();
+    STAMP(8);
 }
 
 // MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229) with one regularisation value.
@@ -537,6 +658,9 @@ __global__ __launch_bounds__(64, 4) void k_riccati(Params p, Bufs d)
     const size_t b = blockIdx.x;
     ElemState &E = d.el[b];
     if (E.done || E.inner_done) return;
+#if HSDDP_STAMPS
+    if (lane < 10) S.st[lane] = 0;
+#endif
     // compute_cost + feasibility at the start of the inner iteration (MultiPhaseDDP.cpp:306-307)
     if (lane == 0) {
         double cost = 0.0, feas = 0.0;
@@ -564,6 +688,10 @@ __global__ __launch_bounds__(64, 4) void k_riccati(Params p, Bufs d)
     }
     reg = reg / 20;
     if (reg < 1e-06) reg = 0;
+#if HSDDP_STAMPS
+    HSYNC();
+    if (lane < 10) d.dbg[b * 16 + lane] += S.st[lane];
+#endif
     if (lane == 0) {
         E.iters += 1; E.cost = cost; E.feas = feas; E.reg = reg; E.accepted = 0;
         if (!ok) { E.status = 1; E.done = 1; E.ls_active = 0; } // goto bad_solve

@@ -72,6 +72,7 @@ struct Bufs {
     int *slot_div;
     ElemState *el;
     int *counter;                          // [4] host-visible activity counters
+    unsigned long long *dbg;               // [B][16] diagnostic builds only (in-kernel stamps)
 };
 
 // kernel launchers (hsddp_kernels.hip)

@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libhsddp_amd.so")
+# HSDDP_LIB selects another in-tree build of the same ABI (kernel A/B measurements)
+LIB_PATH = os.environ.get("HSDDP_LIB") or os.path.join(PKG_DIR, "libhsddp_amd.so")
 
 DP = C.POINTER(C.c_double)
 IP = C.POINTER(C.c_int)

@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Where a k_riccati knot spends its cycles: run the diagnostic build (-DHSDDP_STAMPS=1,
+hkd-mpc_amd/libhsddp_amd_stamps.so, selected through HSDDP_LIB) and print each stage's share of
+the stamped cycles.  Read the shares, not the totals: the stamps' fences forbid overlaps.
+
+    HSDDP_LIB=$PWD/hkd-mpc_amd/libhsddp_amd_stamps.so python tools/stamps.py
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch  # noqa: F401  (bind to torch's HIP runtime first, as bench.py does)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hkd-mpc_amd"))
+import hsddp  # noqa: E402
+from hsddp import synthetic  # noqa: E402
+
+STAGES = ["stage inputs -> LDS", "T_c, M rows (stage A)", "sc/qx/rb + Qxx rows", "Qux/Quu/Qu columns",
+          "symmetrise Qxx", "Gauss-Jordan (12 steps)", "K, dU stores, dV", "value update H, G"]
+
+
+def main():
+    B = int(os.environ.get("STAMP_B", "4096"))
+    prob = synthetic.make_batch(B, 4, 50, "trot")
+    s = hsddp.Solver(prob, hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=4))
+    s.begin()
+    s.iterate(3)
+    out = np.zeros((B, 16), np.uint64)
+    L = hsddp._lib.lib()
+    L.hsddp_debug_stamps.argtypes = [C.c_void_p, C.c_void_p]
+    rc = L.hsddp_debug_stamps(s._h, out.ctypes.data)
+    s.close()
+    assert rc == 0, rc
+    cyc = out[:, 1:9].astype(np.float64).mean(0)
+    tot = cyc.sum()
+    for name, c in zip(STAGES, cyc):
+        print(f"{name:28s} {c / (3 * 200):10.0f} cycles/knot  {100 * c / tot:5.1f} %")
+    print(f"{'total':28s} {tot / (3 * 200):10.0f} cycles/knot")
+
+
+if __name__ == "__main__":
+    main()
