@@ -45,7 +45,7 @@ struct BwdElem {
     unsigned long long st[10], tprev;  // diagnostic build: cycles per knot stage (lane 0)
 #endif
     double A[NX * XS];             // LQ record copy -> Qxx rows (symmetrisation) -> Qux_c [12][24] | Kp [12][24]
-    double Bm[NX * HC + 9 * NX];   // T_c = H B_c [24][12] | M rows 0..8 [9][24] -> packed symmetric Qxx
+    double Bm[NX * XS];            // T_c = H B_c [24][12] | M rows 0..8 [9][24] -> symmetric Qxx -> H (rows, stride XS)
     double Gn[NX], d[NX], wqu[HC];
     double red[4];
 };
@@ -436,8 +436,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         static_for<HC>([&](auto I) {
             constexpr int i = I;
             const int c = cb + i;
-            const double q = lxx_half<i>(lx_, r, hf) + (c == r ? reg : 0.0) + (S.A[r * XS + c] + S.A[c * XS + r]) / 2;
-            if (r <= c) S.Bm[tri(r, c)] = q;
+            S.Bm[r * XS + c] = lxx_half<i>(lx_, r, hf) + (c == r ? reg : 0.0) + (S.A[r * XS + c] + S.A[c * XS + r]) / 2;
         });
     }
     HSYNC();
@@ -557,23 +556,37 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
 #pragma unroll
     for (int q = 0; q < HC; ++q) gp += S.A[q * NX + rr] * S.wqu[q];
     g = rowl ? qx - gp : 0.0;
-    double acc[HC];
+    // P = Qux_c^T Kp (24 x 24, K = 12) on the matrix cores: v_mfma_f64_16x16x4_f64 over 2 x 2
+    // output tiles (rows / columns 24..31 are padding and discarded) and 3 k-steps.  Operands
+    // (MI355X layout): A[l & 15][k = l >> 4], B[k = l >> 4][l & 15]; result rows
+    // (l >> 4) + 4 reg, column l & 15.  H = Qxx - P is formed in place of Qxx in LDS (each entry
+    // read and written by the same lane), then read back as rows.
+    {
+        typedef double d4 __attribute__((ext_vector_type(4)));
+        d4 t00 = {0, 0, 0, 0}, t01 = t00, t10 = t00, t11 = t00;
+        const int li = lane & 15, lk = lane >> 4;
 #pragma unroll
-    for (int i = 0; i < HC; ++i) acc[i] = 0.0;
-    static_for<HC>([&](auto Q) {
-        constexpr int q = Q;
-        const double qr = S.A[q * NX + rr];
+        for (int ks = 0; ks < 3; ++ks) {
+            const int q = 4 * ks + lk;
+            const double a0 = S.A[q * NX + li], a1 = S.A[q * NX + 16 + li];
+            const double b0 = S.A[OFF_KP + q * NX + li], b1 = S.A[OFF_KP + q * NX + 16 + li];
+            t00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, t00, 0, 0, 0);
+            t01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, t01, 0, 0, 0);
+            t10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, t10, 0, 0, 0);
+            t11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, t11, 0, 0, 0);
+        }
 #pragma unroll
-        for (int i = 0; i < HC; ++i) acc[i] += qr * S.A[OFF_KP + q * NX + cb + i];
-        pin(acc);
-        SFENCE();
-    });
-#pragma unroll
-    for (int i = 0; i < HC; ++i) {
-        const int c = cb + i;
-        const double q = S.Bm[tri(min(rr, c), max(rr, c))];
-        h[i] = rowl ? q - acc[i] : 0.0;
+        for (int g = 0; g < 4; ++g) {
+            const int r0 = lk + 4 * g, r1 = 16 + r0, c1 = 16 + li;
+            S.Bm[r0 * XS + li] -= t00[g];
+            if (c1 < NX) S.Bm[r0 * XS + c1] -= t01[g];
+            if (r1 < NX) S.Bm[r1 * XS + li] -= t10[g];
+            if (r1 < NX && c1 < NX) S.Bm[r1 * XS + c1] -= t11[g];
+        }
     }
+    HSYNC();
+#pragma unroll
+    for (int i = 0; i < HC; ++i) h[i] = rowl ? S.Bm[rr * XS + cb + i] : 0.0;
     HSYNC();
     STAMP(8);
 }
