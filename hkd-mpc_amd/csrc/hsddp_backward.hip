@@ -715,35 +715,151 @@ __global__ __launch_bounds__(64, 4) void k_riccati(Params p, Bufs d)
 // MultiPhaseDDP::linear_rollout(1.0): dX, du = dU + K dX, and the expected cost change (quirk
 // A3: it replaces the sweep's dV), then the merit function (MultiPhaseDDP.cpp:309-318).
 // Lanes r < 24 of each half compute row r of the same vectors; the first half stores them.
-struct LinElem {
-    double lq[LQW + 2];
-    double dx[NX], du[NX], d[NX];
+// A knot's inputs (compact K, LQ record, Defect[k+1], dU) are one 4080-byte LDS image filled by
+// four 16-byte-per-lane LDS-DMA loads (global_load_lds_dwordx4); the next knot's image is loaded
+// into the other buffer while this knot computes.
+constexpr int LB_K = 0, LB_LQ = KCW, LB_D = KCW + LQW, LB_DU = KCW + LQW + NX, LBW = KCW + LQW + 2 * NX;
+static_assert(LBW % 2 == 0 && LB_LQ % 2 == 0 && LB_D % 2 == 0 && LB_DU % 2 == 0 && LBW <= 4 * 64 * 2,
+              "16-byte pieces, four DMA instructions");
+struct LinBuf {
+    double v[2 * 4 * 64];
 };
+struct LinElem {
+    double dx[NX], du[NX];
+};
+
+// single-wave workgroup: LDS operations of one wave complete in order, so a compiler barrier is
+// enough between stages, and no __syncthreads fence drains the LDS-DMA in flight
+#define LSYNC() asm volatile("" ::: "memory")
+
+// Issued as inline asm so the waitcnt pass does not track the LDS writes (it would otherwise wait
+// for every DMA in flight before any LDS read); lin_knot waits explicitly.  LDS destination of
+// piece t: M0 + 16 * lane, contiguous.
+DEV void lin_fetch(LinBuf &buf, const Params &p, const Bufs &d, size_t b, int s, int kc, int lane)
+{
+    const size_t kq = b * p.Kc + kc;
+    // one base per segment, biased so that base + 8 * o addresses image double o
+    const size_t kB = (size_t)(d.K + kq * KCW), lB = (size_t)(d.lq + kq * LQW) - 8 * LB_LQ,
+                 dB = (size_t)(d.Defect + (b * p.S + s + 1) * NX) - 8 * LB_D, uB = (size_t)(d.dU + kq * NX) - 8 * LB_DU;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        int o = 2 * (64 * t + lane);  // first double of this lane's 16-byte piece
+        o = o < LBW ? o : LBW - 2;   // the one spare piece repeats the last
+        const size_t base = o < LB_LQ ? kB : o < LB_D ? lB : o < LB_DU ? dB : uB;
+        const double *src = (const double *)(base + 8 * (size_t)o);
+        const unsigned m0 = (unsigned)(size_t)(buf.v + 128 * t);
+        asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(m0) : "memory");
+    }
+}
+
+// one knot of SinglePhase::linear_rollout (SinglePhase.cpp:144-178) from the LDS image `cur`;
+// when `more`, the next knot's image is requested into `nxt` first
+DEV void lin_knot(const Params &p, const Bufs &d, LinElem &S, LinBuf &cur, LinBuf &nxt, bool more, size_t b,
+                  int s, int kc, const PhaseConst &pc, const LxxRow &lx_, double ru, bool cpl, int krow0,
+                  double &dx, double &v1, double &v2)
+{
+    const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5, cb = HC * hf;
+    const bool rowl = r < NX, st = rowl && hf == 0;
+    const int rr = rowl ? r : 0;
+    const double dt = p.dt;
+    if (more) {
+        lin_fetch(nxt, p, d, b, s + 1, kc + 1, lane);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // all but the four just issued
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    LSYNC();
+    const double *lq = cur.v + LB_LQ, *dd = cur.v + LB_D;
+    double krow[HC];
+#pragma unroll
+    for (int c = 0; c < HC; ++c) krow[c] = cpl ? cur.v[LB_K + krow0 + c] : 0.0;
+    const double dUr = cur.v[LB_DU + rr];
+    if (lane < NX) S.dx[lane] = dx;
+    LSYNC();
+    double kd = 0.0;
+#pragma unroll
+    for (int c = 0; c < HC; ++c) kd += krow[c] * S.dx[cb + c];
+    kd += other_half(kd);
+    const double du = dUr + kd;
+    if (lane < NX) S.du[lane] = du;
+    LSYNC();
+    double nx = 0.0, q1 = 0.0, q2 = 0.0;
+    if (rowl) {
+        double sdx = 0.0;
+        if (r < 3) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q) sdx += lq[LQ_SE + 5 * r + q] * S.dx[se_col(q)];
+        } else if (r < 6) {
+            sdx = dt * S.dx[r + 6];
+        } else if (r < 9) {
+#pragma unroll
+            for (int q = 0; q < 17; ++q) sdx += lq[LQ_SW + 17 * (r - 6) + q] * S.dx[sw_col(q)];
+        }
+        double bdu = 0.0, lxd = lx_.diag * dx, lud = ru * du;
+        if (r < 6) {
+            if (r >= 3) {
+#pragma unroll
+                for (int l = 0; l < 4; ++l) lxd += lx_.xq[l] * S.dx[12 + 3 * l + r - 3];
+            }
+        } else if (r < 9) {
+#pragma unroll
+            for (int c = 0; c < 12; ++c) bdu += lq[LQ_BW + 12 * (r - 6) + c] * S.du[c];
+        } else if (r < 12) {
+#pragma unroll
+            for (int l = 0; l < 4; ++l) bdu += pc.bv[l] * S.du[3 * l + r - 9];
+        } else {
+            bdu = pick4(pc.bq, (r - 12) / 3) * S.du[r];
+            lxd += lx_.xp * S.dx[3 + (r - 12) % 3];
+        }
+        if (r < 12) {
+            const double *rb = lq + LQ_RB + 6 * (r / 3);
+            const int a = r % 3, u0 = 3 * (r / 3);
+            const double b0 = a == 0 ? rb[0] : a == 1 ? rb[1] : rb[2];
+            const double b1 = a == 0 ? rb[1] : a == 1 ? rb[3] : rb[4];
+            const double b2 = a == 0 ? rb[2] : a == 1 ? rb[4] : rb[5];
+            lud += b0 * S.du[u0] + b1 * S.du[u0 + 1] + b2 * S.du[u0 + 2];
+        }
+        nx = (dx + sdx) + bdu + dd[r];
+        q1 = lq[LQ_LX + r] * dx + lq[LQ_LU + r] * du;
+        q2 = dx * lxd + du * lud;
+        if (st) {
+            const size_t kq = b * p.Kc + kc;
+            d.du[kq * NX + r] = du;
+            d.dX[(b * p.S + s + 1) * NX + r] = nx;
+        }
+    }
+    v1 += half_sum(q1);
+    v2 += half_sum(q2);
+    dx = nx;
+    LSYNC();
+}
 
 __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
 {
     __shared__ LinElem S;
+    __shared__ LinBuf B0;
+    __shared__ LinBuf B1;
     const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5, cb = HC * hf;
     const size_t b = blockIdx.x;
     ElemState &E = d.el[b];
     if (E.done || E.inner_done) return;
     const bool rowl = r < NX, st = rowl && hf == 0;
     const int rr = rowl ? r : 0;
-    const double dt = p.dt;
     double v1 = 0.0, v2 = 0.0, dx = 0.0;
     for (int i = 0; i < p.P; ++i) {
         PhaseConst pc;
         load_phase(p, d, b, i, pc);
         const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
+        lin_fetch(B0, p, d, b, s0, k0, lane);  // the phase's first knot (its wait is in lin_knot)
         if (i > 0) { // dx_init = Px dX_end
             const double *Px = d.term + (b * p.P + (i - 1)) * TW + TM_PX;
             if (lane < NX) S.dx[lane] = dx;
-            HSYNC();
+            LSYNC();
             double a = 0.0;
             if (rowl)
                 for (int j = 0; j < NX; ++j) a += Px[r * NX + j] * S.dx[j];
             dx = a;
-            HSYNC();
+            LSYNC();
         } else {
             dx = 0.0;
         }
@@ -758,79 +874,15 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
         // control r has a gain row only when its B column is non-zero (KCW layout)
         const bool stl = pick4(pc.c, (rr % HC) / 3) != 0;
         const bool cpl = rowl && (rr < HC ? stl : !stl);
-        const size_t krow0 = (size_t)(rr % HC) * NX + cb;
-        for (int k = 0; k < N; ++k) {
-            const int s = s0 + k, kc = k0 + k;
-            const size_t kq = b * p.Kc + kc;
-            double krow[HC];
-#pragma unroll
-            for (int c = 0; c < HC; ++c) krow[c] = 0.0;
-            if (cpl)
-#pragma unroll
-                for (int c = 0; c < HC; ++c) krow[c] = d.K[kq * KCW + krow0 + c];
-            const double dUr = d.dU[kq * NX + rr];
-            stage_knot_inputs(S.lq, d.lq + kq * LQW, S.d, d.Defect + (b * p.S + s + 1) * NX, lane);
-            if (lane < NX) S.dx[lane] = dx;
-            HSYNC();
-            double kd = 0.0;
-#pragma unroll
-            for (int c = 0; c < HC; ++c) kd += krow[c] * S.dx[cb + c];
-            kd += other_half(kd);
-            const double du = dUr + kd;
-            if (lane < NX) S.du[lane] = du;
-            HSYNC();
-            double nx = 0.0, q1 = 0.0, q2 = 0.0;
-            if (rowl) {
-                double sdx = 0.0;
-                if (r < 3) {
-#pragma unroll
-                    for (int q = 0; q < 5; ++q) sdx += S.lq[LQ_SE + 5 * r + q] * S.dx[se_col(q)];
-                } else if (r < 6) {
-                    sdx = dt * S.dx[r + 6];
-                } else if (r < 9) {
-#pragma unroll
-                    for (int q = 0; q < 17; ++q) sdx += S.lq[LQ_SW + 17 * (r - 6) + q] * S.dx[sw_col(q)];
-                }
-                double bdu = 0.0, lxd = lx_.diag * dx, lud = ru * du;
-                if (r < 6) {
-                    if (r >= 3) {
-#pragma unroll
-                        for (int l = 0; l < 4; ++l) lxd += lx_.xq[l] * S.dx[12 + 3 * l + r - 3];
-                    }
-                } else if (r < 9) {
-#pragma unroll
-                    for (int c = 0; c < 12; ++c) bdu += S.lq[LQ_BW + 12 * (r - 6) + c] * S.du[c];
-                } else if (r < 12) {
-#pragma unroll
-                    for (int l = 0; l < 4; ++l) bdu += pc.bv[l] * S.du[3 * l + r - 9];
-                } else {
-                    bdu = pick4(pc.bq, (r - 12) / 3) * S.du[r];
-                    lxd += lx_.xp * S.dx[3 + (r - 12) % 3];
-                }
-                if (r < 12) {
-                    const double *rb = S.lq + LQ_RB + 6 * (r / 3);
-                    const int a = r % 3, u0 = 3 * (r / 3);
-                    const double b0 = a == 0 ? rb[0] : a == 1 ? rb[1] : rb[2];
-                    const double b1 = a == 0 ? rb[1] : a == 1 ? rb[3] : rb[4];
-                    const double b2 = a == 0 ? rb[2] : a == 1 ? rb[4] : rb[5];
-                    lud += b0 * S.du[u0] + b1 * S.du[u0 + 1] + b2 * S.du[u0 + 2];
-                }
-                nx = (dx + sdx) + bdu + S.d[r];
-                q1 = S.lq[LQ_LX + r] * dx + S.lq[LQ_LU + r] * du;
-                q2 = dx * lxd + du * lud;
-                if (st) {
-                    d.du[kq * NX + r] = du;
-                    d.dX[(b * p.S + s + 1) * NX + r] = nx;
-                }
-            }
-            v1 += half_sum(q1);
-            v2 += half_sum(q2);
-            dx = nx;
-            HSYNC();
+        const int krow0 = (rr % HC) * NX + cb;
+        for (int k = 0; k < N; k += 2) {
+            lin_knot(p, d, S, B0, B1, k + 1 < N, b, s0 + k, k0 + k, pc, lx_, ru, cpl, krow0, dx, v1, v2);
+            if (k + 1 < N)
+                lin_knot(p, d, S, B1, B0, k + 2 < N, b, s0 + k + 1, k0 + k + 1, pc, lx_, ru, cpl, krow0, dx, v1, v2);
         }
         const double *rec = d.term + (b * p.P + i) * TW;
         if (lane < NX) S.dx[lane] = dx;
-        HSYNC();
+        LSYNC();
         double q1 = 0.0, q2 = 0.0;
         if (rowl) {
             q1 = rec[TM_PHIX + r] * dx;
@@ -840,7 +892,7 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
         }
         v1 += half_sum(q1);
         v2 += half_sum(q2);
-        HSYNC();
+        LSYNC();
     }
     if (lane == 0) {
         const double cost = E.cost, feas = E.feas;
