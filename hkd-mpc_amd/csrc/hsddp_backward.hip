@@ -34,7 +34,13 @@ using namespace hkd;
 constexpr int HC = 12;      // columns per half-wave; coupled controls per knot
 constexpr int XS = 25;      // padded row stride of the LDS matrix (row-per-lane writes without conflicts)
 constexpr int OFF_M9 = NX * HC;  // M rows 0..8 after T_c in Bm
-constexpr int OFF_KP = HC * NX;  // Quu_cc^-1 Qux_c after Qux_c in A
+// S.A regions (doubles): the knot's LQ record [0, LQW) until Qux_c [12][XS] takes its place;
+// above it Quu_cc by columns [12][12], then Quu_cc^-1 by columns [12][16], then Kp [12][XS] (each
+// read before the next overwrites it).
+constexpr int OFF_QX = 0;
+constexpr int OFF_QU = HC * XS;
+constexpr int OFF_QI = HC * XS;
+constexpr int OFF_KP = HC * XS;
 
 #ifndef HSDDP_STAMPS
 #define HSDDP_STAMPS 0
@@ -44,8 +50,8 @@ struct BwdElem {
 #if HSDDP_STAMPS
     unsigned long long st[10], tprev;  // diagnostic build: cycles per knot stage (lane 0)
 #endif
-    double A[NX * XS];             // LQ record copy -> Qxx rows (symmetrisation) -> Qux_c [12][24] | Kp [12][24]
-    double Bm[NX * XS];            // T_c = H B_c [24][12] | M rows 0..8 [9][24] -> symmetric Qxx -> H (rows, stride XS)
+    double A[NX * XS];             // LQ record copy -> Qux_c [12][XS] | Quu_cc^-1 [12][16] -> Kp [12][XS]
+    double Bm[NX * XS];            // T_c = H B_c [24][12] | M rows 0..8 [9][24] -> Z rows -> symmetric Qxx -> H (stride XS)
     double Gn[NX], d[NX], wqu[HC];
     double red[4];
 };
@@ -70,9 +76,6 @@ struct BwdElem {
     } while (0)
 #endif
 
-// packed upper-triangle index of (a, b), a <= b
-DEV int tri(int a, int b) { return a * (2 * NX - a + 1) / 2 + (b - a); }
-
 // A 64-thread workgroup is one wave, so __syncthreads() lowers to no instruction and stops no
 // code motion; the memory clobber keeps each phase's LDS loads in their phase.
 #define HSYNC()                        \
@@ -80,6 +83,10 @@ DEV int tri(int a, int b) { return a * (2 * NX - a + 1) / 2 + (b - a); }
         __syncthreads();               \
         asm volatile("" ::: "memory"); \
     } while (0)
+
+// The same inside divergent code and where no fence may drain memory operations in flight: LDS
+// operations of one wave complete in order, so a compiler barrier suffices in a one-wave group.
+#define LSYNC() asm volatile("" ::: "memory")
 
 // Compile-time loop: the body sees its index as a constant, so per-lane register arrays indexed
 // by it stay in VGPRs (a runtime index would demote them to scratch).
@@ -134,6 +141,29 @@ DEV double other_half(double v)
     return threadIdx.x < 32 ? __hiloint2double(b[1], a[1]) : __hiloint2double(b[0], a[0]);
 }
 
+// v on lane j of this lane's 16-lane row (DPP row_newbcast; the s_nop gives a VGPR written by
+// the previous VALU instruction its two wait states before the DPP read)
+template <int j>
+DEV double row_bcast(double v)
+{
+    double r;
+    asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "i"(j));
+    return r;
+}
+
+// w += (w on lane j of this lane's 16-lane row) * s, the broadcast fused into the FMA;
+// `fresh`: w may have been written by the instruction just before
+template <int j, bool fresh>
+DEV void fmac_row_bcast(double &w, double s)
+{
+    if constexpr (fresh)
+        asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+                     : "+v"(w)
+                     : "v"(s), "i"(j));
+    else
+        asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(w) : "v"(s), "i"(j));
+}
+
 // per-phase constants of one element
 struct PhaseConst {
     int c[4];
@@ -167,25 +197,44 @@ DEV T pick4(const T (&a)[4], int i)
     return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
 }
 
-// q_diag / foot_weight (hsddp_device.h) with the contact index resolved by selects
+// a[i] for a runtime i < N, as selects over the (wave-uniform) entries
+template <int N>
+DEV double pick(const double (&a)[N], int i)
+{
+    double e[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        e[k] = a[k];
+        asm volatile("" : "+s"(e[k]));  // opaque: keeps the selects from folding back into an indexed load
+    }
+    double v = e[0];
+#pragma unroll
+    for (int k = 1; k < N; ++k) v = i == k ? e[k] : v;
+    return v;
+}
+
+// q_diag / foot_weight (hsddp_device.h) with the lane-dependent indices resolved by selects:
+// a lane-indexed read of a kernel-argument array is a memory round trip
 DEV void lxx_row(const Params &p, const PhaseConst &pc, int r, LxxRow &L)
 {
     L.diag = 0.0; L.xp = 0.0;
 #pragma unroll
     for (int l = 0; l < 4; ++l) L.xq[l] = 0.0;
     if (r >= NX) return;
-    L.diag = p.dt * (r < 12 ? p.qbase[r] : p.q_qJ * (1 - pick4(pc.c, (r - 12) / 3)));
+    L.diag = p.dt * (r < 12 ? pick(p.qbase, r) : p.q_qJ * (1 - pick4(pc.c, (r - 12) / 3)));
     if (r >= 3 && r < 6) {
+        // dt c^2 (foot_gain w c) = dt foot_gain w for c = 1, else 0 (selects: no per-phase
+        // conversions kept live across the knot loop)
+        const double fw = p.dt * (p.foot_gain * pick(p.foot_w, r - 3));
 #pragma unroll
         for (int l = 0; l < 4; ++l) {
-            const int cl = pc.c[l];
-            double w = p.dt * cl * cl * (p.foot_gain * p.foot_w[r - 3] * cl);
+            const double w = pc.c[l] ? fw : 0.0;
             L.diag += w;
             L.xq[l] = -w;
         }
     } else if (r >= 12) {
-        const int m = r - 12, cl = pick4(pc.c, m / 3);
-        double w = p.dt * cl * cl * (p.foot_gain * p.foot_w[m % 3] * cl);
+        const int m = r - 12;
+        const double w = pick4(pc.c, m / 3) ? p.dt * (p.foot_gain * pick(p.foot_w, m % 3)) : 0.0;
         L.diag += w;
         L.xp = -w;
     }
@@ -204,7 +253,7 @@ DEV double lxx_half(const LxxRow &L, int r, int hf)
 
 // out[i] = sum_j S[j][12 hf + i] col[j] for this half's 12 columns of S (= A - I; rows 0..2:
 // eul, cols {1,2,6,7,8}; rows 3..5: dt at cols 9..11; rows 6..8: omega, cols {0..8, 12, 13, 15,
-// 16, 18, 19, 21, 22}), S values wave-uniform from the LQ record
+// 16, 18, 19, 21, 22}), S values wave-uniform from the LQ record (scalar loads)
 DEV void st_apply(cdouble *lqs, double dt, int hf, const double (&col)[9], double (&out)[12])
 {
     if (hf == 0) {
@@ -286,9 +335,12 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     asm volatile("" : "+v"(reg));
     const int r = lane & 31, hf = lane >> 5, cb = HC * hf;
     const bool rowl = r < NX;
-    const bool xl = hf == 0 && r < NX;  // lanes holding column r of Qux_c^T ... (A^T H B_c) row r
-    const bool ql = hf == 1 && r < HC;  // lanes holding column r of Quu_cc, and decoupled control z(r)
-    const bool ul = hf == 1 && r == HC; // lane holding Qu_c
+    const int pos = lane & 15, R = lane >> 4;  // position in the 16-lane DPP row R
+    const bool qr = pos < HC;                    // elimination column pos of Quu_cc (all four rows)
+    const bool il = pos >= HC && R < 3;          // elimination column ic of the identity
+    const int ic = il ? 4 * R + pos - HC : 0;
+    const bool ul = lane == 60;                  // elimination column Qu_c
+    const bool ql = hf == 1 && r < HC;           // decoupled control z(r)
     const double dt = p.dt;
     const size_t kq = b * p.Kc + kc;
     STAMP(0);
@@ -363,8 +415,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         for (int j = 0; j < 9; ++j) a += sc[j] * S.Gn[j];
         qx = lq[LQ_LX + r] + (gn + a);
     }
-    const int rx = xl ? r : 0;  // row of T_c on the Qux lanes
-    const int rq = ql ? r : 0;  // column of T_c on the Quu lanes
+    const int rq = qr ? pos : 0;  // column of T_c on the Quu lanes (= r on the ql lanes)
     const int lr = rq / 3, ar = rq % 3;
     double rb3[3];              // row ar of leg lr's ReB Hessian block, stored (00,01,02,11,12,22)
 #pragma unroll
@@ -376,160 +427,116 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     const bool stz = pick4(pc.c, lr) != 0;
     const double qzz = dt * (stz ? p.r_qJd : p.r_grf) + reg;
     const double quz = lq[LQ_LU + (stz ? HC + rq : rq)];
-    HSYNC();  // the LQ copy is dead from here; S.A takes Y2, then the Z rows
-    double z[HC];
+    HSYNC();  // the LQ copy is dead from here: S.A takes Qux_c, Quu_cc, then Quu^-1 and Kp
     {
-        const int rr = rowl ? r : 0, rt = r < HC ? r : 0;
+        const int rt = r < HC ? r : 0;
         double col[9], y[HC];
-        // Y2 = S^T T_c: column r (< 12) of it, this half's rows -> S.A row-major [24][12]
+        // Qux_c^T = A^T T_c = T_c + S^T T_c: lane (hf, q < 12) forms column q of S^T T_c on its
+        // half's rows and writes row q of Qux_c [12][XS] (its half's columns)
 #pragma unroll
         for (int j = 0; j < 9; ++j) col[j] = S.Bm[j * HC + rt];
         st_apply(lqs, dt, hf, col, y);
         if (r < HC)
 #pragma unroll
-            for (int i = 0; i < HC; ++i) S.A[(cb + i) * HC + r] = y[i];
-        // Z = M + (S^T M9)^T on this lane's row: Qxx = lxx + Z^T-symmetric part (below)
-#pragma unroll
-        for (int j = 0; j < 9; ++j) col[j] = S.Bm[OFF_M9 + j * NX + rr];
-        st_apply(lqs, dt, hf, col, y);
-#pragma unroll
-        for (int i = 0; i < HC; ++i) z[i] = m[i] + y[i];
+            for (int i = 0; i < HC; ++i) S.A[OFF_QX + r * XS + cb + i] = S.Bm[(cb + i) * HC + r] + y[i];
     }
-    pin(z);
-    HSYNC();
-    STAMP(3);
-    // Every lane evaluates all three column roles and selects its own: the two halves would run
-    // both sides of a divergent branch anyway, and straight-line code keeps the register
-    // allocator from spilling live values around the branches.
-    double w[HC];
+    // Quu_cc = luu + B_c^T T_c + reg I by columns (lane 32 + q writes column q into S.A at OFF_QU)
+    // and Qu_c = lu_c + B_c^T Gnext (lane 60, into S.d).  Every lane evaluates both formulas: the
+    // instructions are issued for all lanes either way.
     static_for<HC>([&](auto I) {
         constexpr int q = I, l = q / 3, a = q % 3;
         const bool st = pc.c[l] != 0;
-        // (A^T T_c)[r][q] = T_c[r][q] + (S^T T_c)[r][q]: row r of Qux_c^T
-        const double vx = S.Bm[rx * HC + q] + S.A[rx * HC + q];
-        // column r of Quu_cc = luu + B_c^T T_c + reg I
         const double vs = lqs[LQ_BW + q] * S.Bm[6 * HC + rq] + lqs[LQ_BW + 12 + q] * S.Bm[7 * HC + rq] +
                           lqs[LQ_BW + 24 + q] * S.Bm[8 * HC + rq] + pc.bv[l] * S.Bm[(9 + a) * HC + rq];
         const double vw = pc.bq[l] * S.Bm[(HC + q) * HC + rq];
         const double lu =
             st ? (q == rq ? dt * p.r_grf : 0.0) + (lr == l ? rb3[a] : 0.0) : (q == rq ? dt * p.r_qJd : 0.0);
         const double vu = lu + (st ? vs : vw) + (q == rq ? reg : 0.0);
-        // Qu_c = lu_c + B_c^T Gnext
         const double vg = st ? lqs[LQ_LU + q] + (lqs[LQ_BW + q] * S.Gn[6] + lqs[LQ_BW + 12 + q] * S.Gn[7] +
                                                  lqs[LQ_BW + 24 + q] * S.Gn[8] + pc.bv[l] * S.Gn[9 + a])
                              : lqs[LQ_LU + HC + q] + pc.bq[l] * S.Gn[HC + q];
-        w[q] = xl ? vx : ql ? vu : ul ? vg : 0.0;
-        asm volatile("" : "+v"(w[q]));
+        if (ql) S.A[OFF_QU + r * HC + q] = vu;
+        if (ul) S.d[q] = vg;
         SFENCE();
     });
-    HSYNC();
-    // Qxx = lxx + M + S^T M9 and lxx is symmetric, so (Qxx + Qxx^T) / 2 (SinglePhase.cpp:352)
-    // = lxx + (Z + Z^T) / 2 with Z = M + (S^T M9)^T; kept in LDS as a packed upper triangle
+    STAMP(3);
+    // Z = M + (S^T M9)^T on this lane's row: Qxx = lxx + Z^T-symmetric part (below)
+    double z[HC];
+    {
+        const int rr = rowl ? r : 0;
+        double col[9], y[HC];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) col[j] = S.Bm[OFF_M9 + j * NX + rr];
+        st_apply(lqs, dt, hf, col, y);
+#pragma unroll
+        for (int i = 0; i < HC; ++i) z[i] = m[i] + y[i];
+    }
+    HSYNC();  // T_c and M9 are dead: Bm takes the Z rows
     if (rowl)
 #pragma unroll
-        for (int i = 0; i < HC; ++i) S.A[r * XS + cb + i] = z[i];
+        for (int i = 0; i < HC; ++i) S.Bm[r * XS + cb + i] = z[i];
     HSYNC();
     STAMP(4);
+    // Qxx = lxx + M + S^T M9 and lxx is symmetric, so (Qxx + Qxx^T) / 2 (SinglePhase.cpp:352)
+    // = lxx + (Z + Z^T) / 2, symmetrised in place: every lane reads its 12 transposed entries
+    // before any lane writes, then updates its own row entry by entry (only it reads that row
+    // from here on)
     if (rowl) {
         LxxRow lx_;
         lxx_row(p, pc, r, lx_);
+        double zt[HC];
+#pragma unroll
+        for (int i = 0; i < HC; ++i) zt[i] = S.Bm[(cb + i) * XS + r];
+        LSYNC();
         static_for<HC>([&](auto I) {
             constexpr int i = I;
             const int c = cb + i;
-            S.Bm[r * XS + c] = lxx_half<i>(lx_, r, hf) + (c == r ? reg : 0.0) + (S.A[r * XS + c] + S.A[c * XS + r]) / 2;
+            S.Bm[r * XS + c] = lxx_half<i>(lx_, r, hf) + (c == r ? reg : 0.0) + (S.Bm[r * XS + c] + zt[i]) / 2;
         });
     }
     HSYNC();
+    // elimination operand, one column of [Quu_cc | I | Qu_c] per lane: lane 16 R + j (j < 12)
+    // holds column j of Quu_cc in each of the four 16-lane DPP rows R, lanes 16 R + 12 + t
+    // (R < 3) column 4 R + t of the identity, lane 60 Qu_c
+    double w[HC];
+#pragma unroll
+    for (int q = 0; q < HC; ++q) {
+        const double vu = S.A[OFF_QU + (qr ? pos : 0) * HC + q], vg = S.d[q];
+        w[q] = qr ? vu : il ? (q == ic ? 1.0 : 0.0) : ul ? vg : 0.0;
+    }
     STAMP(5);
-    // pre-elimination Qux_c (rows q) and Qu_c for the value update
-    if (xl)
-#pragma unroll
-        for (int q = 0; q < HC; ++q) S.A[q * NX + r] = w[q];
-    if (ul)
-#pragma unroll
-        for (int q = 0; q < HC; ++q) S.d[q] = w[q];
-    SFENCE();
     // PSD test (LDLT of Quu - 1e-9 I, SinglePhase.cpp:342-348): the decoupled diagonal, then
     // every Gauss-Jordan pivot of the coupled block.  ballot is convergent, so each test stays
     // in its step.
     unsigned long long bad = __builtin_amdgcn_ballot_w64(ql && !(qzz > 1e-9));
-    // Gauss-Jordan on [Quu_cc | Qux_c | Qu_c] (one column per lane): pivot column j comes from
-    // lane 32 + j (GJ_BCAST 0: v_readlane through SGPRs; 1: LDS store + broadcast read;
-    // 2: ds_bpermute)
-#ifndef GJ_BCAST
-#define GJ_BCAST 0
-#endif
-    double *pcol = S.Bm + NX * (NX + 1) / 2;  // free during the elimination: Bm past the packed Qxx
-#if GJ_PIPE
-    // pivot reciprocal one step ahead: row j+1 is updated first, its value on lane 32 + j + 1 is
-    // the next pivot, and its reciprocal is formed while the other rows are updated
-    double inv = recip(lane_value(w[0], 32));
+    // Gauss-Jordan without pivoting (Quu_cc is SPD when it passes): step j takes column j of
+    // Quu_cc from position j of the lane's own DPP row (row_newbcast, fused into the FMA), so no
+    // value leaves the VALU.  Afterwards the identity lanes hold Quu_cc^-1 — the reference's
+    // explicit inverse (Quu.inverse(), SinglePhase.cpp:351) — and lane 60 Quu_cc^-1 Qu_c.
     static_for<HC>([&](auto J) {
         constexpr int j = J;
-        double col[HC];
-#pragma unroll
-        for (int i = 0; i < HC; ++i) col[i] = (i == j) ? 0.0 : lane_value(w[i], 32 + j);
-        const double piv = lane_value(w[j], 32 + j);
+        const double piv = row_bcast<j>(w[j]);
         bad |= __builtin_amdgcn_ballot_w64(!(piv > 1e-9));
-        const double f = w[j] * inv;
-        if constexpr (j + 1 < HC) {
-            w[j + 1] -= col[j + 1] * f;
-            inv = recip(lane_value(w[j + 1], 32 + j + 1));
-        }
-#pragma unroll
-        for (int i = 0; i < HC; ++i)
-            if (i != j && i != j + 1) w[i] -= col[i] * f;
+        const double f = w[j] * recip(piv), nf = -f;
+        static_for<HC>([&](auto I) {
+            constexpr int i = I;
+            if constexpr (i != j) fmac_row_bcast<j, i == (j + HC - 1) % HC>(w[i], nf);
+        });
         w[j] = f;
-        pin(w);
-    });
-#else
-    static_for<HC>([&](auto J) {
-        constexpr int j = J;
-        double col[HC];
-#if GJ_BCAST == 0
-#pragma unroll
-        for (int i = 0; i < HC; ++i) col[i] = lane_value(w[i], 32 + j);
-#elif GJ_BCAST == 1
-        if (lane == 32 + j)
-#pragma unroll
-            for (int i = 0; i < HC; ++i) pcol[i] = w[i];
-        HSYNC();
-#pragma unroll
-        for (int i = 0; i < HC; ++i) col[i] = pcol[i];
-#else
-#pragma unroll
-        for (int i = 0; i < HC; ++i) col[i] = __shfl(w[i], 32 + j);
-#endif
-        const double piv = col[j];
-        bad |= __builtin_amdgcn_ballot_w64(!(piv > 1e-9));
-        const double f = w[j] * recip(piv);
-#pragma unroll
-        for (int i = 0; i < HC; ++i)
-            if (i != j) w[i] -= col[i] * f;
-        w[j] = f;
-        pin(w);
-#if GJ_BCAST == 1
-        HSYNC();
-#endif
         SFENCE();
     });
-#endif
     STAMP(6);
     live = live && bad == 0;
     if (!live) return;
-    // K = -Quu^-1 Qux, dU = -Quu^-1 Qu; K rows of decoupled controls are zero
-    if (xl)
+    // Quu_cc^-1 by columns [c][16] (rows 12..15 read as zero) and Quu_cc^-1 Qu_c into LDS
+    if (il)
 #pragma unroll
-        for (int q = 0; q < HC; ++q) S.A[OFF_KP + q * NX + r] = w[q];
+        for (int q = 0; q < HC; ++q) S.A[OFF_QI + ic * 16 + q] = w[q];
     if (ul)
 #pragma unroll
         for (int q = 0; q < HC; ++q) S.wqu[q] = w[q];
+    // dU = -Quu^-1 Qu: coupled controls from lane 60, decoupled ones (Qu_z / Quu_zz) from the ql lanes
     double *dUg = d.dU + kq * NX;
-    if (xl) { // compact gain rows (KCW layout)
-        double *Kg = d.K + kq * KCW + r;
-#pragma unroll
-        for (int q = 0; q < HC; ++q) Kg[q * NX] = -w[q];
-    }
     if (ul)
         static_for<HC>([&](auto I) {
             constexpr int q = I;
@@ -542,10 +549,39 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         dvp = quz * duz;
     }
     HSYNC();
+    typedef double d4 __attribute__((ext_vector_type(4)));
+    const int li = lane & 15, lk = lane >> 4;
+    // Kp = Quu_cc^-1 Qux_c (12 x 24, K = 12) on the matrix cores (v_mfma_f64_16x16x4_f64; operands
+    // A[l & 15][k = l >> 4], B[k = l >> 4][l & 15]; result rows (l >> 4) + 4 reg, column l & 15):
+    // into LDS for the value update, and K = -Kp to the compact gain rows (KCW layout)
+    {
+        d4 k0 = {0, 0, 0, 0}, k1 = k0;
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+            const int c = 4 * ks + lk;
+            const double a = li < HC ? S.A[OFF_QI + c * 16 + li] : 0.0;
+            const double b0 = S.A[OFF_QX + c * XS + li], b1 = S.A[OFF_QX + c * XS + 16 + li];
+            k0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b0, k0, 0, 0, 0);
+            k1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b1, k1, 0, 0, 0);
+        }
+        HSYNC();  // Quu^-1 is read; Kp takes its place
+        double *Kg = d.K + kq * KCW;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            const int q = lk + 4 * g;
+            S.A[OFF_KP + q * XS + li] = k0[g];
+            Kg[q * NX + li] = -k0[g];
+            if (li < NX - 16) {
+                S.A[OFF_KP + q * XS + 16 + li] = k1[g];
+                Kg[q * NX + 16 + li] = -k1[g];
+            }
+        }
+    }
+    HSYNC();
     STAMP(7);
     if (ul)
 #pragma unroll
-        for (int q = 0; q < HC; ++q) dvp += S.d[q] * w[q];
+        for (int q = 0; q < HC; ++q) dvp += S.d[q] * S.wqu[q];
     // expected cost change Qu^T Quu^-1 Qu (SinglePhase.cpp:357-358): half 1 holds every term
     const double dvk = lane_value(half_sum(dvp), 32);
     dV1 -= dvk;
@@ -554,33 +590,31 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     const int rr = rowl ? r : 0;
     double gp = 0.0;
 #pragma unroll
-    for (int q = 0; q < HC; ++q) gp += S.A[q * NX + rr] * S.wqu[q];
+    for (int q = 0; q < HC; ++q) gp += S.A[OFF_QX + q * XS + rr] * S.wqu[q];
     g = rowl ? qx - gp : 0.0;
-    // P = Qux_c^T Kp (24 x 24, K = 12) on the matrix cores: v_mfma_f64_16x16x4_f64 over 2 x 2
-    // output tiles (rows / columns 24..31 are padding and discarded) and 3 k-steps.  Operands
-    // (MI355X layout): A[l & 15][k = l >> 4], B[k = l >> 4][l & 15]; result rows
-    // (l >> 4) + 4 reg, column l & 15.  H = Qxx - P is formed in place of Qxx in LDS (each entry
-    // read and written by the same lane), then read back as rows.
+    // P = Qux_c^T Kp (24 x 24, K = 12) on the matrix cores over the output tiles (0,0), (0,1) and
+    // (1,1) — P is symmetric, tile (1,0) is (0,1)^T — rows / columns 24..31 are padding.  H = Qxx - P
+    // is formed in place of Qxx in LDS (each entry read and written by one lane), then read back
+    // as rows.
     {
-        typedef double d4 __attribute__((ext_vector_type(4)));
-        d4 t00 = {0, 0, 0, 0}, t01 = t00, t10 = t00, t11 = t00;
-        const int li = lane & 15, lk = lane >> 4;
+        d4 t00 = {0, 0, 0, 0}, t01 = t00, t11 = t00;
 #pragma unroll
         for (int ks = 0; ks < 3; ++ks) {
             const int q = 4 * ks + lk;
-            const double a0 = S.A[q * NX + li], a1 = S.A[q * NX + 16 + li];
-            const double b0 = S.A[OFF_KP + q * NX + li], b1 = S.A[OFF_KP + q * NX + 16 + li];
+            const double a0 = S.A[OFF_QX + q * XS + li], a1 = S.A[OFF_QX + q * XS + 16 + li];
+            const double b0 = S.A[OFF_KP + q * XS + li], b1 = S.A[OFF_KP + q * XS + 16 + li];
             t00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, t00, 0, 0, 0);
             t01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, t01, 0, 0, 0);
-            t10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, t10, 0, 0, 0);
             t11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, t11, 0, 0, 0);
         }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int r0 = lk + 4 * g, r1 = 16 + r0, c1 = 16 + li;
             S.Bm[r0 * XS + li] -= t00[g];
-            if (c1 < NX) S.Bm[r0 * XS + c1] -= t01[g];
-            if (r1 < NX) S.Bm[r1 * XS + li] -= t10[g];
+            if (c1 < NX) {
+                S.Bm[r0 * XS + c1] -= t01[g];
+                S.Bm[c1 * XS + r0] -= t01[g];
+            }
             if (r1 < NX && c1 < NX) S.Bm[r1 * XS + c1] -= t11[g];
         }
     }
@@ -728,10 +762,6 @@ struct LinElem {
     double dx[NX], du[NX];
 };
 
-// single-wave workgroup: LDS operations of one wave complete in order, so a compiler barrier is
-// enough between stages, and no __syncthreads fence drains the LDS-DMA in flight
-#define LSYNC() asm volatile("" ::: "memory")
-
 // Issued as inline asm so the waitcnt pass does not track the LDS writes (it would otherwise wait
 // for every DMA in flight before any LDS read); lin_knot waits explicitly.  LDS destination of
 // piece t: M0 + 16 * lane, contiguous.
@@ -748,7 +778,11 @@ DEV void lin_fetch(LinBuf &buf, const Params &p, const Bufs &d, size_t b, int s,
         const size_t base = o < LB_LQ ? kB : o < LB_D ? lB : o < LB_DU ? dB : uB;
         const double *src = (const double *)(base + 8 * (size_t)o);
         const unsigned m0 = (unsigned)(size_t)(buf.v + 128 * t);
-        asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(m0) : "memory");
+        unsigned keep;  // M0 is compiler-reserved: saved, set (one wait state before the DMA), restored
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(src), "s"(m0)
+                     : "memory");
     }
 }
 

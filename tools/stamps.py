@@ -17,8 +17,9 @@ sys.path.insert(0, os.path.join(ROOT, "hkd-mpc_amd"))
 import hsddp  # noqa: E402
 from hsddp import synthetic  # noqa: E402
 
-STAGES = ["stage inputs -> LDS", "T_c, M rows (stage A)", "sc/qx/rb + Qxx rows", "Qux/Quu/Qu columns",
-          "symmetrise Qxx", "Gauss-Jordan (12 steps)", "K, dU stores, dV", "value update H, G"]
+STAGES = ["stage inputs -> LDS", "M, T_c rows (stage A)", "Qx, Qux_c, Quu/Qu columns", "Z rows",
+          "symmetrise Qxx, load operand", "Gauss-Jordan (12 steps)", "Quu^-1, dU, Kp/K (MFMA)",
+          "dV, G, value update (MFMA)"]
 
 
 def main():
