@@ -33,14 +33,15 @@ using namespace hkd;
 
 constexpr int HC = 12;      // columns per half-wave; coupled controls per knot
 constexpr int XS = 25;      // padded row stride of the LDS matrix (row-per-lane writes without conflicts)
-constexpr int OFF_M9 = NX * HC;  // M rows 0..8 after T_c in Bm
+constexpr int OFF_M9 = 0;  // M rows 0..8 [9][24] in Bm until the Z rows take their place
 // S.A regions (doubles): the knot's LQ record [0, LQW) until Qux_c [12][XS] takes its place;
-// above it Quu_cc by columns [12][12], then Quu_cc^-1 by columns [12][16], then Kp [12][XS] (each
-// read before the next overwrites it).
+// above it T_c = H B_c [24][12], then Quu_cc^-1 by columns [12][16], then Kp [12][XS] (each read
+// before the next overwrites it).
 constexpr int OFF_QX = 0;
-constexpr int OFF_QU = HC * XS;
+constexpr int OFF_TC = HC * XS;
 constexpr int OFF_QI = HC * XS;
 constexpr int OFF_KP = HC * XS;
+static_assert(LQW <= OFF_TC && OFF_TC + NX * HC <= NX * XS, "S.A layout");
 
 #ifndef HSDDP_STAMPS
 #define HSDDP_STAMPS 0
@@ -313,9 +314,9 @@ DEV double half_sum(double v)
     return v;
 }
 
-// One knot of SinglePhase::backward_sweep (SinglePhase.cpp:298-362).  h/g hold this lane's
-// columns of H[k+1] row r and G[k+1][r] on entry, H[k] and G[k] on exit.  `live` turns false
-// when Quu fails the PSD test (wave-uniform).
+// One knot of SinglePhase::backward_sweep (SinglePhase.cpp:298-362).  H[k+1] rows are in S.Bm
+// (stride XS) and g holds G[k+1][r] on entry; H[k] and G[k] on exit.  `live` turns false when
+// Quu fails the PSD test (wave-uniform).
 //
 // Coupled controls: for leg l the three GRF columns of B carry a factor c_l and the three
 // joint-velocity columns a factor (1 - c_l) (HKDDynamics: contact_moment, B rows 9..23), so
@@ -326,7 +327,7 @@ DEV double half_sum(double v)
 // so Quu^-1 [Qux | Qu] = [Quu_cc^-1 [Qux_c | Qu_c] ; 0 | Qu_z / Quu_zz] exactly, and the
 // reference's 24-control solve reduces to a 12 x 12 one plus 12 divisions.
 DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &pc, size_t b, int s, int kc,
-                  double reg, bool &live, double (&h)[HC], double &g, double &dV1, double &dV2)
+                  double reg, bool &live, double &g, double &dV1, double &dV2)
 {
     // opaque per knot: keeps LICM from hoisting lane-dependent constants of the knot body
     // (regularised diagonals, lxx entries) out of the knot loop into long-lived VGPRs
@@ -347,6 +348,9 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     cdouble *lqs = uniform_ptr(d.lq + kq * LQW);
     double *lq = S.A;  // LDS copy for lane-indexed reads
     stage_knot_inputs(lq, d.lq + kq * LQW, S.d, d.Defect + (b * p.S + s + 1) * NX, lane);
+    double h[HC];  // this lane's columns of H[k+1] row r
+#pragma unroll
+    for (int i = 0; i < HC; ++i) h[i] = rowl ? S.Bm[r * XS + cb + i] : 0.0;
     HSYNC();
     STAMP(1);
     // Gnext = G + H Defect[k+1] (SinglePhase.cpp:320)
@@ -389,11 +393,13 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     }
     pin(m);
     pin(tc);
+    // T_c[r][q] = the two halves' values summed (one of them is exactly 0): every lane gets the
+    // full row, half 0 stores columns 0..5 and half 1 columns 6..11 (no branch on the contacts)
+#pragma unroll
+    for (int q = 0; q < HC; ++q) tc[q] += other_half(tc[q]);
     if (rowl)
-        static_for<HC>([&](auto I) {
-            constexpr int q = I;
-            if ((hf == 0) == (pc.c[q / 3] != 0)) S.Bm[r * HC + q] = tc[q];
-        });
+#pragma unroll
+        for (int i = 0; i < HC / 2; ++i) S.A[OFF_TC + r * HC + HC / 2 * hf + i] = hf ? tc[HC / 2 + i] : tc[i];
     if (r < 9)
 #pragma unroll
         for (int i = 0; i < HC; ++i) S.Bm[OFF_M9 + r * NX + cb + i] = m[i];
@@ -415,51 +421,27 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         for (int j = 0; j < 9; ++j) a += sc[j] * S.Gn[j];
         qx = lq[LQ_LX + r] + (gn + a);
     }
-    const int rq = qr ? pos : 0;  // column of T_c on the Quu lanes (= r on the ql lanes)
+    // lane-indexed coefficients of control rq (the Quu row / decoupled-control lanes): leg lr,
+    // axis ar, B_c column rq (rows 6..8 from the LQ record, row 9 + ar or 12 + rq from the contact)
+    const int rq = qr ? pos : 0;
     const int lr = rq / 3, ar = rq % 3;
-    double rb3[3];              // row ar of leg lr's ReB Hessian block, stored (00,01,02,11,12,22)
+    const bool stz = pick4(pc.c, lr) != 0;
+    double rb3[3];  // row ar of leg lr's ReB Hessian block, stored (00,01,02,11,12,22)
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const int lo = min(a, ar), hi = max(a, ar);
         rb3[a] = lq[LQ_RB + 6 * lr + (lo == 0 ? hi : lo == 1 ? 2 + hi : 5)];
     }
+    const double bw0 = lq[LQ_BW + rq], bw1 = lq[LQ_BW + 12 + rq], bw2 = lq[LQ_BW + 24 + rq];
     // decoupled control z(r) on the ql lanes: Qu_z, Quu_zz
-    const bool stz = pick4(pc.c, lr) != 0;
     const double qzz = dt * (stz ? p.r_qJd : p.r_grf) + reg;
     const double quz = lq[LQ_LU + (stz ? HC + rq : rq)];
-    HSYNC();  // the LQ copy is dead from here: S.A takes Qux_c, Quu_cc, then Quu^-1 and Kp
-    {
-        const int rt = r < HC ? r : 0;
-        double col[9], y[HC];
-        // Qux_c^T = A^T T_c = T_c + S^T T_c: lane (hf, q < 12) forms column q of S^T T_c on its
-        // half's rows and writes row q of Qux_c [12][XS] (its half's columns)
-#pragma unroll
-        for (int j = 0; j < 9; ++j) col[j] = S.Bm[j * HC + rt];
-        st_apply(lqs, dt, hf, col, y);
-        if (r < HC)
-#pragma unroll
-            for (int i = 0; i < HC; ++i) S.A[OFF_QX + r * XS + cb + i] = S.Bm[(cb + i) * HC + r] + y[i];
+    // Qu_c[q] = lu_c + B_c^T Gnext on lane q < 12 (into S.d)
+    if (lane < HC) {
+        const double gb = stz ? (bw0 * S.Gn[6] + bw1 * S.Gn[7] + bw2 * S.Gn[8]) + p.dt_m * S.Gn[9 + ar]
+                              : dt * S.Gn[HC + rq];
+        S.d[lane] = lq[LQ_LU + (stz ? rq : HC + rq)] + gb;
     }
-    // Quu_cc = luu + B_c^T T_c + reg I by columns (lane 32 + q writes column q into S.A at OFF_QU)
-    // and Qu_c = lu_c + B_c^T Gnext (lane 60, into S.d).  Every lane evaluates both formulas: the
-    // instructions are issued for all lanes either way.
-    static_for<HC>([&](auto I) {
-        constexpr int q = I, l = q / 3, a = q % 3;
-        const bool st = pc.c[l] != 0;
-        const double vs = lqs[LQ_BW + q] * S.Bm[6 * HC + rq] + lqs[LQ_BW + 12 + q] * S.Bm[7 * HC + rq] +
-                          lqs[LQ_BW + 24 + q] * S.Bm[8 * HC + rq] + pc.bv[l] * S.Bm[(9 + a) * HC + rq];
-        const double vw = pc.bq[l] * S.Bm[(HC + q) * HC + rq];
-        const double lu =
-            st ? (q == rq ? dt * p.r_grf : 0.0) + (lr == l ? rb3[a] : 0.0) : (q == rq ? dt * p.r_qJd : 0.0);
-        const double vu = lu + (st ? vs : vw) + (q == rq ? reg : 0.0);
-        const double vg = st ? lqs[LQ_LU + q] + (lqs[LQ_BW + q] * S.Gn[6] + lqs[LQ_BW + 12 + q] * S.Gn[7] +
-                                                 lqs[LQ_BW + 24 + q] * S.Gn[8] + pc.bv[l] * S.Gn[9 + a])
-                             : lqs[LQ_LU + HC + q] + pc.bq[l] * S.Gn[HC + q];
-        if (ql) S.A[OFF_QU + r * HC + q] = vu;
-        if (ul) S.d[q] = vg;
-        SFENCE();
-    });
-    STAMP(3);
     // Z = M + (S^T M9)^T on this lane's row: Qxx = lxx + Z^T-symmetric part (below)
     double z[HC];
     {
@@ -471,38 +453,65 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
 #pragma unroll
         for (int i = 0; i < HC; ++i) z[i] = m[i] + y[i];
     }
-    HSYNC();  // T_c and M9 are dead: Bm takes the Z rows
+    HSYNC();  // the LQ copy and M9 are dead: S.A takes Qux_c below T_c, Bm the Z rows
+    STAMP(3);
     if (rowl)
 #pragma unroll
         for (int i = 0; i < HC; ++i) S.Bm[r * XS + cb + i] = z[i];
+    {
+        // Qux_c^T = A^T T_c = T_c + S^T T_c: lane (hf, q < 12) forms column q of S^T T_c on its
+        // half's rows and writes row q of Qux_c [12][XS] (its half's columns); every read is
+        // issued before the first write
+        const int rt = r < HC ? r : 0;
+        double col[9], y[HC], t[HC];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) col[j] = S.A[OFF_TC + j * HC + rt];
+#pragma unroll
+        for (int i = 0; i < HC; ++i) t[i] = S.A[OFF_TC + (cb + i) * HC + rt];
+        st_apply(lqs, dt, hf, col, y);
+        if (r < HC)
+#pragma unroll
+            for (int i = 0; i < HC; ++i) S.A[OFF_QX + r * XS + cb + i] = t[i] + y[i];
+    }
     HSYNC();
     STAMP(4);
     // Qxx = lxx + M + S^T M9 and lxx is symmetric, so (Qxx + Qxx^T) / 2 (SinglePhase.cpp:352)
-    // = lxx + (Z + Z^T) / 2, symmetrised in place: every lane reads its 12 transposed entries
-    // before any lane writes, then updates its own row entry by entry (only it reads that row
-    // from here on)
+    // = lxx + (Z + Z^T) / 2, symmetrised in place: every lane reads its row and its 12 transposed
+    // entries before any lane writes
     if (rowl) {
         LxxRow lx_;
         lxx_row(p, pc, r, lx_);
-        double zt[HC];
+        double zt[HC], zo[HC];
 #pragma unroll
-        for (int i = 0; i < HC; ++i) zt[i] = S.Bm[(cb + i) * XS + r];
+        for (int i = 0; i < HC; ++i) {
+            zt[i] = S.Bm[(cb + i) * XS + r];
+            zo[i] = S.Bm[r * XS + cb + i];
+        }
         LSYNC();
         static_for<HC>([&](auto I) {
             constexpr int i = I;
             const int c = cb + i;
-            S.Bm[r * XS + c] = lxx_half<i>(lx_, r, hf) + (c == r ? reg : 0.0) + (S.Bm[r * XS + c] + zt[i]) / 2;
+            S.Bm[r * XS + c] = lxx_half<i>(lx_, r, hf) + (c == r ? reg : 0.0) + (zo[i] + zt[i]) / 2;
         });
     }
-    HSYNC();
     // elimination operand, one column of [Quu_cc | I | Qu_c] per lane: lane 16 R + j (j < 12)
-    // holds column j of Quu_cc in each of the four 16-lane DPP rows R, lanes 16 R + 12 + t
-    // (R < 3) column 4 R + t of the identity, lane 60 Qu_c
+    // holds column j of Quu_cc = luu + B_c^T T_c + reg I in each of the four 16-lane DPP rows R,
+    // lanes 16 R + 12 + t (R < 3) column 4 R + t of the identity, lane 60 Qu_c
+    // (SinglePhase.cpp:323-327; regularisation MultiPhaseDDP.cpp:160)
     double w[HC];
-#pragma unroll
-    for (int q = 0; q < HC; ++q) {
-        const double vu = S.A[OFF_QU + (qr ? pos : 0) * HC + q], vg = S.d[q];
-        w[q] = qr ? vu : il ? (q == ic ? 1.0 : 0.0) : ul ? vg : 0.0;
+    {
+        const double *tc = S.A + OFF_TC;
+        static_for<HC>([&](auto I) {
+            constexpr int q = I, l = q / 3, a = q % 3;
+            const bool st = pc.c[l] != 0;
+            const double vs = lqs[LQ_BW + q] * tc[6 * HC + rq] + lqs[LQ_BW + 12 + q] * tc[7 * HC + rq] +
+                              lqs[LQ_BW + 24 + q] * tc[8 * HC + rq] + pc.bv[l] * tc[(9 + a) * HC + rq];
+            const double vw = pc.bq[l] * tc[(HC + q) * HC + rq];
+            const double lu =
+                st ? (q == rq ? dt * p.r_grf : 0.0) + (lr == l ? rb3[a] : 0.0) : (q == rq ? dt * p.r_qJd : 0.0);
+            const double vu = lu + (st ? vs : vw) + (q == rq ? reg : 0.0);
+            w[q] = qr ? vu : il ? (q == ic ? 1.0 : 0.0) : ul ? S.d[q] : 0.0;
+        });
     }
     STAMP(5);
     // PSD test (LDLT of Quu - 1e-9 I, SinglePhase.cpp:342-348): the decoupled diagonal, then
@@ -619,9 +628,6 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         }
     }
     HSYNC();
-#pragma unroll
-    for (int i = 0; i < HC; ++i) h[i] = rowl ? S.Bm[rr * XS + cb + i] : 0.0;
-    HSYNC();
     STAMP(8);
 }
 
@@ -631,36 +637,32 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double 
 {
     const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5, cb = HC * hf;
     const bool rowl = r < NX;
-    double h[HC], g = 0.0;
+    double g = 0.0;  // G[r]; the value Hessian H stays in S.Bm rows
     bool live = true;
     dV1 = 0.0; dV2 = 0.0;
     for (int i = p.P - 1; i >= 0; --i) {
         PhaseConst pc;
         load_phase(p, d, b, i, pc);
         const double *rec = d.term + (b * p.P + i) * TW;
+        double h[HC];
         if (i == p.P - 1) {
 #pragma unroll
             for (int c = 0; c < HC; ++c) h[c] = rowl ? rec[TM_PHIXX + r * NX + cb + c] : 0.0;
             g = rowl ? rec[TM_PHIX + r] : 0.0;
         } else {
             // impact-aware step G' = Phix + Px^T G0, H' = Phixx + Px^T H0 Px
-            // (MultiPhaseDDP.cpp:480-484): W = H0 Px in place of H0 in LDS, then Px^T W.
+            // (MultiPhaseDDP.cpp:480-484): W = H0 Px into S.A, then Px^T W.
             const double *Px = rec + TM_PX;
-            if (rowl)
-#pragma unroll
-                for (int c = 0; c < HC; ++c) S.A[r * XS + cb + c] = h[c];
             if (lane < NX) S.Gn[lane] = g;
-            HSYNC();
             double w[HC];
 #pragma unroll
             for (int c = 0; c < HC; ++c) w[c] = 0.0;
             if (rowl)
                 for (int k = 0; k < NX; ++k) {
-                    const double hk = S.A[r * XS + k];
+                    const double hk = S.Bm[r * XS + k];
 #pragma unroll
                     for (int c = 0; c < HC; ++c) w[c] += hk * Px[k * NX + cb + c];
                 }
-            HSYNC();
             if (rowl)
 #pragma unroll
                 for (int c = 0; c < HC; ++c) S.A[r * XS + cb + c] = w[c];
@@ -678,19 +680,24 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double 
 #pragma unroll
             for (int c = 0; c < HC; ++c) h[c] = rowl ? rec[TM_PHIXX + r * NX + cb + c] + w[c] : 0.0;
             g = rowl ? rec[TM_PHIX + r] + gp : 0.0;
-            HSYNC();
         }
+        HSYNC();
+        if (rowl)
+#pragma unroll
+            for (int c = 0; c < HC; ++c) S.Bm[r * XS + cb + c] = h[c];
+        HSYNC();
         const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
 #pragma unroll 1
         for (int k = N - 1; k >= 0 && live; --k)
-            bwd_knot(p, d, S, pc, b, s0 + k, k0 + k, reg, live, h, g, dV1, dV2);
+            bwd_knot(p, d, S, pc, b, s0 + k, k0 + k, reg, live, g, dV1, dV2);
         if (!live) return false;
         // G[0] += H[0] Defect[0] (SinglePhase.cpp:365)
         if (lane < NX) S.d[lane] = d.Defect[(b * p.S + s0) * NX + lane];
         HSYNC();
         double a = 0.0;
+        if (rowl)
 #pragma unroll
-        for (int c = 0; c < HC; ++c) a += h[c] * S.d[cb + c];
+            for (int c = 0; c < HC; ++c) a += S.Bm[r * XS + cb + c] * S.d[cb + c];
         a += other_half(a);
         if (rowl) g += a;
         HSYNC();

@@ -2,7 +2,8 @@
 
 Tolerances (fp64): model primitives 1e-12 relative to the largest entry (different operation
 order than the CasADi graph); one/three inner iterations 1e-9 relative on K, dU, dX, X, U, Xbar,
-Ubar and exact equality of every branch decision (line-search trial counts, iteration counts,
+Ubar (or 10x the oracle's own deviation under a 1e-15 relative perturbation of x0, where that is
+larger: three jump iterations amplify rounding to ~1e-9) and exact equality of every branch decision (line-search trial counts, iteration counts,
 statuses); full solves 1e-7 relative on elements whose own oracle solution is insensitive to a
 1e-15 relative perturbation of x0 (the "chaos screen": a few jump elements wander for 50
 iterations and flip line-search decisions on rounding alone — the oracle disagrees with itself
@@ -86,8 +87,12 @@ def test_fixed_iterations_match_oracle(gait, P, N, n_iter):
     kw = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=n_iter)
     g = _run(prob, **kw)
     r = O.solve_batch(prob, O.default_options(**kw), n_threads=8)
+    # the oracle's own rounding envelope: its deviation under a 1e-15 relative change of x0
+    # (three jump iterations amplify rounding to ~1e-9 in dX; everywhere else it is ~1e-13)
+    p2 = dict(prob); p2["x0"] = prob["x0"] * (1 + 1e-15)
+    r2 = O.solve_batch(p2, O.default_options(**kw), n_threads=8)
     for f in ("Xbar", "Ubar", "K", "X", "U", "dX", "dU"):
-        assert rel(g[f], r[f]) < 1e-9, f
+        assert rel(g[f], r[f]) < max(1e-9, 10 * rel(r2[f], r[f])), f
     for f in ("cost", "feas", "max_tconstr"):
         assert rel(g[f], r[f]) < 1e-9, f
     for f in ("iters", "outer_iters", "status", "n_ls_trials"):
