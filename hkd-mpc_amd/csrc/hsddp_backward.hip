@@ -33,7 +33,7 @@ using namespace hkd;
 
 constexpr int HC = 12;      // columns per half-wave; coupled controls per knot
 constexpr int XS = 25;      // padded row stride of the LDS matrix (row-per-lane writes without conflicts)
-constexpr int OFF_M9 = 0;  // M rows 0..8 [9][24] in Bm until the Z rows take their place
+constexpr int OFF_M9 = 0;  // M rows 0..8 [9][XS] in Bm until the Z rows take their place
 // S.A regions (doubles): the knot's LQ record [0, LQW) until Qux_c [12][XS] takes its place;
 // above it T_c = H B_c [24][12], then Quu_cc^-1 by columns [12][16], then Kp [12][XS] (each read
 // before the next overwrites it).
@@ -241,6 +241,22 @@ DEV void lxx_row(const Params &p, const PhaseConst &pc, int r, LxxRow &L)
     }
 }
 
+// lxx row r from the per-phase diagonal table (column XS - 1 of the S.Bm rows, written by
+// bwd_sweep at the phase start): the foot cross terms are the negated diagonal entries of the
+// stance feet's rows, -lxx[12 + 3 l + a][12 + 3 l + a] (= -dt foot_gain w_a), so no parameter
+// is needed inside the knot loop
+DEV void lxx_row_table(const double *Bm, const PhaseConst &pc, int r, LxxRow &L)
+{
+    const int rr = r < NX ? r : 0;
+    const double dr = Bm[rr * XS + NX];
+    L.diag = r < NX ? dr : 0.0;
+    const bool pos = r >= 3 && r < 6;
+    const int a = pos ? r - 3 : 0;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) L.xq[l] = (pos && pc.c[l]) ? -Bm[(12 + 3 * l + a) * XS + NX] : 0.0;
+    L.xp = (r >= 12 && r < NX && pick4(pc.c, (rr - 12) / 3)) ? -dr : 0.0;
+}
+
 // lxx(r, 12 hf + i) for a compile-time i
 template <int i>
 DEV double lxx_half(const LxxRow &L, int r, int hf)
@@ -402,7 +418,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         for (int i = 0; i < HC / 2; ++i) S.A[OFF_TC + r * HC + HC / 2 * hf + i] = hf ? tc[HC / 2 + i] : tc[i];
     if (r < 9)
 #pragma unroll
-        for (int i = 0; i < HC; ++i) S.Bm[OFF_M9 + r * NX + cb + i] = m[i];
+        for (int i = 0; i < HC; ++i) S.Bm[OFF_M9 + r * XS + cb + i] = m[i];
     if (lane < NX) S.Gn[lane] = gn;
     HSYNC();
     SFENCE();
@@ -448,7 +464,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         const int rr = rowl ? r : 0;
         double col[9], y[HC];
 #pragma unroll
-        for (int j = 0; j < 9; ++j) col[j] = S.Bm[OFF_M9 + j * NX + rr];
+        for (int j = 0; j < 9; ++j) col[j] = S.Bm[OFF_M9 + j * XS + rr];
         st_apply(lqs, dt, hf, col, y);
 #pragma unroll
         for (int i = 0; i < HC; ++i) z[i] = m[i] + y[i];
@@ -480,7 +496,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     // entries before any lane writes
     if (rowl) {
         LxxRow lx_;
-        lxx_row(p, pc, r, lx_);
+        lxx_row_table(S.Bm, pc, r, lx_);
         double zt[HC], zo[HC];
 #pragma unroll
         for (int i = 0; i < HC; ++i) {
@@ -495,22 +511,23 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         });
     }
     // elimination operand, one column of [Quu_cc | I | Qu_c] per lane: lane 16 R + j (j < 12)
-    // holds column j of Quu_cc = luu + B_c^T T_c + reg I in each of the four 16-lane DPP rows R,
-    // lanes 16 R + 12 + t (R < 3) column 4 R + t of the identity, lane 60 Qu_c
+    // holds Quu_cc = luu + B_c^T T_c + reg I as row j (B_c column j against the rows of T_c:
+    // lane-indexed coefficients, broadcast rows, no scalar loads) in each of the four 16-lane DPP
+    // rows R, lanes 16 R + 12 + t (R < 3) column 4 R + t of the identity, lane 60 Qu_c
     // (SinglePhase.cpp:323-327; regularisation MultiPhaseDDP.cpp:160)
     double w[HC];
     {
-        const double *tc = S.A + OFF_TC;
+        const double bv = stz ? p.dt_m : 0.0, bq = stz ? 0.0 : dt;
+        const double ld = dt * (stz ? p.r_grf : p.r_qJd);
+        const double *t6 = S.A + OFF_TC + 6 * HC, *t9 = S.A + OFF_TC + (9 + ar) * HC,
+                     *tq = S.A + OFF_TC + (HC + rq) * HC;
         static_for<HC>([&](auto I) {
-            constexpr int q = I, l = q / 3, a = q % 3;
-            const bool st = pc.c[l] != 0;
-            const double vs = lqs[LQ_BW + q] * tc[6 * HC + rq] + lqs[LQ_BW + 12 + q] * tc[7 * HC + rq] +
-                              lqs[LQ_BW + 24 + q] * tc[8 * HC + rq] + pc.bv[l] * tc[(9 + a) * HC + rq];
-            const double vw = pc.bq[l] * tc[(HC + q) * HC + rq];
-            const double lu =
-                st ? (q == rq ? dt * p.r_grf : 0.0) + (lr == l ? rb3[a] : 0.0) : (q == rq ? dt * p.r_qJd : 0.0);
-            const double vu = lu + (st ? vs : vw) + (q == rq ? reg : 0.0);
-            w[q] = qr ? vu : il ? (q == ic ? 1.0 : 0.0) : ul ? S.d[q] : 0.0;
+            constexpr int c = I;
+            const double vs = bw0 * t6[c] + bw1 * t6[HC + c] + bw2 * t6[2 * HC + c] + bv * t9[c];
+            const double vw = bq * tq[c];
+            const double lu = stz ? (c == rq ? ld : 0.0) + (c / 3 == lr ? rb3[c % 3] : 0.0) : (c == rq ? ld : 0.0);
+            const double vu = lu + (stz ? vs : vw) + (c == rq ? reg : 0.0);
+            w[c] = qr ? vu : il ? (c == ic ? 1.0 : 0.0) : ul ? S.d[c] : 0.0;
         });
     }
     STAMP(5);
@@ -685,6 +702,11 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double 
         if (rowl)
 #pragma unroll
             for (int c = 0; c < HC; ++c) S.Bm[r * XS + cb + c] = h[c];
+        if (rowl && hf == 0) { // this phase's lxx diagonal into the padding column (lxx_row_table)
+            LxxRow lx_;
+            lxx_row(p, pc, r, lx_);
+            S.Bm[r * XS + NX] = lx_.diag;
+        }
         HSYNC();
         const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
 #pragma unroll 1
