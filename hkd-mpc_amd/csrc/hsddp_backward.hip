@@ -168,6 +168,7 @@ DEV void fmac_row_bcast(double &w, double s)
 // per-phase constants of one element
 struct PhaseConst {
     int c[4];
+    int cmask;     // bit l = c_l: a lane-dependent leg index becomes one shift, not a select chain
     double bv[4];  // dt c_l / m     (B rows 9..11)
     double bq[4];  // dt (1 - c_l)   (B rows 12..23)
 };
@@ -178,9 +179,11 @@ DEV void load_phase(const Params &p, const Bufs &d, size_t b, int i, PhaseConst 
 {
     typedef const __attribute__((address_space(4))) int cint;
     cint *cs = (cint *)(d.contacts + (b * (p.P + 1) + i) * 4);
+    pc.cmask = 0;
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
         pc.c[l] = cs[l];
+        pc.cmask |= (pc.c[l] != 0) << l;
         pc.bv[l] = pc.c[l] ? p.dt_m : 0.0;
         pc.bq[l] = pc.c[l] ? 0.0 : p.dt;
     }
@@ -190,6 +193,9 @@ DEV void load_phase(const Params &p, const Bufs &d, size_t b, int i, PhaseConst 
 struct LxxRow {
     double diag, xq[4], xp;  // xq[l]: (r in pos) x (col 12+3l+(r-3)); xp: (r in q) x (col 3+(r-12)%3)
 };
+
+// contact of leg l (runtime, lane-dependent) as 0 / 1
+DEV int contact(const PhaseConst &pc, int l) { return (pc.cmask >> l) & 1; }
 
 // a[i] for a runtime i, as selects (a runtime index would put the array in scratch)
 template <typename T>
@@ -222,7 +228,7 @@ DEV void lxx_row(const Params &p, const PhaseConst &pc, int r, LxxRow &L)
 #pragma unroll
     for (int l = 0; l < 4; ++l) L.xq[l] = 0.0;
     if (r >= NX) return;
-    L.diag = p.dt * (r < 12 ? pick(p.qbase, r) : p.q_qJ * (1 - pick4(pc.c, (r - 12) / 3)));
+    L.diag = p.dt * (r < 12 ? pick(p.qbase, r) : p.q_qJ * (1 - contact(pc, (r - 12) / 3)));
     if (r >= 3 && r < 6) {
         // dt c^2 (foot_gain w c) = dt foot_gain w for c = 1, else 0 (selects: no per-phase
         // conversions kept live across the knot loop)
@@ -235,7 +241,7 @@ DEV void lxx_row(const Params &p, const PhaseConst &pc, int r, LxxRow &L)
         }
     } else if (r >= 12) {
         const int m = r - 12;
-        const double w = pick4(pc.c, m / 3) ? p.dt * (p.foot_gain * pick(p.foot_w, m % 3)) : 0.0;
+        const double w = contact(pc, m / 3) ? p.dt * (p.foot_gain * pick(p.foot_w, m % 3)) : 0.0;
         L.diag += w;
         L.xp = -w;
     }
@@ -248,13 +254,17 @@ DEV void lxx_row(const Params &p, const PhaseConst &pc, int r, LxxRow &L)
 DEV void lxx_row_table(const double *Bm, const PhaseConst &pc, int r, LxxRow &L)
 {
     const int rr = r < NX ? r : 0;
-    const double dr = Bm[rr * XS + NX];
-    L.diag = r < NX ? dr : 0.0;
     const bool pos = r >= 3 && r < 6;
     const int a = pos ? r - 3 : 0;
+    // every read unconditional (then opaque): the selects below must not become branches
+    double dr = Bm[rr * XS + NX], dq[4];
 #pragma unroll
-    for (int l = 0; l < 4; ++l) L.xq[l] = (pos && pc.c[l]) ? -Bm[(12 + 3 * l + a) * XS + NX] : 0.0;
-    L.xp = (r >= 12 && r < NX && pick4(pc.c, (rr - 12) / 3)) ? -dr : 0.0;
+    for (int l = 0; l < 4; ++l) dq[l] = Bm[(12 + 3 * l + a) * XS + NX];
+    asm volatile("" : "+v"(dr), "+v"(dq[0]), "+v"(dq[1]), "+v"(dq[2]), "+v"(dq[3]));
+    L.diag = r < NX ? dr : 0.0;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) L.xq[l] = (pos && pc.c[l]) ? -dq[l] : 0.0;
+    L.xp = (r >= 12 && r < NX && contact(pc, (rr - 12) / 3)) ? -dr : 0.0;
 }
 
 // lxx(r, 12 hf + i) for a compile-time i
@@ -441,7 +451,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     // axis ar, B_c column rq (rows 6..8 from the LQ record, row 9 + ar or 12 + rq from the contact)
     const int rq = qr ? pos : 0;
     const int lr = rq / 3, ar = rq % 3;
-    const bool stz = pick4(pc.c, lr) != 0;
+    const bool stz = contact(pc, lr) != 0;
     double rb3[3];  // row ar of leg lr's ReB Hessian block, stored (00,01,02,11,12,22)
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -510,6 +520,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
             S.Bm[r * XS + c] = lxx_half<i>(lx_, r, hf) + (c == r ? reg : 0.0) + (zo[i] + zt[i]) / 2;
         });
     }
+    STAMP(5);
     // elimination operand, one column of [Quu_cc | I | Qu_c] per lane: lane 16 R + j (j < 12)
     // holds Quu_cc = luu + B_c^T T_c + reg I as row j (B_c column j against the rows of T_c:
     // lane-indexed coefficients, broadcast rows, no scalar loads) in each of the four 16-lane DPP
@@ -530,7 +541,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
             w[c] = qr ? vu : il ? (c == ic ? 1.0 : 0.0) : ul ? S.d[c] : 0.0;
         });
     }
-    STAMP(5);
+    STAMP(6);
     // PSD test (LDLT of Quu - 1e-9 I, SinglePhase.cpp:342-348): the decoupled diagonal, then
     // every Gauss-Jordan pivot of the coupled block.  ballot is convergent, so each test stays
     // in its step.
@@ -551,7 +562,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         w[j] = f;
         SFENCE();
     });
-    STAMP(6);
+    STAMP(7);
     live = live && bad == 0;
     if (!live) return;
     // Quu_cc^-1 by columns [c][16] (rows 12..15 read as zero) and Quu_cc^-1 Qu_c into LDS
@@ -571,7 +582,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     double dvp = 0.0;
     if (ql) {
         const double duz = quz / qzz;
-        dUg[pick4(pc.c, r / 3) ? HC + r : r] = -duz;
+        dUg[contact(pc, r / 3) ? HC + r : r] = -duz;
         dvp = quz * duz;
     }
     HSYNC();
@@ -604,7 +615,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         }
     }
     HSYNC();
-    STAMP(7);
+    STAMP(8);
     if (ul)
 #pragma unroll
         for (int q = 0; q < HC; ++q) dvp += S.d[q] * S.wqu[q];
@@ -645,7 +656,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         }
     }
     HSYNC();
-    STAMP(8);
+    STAMP(9);
 }
 
 // MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229) with one regularisation value.
@@ -935,7 +946,7 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
         lxx_row(p, pc, r, lx_);
         const double ru = rowl ? p.dt * r_diag(p, r) : 0.0;
         // control r has a gain row only when its B column is non-zero (KCW layout)
-        const bool stl = pick4(pc.c, (rr % HC) / 3) != 0;
+        const bool stl = contact(pc, (rr % HC) / 3) != 0;
         const bool cpl = rowl && (rr < HC ? stl : !stl);
         const int krow0 = (rr % HC) * NX + cb;
         for (int k = 0; k < N; k += 2) {
