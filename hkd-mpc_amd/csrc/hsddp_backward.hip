@@ -532,13 +532,18 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         const double ld = dt * (stz ? p.r_grf : p.r_qJd);
         const double *t6 = S.A + OFF_TC + 6 * HC, *t9 = S.A + OFF_TC + (9 + ar) * HC,
                      *tq = S.A + OFF_TC + (HC + rq) * HC;
+        // B_c column rq is (bw0, bw1, bw2, bv) on rows 6, 7, 8, 9 + ar for a stance leg and bq on
+        // row 12 + rq for a swing leg, the other entries exactly 0 (HKDDynamics: c_l factors), so
+        // the stance and swing sums add exact zeros: one select-free formula, every read
+        // unconditional (a select on a loaded value becomes a branch around the load)
+        const double ul1 = ul ? 1.0 : 0.0;
         static_for<HC>([&](auto I) {
             constexpr int c = I;
-            const double vs = bw0 * t6[c] + bw1 * t6[HC + c] + bw2 * t6[2 * HC + c] + bv * t9[c];
-            const double vw = bq * tq[c];
-            const double lu = stz ? (c == rq ? ld : 0.0) + (c / 3 == lr ? rb3[c % 3] : 0.0) : (c == rq ? ld : 0.0);
-            const double vu = lu + (stz ? vs : vw) + (c == rq ? reg : 0.0);
-            w[c] = qr ? vu : il ? (c == ic ? 1.0 : 0.0) : ul ? S.d[c] : 0.0;
+            const double vb = bw0 * t6[c] + bw1 * t6[HC + c] + bw2 * t6[2 * HC + c] + bv * t9[c] + bq * tq[c];
+            const double lu = (c == rq ? ld : 0.0) + ((stz && c / 3 == lr) ? rb3[c % 3] : 0.0);
+            const double vu = lu + vb + (c == rq ? reg : 0.0);
+            const double vo = (il && c == ic ? 1.0 : 0.0) + ul1 * S.d[c];
+            w[c] = qr ? vu : vo;
         });
     }
     STAMP(6);
