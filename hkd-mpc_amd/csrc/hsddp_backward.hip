@@ -55,6 +55,7 @@ struct BwdElem {
     double Bm[NX * XS];            // T_c = H B_c [24][12] | M rows 0..8 [9][24] -> Z rows -> symmetric Qxx -> H (stride XS)
     double Gn[NX], d[NX], wqu[HC];
     double red[4];
+    double pf[8];                  // landing area of the next knot's L2 prefetch (never read)
 };
 
 // In-kernel stamps (diagnostic build only, -DHSDDP_STAMPS=1): s_memtime at the stage boundaries
@@ -353,7 +354,7 @@ DEV double half_sum(double v)
 // so Quu^-1 [Qux | Qu] = [Quu_cc^-1 [Qux_c | Qu_c] ; 0 | Qu_z / Quu_zz] exactly, and the
 // reference's 24-control solve reduces to a 12 x 12 one plus 12 divisions.
 DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &pc, size_t b, int s, int kc,
-                  double reg, bool &live, double &g, double &dV1, double &dV2)
+                  double reg, bool more, bool &live, double &g, double &dV1, double &dV2)
 {
     // opaque per knot: keeps LICM from hoisting lane-dependent constants of the knot body
     // (regularised diagonals, lxx entries) out of the knot loop into long-lived VGPRs
@@ -378,6 +379,18 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
 #pragma unroll
     for (int i = 0; i < HC; ++i) h[i] = rowl ? S.Bm[r * XS + cb + i] : 0.0;
     HSYNC();
+    // Touch the next knot's LQ record (11 lines) and Defect (2 lines) with one 4-byte LDS-DMA
+    // read per line (into S.pf, never read): its loads then hit L2 instead of HBM.  Inline asm, so
+    // no wait is attached to it; later waits of the compiler's own loads may cover it (harmless).
+    if (more && lane < 13) {
+        const double *src = lane < 11 ? d.lq + (kq - 1) * LQW + 16 * lane : d.Defect + (b * p.S + s) * NX + 16 * (lane - 11);
+        const unsigned m0 = (unsigned)(size_t)(S.pf);
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(src), "s"(m0)
+                     : "memory");
+    }
     STAMP(1);
     // Gnext = G + H Defect[k+1] (SinglePhase.cpp:320)
     double part = 0.0;
@@ -727,7 +740,7 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double 
         const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
 #pragma unroll 1
         for (int k = N - 1; k >= 0 && live; --k)
-            bwd_knot(p, d, S, pc, b, s0 + k, k0 + k, reg, live, g, dV1, dV2);
+            bwd_knot(p, d, S, pc, b, s0 + k, k0 + k, reg, k > 0, live, g, dV1, dV2);
         if (!live) return false;
         // G[0] += H[0] Defect[0] (SinglePhase.cpp:365)
         if (lane < NX) S.d[lane] = d.Defect[(b * p.S + s0) * NX + lane];
