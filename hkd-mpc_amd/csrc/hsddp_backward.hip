@@ -51,11 +51,11 @@ struct BwdElem {
 #if HSDDP_STAMPS
     unsigned long long st[10], tprev;  // diagnostic build: cycles per knot stage (lane 0)
 #endif
-    double A[NX * XS];             // LQ record copy -> Qux_c [12][XS] | Quu_cc^-1 [12][16] -> Kp [12][XS]
-    double Bm[NX * XS];            // T_c = H B_c [24][12] | M rows 0..8 [9][24] -> Z rows -> symmetric Qxx -> H (stride XS)
-    double Gn[NX], d[NX], wqu[HC];
+    alignas(16) double A[NX * XS];  // LQ record copy -> Qux_c [12][XS] | Quu_cc^-1 [12][16] -> Kp [12][XS]
+    double Bm[NX * XS];             // T_c = H B_c [24][12] | M rows 0..8 [9][24] -> Z rows -> symmetric Qxx -> H (stride XS)
+    alignas(16) double d[NX];       // Defect[k+1] -> Qu_c
+    double Gn[NX], wqu[HC];
     double red[4];
-    double pf[8];                  // landing area of the next knot's L2 prefetch (never read)
 };
 
 // In-kernel stamps (diagnostic build only, -DHSDDP_STAMPS=1): s_memtime at the stage boundaries
@@ -334,6 +334,30 @@ DEV void stage_knot_inputs(double *lq_lds, const double *lq_g, double *v_lds, co
     if (lane < NX) v_lds[lane] = v;
 }
 
+// One knot's LQ record into S.A[0, LQW) and its Defect[k+1] into S.d by LDS-DMA (16 bytes per
+// lane per instruction, contiguous from M0).  Inline asm: the compiler neither waits for it nor
+// knows it writes LDS; the consumer waits with vmcnt(0) (bwd_knot).  The leading lgkmcnt(0)
+// retires every LDS read of the old contents first.  (M0 is compiler-reserved: saved, set with one
+// wait state before the DMA, restored.)
+DEV void knot_fetch(BwdElem &S, const double *lq_g, const double *def_g, int lane)
+{
+    static_assert(LQW % 2 == 0 && LQW > 128 && LQW <= 256 && NX % 2 == 0, "16-byte pieces, two instructions");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int n = t == 0 ? 64 : t == 1 ? LQW / 2 - 64 : NX / 2;  // pieces
+        if (lane < n) {
+            const double *src = t < 2 ? lq_g + 128 * t + 2 * lane : def_g + 2 * lane;
+            const unsigned m0 = (unsigned)(size_t)(t < 2 ? S.A + 128 * t : S.d);
+            unsigned keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(src), "s"(m0)
+                         : "memory");
+        }
+    }
+}
+
 DEV double half_sum(double v)
 {
 #pragma unroll
@@ -354,7 +378,7 @@ DEV double half_sum(double v)
 // so Quu^-1 [Qux | Qu] = [Quu_cc^-1 [Qux_c | Qu_c] ; 0 | Qu_z / Quu_zz] exactly, and the
 // reference's 24-control solve reduces to a 12 x 12 one plus 12 divisions.
 DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &pc, size_t b, int s, int kc,
-                  double reg, bool more, bool &live, double &g, double &dV1, double &dV2)
+                  double reg, bool pre, bool more, bool &live, double &g, double &dV1, double &dV2)
 {
     // opaque per knot: keeps LICM from hoisting lane-dependent constants of the knot body
     // (regularised diagonals, lxx entries) out of the knot loop into long-lived VGPRs
@@ -374,23 +398,14 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     STAMP(0);
     cdouble *lqs = uniform_ptr(d.lq + kq * LQW);
     double *lq = S.A;  // LDS copy for lane-indexed reads
-    stage_knot_inputs(lq, d.lq + kq * LQW, S.d, d.Defect + (b * p.S + s + 1) * NX, lane);
+    if (pre) // the previous knot requested this one's LQ record and Defect (knot_fetch)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+        stage_knot_inputs(lq, d.lq + kq * LQW, S.d, d.Defect + (b * p.S + s + 1) * NX, lane);
     double h[HC];  // this lane's columns of H[k+1] row r
 #pragma unroll
     for (int i = 0; i < HC; ++i) h[i] = rowl ? S.Bm[r * XS + cb + i] : 0.0;
     HSYNC();
-    // Touch the next knot's LQ record (11 lines) and Defect (2 lines) with one 4-byte LDS-DMA
-    // read per line (into S.pf, never read): its loads then hit L2 instead of HBM.  Inline asm, so
-    // no wait is attached to it; later waits of the compiler's own loads may cover it (harmless).
-    if (more && lane < 13) {
-        const double *src = lane < 11 ? d.lq + (kq - 1) * LQW + 16 * lane : d.Defect + (b * p.S + s) * NX + 16 * (lane - 11);
-        const unsigned m0 = (unsigned)(size_t)(S.pf);
-        unsigned keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(src), "s"(m0)
-                     : "memory");
-    }
     STAMP(1);
     // Gnext = G + H Defect[k+1] (SinglePhase.cpp:320)
     double part = 0.0;
@@ -662,6 +677,9 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
             t01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, t01, 0, 0, 0);
             t11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, t11, 0, 0, 0);
         }
+        // S.A and S.d are read: request the next knot's inputs into them (in flight during the
+        // H update and the knot transition)
+        if (more) knot_fetch(S, d.lq + (kq - 1) * LQW, d.Defect + (b * p.S + s) * NX, lane);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int r0 = lk + 4 * g, r1 = 16 + r0, c1 = 16 + li;
@@ -740,7 +758,7 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double 
         const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
 #pragma unroll 1
         for (int k = N - 1; k >= 0 && live; --k)
-            bwd_knot(p, d, S, pc, b, s0 + k, k0 + k, reg, k > 0, live, g, dV1, dV2);
+            bwd_knot(p, d, S, pc, b, s0 + k, k0 + k, reg, k < N - 1, k > 0, live, g, dV1, dV2);
         if (!live) return false;
         // G[0] += H[0] Defect[0] (SinglePhase.cpp:365)
         if (lane < NX) S.d[lane] = d.Defect[(b * p.S + s0) * NX + lane];
