@@ -21,10 +21,14 @@ namespace hsddp {
 
 using namespace hkd;
 
+#ifndef FWD_MINB
+#define FWD_MINB 2  // 256-thread blocks per CU for the knot-parallel kernels (k_lq, k_rollout)
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // k_lq: per (element, state slot): cost and |Defect|^2 at the current (X, U); compact LQ model at
 // control slots (SinglePhase::compute_cost + LQ_approximation, SinglePhase.cpp:235-296).
-__global__ __launch_bounds__(256, 2) void k_lq(Params p, Bufs d)
+__global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 {
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long)p.B * p.S) return;
@@ -189,20 +193,82 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
 // (HKDProblem.cpp:104), so X[k] = Xbar[k] + eps dX[k] and the simulated state at k depends only on
 // knot k-1: the nonlinear rollout is knot-parallel.  U = Ubar + eps du with du = dU + K dX from the
 // linear rollout (equal to the reference's Ubar + eps dU + K (X - Xbar) up to rounding of X - Xbar).
-__global__ __launch_bounds__(256, 2) void k_rollout(Params p, Bufs d, double eps, int init)
+//
+// One wave per 64 consecutive slots.  The trial rows it needs (states of its slots and the one
+// before, their controls and the one before) are formed with coalesced 16-byte loads (lanes over
+// row entries, not rows) into LDS — the output X and U rows are stored from the same pass — and
+// each lane then reads its rows from LDS: the row-per-lane global accesses this replaces touched
+// 64 cache lines per instruction.
+constexpr int RS = NX + 1;  // LDS row stride (doubles): conflict-free row-per-lane reads
+constexpr int RW = 65;      // rows per wave: 64 slots and the one before
+
+// control row (b Kc + kc) of slot g; terminal slots map to the next phase's first control
+DEV long slot_kq(const Params &p, long g)
 {
-    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (long)p.B * p.S) return;
+    const int b = (int)(g / p.S), s = (int)(g % p.S);
+    int i, k;
+    slot_phase(p, s, i, k);
+    return (long)b * p.Kc + s - i;
+}
+
+// X_t = Xbar + eps dX (or U_t = Ubar + eps du) for rows r0 .. r0 + RW - 1 of an [rows][24] pair
+// into LDS; rows of inactive elements are skipped, own rows (own(r)) are stored to `out`
+template <typename Act, typename Own>
+DEV void stage_trial(double *L, const double *bar, const double *del, double *out, long r0, long nrows, int per,
+                     double eps, int lane, Act active, Own own)
+{
+    constexpr int CH = NX / 2;  // 16-byte chunks per row
+#pragma unroll 1
+    for (int f = lane; f < RW * CH; f += 64) {
+        const int row = f / CH, cc = 2 * (f % CH);
+        const long r = r0 + row;
+        if (r < 0 || r >= nrows || !active((int)(r / per))) continue;
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        const d2 xb = *(const d2 *)(bar + r * NX + cc), dx = *(const d2 *)(del + r * NX + cc);
+        d2 v;
+        v.x = xb.x + eps * dx.x;
+        v.y = xb.y + eps * dx.y;
+        L[row * RS + cc] = v.x;
+        L[row * RS + cc + 1] = v.y;
+        if (own(r)) *(d2 *)(out + r * NX + cc) = v;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_rollout(Params p, Bufs d, double eps, int init)
+{
+    __shared__ double Xt[RW * RS], Ut[RW * RS];
+    const int lane = threadIdx.x;
+    const long total = (long)p.B * p.S, g0 = (long)blockIdx.x * 64, gid = g0 + lane;
+    const long gl = min(g0 + 63, total - 1);
+    // the wave's slots span at most two elements
+    const int bA = (int)(g0 / p.S), bB = (int)(gl / p.S);
+    auto act = [&](int b) { const ElemState &E = d.el[b]; return init ? !E.done : E.ls_active != 0; };
+    const bool aA = act(bA), aB = act(bB);
+    if (!aA && !aB) return;
+    auto active = [&](int b) { return (b == bA && aA) || (b == bB && aB); };
+    const long xr0 = g0 - 1;
+    stage_trial(Xt, d.Xbar, d.dX, d.X, xr0, total, p.S, eps, lane, active,
+                [&](long r) { return r >= g0; });
+    const long ur0 = slot_kq(p, g0) - 1, nk = (long)p.B * p.Kc;
+    // own control rows: the controls of this wave's non-terminal slots
+    stage_trial(Ut, d.Ubar, d.du, d.U, ur0, nk, p.Kc, eps, lane, active, [&](long r) {
+        const int b = (int)(r / p.Kc), kc = (int)(r % p.Kc);
+        int i = 0;
+        for (int j = 1; j < p.P; ++j)
+            if (kc >= p.k0[j]) i = j;
+        const long g = (long)b * p.S + kc + i;
+        return g >= g0 && g <= gl;
+    });
+    __syncthreads();
+    if (gid >= total) return;
     const int b = (int)(gid / p.S), s = (int)(gid % p.S);
-    const ElemState &E = d.el[b];
-    if (init ? E.done : !E.ls_active) return;
+    if (!active(b)) return;
     int i, k;
     slot_phase(p, s, i, k);
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     const size_t sb = (size_t)b * p.S;
-    // simulated state first, then the shooting state: the inputs of one are dead before the
-    // other's are loaded (register pressure sets this kernel's occupancy)
+    const double *x = Xt + (gid - xr0) * RS;
     double xs[NX];
     if (k == 0) {
         if (i == 0) {
@@ -211,44 +277,24 @@ __global__ __launch_bounds__(256, 2) void k_rollout(Params p, Bufs d, double eps
         } else { // x_init = resetmap(X_{i-1}[N]) (MultiPhaseDDP.cpp:73-81)
             int cp_[4], cpn[4];
             load_contacts(d, p, b, i - 1, cp_, cpn);
-            double xe[NX];
-            const double *xbp = d.Xbar + (sb + s - 1) * NX, *dxp = d.dX + (sb + s - 1) * NX;
-#pragma unroll
-            for (int j = 0; j < NX; ++j) xe[j] = xbp[j] + eps * dxp[j];
-            hkd_resetmap(xe, cp_, cpn, xs);
+            hkd_resetmap(x - RS, cp_, cpn, xs);
         }
     } else {
-        const int kcp = p.k0[i] + k - 1;
-        double xp[NX], up[NU];
-        const double *xbp = d.Xbar + (sb + s - 1) * NX, *dxp = d.dX + (sb + s - 1) * NX;
-        const double *ubp = d.Ubar + ((size_t)b * p.Kc + kcp) * NU, *dup = d.du + ((size_t)b * p.Kc + kcp) * NU;
-#pragma unroll
-        for (int j = 0; j < NX; ++j) xp[j] = xbp[j] + eps * dxp[j];
-#pragma unroll
-        for (int j = 0; j < NU; ++j) up[j] = ubp[j] + eps * dup[j];
+        const long kq = (long)b * p.Kc + s - i;
         double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
-        hkd_step(xp, up, cd, p.dt, xs);
+        hkd_step(x - RS, Ut + (kq - 1 - ur0) * RS, cd, p.dt, xs);
     }
-    pin(xs);
-    SFENCE();
-    double x[NX];
-    const double *xb = d.Xbar + (sb + s) * NX, *dxg = d.dX + (sb + s) * NX;
-#pragma unroll
-    for (int j = 0; j < NX; ++j) x[j] = xb[j] + eps * dxg[j];
     double nrm = 0.0, fs = 0.0;
-    double *Xg = d.X + (sb + s) * NX, *Dg = d.Defect + (sb + s) * NX;
+    double *Dg = d.Defect + (sb + s) * NX;
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
         nrm += xs[j] * xs[j];
-        double df = xs[j] - x[j];
+        const double df = xs[j] - x[j];
         fs += df * df;
-        Xg[j] = x[j];
         Dg[j] = df;
     }
     d.slot_feas[sb + s] = fs;
     d.slot_div[sb + s] = (k > 0 && sqrt(nrm) > 1e6) ? 1 : 0;
-    pin(x);
-    SFENCE();
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
     if (k == p.N[i]) {
         double tv, h[4];
@@ -259,11 +305,7 @@ __global__ __launch_bounds__(256, 2) void k_rollout(Params p, Bufs d, double eps
         for (int l = 0; l < 4; ++l) d.term_h[((size_t)b * p.P + i) * 4 + l] = h[l];
     } else {
         const int kc = p.k0[i] + k;
-        double u[NU];
-        const double *ub = d.Ubar + ((size_t)b * p.Kc + kc) * NU, *dug = d.du + ((size_t)b * p.Kc + kc) * NU;
-        double *Ug = d.U + ((size_t)b * p.Kc + kc) * NU;
-#pragma unroll
-        for (int j = 0; j < NU; ++j) { u[j] = ub[j] + eps * dug[j]; Ug[j] = u[j]; }
+        const double *u = Ut + ((long)b * p.Kc + kc - ur0) * RS;
         const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
         const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
         double viol;
@@ -500,7 +542,7 @@ static inline unsigned blocks_for(long n, int bs) { return (unsigned)((n + bs - 
 
 void launch_rollout(const Params &p, const Bufs &d, double eps, int init, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_rollout, dim3(blocks_for((long)p.B * p.S, 256)), dim3(256), 0, st, p, d, eps, init);
+    hipLaunchKernelGGL(k_rollout, dim3(blocks_for((long)p.B * p.S, 64)), dim3(64), 0, st, p, d, eps, init);
 }
 void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, hipStream_t st)
 {
