@@ -3,6 +3,8 @@
 // ReB / GRF: ConstraintsBase.h:204-263, HKDConstraints.cpp:7-66.  AL / touchdown: ConstraintsBase.h:374-399,
 // HKDConstraints.cpp:69-171.
 #pragma once
+#include <type_traits>
+
 #include "hsddp_internal.h"
 
 namespace hsddp {
@@ -51,11 +53,11 @@ DEV const double *ref_ptr(const Params &p, const double *base, int b, int s, int
 }
 
 // ReB barrier (ConstraintsBase.h:204-263)
-DEV double reb_cost(double g, double delta)
+DEV double reb_cost(double g, double delta, double log_delta)
 {
     if (g > delta) return -log(g);
     double t = (g - 2 * delta) / delta;
-    return .5 * (t * t - 1) - log(delta);
+    return .5 * (t * t - 1) - log_delta;
 }
 DEV void reb_derivs(double g, double delta, double &d1, double &d2)
 {
@@ -98,18 +100,25 @@ DEV double running_cost(const Params &p, const int *c, const double *x, const do
     lf *= p.dt;
     double l = lt + lf;
     double rc = 0.0, mk = 0.0;
-    // unrolled: a runtime leg index into u would put the control vector in scratch
+    // unrolled: a runtime leg index into u would put the control vector in scratch.  Uniform ReB
+    // parameters (the default schedule): one log(delta) for the 20 rows, the value each would compute
+    auto reb_sum = [&](auto uniform) {
+        const double log_du = uniform ? log(p.grf_delta) : 0.0;
 #pragma unroll
-    for (int lg = 0; lg < 4; ++lg) {
-        if (!c[lg]) continue;
+        for (int lg = 0; lg < 4; ++lg) {
+            if (!c[lg]) continue;
 #pragma unroll
-        for (int r = 0; r < 5; ++r) {
-            double g = grf_value(p.mu, r, u + 3 * lg);
-            mk = fmin(mk, g);
-            const double e = p.reb_uniform ? p.grf_eps : eps[5 * lg + r];
-            rc += e * reb_cost(g, p.reb_uniform ? p.grf_delta : delta[5 * lg + r]);
+            for (int r = 0; r < 5; ++r) {
+                double g = grf_value(p.mu, r, u + 3 * lg);
+                mk = fmin(mk, g);
+                const double e = uniform ? p.grf_eps : eps[5 * lg + r];
+                const double dl = uniform ? p.grf_delta : delta[5 * lg + r];
+                rc += e * reb_cost(g, dl, uniform ? log_du : log(dl));
+            }
         }
-    }
+    };
+    if (p.reb_uniform) reb_sum(std::true_type{});
+    else reb_sum(std::false_type{});
     if (p.ReB_active && (c[0] + c[1] + c[2] + c[3]) > 0) l += p.dt * rc;
     viol = mk;
     return l;
