@@ -240,12 +240,15 @@ __global__ __launch_bounds__(64) void k_rollout(Params p, Bufs d, double eps, in
     const int lane = threadIdx.x;
     const long total = (long)p.B * p.S, g0 = (long)blockIdx.x * 64, gid = g0 + lane;
     const long gl = min(g0 + 63, total - 1);
-    // the wave's slots span at most two elements
+    // the wave's slots span elements bA .. bB: two when S >= 64 (the metric's 204), more for short
+    // horizons; the first and last flags are kept in registers, any between are read again
     const int bA = (int)(g0 / p.S), bB = (int)(gl / p.S);
     auto act = [&](int b) { const ElemState &E = d.el[b]; return init ? !E.done : E.ls_active != 0; };
     const bool aA = act(bA), aB = act(bB);
-    if (!aA && !aB) return;
-    auto active = [&](int b) { return (b == bA && aA) || (b == bB && aB); };
+    bool any = aA || aB;
+    for (int b = bA + 1; b < bB && !any; ++b) any = act(b);
+    if (!any) return;
+    auto active = [&](int b) { return b == bA ? aA : b == bB ? aB : act(b); };
     const long xr0 = g0 - 1;
     stage_trial(Xt, d.Xbar, d.dX, d.X, xr0, total, p.S, eps, lane, active,
                 [&](long r) { return r >= g0; });

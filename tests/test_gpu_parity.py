@@ -99,6 +99,23 @@ def test_fixed_iterations_match_oracle(gait, P, N, n_iter):
         assert np.array_equal(g[f], r[f]), f
 
 
+@pytest.mark.parametrize("B,gait,P,N", [(1, "trot", 1, 50), (5, "trot", 2, 10), (7, "pronk", 3, 4),
+                                         (9, "jump", 8, 3)])
+def test_short_horizons_match_oracle(B, gait, P, N):
+    """Horizons with S < 64 state slots: one k_rollout wave spans several elements (C1 is 1 x 50,
+    batch 1); ragged batch sizes."""
+    prob = syn.make_batch(B, P, N, gait)
+    kw = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=2)
+    g = _run(prob, **kw)
+    r = O.solve_batch(prob, O.default_options(**kw), n_threads=8)
+    for f in ("Xbar", "Ubar", "K", "X", "U", "dX", "dU"):
+        assert rel(g[f], r[f]) < 1e-9, f
+    for f in ("cost", "feas"):
+        assert rel(g[f], r[f]) < 1e-9, f
+    for f in ("iters", "outer_iters", "status", "n_ls_trials"):
+        assert np.array_equal(g[f], r[f]), f
+
+
 @pytest.mark.parametrize("gait,P,N,mixed", [("trot", 4, 50, False), ("jump", 8, 25, False),
                                               ("trot", 4, 50, True)])
 def test_full_solve_matches_oracle(gait, P, N, mixed):
