@@ -74,10 +74,12 @@ def main():
     ap.add_argument("--phases", type=int, default=4)
     ap.add_argument("--knots", type=int, default=50)
     ap.add_argument("--gait", default="trot")
-    ap.add_argument("--cpu-elements", type=int, default=256)
+    ap.add_argument("--cpu-elements", type=int, default=2048)
     ap.add_argument("--cpu-iters", type=int, default=10)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--riccati-fp32", action="store_true",
+                    help="config C5: fp32 LQ records / Riccati sweep / linear rollout (fp64 rollout, costs, outer loop)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -95,7 +97,7 @@ def main():
     B = args.batch
     prob = synthetic.make_batch(B, args.phases, args.knots, args.gait, first_element=rank * B)
     opt = hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=args.warmup + args.steps)
-    solver = hsddp.Solver(prob, opt, device=local)
+    solver = hsddp.Solver(prob, opt, device=local, riccati_fp32=args.riccati_fp32)
     solver.begin()
     if args.warmup:
         solver.iterate(args.warmup)
@@ -127,18 +129,21 @@ def main():
         S, Kc, P = prob["S"], prob["Kc"], len(prob["horizons"])
         # k_riccati time from HIP events recorded around its launches on the solver's stream
         avg_bwd_ms = st.ms_backward / max(1, st.n_backward_launches)
-        bytes_launch = BWD_BYTES_PER_KNOT * Kc * B
+        # fp32 mode (C5) halves every term of the per-knot bytes
+        bytes_launch = BWD_BYTES_PER_KNOT * Kc * B // (2 if args.riccati_fp32 else 1)
         achieved = bytes_launch / (avg_bwd_ms * 1e-3) / 1e9
-        cfg_key = f"{args.gait}_{args.phases}x{args.knots}_b{B}"
+        cfg_key = f"{args.gait}_{args.phases}x{args.knots}_b{B}" + ("_fp32" if args.riccati_fp32 else "")
         traffic = load_traffic(cfg_key)
         out = {
             "metric": METRIC, "value": total_iters / elapsed, "unit": UNIT, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32 Riccati / f64 rollout" if args.riccati_fp32 else "f64",
             "data": "synthetic: seeded random initial states (splitmix64), closed-form trot reference "
                     "(SURVEY.md §8d); no dataset or checkpoint",
             "config": {"workload": f"HKD {args.gait}, {args.phases} phases x {args.knots} knots, "
-                                   f"batch={B} per GPU (BASELINE metric config)",
+                                   f"batch={B} per GPU " + ("(config C5: fp32 Riccati)" if args.riccati_fp32
+                                                            else "(BASELINE metric config)"),
                        "global_batch": B * world, "batch_per_gpu": B, "phases": args.phases,
                        "knots_per_phase": args.knots, "nx": 24, "nu": 24, "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_riccati", "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -153,7 +158,7 @@ def main():
                                              "forward_ls": st.ms_forward / args.steps},
                       "all_costs_finite": finite, "device_bytes": solver.device_bytes()},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not args.riccati_fp32:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     solver.close()

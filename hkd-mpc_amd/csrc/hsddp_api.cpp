@@ -290,6 +290,7 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
     }
     p.S = s; p.Kc = k;
     p.ref_per_element = desc->ref_per_element ? 1 : 0;
+    p.fp32 = desc->riccati_fp32 ? 1 : 0;
     h->Bref = p.ref_per_element ? p.B : 1;
     fill_params(h);
     const size_t B = p.B, S = p.S, Kc = p.Kc, P = p.P, Br = h->Bref;
@@ -301,7 +302,10 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         (rc = dalloc(h, d.Xbar, B * S * NX)) || (rc = dalloc(h, d.Defect, B * S * NX)) ||
         (rc = dalloc(h, d.Defect_bar, B * S * NX)) || (rc = dalloc(h, d.dX, B * S * NX)) ||
         (rc = dalloc(h, d.U, B * Kc * NX)) || (rc = dalloc(h, d.Ubar, B * Kc * NX)) || (rc = dalloc(h, d.dU, B * Kc * NX)) ||
-        (rc = dalloc(h, d.du, B * Kc * NX)) || (rc = dalloc(h, d.K, B * Kc * KCW)) || (rc = dalloc(h, d.dbg, B * 16)) || (rc = dalloc(h, d.lq, B * Kc * LQW)) ||
+        (rc = dalloc(h, d.du, B * Kc * NX)) || (rc = dalloc(h, d.dbg, B * 16)) ||
+        (p.fp32 ? ((rc = dalloc(h, d.K32, B * Kc * KCW)) || (rc = dalloc(h, d.lq32, B * Kc * LQW32)) ||
+                   (rc = dalloc(h, d.def32, B * S * NX)))
+                : ((rc = dalloc(h, d.K, B * Kc * KCW)) || (rc = dalloc(h, d.lq, B * Kc * LQW)))) ||
         (rc = dalloc(h, d.term, B * P * TW)) || (rc = dalloc(h, d.reb_delta, B * Kc * 20)) ||
         (rc = dalloc(h, d.reb_eps, B * Kc * 20)) || (rc = dalloc(h, d.al_sigma, B * P * 4)) ||
         (rc = dalloc(h, d.al_lambda, B * P * 4)) || (rc = dalloc(h, d.term_h, B * P * 4)) ||
@@ -375,7 +379,8 @@ extern "C" int hsddp_upload_problem(hsddp_handle h, const int *contacts, const d
     if (Br == 1) launch_broadcast(h->d.Xbar, h->d.ref_x, S * NX, B, h->stream);
     else HIPCHK(hipMemcpyAsync(h->d.Xbar, h->d.ref_x, B * S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
     HIPCHK(hipMemsetAsync(h->d.Ubar, 0, B * p.Kc * NX * sizeof(double), h->stream));
-    HIPCHK(hipMemsetAsync(h->d.K, 0, B * p.Kc * KCW * sizeof(double), h->stream));
+    if (p.fp32) HIPCHK(hipMemsetAsync(h->d.K32, 0, B * p.Kc * KCW * sizeof(float), h->stream));
+    else HIPCHK(hipMemsetAsync(h->d.K, 0, B * p.Kc * KCW * sizeof(double), h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     h->have_problem = true;
     return hsddp_upload_warm_start(h, nullptr, nullptr, nullptr);
@@ -400,7 +405,13 @@ extern "C" int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const
                     const int u = coupled_control(h, b, k, q);
                     std::memcpy(&kc[((b * Kc + k) * 12 + q) * NX], K + ((b * Kc + k) * NX + u) * NX, NX * sizeof(double));
                 }
-        if ((rc = h2d(d.K, kc.data(), B * Kc * KCW * sizeof(double), h->stream))) return rc;
+        if (p.fp32) {
+            std::vector<float> k32(kc.begin(), kc.end());
+            if ((rc = h2d(d.K32, k32.data(), B * Kc * KCW * sizeof(float), h->stream))) return rc;
+            HIPCHK(hipStreamSynchronize(h->stream));
+        } else if ((rc = h2d(d.K, kc.data(), B * Kc * KCW * sizeof(double), h->stream))) {
+            return rc;
+        }
         HIPCHK(hipStreamSynchronize(h->stream));
     }
     HIPCHK(hipMemcpyAsync(d.X, d.Xbar, B * S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
@@ -649,7 +660,13 @@ extern "C" int hsddp_download_trajectory(hsddp_handle h, double *Xbar, double *U
         return rc;
     if (K) { // expand the coupled rows; the decoupled controls' rows are exactly zero
         std::vector<double> kc(B * Kc * KCW);
-        if ((rc = d2h(kc.data(), h->d.K, B * Kc * KCW * 8))) return rc;
+        if (h->p.fp32) {
+            std::vector<float> k32(B * Kc * KCW);
+            if ((rc = d2h(k32.data(), h->d.K32, B * Kc * KCW * 4))) return rc;
+            std::copy(k32.begin(), k32.end(), kc.begin());
+        } else if ((rc = d2h(kc.data(), h->d.K, B * Kc * KCW * 8))) {
+            return rc;
+        }
         std::memset(K, 0, B * Kc * NN * sizeof(double));
         for (size_t b = 0; b < B; ++b)
             for (size_t k = 0; k < Kc; ++k)

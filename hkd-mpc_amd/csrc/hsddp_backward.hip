@@ -23,6 +23,12 @@
 // accepts passes here too.
 //
 // k_lin_rollout: the linear rollout that follows a successful sweep, one wave per element.
+//
+// Both kernels are templates on the arithmetic type `real`: double is the reference's arithmetic
+// (T = double throughout HSDDPSolver); float is the fp32 Riccati mode (SURVEY.md §8 config C5:
+// fp32 LQ records, fp32 sweep and linear rollout, fp64 line search / costs / outer loop).  The
+// float instantiation keeps the lane mapping and uses the f32 forms of the same instructions
+// (v_mov_b32_dpp / v_fmac_f32_dpp, one permlane32 swap, v_mfma_f32_16x16x4_f32).
 #include <utility>
 
 #include "hsddp_device.h"
@@ -47,15 +53,31 @@ static_assert(LQW <= OFF_TC && OFF_TC + NX * HC <= NX * XS, "S.A layout");
 #define HSDDP_STAMPS 0
 #endif
 
+template <typename real>
 struct BwdElem {
 #if HSDDP_STAMPS
     unsigned long long st[10], tprev;  // diagnostic build: cycles per knot stage (lane 0)
 #endif
-    alignas(16) double A[NX * XS];  // LQ record copy -> Qux_c [12][XS] | Quu_cc^-1 [12][16] -> Kp [12][XS]
-    double Bm[NX * XS];             // T_c = H B_c [24][12] | M rows 0..8 [9][24] -> Z rows -> symmetric Qxx -> H (stride XS)
-    alignas(16) double d[NX];       // Defect[k+1] -> Qu_c
-    double Gn[NX], wqu[HC];
+    alignas(16) real A[NX * XS];  // LQ record copy -> Qux_c [12][XS] | Quu_cc^-1 [12][16] -> Kp [12][XS]
+    real Bm[NX * XS];             // T_c = H B_c [24][12] | M rows 0..8 [9][24] -> Z rows -> symmetric Qxx -> H (stride XS)
+    alignas(16) real d[NX];       // Defect[k+1] -> Qu_c
+    real Gn[NX], wqu[HC];
     double red[4];
+};
+
+// Per-precision buffers: LQ record (stride LQS), compact gains and the Defect copy the sweep reads.
+template <typename real> struct Prec;
+template <> struct Prec<double> {
+    static constexpr int LQS = LQW;
+    static DEV const double *lq(const Bufs &d) { return d.lq; }
+    static DEV double *K(const Bufs &d) { return d.K; }
+    static DEV const double *def(const Bufs &d) { return d.Defect; }
+};
+template <> struct Prec<float> {
+    static constexpr int LQS = LQW32;
+    static DEV const float *lq(const Bufs &d) { return d.lq32; }
+    static DEV float *K(const Bufs &d) { return d.K32; }
+    static DEV const float *def(const Bufs &d) { return d.def32; }
 };
 
 // In-kernel stamps (diagnostic build only, -DHSDDP_STAMPS=1): s_memtime at the stage boundaries
@@ -104,8 +126,11 @@ DEV void static_for(F &&f)
 }
 
 // read-only, wave-uniform data: the constant address space lets the compiler use scalar loads
-typedef const __attribute__((address_space(4))) double cdouble;
-DEV cdouble *uniform_ptr(const double *p) { return (cdouble *)p; }
+template <typename real>
+DEV const __attribute__((address_space(4))) real *uniform_ptr(const real *p)
+{
+    return (const __attribute__((address_space(4))) real *)p;
+}
 
 // a value known to be equal on all lanes, moved to SGPRs
 DEV double uniform(double v)
@@ -114,6 +139,7 @@ DEV double uniform(double v)
     const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
     return __hiloint2double(hi, lo);
 }
+DEV float uniform(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
 // v on lane `src` (a constant), broadcast to every lane through SGPRs
 DEV double lane_value(double v, int src)
@@ -122,6 +148,7 @@ DEV double lane_value(double v, int src)
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
     return __hiloint2double(hi, lo);
 }
+DEV float lane_value(float v, int src) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src)); }
 
 // 1 / x from the hardware reciprocal refined by two Newton steps (within an ulp of the IEEE
 // quotient; 5 VALU operations instead of the ~10 of a correctly rounded division)
@@ -133,6 +160,13 @@ DEV double recip(double x)
     e = __builtin_fma(-x, r, 1.0);
     return __builtin_fma(r, e, r);
 }
+// f32: v_rcp_f32 is good to 1 ulp; one Newton step
+DEV float recip(float x)
+{
+    float r = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(r, e, r);
+}
 
 // value held by the same lane of the other half-wave (call with all 64 lanes active)
 DEV double other_half(double v)
@@ -142,41 +176,72 @@ DEV double other_half(double v)
     const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
     return threadIdx.x < 32 ? __hiloint2double(b[1], a[1]) : __hiloint2double(b[0], a[0]);
 }
+DEV float other_half(float v)
+{
+    const unsigned u = __float_as_uint(v);
+    const auto a = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __uint_as_float(threadIdx.x < 32 ? a[1] : a[0]);
+}
 
 // v on lane j of this lane's 16-lane row (DPP row_newbcast; the s_nop gives a VGPR written by
 // the previous VALU instruction its two wait states before the DPP read)
-template <int j>
-DEV double row_bcast(double v)
+template <int j, typename T>
+DEV T row_bcast(T v)
 {
-    double r;
-    asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "i"(j));
+    T r;
+    if constexpr (sizeof(T) == 8)
+        asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "i"(j));
+    else
+        asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "i"(j));
     return r;
 }
 
 // w += (w on lane j of this lane's 16-lane row) * s, the broadcast fused into the FMA;
 // `fresh`: w may have been written by the instruction just before
-template <int j, bool fresh>
-DEV void fmac_row_bcast(double &w, double s)
+template <int j, bool fresh, typename T>
+DEV void fmac_row_bcast(T &w, T s)
 {
-    if constexpr (fresh)
-        asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
-                     : "+v"(w)
-                     : "v"(s), "i"(j));
-    else
-        asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(w) : "v"(s), "i"(j));
+    if constexpr (sizeof(T) == 8) {
+        if constexpr (fresh)
+            asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+                         : "+v"(w)
+                         : "v"(s), "i"(j));
+        else
+            asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(w) : "v"(s), "i"(j));
+    } else {
+        if constexpr (fresh)
+            asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+                         : "+v"(w)
+                         : "v"(s), "i"(j));
+        else
+            asm volatile("v_fmac_f32_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(w) : "v"(s), "i"(j));
+    }
 }
 
+// D = A B + C on a 16 x 16 x 4 MFMA tile (one operand value per lane: A[l & 15][l >> 4],
+// B[l >> 4][l & 15]); result register g of lane l is row mfma_row(l >> 4, g), column l & 15 —
+// the f64 form interleaves rows, the f32 form blocks them (cdna_hip_programming.md, fragment layout)
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+DEV d4 mfma16(double a, double b, d4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+DEV f4 mfma16(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+template <typename real> using acc4 = std::conditional_t<sizeof(real) == 8, d4, f4>;
+template <typename real>
+DEV constexpr int mfma_row(int lk, int g) { return sizeof(real) == 8 ? lk + 4 * g : 4 * lk + g; }
+
 // per-phase constants of one element
+template <typename real>
 struct PhaseConst {
     int c[4];
-    int cmask;     // bit l = c_l: a lane-dependent leg index becomes one shift, not a select chain
-    double bv[4];  // dt c_l / m     (B rows 9..11)
-    double bq[4];  // dt (1 - c_l)   (B rows 12..23)
+    int cmask;   // bit l = c_l: a lane-dependent leg index becomes one shift, not a select chain
+    real bv[4];  // dt c_l / m     (B rows 9..11)
+    real bq[4];  // dt (1 - c_l)   (B rows 12..23)
 };
 
 // Wave-uniform: contacts through the scalar cache, and selects instead of arithmetic so the
 // constants stay in SGPRs (dt * c / m is dt / m or 0 exactly for c in {0, 1}).
-DEV void load_phase(const Params &p, const Bufs &d, size_t b, int i, PhaseConst &pc)
+template <typename real>
+DEV void load_phase(const Params &p, const Bufs &d, size_t b, int i, PhaseConst<real> &pc)
 {
     typedef const __attribute__((address_space(4))) int cint;
     cint *cs = (cint *)(d.contacts + (b * (p.P + 1) + i) * 4);
@@ -185,18 +250,20 @@ DEV void load_phase(const Params &p, const Bufs &d, size_t b, int i, PhaseConst 
     for (int l = 0; l < 4; ++l) {
         pc.c[l] = cs[l];
         pc.cmask |= (pc.c[l] != 0) << l;
-        pc.bv[l] = pc.c[l] ? p.dt_m : 0.0;
-        pc.bq[l] = pc.c[l] ? 0.0 : p.dt;
+        pc.bv[l] = pc.c[l] ? (real)p.dt_m : (real)0;
+        pc.bq[l] = pc.c[l] ? (real)0 : (real)p.dt;
     }
 }
 
 // lxx (dt Q + dt D^T Qfoot D, HKDCost.cpp:32) row r as: diagonal + cross terms with the foot columns
+template <typename real>
 struct LxxRow {
-    double diag, xq[4], xp;  // xq[l]: (r in pos) x (col 12+3l+(r-3)); xp: (r in q) x (col 3+(r-12)%3)
+    real diag, xq[4], xp;  // xq[l]: (r in pos) x (col 12+3l+(r-3)); xp: (r in q) x (col 3+(r-12)%3)
 };
 
 // contact of leg l (runtime, lane-dependent) as 0 / 1
-DEV int contact(const PhaseConst &pc, int l) { return (pc.cmask >> l) & 1; }
+template <typename real>
+DEV int contact(const PhaseConst<real> &pc, int l) { return (pc.cmask >> l) & 1; }
 
 // a[i] for a runtime i, as selects (a runtime index would put the array in scratch)
 template <typename T>
@@ -223,13 +290,14 @@ DEV double pick(const double (&a)[N], int i)
 
 // q_diag / foot_weight (hsddp_device.h) with the lane-dependent indices resolved by selects:
 // a lane-indexed read of a kernel-argument array is a memory round trip
-DEV void lxx_row(const Params &p, const PhaseConst &pc, int r, LxxRow &L)
+template <typename real>
+DEV void lxx_row(const Params &p, const PhaseConst<real> &pc, int r, LxxRow<real> &L)
 {
     L.diag = 0.0; L.xp = 0.0;
 #pragma unroll
     for (int l = 0; l < 4; ++l) L.xq[l] = 0.0;
     if (r >= NX) return;
-    L.diag = p.dt * (r < 12 ? pick(p.qbase, r) : p.q_qJ * (1 - contact(pc, (r - 12) / 3)));
+    double dg = p.dt * (r < 12 ? pick(p.qbase, r) : p.q_qJ * (1 - contact(pc, (r - 12) / 3)));
     if (r >= 3 && r < 6) {
         // dt c^2 (foot_gain w c) = dt foot_gain w for c = 1, else 0 (selects: no per-phase
         // conversions kept live across the knot loop)
@@ -237,58 +305,61 @@ DEV void lxx_row(const Params &p, const PhaseConst &pc, int r, LxxRow &L)
 #pragma unroll
         for (int l = 0; l < 4; ++l) {
             const double w = pc.c[l] ? fw : 0.0;
-            L.diag += w;
+            dg += w;
             L.xq[l] = -w;
         }
     } else if (r >= 12) {
         const int m = r - 12;
         const double w = contact(pc, m / 3) ? p.dt * (p.foot_gain * pick(p.foot_w, m % 3)) : 0.0;
-        L.diag += w;
+        dg += w;
         L.xp = -w;
     }
+    L.diag = dg;
 }
 
 // lxx row r from the per-phase diagonal table (column XS - 1 of the S.Bm rows, written by
 // bwd_sweep at the phase start): the foot cross terms are the negated diagonal entries of the
 // stance feet's rows, -lxx[12 + 3 l + a][12 + 3 l + a] (= -dt foot_gain w_a), so no parameter
 // is needed inside the knot loop
-DEV void lxx_row_table(const double *Bm, const PhaseConst &pc, int r, LxxRow &L)
+template <typename real>
+DEV void lxx_row_table(const real *Bm, const PhaseConst<real> &pc, int r, LxxRow<real> &L)
 {
     const int rr = r < NX ? r : 0;
     const bool pos = r >= 3 && r < 6;
     const int a = pos ? r - 3 : 0;
     // every read unconditional (then opaque): the selects below must not become branches
-    double dr = Bm[rr * XS + NX], dq[4];
+    real dr = Bm[rr * XS + NX], dq[4];
 #pragma unroll
     for (int l = 0; l < 4; ++l) dq[l] = Bm[(12 + 3 * l + a) * XS + NX];
     asm volatile("" : "+v"(dr), "+v"(dq[0]), "+v"(dq[1]), "+v"(dq[2]), "+v"(dq[3]));
-    L.diag = r < NX ? dr : 0.0;
+    L.diag = r < NX ? dr : (real)0;
 #pragma unroll
-    for (int l = 0; l < 4; ++l) L.xq[l] = (pos && pc.c[l]) ? -dq[l] : 0.0;
-    L.xp = (r >= 12 && r < NX && contact(pc, (rr - 12) / 3)) ? -dr : 0.0;
+    for (int l = 0; l < 4; ++l) L.xq[l] = (pos && pc.c[l]) ? -dq[l] : (real)0;
+    L.xp = (r >= 12 && r < NX && contact(pc, (rr - 12) / 3)) ? -dr : (real)0;
 }
 
 // lxx(r, 12 hf + i) for a compile-time i
-template <int i>
-DEV double lxx_half(const LxxRow &L, int r, int hf)
+template <int i, typename real>
+DEV real lxx_half(const LxxRow<real> &L, int r, int hf)
 {
-    const double dg = (HC * hf + i == r) ? L.diag : 0.0;
-    const double x1 = (r == 3 + i % 3) ? L.xq[i / 3] : 0.0;  // hf = 1
-    double x0 = 0.0;                                         // hf = 0
-    if constexpr (i >= 3 && i < 6) x0 = (r >= 12 && r < NX && (r - 12) % 3 == i - 3) ? L.xp : 0.0;
+    const real dg = (HC * hf + i == r) ? L.diag : (real)0;
+    const real x1 = (r == 3 + i % 3) ? L.xq[i / 3] : (real)0;  // hf = 1
+    real x0 = 0;                                               // hf = 0
+    if constexpr (i >= 3 && i < 6) x0 = (r >= 12 && r < NX && (r - 12) % 3 == i - 3) ? L.xp : (real)0;
     return dg + (hf ? x1 : x0);
 }
 
 // out[i] = sum_j S[j][12 hf + i] col[j] for this half's 12 columns of S (= A - I; rows 0..2:
 // eul, cols {1,2,6,7,8}; rows 3..5: dt at cols 9..11; rows 6..8: omega, cols {0..8, 12, 13, 15,
 // 16, 18, 19, 21, 22}), S values wave-uniform from the LQ record (scalar loads)
-DEV void st_apply(cdouble *lqs, double dt, int hf, const double (&col)[9], double (&out)[12])
+template <typename real>
+DEV void st_apply(const __attribute__((address_space(4))) real *lqs, real dt, int hf, const real (&col)[9], real (&out)[12])
 {
     if (hf == 0) {
         static_for<12>([&](auto I) {
             constexpr int c = I;
             constexpr int qe = se_index(c), qw = sw_index(c);
-            double v = 0.0;
+            real v = 0;
             if constexpr (qe >= 0)
                 v += lqs[LQ_SE + qe] * col[0] + lqs[LQ_SE + 5 + qe] * col[1] + lqs[LQ_SE + 10 + qe] * col[2];
             if constexpr (c >= 9) v += dt * col[c - 6];
@@ -302,32 +373,34 @@ DEV void st_apply(cdouble *lqs, double dt, int hf, const double (&col)[9], doubl
             if constexpr (qw >= 0)
                 out[i] = lqs[LQ_SW + qw] * col[6] + lqs[LQ_SW + 17 + qw] * col[7] + lqs[LQ_SW + 34 + qw] * col[8];
             else
-                out[i] = 0.0;
+                out[i] = 0;
         });
     }
 }
 
 // Column r of S (= A - I): coefficients S[j][r], j = 0..8
-DEV void s_column(const double *lq, double dt, int r, double *sc)
+template <typename real>
+DEV void s_column(const real *lq, real dt, int r, real *sc)
 {
     int q = (r < NX) ? se_index(r) : -1;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) sc[j] = q >= 0 ? lq[LQ_SE + 5 * j + q] : 0.0;
+    for (int j = 0; j < 3; ++j) sc[j] = q >= 0 ? lq[LQ_SE + 5 * j + q] : (real)0;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) sc[3 + j] = (r == j + 9) ? dt : 0.0;
+    for (int j = 0; j < 3; ++j) sc[3 + j] = (r == j + 9) ? dt : (real)0;
     q = (r < NX) ? sw_index(r) : -1;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) sc[6 + j] = q >= 0 ? lq[LQ_SW + 17 * j + q] : 0.0;
+    for (int j = 0; j < 3; ++j) sc[6 + j] = q >= 0 ? lq[LQ_SW + 17 * j + q] : (real)0;
 }
 
 // one knot's LQ record (LQW doubles) and a 24-vector from global memory into LDS: every load is
 // issued before the first store, so the wave waits for one memory round trip, not four
-DEV void stage_knot_inputs(double *lq_lds, const double *lq_g, double *v_lds, const double *v_g, int lane)
+template <typename real>
+DEV void stage_knot_inputs(real *lq_lds, const real *lq_g, real *v_lds, const real *v_g, int lane)
 {
     static_assert(LQW > 128 && LQW <= 192, "three loads per lane");
-    const double a0 = lq_g[lane], a1 = lq_g[64 + lane];
-    const double a2 = lane < LQW - 128 ? lq_g[128 + lane] : 0.0;
-    const double v = lane < NX ? v_g[lane] : 0.0;
+    const real a0 = lq_g[lane], a1 = lq_g[64 + lane];
+    const real a2 = lane < LQW - 128 ? lq_g[128 + lane] : (real)0;
+    const real v = lane < NX ? v_g[lane] : (real)0;
     lq_lds[lane] = a0;
     lq_lds[64 + lane] = a1;
     if (lane < LQW - 128) lq_lds[128 + lane] = a2;
@@ -339,16 +412,19 @@ DEV void stage_knot_inputs(double *lq_lds, const double *lq_g, double *v_lds, co
 // knows it writes LDS; the consumer waits with vmcnt(0) (bwd_knot).  The leading lgkmcnt(0)
 // retires every LDS read of the old contents first.  (M0 is compiler-reserved: saved, set with one
 // wait state before the DMA, restored.)
-DEV void knot_fetch(BwdElem &S, const double *lq_g, const double *def_g, int lane)
+template <typename real>
+DEV void knot_fetch(BwdElem<real> &S, const real *lq_g, const real *def_g, int lane)
 {
-    static_assert(LQW % 2 == 0 && LQW > 128 && LQW <= 256 && NX % 2 == 0, "16-byte pieces, two instructions");
+    constexpr int E = 16 / sizeof(real);  // values per 16-byte piece
+    constexpr int LP = LQW / E + (LQW % E != 0), NL = (LP + 63) / 64;  // record pieces, instructions
+    static_assert(LP * E <= Prec<real>::LQS && NL <= 2 && NX % E == 0, "16-byte pieces, at most two instructions");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-        const int n = t == 0 ? 64 : t == 1 ? LQW / 2 - 64 : NX / 2;  // pieces
+    for (int t = 0; t < NL + 1; ++t) {
+        const int n = t < NL ? min(64, LP - 64 * t) : NX / E;  // pieces
         if (lane < n) {
-            const double *src = t < 2 ? lq_g + 128 * t + 2 * lane : def_g + 2 * lane;
-            const unsigned m0 = (unsigned)(size_t)(t < 2 ? S.A + 128 * t : S.d);
+            const real *src = t < NL ? lq_g + 64 * E * t + E * lane : def_g + E * lane;
+            const unsigned m0 = (unsigned)(size_t)(t < NL ? S.A + 64 * E * t : S.d);
             unsigned keep;
             asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                          : "=&s"(keep)
@@ -358,7 +434,8 @@ DEV void knot_fetch(BwdElem &S, const double *lq_g, const double *def_g, int lan
     }
 }
 
-DEV double half_sum(double v)
+template <typename real>
+DEV real half_sum(real v)
 {
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -377,8 +454,9 @@ DEV double half_sum(double v)
 // (the ReB Hessian only touches stance GRFs).  Quu is block diagonal under this permutation,
 // so Quu^-1 [Qux | Qu] = [Quu_cc^-1 [Qux_c | Qu_c] ; 0 | Qu_z / Quu_zz] exactly, and the
 // reference's 24-control solve reduces to a 12 x 12 one plus 12 divisions.
-DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &pc, size_t b, int s, int kc,
-                  double reg, bool pre, bool more, bool &live, double &g, double &dV1, double &dV2)
+template <typename real>
+DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem<real> &S, const PhaseConst<real> &pc, size_t b, int s, int kc,
+                  real reg, bool pre, bool more, bool &live, real &g, real &dV1, real &dV2)
 {
     // opaque per knot: keeps LICM from hoisting lane-dependent constants of the knot body
     // (regularised diagonals, lxx entries) out of the knot loop into long-lived VGPRs
@@ -393,37 +471,39 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     const int ic = il ? 4 * R + pos - HC : 0;
     const bool ul = lane == 60;                  // elimination column Qu_c
     const bool ql = hf == 1 && r < HC;           // decoupled control z(r)
-    const double dt = p.dt;
+    const real dt = p.dt;
     const size_t kq = b * p.Kc + kc;
     STAMP(0);
-    cdouble *lqs = uniform_ptr(d.lq + kq * LQW);
-    double *lq = S.A;  // LDS copy for lane-indexed reads
+    constexpr int LQS = Prec<real>::LQS;
+    const real *lqg = Prec<real>::lq(d), *defg = Prec<real>::def(d);
+    const auto lqs = uniform_ptr(lqg + kq * LQS);
+    real *lq = S.A;  // LDS copy for lane-indexed reads
     if (pre) // the previous knot requested this one's LQ record and Defect (knot_fetch)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else
-        stage_knot_inputs(lq, d.lq + kq * LQW, S.d, d.Defect + (b * p.S + s + 1) * NX, lane);
-    double h[HC];  // this lane's columns of H[k+1] row r
+        stage_knot_inputs(lq, lqg + kq * LQS, S.d, defg + (b * p.S + s + 1) * NX, lane);
+    real h[HC];  // this lane's columns of H[k+1] row r
 #pragma unroll
-    for (int i = 0; i < HC; ++i) h[i] = rowl ? S.Bm[r * XS + cb + i] : 0.0;
+    for (int i = 0; i < HC; ++i) h[i] = rowl ? S.Bm[r * XS + cb + i] : (real)0;
     HSYNC();
     STAMP(1);
     // Gnext = G + H Defect[k+1] (SinglePhase.cpp:320)
-    double part = 0.0;
+    real part = 0.0;
 #pragma unroll
     for (int i = 0; i < HC; ++i) part += h[i] * S.d[cb + i];
-    const double gn = g + (part + other_half(part));
+    const real gn = g + (part + other_half(part));
     // M = H A on this half's columns (the second half needs H[r][6..8] from the first);
     // T_c = H B_c, each coupled column written by the half that holds its H entries
-    double h68[3];
+    real h68[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) h68[j] = other_half(h[6 + j]);
     // (for a swing leg the first half's GRF column value is exactly 0, for a stance leg the second
     // half's joint-velocity value is: each half stores only the columns it owns)
-    double m[HC], tc[HC];
+    real m[HC], tc[HC];
     if (hf == 0) {
         static_for<HC>([&](auto I) {
             constexpr int c = I;
-            double v = h[c];
+            real v = h[c];
             constexpr int qe = se_index(c), qw = sw_index(c);
             if constexpr (qe >= 0)
                 v += h[0] * lqs[LQ_SE + qe] + h[1] * lqs[LQ_SE + 5 + qe] + h[2] * lqs[LQ_SE + 10 + qe];
@@ -437,7 +517,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     } else {
         static_for<HC>([&](auto I) {
             constexpr int i = I;
-            double v = h[i];
+            real v = h[i];
             constexpr int qw = sw_index(HC + i);
             if constexpr (qw >= 0)
                 v += h68[0] * lqs[LQ_SW + qw] + h68[1] * lqs[LQ_SW + 17 + qw] + h68[2] * lqs[LQ_SW + 34 + qw];
@@ -466,11 +546,11 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     // The S^T X products (S = A - I) are evaluated transposed: a lane gathers one column of X
     // and applies S, whose sparsity is known at compile time and whose values are wave-uniform
     // (SGPRs) — 9 LDS reads per product instead of one broadcast read per multiply.
-    double sc[9];
+    real sc[9];
     s_column(lq, dt, r, sc);
-    double qx = 0.0;
+    real qx = 0.0;
     if (rowl) {
-        double a = 0.0;
+        real a = 0.0;
 #pragma unroll
         for (int j = 0; j < 9; ++j) a += sc[j] * S.Gn[j];
         qx = lq[LQ_LX + r] + (gn + a);
@@ -480,27 +560,27 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     const int rq = qr ? pos : 0;
     const int lr = rq / 3, ar = rq % 3;
     const bool stz = contact(pc, lr) != 0;
-    double rb3[3];  // row ar of leg lr's ReB Hessian block, stored (00,01,02,11,12,22)
+    real rb3[3];  // row ar of leg lr's ReB Hessian block, stored (00,01,02,11,12,22)
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const int lo = min(a, ar), hi = max(a, ar);
         rb3[a] = lq[LQ_RB + 6 * lr + (lo == 0 ? hi : lo == 1 ? 2 + hi : 5)];
     }
-    const double bw0 = lq[LQ_BW + rq], bw1 = lq[LQ_BW + 12 + rq], bw2 = lq[LQ_BW + 24 + rq];
+    const real bw0 = lq[LQ_BW + rq], bw1 = lq[LQ_BW + 12 + rq], bw2 = lq[LQ_BW + 24 + rq];
     // decoupled control z(r) on the ql lanes: Qu_z, Quu_zz
-    const double qzz = dt * (stz ? p.r_qJd : p.r_grf) + reg;
-    const double quz = lq[LQ_LU + (stz ? HC + rq : rq)];
+    const real qzz = dt * (real)(stz ? p.r_qJd : p.r_grf) + reg;
+    const real quz = lq[LQ_LU + (stz ? HC + rq : rq)];
     // Qu_c[q] = lu_c + B_c^T Gnext on lane q < 12 (into S.d)
     if (lane < HC) {
-        const double gb = stz ? (bw0 * S.Gn[6] + bw1 * S.Gn[7] + bw2 * S.Gn[8]) + p.dt_m * S.Gn[9 + ar]
+        const real gb = stz ? (bw0 * S.Gn[6] + bw1 * S.Gn[7] + bw2 * S.Gn[8]) + (real)p.dt_m * S.Gn[9 + ar]
                               : dt * S.Gn[HC + rq];
         S.d[lane] = lq[LQ_LU + (stz ? rq : HC + rq)] + gb;
     }
     // Z = M + (S^T M9)^T on this lane's row: Qxx = lxx + Z^T-symmetric part (below)
-    double z[HC];
+    real z[HC];
     {
         const int rr = rowl ? r : 0;
-        double col[9], y[HC];
+        real col[9], y[HC];
 #pragma unroll
         for (int j = 0; j < 9; ++j) col[j] = S.Bm[OFF_M9 + j * XS + rr];
         st_apply(lqs, dt, hf, col, y);
@@ -517,7 +597,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         // half's rows and writes row q of Qux_c [12][XS] (its half's columns); every read is
         // issued before the first write
         const int rt = r < HC ? r : 0;
-        double col[9], y[HC], t[HC];
+        real col[9], y[HC], t[HC];
 #pragma unroll
         for (int j = 0; j < 9; ++j) col[j] = S.A[OFF_TC + j * HC + rt];
 #pragma unroll
@@ -533,9 +613,9 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     // = lxx + (Z + Z^T) / 2, symmetrised in place: every lane reads its row and its 12 transposed
     // entries before any lane writes
     if (rowl) {
-        LxxRow lx_;
+        LxxRow<real> lx_;
         lxx_row_table(S.Bm, pc, r, lx_);
-        double zt[HC], zo[HC];
+        real zt[HC], zo[HC];
 #pragma unroll
         for (int i = 0; i < HC; ++i) {
             zt[i] = S.Bm[(cb + i) * XS + r];
@@ -545,7 +625,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
         static_for<HC>([&](auto I) {
             constexpr int i = I;
             const int c = cb + i;
-            S.Bm[r * XS + c] = lxx_half<i>(lx_, r, hf) + (c == r ? reg : 0.0) + (zo[i] + zt[i]) / 2;
+            S.Bm[r * XS + c] = lxx_half<i>(lx_, r, hf) + (c == r ? reg : (real)0) + (zo[i] + zt[i]) / 2;
         });
     }
     STAMP(5);
@@ -554,23 +634,23 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     // lane-indexed coefficients, broadcast rows, no scalar loads) in each of the four 16-lane DPP
     // rows R, lanes 16 R + 12 + t (R < 3) column 4 R + t of the identity, lane 60 Qu_c
     // (SinglePhase.cpp:323-327; regularisation MultiPhaseDDP.cpp:160)
-    double w[HC];
+    real w[HC];
     {
-        const double bv = stz ? p.dt_m : 0.0, bq = stz ? 0.0 : dt;
-        const double ld = dt * (stz ? p.r_grf : p.r_qJd);
-        const double *t6 = S.A + OFF_TC + 6 * HC, *t9 = S.A + OFF_TC + (9 + ar) * HC,
+        const real bv = stz ? (real)p.dt_m : (real)0, bq = stz ? (real)0 : dt;
+        const real ld = dt * (real)(stz ? p.r_grf : p.r_qJd);
+        const real *t6 = S.A + OFF_TC + 6 * HC, *t9 = S.A + OFF_TC + (9 + ar) * HC,
                      *tq = S.A + OFF_TC + (HC + rq) * HC;
         // B_c column rq is (bw0, bw1, bw2, bv) on rows 6, 7, 8, 9 + ar for a stance leg and bq on
         // row 12 + rq for a swing leg, the other entries exactly 0 (HKDDynamics: c_l factors), so
         // the stance and swing sums add exact zeros: one select-free formula, every read
         // unconditional (a select on a loaded value becomes a branch around the load)
-        const double ul1 = ul ? 1.0 : 0.0;
+        const real ul1 = ul ? (real)1 : (real)0;
         static_for<HC>([&](auto I) {
             constexpr int c = I;
-            const double vb = bw0 * t6[c] + bw1 * t6[HC + c] + bw2 * t6[2 * HC + c] + bv * t9[c] + bq * tq[c];
-            const double lu = (c == rq ? ld : 0.0) + ((stz && c / 3 == lr) ? rb3[c % 3] : 0.0);
-            const double vu = lu + vb + (c == rq ? reg : 0.0);
-            const double vo = (il && c == ic ? 1.0 : 0.0) + ul1 * S.d[c];
+            const real vb = bw0 * t6[c] + bw1 * t6[HC + c] + bw2 * t6[2 * HC + c] + bv * t9[c] + bq * tq[c];
+            const real lu = (c == rq ? ld : (real)0) + ((stz && c / 3 == lr) ? rb3[c % 3] : (real)0);
+            const real vu = lu + vb + (c == rq ? reg : (real)0);
+            const real vo = (il && c == ic ? (real)1 : (real)0) + ul1 * S.d[c];
             w[c] = qr ? vu : vo;
         });
     }
@@ -578,16 +658,16 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
     // PSD test (LDLT of Quu - 1e-9 I, SinglePhase.cpp:342-348): the decoupled diagonal, then
     // every Gauss-Jordan pivot of the coupled block.  ballot is convergent, so each test stays
     // in its step.
-    unsigned long long bad = __builtin_amdgcn_ballot_w64(ql && !(qzz > 1e-9));
+    unsigned long long bad = __builtin_amdgcn_ballot_w64(ql && !(qzz > (real)1e-9));
     // Gauss-Jordan without pivoting (Quu_cc is SPD when it passes): step j takes column j of
     // Quu_cc from position j of the lane's own DPP row (row_newbcast, fused into the FMA), so no
     // value leaves the VALU.  Afterwards the identity lanes hold Quu_cc^-1 — the reference's
     // explicit inverse (Quu.inverse(), SinglePhase.cpp:351) — and lane 60 Quu_cc^-1 Qu_c.
     static_for<HC>([&](auto J) {
         constexpr int j = J;
-        const double piv = row_bcast<j>(w[j]);
-        bad |= __builtin_amdgcn_ballot_w64(!(piv > 1e-9));
-        const double f = w[j] * recip(piv), nf = -f;
+        const real piv = row_bcast<j>(w[j]);
+        bad |= __builtin_amdgcn_ballot_w64(!(piv > (real)1e-9));
+        const real f = w[j] * recip(piv), nf = -f;
         static_for<HC>([&](auto I) {
             constexpr int i = I;
             if constexpr (i != j) fmac_row_bcast<j, i == (j + HC - 1) % HC>(w[i], nf);
@@ -612,33 +692,34 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
             constexpr int q = I;
             dUg[pc.c[q / 3] ? q : HC + q] = -w[q];
         });
-    double dvp = 0.0;
+    real dvp = 0.0;
     if (ql) {
-        const double duz = quz / qzz;
+        const real duz = quz / qzz;
         dUg[contact(pc, r / 3) ? HC + r : r] = -duz;
         dvp = quz * duz;
     }
     HSYNC();
-    typedef double d4 __attribute__((ext_vector_type(4)));
     const int li = lane & 15, lk = lane >> 4;
     // Kp = Quu_cc^-1 Qux_c (12 x 24, K = 12) on the matrix cores (v_mfma_f64_16x16x4_f64; operands
     // A[l & 15][k = l >> 4], B[k = l >> 4][l & 15]; result rows (l >> 4) + 4 reg, column l & 15):
     // into LDS for the value update, and K = -Kp to the compact gain rows (KCW layout)
     {
-        d4 k0 = {0, 0, 0, 0}, k1 = k0;
+        acc4<real> k0 = {0, 0, 0, 0}, k1 = k0;
 #pragma unroll
         for (int ks = 0; ks < 3; ++ks) {
             const int c = 4 * ks + lk;
-            const double a = li < HC ? S.A[OFF_QI + c * 16 + li] : 0.0;
-            const double b0 = S.A[OFF_QX + c * XS + li], b1 = S.A[OFF_QX + c * XS + 16 + li];
-            k0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b0, k0, 0, 0, 0);
-            k1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b1, k1, 0, 0, 0);
+            const real a = li < HC ? S.A[OFF_QI + c * 16 + li] : (real)0;
+            const real b0 = S.A[OFF_QX + c * XS + li], b1 = S.A[OFF_QX + c * XS + 16 + li];
+            k0 = mfma16(a, b0, k0);
+            k1 = mfma16(a, b1, k1);
         }
         HSYNC();  // Quu^-1 is read; Kp takes its place
-        double *Kg = d.K + kq * KCW;
+        real *Kg = Prec<real>::K(d) + kq * KCW;
+        // rows 0..11 hold the result: registers 0..2 in the f64 layout, 0..3 (rows < 12) in the f32 one
 #pragma unroll
-        for (int g = 0; g < 3; ++g) {
-            const int q = lk + 4 * g;
+        for (int g = 0; g < (sizeof(real) == 8 ? 3 : 4); ++g) {
+            const int q = mfma_row<real>(lk, g);
+            if (sizeof(real) == 4 && q >= HC) continue;
             S.A[OFF_KP + q * XS + li] = k0[g];
             Kg[q * NX + li] = -k0[g];
             if (li < NX - 16) {
@@ -653,36 +734,36 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
 #pragma unroll
         for (int q = 0; q < HC; ++q) dvp += S.d[q] * S.wqu[q];
     // expected cost change Qu^T Quu^-1 Qu (SinglePhase.cpp:357-358): half 1 holds every term
-    const double dvk = lane_value(half_sum(dvp), 32);
+    const real dvk = lane_value(half_sum(dvp), 32);
     dV1 -= dvk;
     dV2 += dvk;
     // G = Qx - Qux_c^T Quu_cc^-1 Qu_c, H = Qxx - Qux_c^T Quu_cc^-1 Qux_c (SinglePhase.cpp:359-361)
     const int rr = rowl ? r : 0;
-    double gp = 0.0;
+    real gp = 0.0;
 #pragma unroll
     for (int q = 0; q < HC; ++q) gp += S.A[OFF_QX + q * XS + rr] * S.wqu[q];
-    g = rowl ? qx - gp : 0.0;
+    g = rowl ? qx - gp : (real)0;
     // P = Qux_c^T Kp (24 x 24, K = 12) on the matrix cores over the output tiles (0,0), (0,1) and
     // (1,1) — P is symmetric, tile (1,0) is (0,1)^T — rows / columns 24..31 are padding.  H = Qxx - P
     // is formed in place of Qxx in LDS (each entry read and written by one lane), then read back
     // as rows.
     {
-        d4 t00 = {0, 0, 0, 0}, t01 = t00, t11 = t00;
+        acc4<real> t00 = {0, 0, 0, 0}, t01 = t00, t11 = t00;
 #pragma unroll
         for (int ks = 0; ks < 3; ++ks) {
             const int q = 4 * ks + lk;
-            const double a0 = S.A[OFF_QX + q * XS + li], a1 = S.A[OFF_QX + q * XS + 16 + li];
-            const double b0 = S.A[OFF_KP + q * XS + li], b1 = S.A[OFF_KP + q * XS + 16 + li];
-            t00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, t00, 0, 0, 0);
-            t01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, t01, 0, 0, 0);
-            t11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, t11, 0, 0, 0);
+            const real a0 = S.A[OFF_QX + q * XS + li], a1 = S.A[OFF_QX + q * XS + 16 + li];
+            const real b0 = S.A[OFF_KP + q * XS + li], b1 = S.A[OFF_KP + q * XS + 16 + li];
+            t00 = mfma16(a0, b0, t00);
+            t01 = mfma16(a0, b1, t01);
+            t11 = mfma16(a1, b1, t11);
         }
         // S.A and S.d are read: request the next knot's inputs into them (in flight during the
         // H update and the knot transition)
-        if (more) knot_fetch(S, d.lq + (kq - 1) * LQW, d.Defect + (b * p.S + s) * NX, lane);
+        if (more) knot_fetch(S, lqg + (kq - 1) * LQS, defg + (b * p.S + s) * NX, lane);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            const int r0 = lk + 4 * g, r1 = 16 + r0, c1 = 16 + li;
+            const int r0 = mfma_row<real>(lk, g), r1 = 16 + r0, c1 = 16 + li;
             S.Bm[r0 * XS + li] -= t00[g];
             if (c1 < NX) {
                 S.Bm[r0 * XS + c1] -= t01[g];
@@ -697,60 +778,61 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem &S, const PhaseConst &
 
 // MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229) with one regularisation value.
 // Returns false (and stops) at the first knot whose Quu fails the PSD test.
-DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double reg, double &dV1, double &dV2)
+template <typename real>
+DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem<real> &S, size_t b, real reg, real &dV1, real &dV2)
 {
     const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5, cb = HC * hf;
     const bool rowl = r < NX;
-    double g = 0.0;  // G[r]; the value Hessian H stays in S.Bm rows
+    real g = 0.0;  // G[r]; the value Hessian H stays in S.Bm rows
     bool live = true;
     dV1 = 0.0; dV2 = 0.0;
     for (int i = p.P - 1; i >= 0; --i) {
-        PhaseConst pc;
+        PhaseConst<real> pc;
         load_phase(p, d, b, i, pc);
         const double *rec = d.term + (b * p.P + i) * TW;
-        double h[HC];
+        real h[HC];
         if (i == p.P - 1) {
 #pragma unroll
-            for (int c = 0; c < HC; ++c) h[c] = rowl ? rec[TM_PHIXX + r * NX + cb + c] : 0.0;
-            g = rowl ? rec[TM_PHIX + r] : 0.0;
+            for (int c = 0; c < HC; ++c) h[c] = rowl ? (real)rec[TM_PHIXX + r * NX + cb + c] : (real)0;
+            g = rowl ? (real)rec[TM_PHIX + r] : (real)0;
         } else {
             // impact-aware step G' = Phix + Px^T G0, H' = Phixx + Px^T H0 Px
             // (MultiPhaseDDP.cpp:480-484): W = H0 Px into S.A, then Px^T W.
             const double *Px = rec + TM_PX;
             if (lane < NX) S.Gn[lane] = g;
-            double w[HC];
+            real w[HC];
 #pragma unroll
             for (int c = 0; c < HC; ++c) w[c] = 0.0;
             if (rowl)
                 for (int k = 0; k < NX; ++k) {
-                    const double hk = S.Bm[r * XS + k];
+                    const real hk = S.Bm[r * XS + k];
 #pragma unroll
-                    for (int c = 0; c < HC; ++c) w[c] += hk * Px[k * NX + cb + c];
+                    for (int c = 0; c < HC; ++c) w[c] += hk * (real)Px[k * NX + cb + c];
                 }
             if (rowl)
 #pragma unroll
                 for (int c = 0; c < HC; ++c) S.A[r * XS + cb + c] = w[c];
             HSYNC();
-            double gp = 0.0;
+            real gp = 0.0;
 #pragma unroll
             for (int c = 0; c < HC; ++c) w[c] = 0.0;
             if (rowl)
                 for (int j = 0; j < NX; ++j) {
-                    const double pj = Px[j * NX + r];
+                    const real pj = (real)Px[j * NX + r];
                     gp += pj * S.Gn[j];
 #pragma unroll
                     for (int c = 0; c < HC; ++c) w[c] += pj * S.A[j * XS + cb + c];
                 }
 #pragma unroll
-            for (int c = 0; c < HC; ++c) h[c] = rowl ? rec[TM_PHIXX + r * NX + cb + c] + w[c] : 0.0;
-            g = rowl ? rec[TM_PHIX + r] + gp : 0.0;
+            for (int c = 0; c < HC; ++c) h[c] = rowl ? (real)rec[TM_PHIXX + r * NX + cb + c] + w[c] : (real)0;
+            g = rowl ? (real)rec[TM_PHIX + r] + gp : (real)0;
         }
         HSYNC();
         if (rowl)
 #pragma unroll
             for (int c = 0; c < HC; ++c) S.Bm[r * XS + cb + c] = h[c];
         if (rowl && hf == 0) { // this phase's lxx diagonal into the padding column (lxx_row_table)
-            LxxRow lx_;
+            LxxRow<real> lx_;
             lxx_row(p, pc, r, lx_);
             S.Bm[r * XS + NX] = lx_.diag;
         }
@@ -761,9 +843,9 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double 
             bwd_knot(p, d, S, pc, b, s0 + k, k0 + k, reg, k < N - 1, k > 0, live, g, dV1, dV2);
         if (!live) return false;
         // G[0] += H[0] Defect[0] (SinglePhase.cpp:365)
-        if (lane < NX) S.d[lane] = d.Defect[(b * p.S + s0) * NX + lane];
+        if (lane < NX) S.d[lane] = Prec<real>::def(d)[(b * p.S + s0) * NX + lane];
         HSYNC();
-        double a = 0.0;
+        real a = 0.0;
         if (rowl)
 #pragma unroll
             for (int c = 0; c < HC; ++c) a += S.Bm[r * XS + cb + c] * S.d[cb + c];
@@ -774,9 +856,10 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem &S, size_t b, double 
     return true;
 }
 
+template <typename real>
 __global__ __launch_bounds__(64, 4) void k_riccati(Params p, Bufs d)
 {
-    __shared__ BwdElem S;
+    __shared__ BwdElem<real> S;
     const int lane = threadIdx.x;
     const size_t b = blockIdx.x;
     ElemState &E = d.el[b];
@@ -802,10 +885,10 @@ __global__ __launch_bounds__(64, 4) void k_riccati(Params p, Bufs d)
     const double cost = uniform(S.red[0]), feas = uniform(S.red[1]);
     double reg = uniform(E.reg);
     bool ok = false;
-    double dV1 = 0.0, dV2 = 0.0;
+    real dV1 = 0, dV2 = 0;
     // backward_sweep_regularized (MultiPhaseDDP.cpp:141-181)
     for (;;) {
-        if (bwd_sweep(p, d, S, b, reg, dV1, dV2)) { ok = true; break; }
+        if (bwd_sweep(p, d, S, b, (real)reg, dV1, dV2)) { ok = true; break; }
         reg = fmax(reg * p.update_regularization, 1e-03);
         if (reg > 1e2) break;
     }
@@ -825,35 +908,49 @@ __global__ __launch_bounds__(64, 4) void k_riccati(Params p, Bufs d)
 // MultiPhaseDDP::linear_rollout(1.0): dX, du = dU + K dX, and the expected cost change (quirk
 // A3: it replaces the sweep's dV), then the merit function (MultiPhaseDDP.cpp:309-318).
 // Lanes r < 24 of each half compute row r of the same vectors; the first half stores them.
-// A knot's inputs (compact K, LQ record, Defect[k+1], dU) are one 4080-byte LDS image filled by
-// four 16-byte-per-lane LDS-DMA loads (global_load_lds_dwordx4); the next knot's image is loaded
-// into the other buffer while this knot computes.
-constexpr int LB_K = 0, LB_LQ = KCW, LB_D = KCW + LQW, LB_DU = KCW + LQW + NX, LBW = KCW + LQW + 2 * NX;
-static_assert(LBW % 2 == 0 && LB_LQ % 2 == 0 && LB_D % 2 == 0 && LB_DU % 2 == 0 && LBW <= 4 * 64 * 2,
-              "16-byte pieces, four DMA instructions");
-struct LinBuf {
-    double v[2 * 4 * 64];
+// A knot's inputs (compact K, LQ record, Defect[k+1], dU) are one LDS image (4080 bytes in fp64,
+// 2144 in the fp32 mode) filled by 16-byte-per-lane LDS-DMA loads (global_load_lds_dwordx4, four
+// or three instructions); the next knot's image is loaded into the other buffer while this knot
+// computes.
+template <typename real>
+struct LinImg {
+    static constexpr int K = 0;                                       // byte offsets
+    static constexpr int LQ = K + KCW * (int)sizeof(real);
+    static constexpr int D = LQ + Prec<real>::LQS * (int)sizeof(real);
+    static constexpr int DU = D + NX * (int)sizeof(real);
+    static constexpr int END = DU + NX * 8;                           // dU stays fp64
+    static constexpr int NI = (END / 16 + 63) / 64;                   // DMA instructions
+    static_assert(LQ % 16 == 0 && D % 16 == 0 && DU % 16 == 0 && END % 16 == 0 && NI <= 4, "16-byte pieces");
 };
+template <typename real>
+struct LinBuf {
+    alignas(16) char v[LinImg<real>::NI * 64 * 16];
+};
+template <typename real>
 struct LinElem {
-    double dx[NX], du[NX];
+    real dx[NX], du[NX];
 };
 
 // Issued as inline asm so the waitcnt pass does not track the LDS writes (it would otherwise wait
 // for every DMA in flight before any LDS read); lin_knot waits explicitly.  LDS destination of
 // piece t: M0 + 16 * lane, contiguous.
-DEV void lin_fetch(LinBuf &buf, const Params &p, const Bufs &d, size_t b, int s, int kc, int lane)
+template <typename real>
+DEV void lin_fetch(LinBuf<real> &buf, const Params &p, const Bufs &d, size_t b, int s, int kc, int lane)
 {
+    using I = LinImg<real>;
     const size_t kq = b * p.Kc + kc;
-    // one base per segment, biased so that base + 8 * o addresses image double o
-    const size_t kB = (size_t)(d.K + kq * KCW), lB = (size_t)(d.lq + kq * LQW) - 8 * LB_LQ,
-                 dB = (size_t)(d.Defect + (b * p.S + s + 1) * NX) - 8 * LB_D, uB = (size_t)(d.dU + kq * NX) - 8 * LB_DU;
+    // one base per segment, biased so that base + o addresses image byte o
+    const size_t kB = (size_t)(Prec<real>::K(d) + kq * KCW) - I::K,
+                 lB = (size_t)(Prec<real>::lq(d) + kq * Prec<real>::LQS) - I::LQ,
+                 dB = (size_t)(Prec<real>::def(d) + (b * p.S + s + 1) * NX) - I::D,
+                 uB = (size_t)(d.dU + kq * NX) - I::DU;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        int o = 2 * (64 * t + lane);  // first double of this lane's 16-byte piece
-        o = o < LBW ? o : LBW - 2;   // the one spare piece repeats the last
-        const size_t base = o < LB_LQ ? kB : o < LB_D ? lB : o < LB_DU ? dB : uB;
-        const double *src = (const double *)(base + 8 * (size_t)o);
-        const unsigned m0 = (unsigned)(size_t)(buf.v + 128 * t);
+    for (int t = 0; t < I::NI; ++t) {
+        int o = 16 * (64 * t + lane);    // first byte of this lane's 16-byte piece
+        o = o < I::END ? o : I::END - 16;  // spare pieces repeat the last
+        const size_t base = o < I::LQ ? kB : o < I::D ? lB : o < I::DU ? dB : uB;
+        const char *src = (const char *)(base + (size_t)o);
+        const unsigned m0 = (unsigned)(size_t)(buf.v + 1024 * t);
         unsigned keep;  // M0 is compiler-reserved: saved, set (one wait state before the DMA), restored
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep)
@@ -864,38 +961,47 @@ DEV void lin_fetch(LinBuf &buf, const Params &p, const Bufs &d, size_t b, int s,
 
 // one knot of SinglePhase::linear_rollout (SinglePhase.cpp:144-178) from the LDS image `cur`;
 // when `more`, the next knot's image is requested into `nxt` first
-DEV void lin_knot(const Params &p, const Bufs &d, LinElem &S, LinBuf &cur, LinBuf &nxt, bool more, size_t b,
-                  int s, int kc, const PhaseConst &pc, const LxxRow &lx_, double ru, bool cpl, int krow0,
-                  double &dx, double &v1, double &v2)
+template <typename real>
+DEV void lin_knot(const Params &p, const Bufs &d, LinElem<real> &S, LinBuf<real> &cur, LinBuf<real> &nxt, bool more,
+                  size_t b, int s, int kc, const PhaseConst<real> &pc, const LxxRow<real> &lx_, real ru, bool cpl,
+                  int krow0, real &dx, real &v1, real &v2)
 {
+    using I = LinImg<real>;
     const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5, cb = HC * hf;
     const bool rowl = r < NX, st = rowl && hf == 0;
     const int rr = rowl ? r : 0;
-    const double dt = p.dt;
+    const real dt = p.dt;
     if (more) {
         lin_fetch(nxt, p, d, b, s + 1, kc + 1, lane);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // all but the four just issued
+        // all but the I::NI just issued
+        if constexpr (I::NI == 4)
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    static_assert(I::NI == 4 || I::NI == 3, "waitcnt above");
     LSYNC();
-    const double *lq = cur.v + LB_LQ, *dd = cur.v + LB_D;
-    double krow[HC];
+    const real *kimg = (const real *)(cur.v + I::K), *lq = (const real *)(cur.v + I::LQ),
+               *dd = (const real *)(cur.v + I::D);
+    const double *dUi = (const double *)(cur.v + I::DU);
+    real krow[HC];
 #pragma unroll
-    for (int c = 0; c < HC; ++c) krow[c] = cpl ? cur.v[LB_K + krow0 + c] : 0.0;
-    const double dUr = cur.v[LB_DU + rr];
+    for (int c = 0; c < HC; ++c) krow[c] = cpl ? kimg[krow0 + c] : (real)0;
+    const real dUr = (real)dUi[rr];
     if (lane < NX) S.dx[lane] = dx;
     LSYNC();
-    double kd = 0.0;
+    real kd = 0;
 #pragma unroll
     for (int c = 0; c < HC; ++c) kd += krow[c] * S.dx[cb + c];
     kd += other_half(kd);
-    const double du = dUr + kd;
+    const real du = dUr + kd;
     if (lane < NX) S.du[lane] = du;
     LSYNC();
-    double nx = 0.0, q1 = 0.0, q2 = 0.0;
+    real nx = 0, q1 = 0, q2 = 0;
     if (rowl) {
-        double sdx = 0.0;
+        real sdx = 0;
         if (r < 3) {
 #pragma unroll
             for (int q = 0; q < 5; ++q) sdx += lq[LQ_SE + 5 * r + q] * S.dx[se_col(q)];
@@ -905,7 +1011,7 @@ DEV void lin_knot(const Params &p, const Bufs &d, LinElem &S, LinBuf &cur, LinBu
 #pragma unroll
             for (int q = 0; q < 17; ++q) sdx += lq[LQ_SW + 17 * (r - 6) + q] * S.dx[sw_col(q)];
         }
-        double bdu = 0.0, lxd = lx_.diag * dx, lud = ru * du;
+        real bdu = 0, lxd = lx_.diag * dx, lud = ru * du;
         if (r < 6) {
             if (r >= 3) {
 #pragma unroll
@@ -922,11 +1028,11 @@ DEV void lin_knot(const Params &p, const Bufs &d, LinElem &S, LinBuf &cur, LinBu
             lxd += lx_.xp * S.dx[3 + (r - 12) % 3];
         }
         if (r < 12) {
-            const double *rb = lq + LQ_RB + 6 * (r / 3);
+            const real *rb = lq + LQ_RB + 6 * (r / 3);
             const int a = r % 3, u0 = 3 * (r / 3);
-            const double b0 = a == 0 ? rb[0] : a == 1 ? rb[1] : rb[2];
-            const double b1 = a == 0 ? rb[1] : a == 1 ? rb[3] : rb[4];
-            const double b2 = a == 0 ? rb[2] : a == 1 ? rb[4] : rb[5];
+            const real b0 = a == 0 ? rb[0] : a == 1 ? rb[1] : rb[2];
+            const real b1 = a == 0 ? rb[1] : a == 1 ? rb[3] : rb[4];
+            const real b2 = a == 0 ? rb[2] : a == 1 ? rb[4] : rb[5];
             lud += b0 * S.du[u0] + b1 * S.du[u0 + 1] + b2 * S.du[u0 + 2];
         }
         nx = (dx + sdx) + bdu + dd[r];
@@ -944,20 +1050,22 @@ DEV void lin_knot(const Params &p, const Bufs &d, LinElem &S, LinBuf &cur, LinBu
     LSYNC();
 }
 
+template <typename real>
 __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
 {
-    __shared__ LinElem S;
-    __shared__ LinBuf B0;
-    __shared__ LinBuf B1;
+    __shared__ LinElem<real> S;
+    __shared__ LinBuf<real> B0;
+    __shared__ LinBuf<real> B1;
     const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5, cb = HC * hf;
     const size_t b = blockIdx.x;
     ElemState &E = d.el[b];
     if (E.done || E.inner_done) return;
     const bool rowl = r < NX, st = rowl && hf == 0;
     const int rr = rowl ? r : 0;
-    double v1 = 0.0, v2 = 0.0, dx = 0.0;
+    const real *defg = Prec<real>::def(d);
+    real v1 = 0, v2 = 0, dx = 0;
     for (int i = 0; i < p.P; ++i) {
-        PhaseConst pc;
+        PhaseConst<real> pc;
         load_phase(p, d, b, i, pc);
         const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
         lin_fetch(B0, p, d, b, s0, k0, lane);  // the phase's first knot (its wait is in lin_knot)
@@ -965,22 +1073,22 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
             const double *Px = d.term + (b * p.P + (i - 1)) * TW + TM_PX;
             if (lane < NX) S.dx[lane] = dx;
             LSYNC();
-            double a = 0.0;
+            real a = 0;
             if (rowl)
-                for (int j = 0; j < NX; ++j) a += Px[r * NX + j] * S.dx[j];
+                for (int j = 0; j < NX; ++j) a += (real)Px[r * NX + j] * S.dx[j];
             dx = a;
             LSYNC();
         } else {
-            dx = 0.0;
+            dx = 0;
         }
         if (rowl) {
-            dx = dx + d.Defect[(b * p.S + s0) * NX + r];
+            dx = dx + defg[(b * p.S + s0) * NX + r];
             if (st) d.dX[(b * p.S + s0) * NX + r] = dx;
         }
         // lxx row r (HKDCost.cpp:32): diagonal + foot cross terms
-        LxxRow lx_;
+        LxxRow<real> lx_;
         lxx_row(p, pc, r, lx_);
-        const double ru = rowl ? p.dt * r_diag(p, r) : 0.0;
+        const real ru = rowl ? (real)(p.dt * r_diag(p, r)) : (real)0;
         // control r has a gain row only when its B column is non-zero (KCW layout)
         const bool stl = contact(pc, (rr % HC) / 3) != 0;
         const bool cpl = rowl && (rr < HC ? stl : !stl);
@@ -993,11 +1101,11 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
         const double *rec = d.term + (b * p.P + i) * TW;
         if (lane < NX) S.dx[lane] = dx;
         LSYNC();
-        double q1 = 0.0, q2 = 0.0;
+        real q1 = 0, q2 = 0;
         if (rowl) {
-            q1 = rec[TM_PHIX + r] * dx;
-            double a = 0.0;
-            for (int c = 0; c < NX; ++c) a += rec[TM_PHIXX + r * NX + c] * S.dx[c];
+            q1 = (real)rec[TM_PHIX + r] * dx;
+            real a = 0;
+            for (int c = 0; c < NX; ++c) a += (real)rec[TM_PHIXX + r * NX + c] * S.dx[c];
             q2 = dx * a;
         }
         v1 += half_sum(q1);
@@ -1005,11 +1113,11 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
         LSYNC();
     }
     if (lane == 0) {
-        const double cost = E.cost, feas = E.feas;
-        const double dV_abs = fabs(v1 + 0.5 * v2);
+        const double cost = E.cost, feas = E.feas, w1 = v1, w2 = v2;
+        const double dV_abs = fabs(w1 + 0.5 * w2);
         const double rho = (feas > p.feas_thresh) ? dV_abs / ((1 - p.merit_scale) * feas) + p.merit_offset : 0;
         const double merit = cost + rho * feas;
-        E.dV1 = v1; E.dV2 = v2; E.merit_rho = rho; E.merit = merit;
+        E.dV1 = w1; E.dV2 = w2; E.merit_rho = rho; E.merit = merit;
         E.cost_prev = cost; E.merit_prev = merit; E.feas_prev = feas;
         if (!p.no_early_exit && dV_abs < p.cost_thresh && feas <= p.feas_thresh) { E.inner_done = 1; E.ls_active = 0; }
         else E.ls_active = 1;
@@ -1018,12 +1126,18 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
 
 void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_riccati, dim3(p.B), dim3(64), 0, st, p, d);
+    if (p.fp32)
+        hipLaunchKernelGGL(k_riccati<float>, dim3(p.B), dim3(64), 0, st, p, d);
+    else
+        hipLaunchKernelGGL(k_riccati<double>, dim3(p.B), dim3(64), 0, st, p, d);
 }
 
 void launch_lin_rollout(const Params &p, const Bufs &d, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_lin_rollout, dim3(p.B), dim3(64), 0, st, p, d);
+    if (p.fp32)
+        hipLaunchKernelGGL(k_lin_rollout<float>, dim3(p.B), dim3(64), 0, st, p, d);
+    else
+        hipLaunchKernelGGL(k_lin_rollout<double>, dim3(p.B), dim3(64), 0, st, p, d);
 }
 
 }  // namespace hsddp

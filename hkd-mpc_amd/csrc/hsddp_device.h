@@ -15,8 +15,8 @@ using namespace hkd;
 // Register pin: the values must exist in VGPRs at this point.  Placed at the end of a stage, it
 // stops LLVM from sinking the stage's arithmetic into a later one (which keeps the stage's
 // operands live and spills).
-template <int N>
-DEV void pin(double (&a)[N])
+template <typename T, int N>
+DEV void pin(T (&a)[N])
 {
 #pragma unroll
     for (int i = 0; i < N; ++i) asm volatile("" : "+v"(a[i]));

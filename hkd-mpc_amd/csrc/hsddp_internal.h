@@ -9,6 +9,8 @@
 //   reb_delta, reb_eps                [B][Kc][20]     ReB params, index leg*5 + row
 //   al_sigma, al_lambda, term_h       [B][P][4]
 //   slot_cost, slot_feas, slot_viol   [B][S]          per-slot partial sums for per-element reductions
+//   fp32 Riccati mode (Params::fp32): lq32 [B][Kc][LQW32], K32 [B][Kc][12][24], def32 [B][S][24]
+//   replace lq and K (the fp64 copies are not allocated) and mirror Defect for the sweep
 // One element's data is contiguous, so the per-element backward kernel streams it coalesced.
 #pragma once
 
@@ -34,6 +36,7 @@ constexpr int LQ_LX = LQ_BW + 36;        // 24
 constexpr int LQ_LU = LQ_LX + 24;        // 24
 constexpr int LQ_RB = LQ_LU + 24;        // 24  dt * ReB Hessian, 4 legs x sym 3x3 (00,01,02,11,12,22)
 constexpr int LQW = LQ_RB + 24;          // 174
+constexpr int LQW32 = 176;               // fp32 record stride: LQW padded to 16-byte pieces
 
 constexpr int TM_PHIX = 0;
 constexpr int TM_PHIXX = 24;
@@ -52,6 +55,7 @@ struct Params {
     double cost_thresh, tconstr_thresh, pconstr_thresh, feas_thresh, merit_scale, merit_offset;
     int AL_active, ReB_active, no_early_exit;
     int reb_uniform;  // every ReB (delta, eps) equals (grf_delta, grf_eps): per-knot arrays not read
+    int fp32;         // fp32 Riccati mode (config C5): LQ records, sweep, gains and linear rollout in fp32
 };
 
 struct ElemState {
@@ -70,6 +74,8 @@ struct Bufs {
     double *reb_delta, *reb_eps, *al_sigma, *al_lambda, *term_h;
     double *slot_cost, *slot_feas, *slot_viol;
     int *slot_div;
+    // fp32 Riccati mode only: LQ records [B][Kc][LQW32], gains [B][Kc][KCW], Defect copy [B][S][24]
+    float *lq32, *K32, *def32;
     ElemState *el;
     int *counter;                          // [4] host-visible activity counters
     unsigned long long *dbg;               // [B][16] diagnostic builds only (in-kernel stamps)

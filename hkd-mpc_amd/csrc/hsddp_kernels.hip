@@ -28,6 +28,8 @@ using namespace hkd;
 // ---------------------------------------------------------------------------------------------
 // k_lq: per (element, state slot): cost and |Defect|^2 at the current (X, U); compact LQ model at
 // control slots (SinglePhase::compute_cost + LQ_approximation, SinglePhase.cpp:235-296).
+// F32: config C5's fp32 Riccati mode (records in fp32 plus an fp32 copy of Defect for the sweep)
+template <bool F32>
 __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 {
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -48,6 +50,11 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 #pragma unroll
     for (int j = 0; j < NX; ++j) fs += dg[j] * dg[j];
     d.slot_feas[(size_t)b * p.S + s] = fs;
+    if constexpr (F32) { // the sweep's and linear rollout's fp32 copy of Defect
+        float *d32 = d.def32 + ((size_t)b * p.S + s) * NX;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) d32[j] = (float)dg[j];
+    }
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
     if (k == p.N[i]) {
         double tv, h[4];
@@ -65,16 +72,21 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     double viol;
     d.slot_cost[(size_t)b * p.S + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
 
-    double *rec = d.lq + ((size_t)b * p.Kc + kc) * LQW;
+    // the record in the solver's Riccati precision (fp64, or fp32 in config C5's mode)
+    struct Rec {
+        std::conditional_t<F32, float, double> *r;
+        DEV void set(int j, double v) const { r[j] = v; }
+    } const rec{F32 ? (decltype(Rec::r))(d.lq32 + ((size_t)b * p.Kc + kc) * LQW32)
+                    : (decltype(Rec::r))(d.lq + ((size_t)b * p.Kc + kc) * LQW)};
     double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
     double Se[SE_N], Sw[SW_N], Bw[BW_N];
     hkd_partial_compact(x, u, cd, p.dt, Se, Sw, Bw);
 #pragma unroll
-    for (int j = 0; j < SE_N; ++j) rec[LQ_SE + j] = Se[j];
+    for (int j = 0; j < SE_N; ++j) rec.set(LQ_SE + j, Se[j]);
 #pragma unroll
-    for (int j = 0; j < SW_N; ++j) rec[LQ_SW + j] = Sw[j];
+    for (int j = 0; j < SW_N; ++j) rec.set(LQ_SW + j, Sw[j]);
 #pragma unroll
-    for (int j = 0; j < BW_N; ++j) rec[LQ_BW + j] = Bw[j];
+    for (int j = 0; j < BW_N; ++j) rec.set(LQ_BW + j, Bw[j]);
     // lx: tracking + foot regularisation (HKDCost.cpp:22-37)
     double lx[NX];
 #pragma unroll
@@ -87,7 +99,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
         lx[12 + j] += v;
     }
 #pragma unroll
-    for (int j = 0; j < NX; ++j) rec[LQ_LX + j] = lx[j];
+    for (int j = 0; j < NX; ++j) rec.set(LQ_LX + j, lx[j]);
     // lu + ReB gradient / Hessian (SinglePhase.cpp:380-394)
     double lu[NU], rb[24];
 #pragma unroll
@@ -116,9 +128,9 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
         }
     }
 #pragma unroll
-    for (int j = 0; j < NU; ++j) rec[LQ_LU + j] = lu[j];
+    for (int j = 0; j < NU; ++j) rec.set(LQ_LU + j, lu[j]);
 #pragma unroll
-    for (int j = 0; j < 24; ++j) rec[LQ_RB + j] = rb[j];
+    for (int j = 0; j < 24; ++j) rec.set(LQ_RB + j, rb[j]);
 }
 
 // k_terminal: one wave per (element, phase): Phix, Phixx (+AL, quirk A4) and reset-map Jacobian Px.
@@ -557,7 +569,10 @@ void launch_update_nominal(const Params &p, const Bufs &d, int init, hipStream_t
 }
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_lq, dim3(blocks_for((long)p.B * p.S, 256)), dim3(256), 0, st, p, d);
+    if (p.fp32)
+        hipLaunchKernelGGL(k_lq<true>, dim3(blocks_for((long)p.B * p.S, 256)), dim3(256), 0, st, p, d);
+    else
+        hipLaunchKernelGGL(k_lq<false>, dim3(blocks_for((long)p.B * p.S, 256)), dim3(256), 0, st, p, d);
     hipLaunchKernelGGL(k_terminal, dim3(p.B * p.P), dim3(64), 0, st, p, d);
 }
 

@@ -53,7 +53,10 @@ class Solver:
     """B independent HKD trajectory optimisations on one GPU (one C-ABI handle)."""
 
     def __init__(self, prob: dict, options: Options | None = None, device: int = 0,
-                 cparams: ConstraintParams | None = None, weights: Weights | None = None):
+                 cparams: ConstraintParams | None = None, weights: Weights | None = None,
+                 riccati_fp32: bool = False):
+        """riccati_fp32: SURVEY.md §8 config C5 — LQ records, backward Riccati sweep, gains and the
+        linear rollout in fp32; dynamics, costs, line search and the AL/ReB outer loop in fp64."""
         L = lib()
         self.prob = prob
         self.B = int(prob["batch"])
@@ -67,6 +70,7 @@ class Solver:
             desc.horizons[i] = int(n)
         desc.dt = float(prob["dt"])
         desc.ref_per_element = 0 if prob["ref_x"].shape[0] == 1 else 1
+        desc.riccati_fp32 = 1 if riccati_fp32 else 0
         if weights is None:
             L.hsddp_default_weights(C.byref(desc.weights))
         else:

@@ -50,7 +50,7 @@ class ConstraintParams(C.Structure):
 class ProblemDesc(C.Structure):
     _fields_ = [("device", C.c_int), ("batch", C.c_int), ("n_phases", C.c_int),
                 ("horizons", C.c_int * MAX_PHASES), ("dt", C.c_double), ("ref_per_element", C.c_int),
-                ("weights", Weights), ("cparams", ConstraintParams)]
+                ("weights", Weights), ("cparams", ConstraintParams), ("riccati_fp32", C.c_int)]
 
 
 class ElementInfo(C.Structure):

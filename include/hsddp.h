@@ -105,6 +105,10 @@ typedef struct hsddp_problem_desc {
     int ref_per_element;                 /* 0: one reference shared by the batch; 1: per element */
     hsddp_hkd_weights weights;
     hsddp_constraint_params cparams;
+    /* extension: 1 = fp32 Riccati mode — LQ records, backward sweep,
+       gains K and the linear rollout in fp32; dynamics, costs, line search and the AL/ReB outer
+       loop stay fp64.  0 (default) = fp64 throughout, as the reference (T = double). */
+    int riccati_fp32;
 } hsddp_problem_desc;
 
 typedef struct hsddp_element_info {

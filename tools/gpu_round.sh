@@ -33,4 +33,14 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
     bash "$R/tools/pmc.sh" || exit $?
 fi
+# config C5: fp32 Riccati mode — bench line, tolerance against fp64, kernel trace and PMC traffic
+if [ "$MODE" = all ] || [ "$MODE" = fp32 ]; then
+    step bench_fp32 300 python bench.py --riccati-fp32
+    step fp32_tolerance 600 python -u tools/fp32_tolerance.py
+    cd /tmp && export TMPDIR=/tmp
+    step rocprof_trace_fp32 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_trace_fp32" -o run -- \
+        python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --riccati-fp32
+    cd "$R"
+    PFX=pmc32 BENCH_ARGS=--riccati-fp32 bash "$R/tools/pmc.sh" || exit $?
+fi
 exit 0

@@ -20,7 +20,9 @@ def read_pass(path):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     with open(path) as f:
         for r in csv.DictReader(f):
-            k = r["Kernel_Name"].split("(")[0].replace("hsddp::", "")
+            # "void hsddp::k_riccati<double>(hsddp::Params, ...)" -> "k_riccati" (the precision is
+            # part of the configuration key)
+            k = r["Kernel_Name"].split("(")[0].replace("hsddp::", "").replace("void ", "").split("<")[0]
             agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
 
@@ -28,9 +30,10 @@ def read_pass(path):
 def main():
     out_dir = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     cfg_key = sys.argv[2] if len(sys.argv) > 2 else "trot_4x50_b4096"
+    pfx = sys.argv[3] if len(sys.argv) > 3 else "pmc"
     kernels = collections.defaultdict(dict)
     for name in ("sq", "fetch", "write"):
-        path = os.path.join(out_dir, f"pmc_{name}", "run_counter_collection.csv")
+        path = os.path.join(out_dir, f"{pfx}_{name}", "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
         for k, cs in read_pass(path).items():
