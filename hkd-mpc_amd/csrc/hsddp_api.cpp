@@ -16,6 +16,7 @@
 
 #include "../../include/hsddp.h"
 #include "hsddp_internal.h"
+#include "hsddp_mpc.h"
 
 using namespace hsddp;
 
@@ -209,7 +210,24 @@ struct hsddp_handle_t {
     int Bref = 1;
     bool have_problem = false;
     std::vector<int> contacts;  // host copy [B][P+1][4]: maps the compact K rows to controls
+    void *scratch = nullptr;    // device staging for the MPC-side calls (grown on demand)
+    size_t scratch_bytes = 0;
 };
+
+// device staging area of at least `bytes` (contents not preserved when it grows)
+static int scratch(hsddp_handle h, size_t bytes, char **out)
+{
+    if (bytes > h->scratch_bytes) {
+        if (h->scratch) hipFree(h->scratch);
+        h->scratch = nullptr;
+        h->scratch_bytes = 0;
+        hipError_t e = hipMalloc(&h->scratch, bytes);
+        if (e != hipSuccess) return fail(HSDDP_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+        h->scratch_bytes = bytes;
+    }
+    *out = (char *)h->scratch;
+    return HSDDP_OK;
+}
 
 // control u of compact gain row q at control slot k of element b (KCW layout, hsddp_internal.h)
 static int coupled_control(hsddp_handle h, size_t b, size_t k, int q)
@@ -336,6 +354,7 @@ extern "C" int hsddp_destroy(hsddp_handle h)
     hipSetDevice(h->desc.device);
     if (h->stream) hipStreamSynchronize(h->stream);
     for (void *p : h->allocs) hipFree(p);
+    if (h->scratch) hipFree(h->scratch);
     if (h->host_counter) hipHostFree(h->host_counter);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
@@ -801,5 +820,54 @@ extern "C" int hsddp_device_synchronize(int device)
 {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipDeviceSynchronize());
+    return HSDDP_OK;
+}
+
+// ---- MPC command extraction (HKDMPCSolver::update_foot_placement + publish_mpc_cmd) ----------
+extern "C" int hsddp_extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
+                                      const double *status_durations, int durations_per_element,
+                                      const float *foot_placements, int feet_per_element, float solve_time,
+                                      hsddp_mpc_command *out)
+{
+    if (!h || !out) return fail(HSDDP_ERR_ARG, "null argument");
+    if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
+    const Params &p = h->p;
+    CmdArgs a{};
+    a.n = nsteps_between_mpc + 7;  // HKDMPC.cpp:232-233
+    if (nsteps_between_mpc < 1 || a.n > HSDDP_CMD_STEPS || a.n > p.Kc)
+        return fail(HSDDP_ERR_ARG, "nsteps_between_mpc + 7 must fit the command (10 rows) and the horizon");
+    // the knot walk of publish_mpc_cmd (HKDMPC.cpp:239-246): s runs over phase i's controls
+    for (int k = 0, i = 0, s = 0; k < a.n; ++k, ++s) {
+        if (s >= p.N[i]) { s = 0; ++i; }
+        a.kc[k] = p.k0[i] + s;
+        a.xs[k] = p.s0[i] + s;
+        a.ph[k] = i;
+    }
+    a.mpc_time = mpc_time;
+    a.dt_mpc = dt_mpc;
+    a.solve_time = solve_time;
+    a.dur_per_elem = durations_per_element ? 1 : 0;
+    a.feet_per_elem = feet_per_element ? 1 : 0;
+    HIPCHK(hipSetDevice(h->desc.device));
+    const size_t B = p.B;
+    const size_t cmd_bytes = (B * sizeof(hsddp_mpc_command) + 255) / 256 * 256;
+    const size_t dur_bytes = status_durations ? ((a.dur_per_elem ? B : 1) * p.P * 4 * sizeof(double) + 255) / 256 * 256 : 0;
+    const size_t feet_bytes = foot_placements ? (a.feet_per_elem ? B : 1) * 12 * sizeof(float) : 0;
+    char *buf;
+    int rc;
+    if ((rc = scratch(h, cmd_bytes + dur_bytes + feet_bytes, &buf))) return rc;
+    hsddp_mpc_command *dcmd = (hsddp_mpc_command *)buf;
+    if (status_durations) {
+        a.durations = (const double *)(buf + cmd_bytes);
+        if ((rc = h2d((void *)a.durations, status_durations, (a.dur_per_elem ? B : 1) * p.P * 4 * sizeof(double), h->stream))) return rc;
+    }
+    if (foot_placements) {
+        a.feet = (const float *)(buf + cmd_bytes + dur_bytes);
+        if ((rc = h2d((void *)a.feet, foot_placements, feet_bytes, h->stream))) return rc;
+    }
+    launch_extract_commands(p, h->d, a, dcmd, h->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, dcmd, B * sizeof(hsddp_mpc_command), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
     return HSDDP_OK;
 }

@@ -1,0 +1,25 @@
+// hsddp_mpc.h — kernel interface of the MPC-side steps around the solve (hsddp_mpc.hip).
+#pragma once
+
+#include "hsddp_internal.h"
+
+struct hsddp_mpc_command;
+
+namespace hsddp {
+
+// publish_mpc_cmd's knot walk resolved on the host (horizons are shared by the batch)
+struct CmdArgs {
+    int n;                         // N_mpcsteps
+    int kc[10], xs[10], ph[10];    // control slot, state slot and phase of command row k
+    double mpc_time, dt_mpc;
+    const double *durations;       // [Bd][P][4] device, or null
+    int dur_per_elem;
+    const float *feet;             // [Bf][12] device, or null
+    int feet_per_elem;
+    float solve_time;
+};
+
+void launch_extract_commands(const Params &p, const Bufs &d, const CmdArgs &a, hsddp_mpc_command *out,
+                             hipStream_t st);
+
+}  // namespace hsddp

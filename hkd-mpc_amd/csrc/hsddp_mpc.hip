@@ -1,0 +1,76 @@
+// hsddp_mpc.hip — the MPC caller's steps on either side of the solve, batched
+// over the B elements of a handle.
+//
+//   k_extract_commands   HKDMPCSolver::update_foot_placement + publish_mpc_cmd (HKDMPC.cpp:207-298):
+//                        the first N_mpcsteps control knots of the solved trajectory into the
+//                        hkd_command_lcmt layout (lcmtypes/hkd_command_lcmt.lcm:1-11), one
+//                        workgroup per element, threads striding over the record's fields.
+#include "../../include/hsddp.h"
+#include "hsddp_mpc.h"
+
+namespace hsddp {
+
+// One element per workgroup.  The knot walk of publish_mpc_cmd (phase i, knot s; HKDMPC.cpp:
+// 239-246) depends only on the horizons, which the batch shares, so the host passes it resolved
+// (a.kc[k], a.ph[k]).
+__global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdArgs a, hsddp_mpc_command *out)
+{
+    const int b = blockIdx.x, t = threadIdx.x;
+    hsddp_mpc_command &o = out[b];
+    const int *cb = d.contacts + (size_t)b * (p.P + 1) * 4;
+    // controls, body states, feedback rows (zero past N_mpcsteps, as a fresh message)
+    for (int e = t; e < HSDDP_CMD_STEPS * 24; e += blockDim.x) {
+        const int k = e / 24, j = e % 24;
+        o.hkd_controls[k][j] = k < a.n ? (float)d.Ubar[((size_t)b * p.Kc + a.kc[k]) * NX + j] : 0.f;
+    }
+    for (int e = t; e < HSDDP_CMD_STEPS * 12; e += blockDim.x) {
+        const int k = e / 12, j = e % 12;
+        o.des_body_state[k][j] = k < a.n ? (float)d.Xbar[((size_t)b * p.S + a.xs[k]) * NX + j] : 0.f;
+    }
+    // K(m, n), m, n < 12: control m is leg m/3's GRF; its gain row is compact row m when the leg
+    // is in stance and exactly zero when it swings (KCW layout, hsddp_internal.h)
+    for (int e = t; e < HSDDP_CMD_STEPS * 144; e += blockDim.x) {
+        const int k = e / 144, m = (e / 12) % 12, n = e % 12;
+        float v = 0.f;
+        if (k < a.n && cb[a.ph[k] * 4 + m / 3]) {
+            const size_t idx = ((size_t)b * p.Kc + a.kc[k]) * KCW + m * NX + n;
+            v = p.fp32 ? d.K32[idx] : (float)d.K[idx];
+        }
+        o.feedback[k][m][n] = v;
+    }
+    for (int e = t; e < HSDDP_CMD_STEPS * 4; e += blockDim.x) {
+        const int k = e / 4, l = e % 4;
+        const bool on = k < a.n;
+        o.contacts[k][l] = on ? cb[a.ph[k] * 4 + l] : 0;
+        const double *dur = a.durations ? a.durations + ((size_t)(a.dur_per_elem ? b : 0) * p.P + a.ph[k]) * 4 : nullptr;
+        o.statusTimes[k][l] = (on && dur) ? dur[l] : 0.0;
+    }
+    // mpc_time + k dt_mpc rounded twice, as written (no fused multiply-add)
+    if (t < HSDDP_CMD_STEPS) o.mpc_times[t] = t < a.n ? __dadd_rn(a.mpc_time, __dmul_rn((double)t, a.dt_mpc)) : 0.0;
+    // update_foot_placement (HKDMPC.cpp:207-230): the first swing -> stance transition of leg l
+    // among phase pairs (i, i + 1), i = 0 .. 4, gives the foot position stored in the next phase's
+    // first state (qdummy, states 12 + 3 l ..); otherwise the current foot position
+    if (t < 12) {
+        const int l = t / 3, ax = t % 3;
+        float pf = a.feet ? a.feet[(size_t)(a.feet_per_elem ? b : 0) * 12 + t] : 0.f;
+        for (int i = 0; i < p.P - 1 && i <= 4; ++i) {
+            if (cb[i * 4 + l] == 0 && cb[(i + 1) * 4 + l] == 1) {
+                pf = (float)d.Xbar[((size_t)b * p.S + p.s0[i + 1]) * NX + 12 + 3 * l + ax];
+                break;
+            }
+        }
+        o.foot_placement[t] = pf;
+    }
+    if (t == 0) {
+        o.N_mpcsteps = a.n;
+        o.solve_time = a.solve_time;
+    }
+}
+
+void launch_extract_commands(const Params &p, const Bufs &d, const CmdArgs &a, hsddp_mpc_command *out,
+                             hipStream_t st)
+{
+    hipLaunchKernelGGL(k_extract_commands, dim3(p.B), dim3(256), 0, st, p, d, a, out);
+}
+
+}  // namespace hsddp

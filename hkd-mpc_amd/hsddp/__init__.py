@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 from . import model, synthetic  # noqa: F401
-from ._lib import (ConstraintParams, ElementInfo, HSDDPError, Options, ProblemDesc, Stats, Weights,
+from ._lib import (MPC_COMMAND, ConstraintParams, ElementInfo, HSDDPError, Options, ProblemDesc, Stats, Weights,
                    check, dp, ip, lib)
 
 SETTINGS_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "settings")
@@ -136,6 +136,21 @@ class Solver:
         out = {}
         for f, _ in ElementInfo._fields_:
             out[f] = np.array([getattr(info[b], f) for b in range(self.B)])
+        return out
+
+    def extract_commands(self, nsteps_between_mpc: int = 1, mpc_time: float = 0.0, dt_mpc: float = 0.01,
+                         status_durations=None, foot_placements=None, solve_time: float = 0.0) -> np.ndarray:
+        """HKDMPCSolver::update_foot_placement + publish_mpc_cmd (HKDMPC.cpp:207-298) for every
+        element: a [B] record array of hsddp_mpc_command (= hkd_command_lcmt).
+        status_durations: [P, 4] or [B, P, 4]; foot_placements: [12] or [B, 12]."""
+        out = np.zeros(self.B, dtype=MPC_COMMAND)
+        dur = None if status_durations is None else np.ascontiguousarray(status_durations, dtype=np.float64)
+        feet = None if foot_placements is None else np.ascontiguousarray(foot_placements, dtype=np.float32)
+        check(lib().hsddp_extract_commands(
+            self._h, int(nsteps_between_mpc), float(mpc_time), float(dt_mpc),
+            None if dur is None else dur.ctypes.data, int(dur is not None and dur.ndim == 3),
+            None if feet is None else feet.ctypes.data, int(feet is not None and feet.ndim == 2),
+            float(solve_time), out.ctypes.data))
         return out
 
     def synchronize(self) -> None:

@@ -65,6 +65,15 @@ class Stats(C.Structure):
                 ("n_backward_launches", C.c_int), ("ms_linear", C.c_double)]
 
 
+# hsddp_mpc_command (include/hsddp.h) = hkd_command_lcmt (lcmtypes/hkd_command_lcmt.lcm:1-11) as a
+# C-aligned numpy record (tests/test_host_logic.py checks size and offsets against the C compiler)
+MPC_COMMAND = np.dtype([("N_mpcsteps", np.int32), ("mpc_times", np.float64, (10,)),
+                        ("hkd_controls", np.float32, (10, 24)), ("des_body_state", np.float32, (10, 12)),
+                        ("contacts", np.int32, (10, 4)), ("statusTimes", np.float64, (10, 4)),
+                        ("foot_placement", np.float32, (12,)), ("feedback", np.float32, (10, 12, 12)),
+                        ("solve_time", np.float32)], align=True)
+
+
 class HSDDPError(RuntimeError):
     pass
 
@@ -80,7 +89,7 @@ EXPORTS = [
     "hsddp_download_element_info", "hsddp_synchronize", "hsddp_device_bytes", "hsddp_hkd_dynamics",
     "hsddp_hkd_dynamics_partial", "hsddp_hkd_foot_position", "hsddp_hkd_foot_jacobian",
     "hsddp_hkd_resetmap", "hsddp_hkd_resetmap_partial", "hsddp_device_alloc", "hsddp_device_free",
-    "hsddp_memcpy_h2d", "hsddp_memcpy_d2h", "hsddp_device_synchronize",
+    "hsddp_memcpy_h2d", "hsddp_memcpy_d2h", "hsddp_device_synchronize", "hsddp_extract_commands",
 ]
 
 
@@ -124,6 +133,8 @@ def lib():
     L.hsddp_memcpy_h2d.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     L.hsddp_memcpy_d2h.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     L.hsddp_device_synchronize.argtypes = [C.c_int]
+    L.hsddp_extract_commands.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_void_p, C.c_int,
+                                         C.c_void_p, C.c_int, C.c_float, C.c_void_p]
     _lib = L
     return L
 

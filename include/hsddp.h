@@ -19,6 +19,7 @@
  *   hsddp_solve_begin/_iterate/_end           the same loop split at its inner iterations (:257-303 / :304-381 / :383-408)
  *   hsddp_download_trajectory                 Trajectory fields read by the caller  HKDMPC.cpp:243-298
  *   hsddp_download_element_info               get_actual_cost / get_solver_info     MultiPhaseDDP.h:416; .cpp:532-541
+ *   hsddp_extract_commands                    update_foot_placement + publish_mpc_cmd HKDMPC.cpp:207-298
  *   hsddp_hkd_dynamics                        HKD::Model::dynamics (hkinodyn)       HKDModel.h:33-45
  *   hsddp_hkd_dynamics_partial                HKD::Model::dynamics_partial          HKDModel.h:46-61
  *   hsddp_hkd_resetmap(_partial)              HKDReset::resetmap(_partial)          HKDReset.h:41-136
@@ -167,6 +168,31 @@ int hsddp_download_working(hsddp_handle h, double *X, double *U, double *Defect,
 int hsddp_download_element_info(hsddp_handle h, hsddp_element_info *info);
 int hsddp_synchronize(hsddp_handle h);
 size_t hsddp_device_bytes(hsddp_handle h);
+
+/* ---- MPC command extraction ------------------------------------------
+ * Mirror of hkd_command_lcmt (lcmtypes/hkd_command_lcmt.lcm:1-11), field for field. */
+#define HSDDP_CMD_STEPS 10
+typedef struct hsddp_mpc_command {
+    int N_mpcsteps;                       /* nsteps_between_mpc + 7 (HKDMPC.cpp:232-235) */
+    double mpc_times[HSDDP_CMD_STEPS];    /* mpc_time + k dt_mpc */
+    float hkd_controls[HSDDP_CMD_STEPS][24];   /* Ubar */
+    float des_body_state[HSDDP_CMD_STEPS][12]; /* Xbar body states */
+    int contacts[HSDDP_CMD_STEPS][4];
+    double statusTimes[HSDDP_CMD_STEPS][4];    /* contact durations of the knot's phase */
+    float foot_placement[12];             /* next touchdown foot positions (update_foot_placement) */
+    float feedback[HSDDP_CMD_STEPS][12][12];   /* K(0:12, 0:12) */
+    float solve_time;
+} hsddp_mpc_command;
+
+/* HKDMPCSolver::update_foot_placement + publish_mpc_cmd (HKDMPC.cpp:207-298) for every element,
+ * on the device, from the solved trajectory.  status_durations [Bd][P][4] (Bd = 1 or B; NULL = 0)
+ * are the phases' contact durations (HKDProblemData::contact_durations); foot_placements [Bf][12]
+ * (Bf = 1 or B; NULL = 0) the current foot positions, kept for legs without a touchdown in the
+ * first five phase transitions; out [B] host array.  Rows k >= N_mpcsteps are zero. */
+int hsddp_extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
+                           const double *status_durations, int durations_per_element,
+                           const float *foot_placements, int feet_per_element, float solve_time,
+                           hsddp_mpc_command *out);
 
 /* ---- batched model primitives (device pointers, n points, async on `stream` (NULL = default)) */
 /* xn[n][24] = hkinodyn(x[n][24], u[n][24], dt, c[n][4]) */
