@@ -212,6 +212,14 @@ struct hsddp_handle_t {
     std::vector<int> contacts;  // host copy [B][P+1][4]: maps the compact K rows to controls
     void *scratch = nullptr;    // device staging for the MPC-side calls (grown on demand)
     size_t scratch_bytes = 0;
+    // receding-horizon state (HKDProblemData, HKDProblem.h:20-66): is_phase_reach_end per phase,
+    // state-slot capacity (a shift keeps Kc and may add phases), and the second Xbar / Ubar / K
+    // set the shift gathers into (allocated by the first shift)
+    std::vector<int> reach_end;
+    size_t S_cap = 0;
+    double *spare_Xbar = nullptr, *spare_Ubar = nullptr;
+    void *spare_K = nullptr;
+    bool need_inputs = false;   // a shift changed the layout: update_problem before solving
 };
 
 // device staging area of at least `bytes` (contents not preserved when it grows)
@@ -311,7 +319,13 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
     p.fp32 = desc->riccati_fp32 ? 1 : 0;
     h->Bref = p.ref_per_element ? p.B : 1;
     fill_params(h);
-    const size_t B = p.B, S = p.S, Kc = p.Kc, P = p.P, Br = h->Bref;
+    for (int i = 0; i < p.P; ++i) p.ss[i] = p.N[i] + 1;  // every knot a shooting state (HKDProblem.cpp:104)
+    p.has_tail = 0;
+    h->reach_end.assign(p.P, 0);  // HKDProblem.cpp:56-57 compares a contact with itself (quirk A15)
+    // State-slot buffers hold Kc + HSDDP_MAX_PHASES slots (a receding-horizon shift keeps Kc and can
+    // add phases, S = Kc + P); per-phase buffers hold HSDDP_MAX_PHASES phases.
+    h->S_cap = (size_t)p.Kc + HSDDP_MAX_PHASES;
+    const size_t B = p.B, S = h->S_cap, Kc = p.Kc, P = HSDDP_MAX_PHASES, Br = h->Bref;
     Bufs &d = h->d;
     int *contacts; double *x0, *rx, *ru, *rf;
     int rc = 0;
@@ -355,6 +369,7 @@ extern "C" int hsddp_destroy(hsddp_handle h)
     if (h->stream) hipStreamSynchronize(h->stream);
     for (void *p : h->allocs) hipFree(p);
     if (h->scratch) hipFree(h->scratch);
+
     if (h->host_counter) hipHostFree(h->host_counter);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
@@ -377,8 +392,9 @@ static int h2d(void *dst, const void *src, size_t bytes, hipStream_t st)
     return HSDDP_OK;
 }
 
-extern "C" int hsddp_upload_problem(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
-                                    const double *ref_u, const double *ref_foot)
+// contacts, x0 and references of the current layout to the device
+static int upload_inputs(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
+                         const double *ref_u, const double *ref_foot)
 {
     if (!h || !contacts || !x0 || !ref_x || !ref_u || !ref_foot) return fail(HSDDP_ERR_ARG, "null argument");
     HIPCHK(hipSetDevice(h->desc.device));
@@ -394,6 +410,16 @@ extern "C" int hsddp_upload_problem(hsddp_handle h, const int *contacts, const d
         (rc = h2d((void *)h->d.ref_foot, ref_foot, Br * S * 12 * sizeof(double), h->stream)))
         return rc;
     h->contacts.assign(contacts, contacts + B * (P + 1) * 4);
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_upload_problem(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
+                                    const double *ref_u, const double *ref_foot)
+{
+    int rc = upload_inputs(h, contacts, x0, ref_x, ref_u, ref_foot);
+    if (rc) return rc;
+    const Params &p = h->p;
+    const size_t B = p.B, S = p.S, Br = h->Bref;
     // default warm start: Xbar = X = reference (HKDProblem.cpp:84-90), Ubar = U = 0, K = 0
     if (Br == 1) launch_broadcast(h->d.Xbar, h->d.ref_x, S * NX, B, h->stream);
     else HIPCHK(hipMemcpyAsync(h->d.Xbar, h->d.ref_x, B * S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
@@ -402,6 +428,20 @@ extern "C" int hsddp_upload_problem(hsddp_handle h, const int *contacts, const d
     else HIPCHK(hipMemsetAsync(h->d.K, 0, B * p.Kc * KCW * sizeof(double), h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     h->have_problem = true;
+    h->need_inputs = false;
+    return hsddp_upload_warm_start(h, nullptr, nullptr, nullptr);
+}
+
+extern "C" int hsddp_update_problem(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
+                                    const double *ref_u, const double *ref_foot)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
+    int rc = upload_inputs(h, contacts, x0, ref_x, ref_u, ref_foot);
+    if (rc) return rc;
+    h->need_inputs = false;
+    // keeps Xbar / Ubar / K; resets X, U, dX, the ReB / AL parameters (reset_params,
+    // HKDProblem.cpp:209) and the per-element solver state
     return hsddp_upload_warm_start(h, nullptr, nullptr, nullptr);
 }
 
@@ -502,6 +542,7 @@ static int solve_check(hsddp_handle h)
 {
     if (!h) return fail(HSDDP_ERR_ARG, "null handle");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
+    if (h->need_inputs) return fail(HSDDP_ERR_ARG, "the layout changed (hsddp_shift): call hsddp_update_problem first");
     if (!h->opt.MS)
         return fail(HSDDP_ERR_UNSUPPORTED, "single shooting (MS = false) is not supported by the knot-parallel rollout");
     HIPCHK(hipSetDevice(h->desc.device));
@@ -677,6 +718,8 @@ extern "C" int hsddp_download_trajectory(hsddp_handle h, double *Xbar, double *U
     int rc;
     if ((rc = d2h(Xbar, h->d.Xbar, B * S * NX * 8)) || (rc = d2h(Ubar, h->d.Ubar, B * Kc * NX * 8)))
         return rc;
+    if (K && h->need_inputs)
+        return fail(HSDDP_ERR_ARG, "the layout changed (hsddp_shift): call hsddp_update_problem before downloading K");
     if (K) { // expand the coupled rows; the decoupled controls' rows are exactly zero
         std::vector<double> kc(B * Kc * KCW);
         if (h->p.fp32) {
@@ -869,5 +912,136 @@ extern "C" int hsddp_extract_commands(hsddp_handle h, int nsteps_between_mpc, do
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, dcmd, B * sizeof(hsddp_mpc_command), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
+    return HSDDP_OK;
+}
+
+// ---- receding-horizon shift (HKDProblem::update, HKDProblem.cpp:117-222) ----------------------
+namespace {
+// one phase of the layout being shifted; slot labels name where each value comes from:
+// state  >= 0: old Xbar slot, -1: zero, <= -2: old (working) X slot -2 - label;
+// control >= 0: old control slot (Ubar and K), -1: zero
+struct ShiftPhase {
+    int N, ss, reach;
+    std::vector<int> xs, us;
+};
+}  // namespace
+
+extern "C" int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_change)
+{
+    if (!h || (n_steps > 0 && !contact_change)) return fail(HSDDP_ERR_ARG, "null argument");
+    if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
+    if (n_steps < 0) return fail(HSDDP_ERR_ARG, "n_steps must be >= 0");
+    Params &p = h->p;
+    std::vector<ShiftPhase> ph(p.P);
+    for (int i = 0; i < p.P; ++i) {
+        ph[i].N = p.N[i]; ph[i].ss = p.ss[i]; ph[i].reach = h->reach_end[i];
+        for (int k = 0; k <= p.N[i]; ++k) ph[i].xs.push_back(p.s0[i] + k);
+        for (int k = 0; k < p.N[i]; ++k) ph[i].us.push_back(p.k0[i] + k);
+    }
+    for (int j = 0; j < n_steps; ++j) {
+        // front: a first phase of one knot shrinks to a point and is removed (pop_front_phase,
+        // HKDProblem.h:56-66); otherwise its first knot is dropped (SinglePhase::pop_front,
+        // SinglePhase.cpp:496-501)
+        if (ph.front().N <= 1) {
+            if (ph.size() == 1) return fail(HSDDP_ERR_ARG, "shift would remove the only phase");
+            ph.erase(ph.begin());
+        } else {
+            ShiftPhase &f = ph.front();
+            f.xs.erase(f.xs.begin());
+            f.us.erase(f.us.begin());
+            f.N--;
+        }
+        // back: a contact change after the last phase reached its end starts a new phase of one
+        // knot with a zero trajectory (Trajectory::create_data); otherwise the last phase grows by
+        // push_back_default: X.back() copied into X and Xbar, zero control and gain
+        // (SinglePhase.cpp:485-490, TrajectoryManagement.cpp:163-190)
+        ShiftPhase &l = ph.back();
+        if (contact_change[j] && l.reach) {
+            if ((int)ph.size() >= HSDDP_MAX_PHASES) return fail(HSDDP_ERR_ARG, "shift exceeds HSDDP_MAX_PHASES phases");
+            ShiftPhase n;
+            n.N = 1; n.ss = 0; n.reach = 0;
+            n.xs = {-1, -1};
+            n.us = {-1};
+            ph.push_back(n);
+        } else {
+            const int last = l.xs.back();
+            l.xs.push_back(last >= 0 ? -2 - last : last);
+            l.us.push_back(-1);
+            l.N++;
+            if (contact_change[j]) l.reach = 1;
+        }
+    }
+    // update_SS_config after the steps (HKDProblem.cpp:203-217): every phase but a last one of
+    // horizon <= 2 gets all its states as shooting states
+    const int P = (int)ph.size();
+    for (int i = 0; i < P; ++i)
+        if (i < P - 1 || ph[i].N > 2) ph[i].ss = ph[i].N + 1;
+    for (int i = 0; i < P - 1; ++i)
+        if (ph[i].ss < ph[i].N + 1) return fail(HSDDP_ERR_UNSUPPORTED, "non-shooting states outside the last phase");
+    std::vector<int> smap, cmap;
+    for (auto &f : ph) {
+        smap.insert(smap.end(), f.xs.begin(), f.xs.end());
+        cmap.insert(cmap.end(), f.us.begin(), f.us.end());
+    }
+    if (smap.size() > h->S_cap || (int)cmap.size() != p.Kc)
+        return fail(HSDDP_ERR_ARG, "shifted layout exceeds the handle's capacity");
+    HIPCHK(hipSetDevice(h->desc.device));
+    Bufs &d = h->d;
+    const size_t B = p.B;
+    int rc;
+    if (!h->spare_Xbar) {
+        double *sx, *su;
+        void *sk;
+        if ((rc = dalloc(h, sx, B * h->S_cap * NX)) || (rc = dalloc(h, su, B * p.Kc * NX))) return rc;
+        if (p.fp32) { float *k32; if ((rc = dalloc(h, k32, B * p.Kc * KCW))) return rc; sk = k32; }
+        else { double *k64; if ((rc = dalloc(h, k64, B * p.Kc * KCW))) return rc; sk = k64; }
+        h->spare_Xbar = sx; h->spare_Ubar = su; h->spare_K = sk;
+    }
+    char *buf;
+    if ((rc = scratch(h, (smap.size() + cmap.size()) * sizeof(int), &buf))) return rc;
+    int *dsm = (int *)buf, *dcm = dsm + smap.size();
+    if ((rc = h2d(dsm, smap.data(), smap.size() * sizeof(int), h->stream)) ||
+        (rc = h2d(dcm, cmap.data(), cmap.size() * sizeof(int), h->stream)))
+        return rc;
+    ShiftArgs a;
+    a.S_old = p.S; a.S_new = (int)smap.size(); a.Kc = p.Kc;
+    a.smap = dsm; a.cmap = dcm;
+    a.fp32 = p.fp32;
+    a.zero_u0 = 1;  // trajectory_ptrs.front()->Ubar[0].setZero() (HKDProblem.cpp:219)
+    launch_shift_gather(p.B, a, d, h->spare_Xbar, h->spare_Ubar, h->spare_K, h->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(h->stream));
+    std::swap(d.Xbar, h->spare_Xbar);
+    std::swap(d.Ubar, h->spare_Ubar);
+    if (p.fp32) { float *t = d.K32; d.K32 = (float *)h->spare_K; h->spare_K = t; }
+    else { double *t = d.K; d.K = (double *)h->spare_K; h->spare_K = t; }
+    // the new layout
+    p.P = P;
+    int s = 0, k = 0;
+    p.has_tail = 0;
+    h->reach_end.resize(P);
+    for (int i = 0; i < P; ++i) {
+        p.N[i] = ph[i].N; p.s0[i] = s; p.k0[i] = k; p.ss[i] = ph[i].ss;
+        s += p.N[i] + 1; k += p.N[i];
+        h->reach_end[i] = ph[i].reach;
+        if (p.ss[i] < p.N[i] + 1) p.has_tail = 1;
+    }
+    p.S = s;
+    h->desc.n_phases = P;
+    for (int i = 0; i < P; ++i) h->desc.horizons[i] = p.N[i];
+    h->need_inputs = true;
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_get_layout(hsddp_handle h, int *n_phases, int *horizons, int *shooting, int *reach_end)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    const Params &p = h->p;
+    if (n_phases) *n_phases = p.P;
+    for (int i = 0; i < p.P; ++i) {
+        if (horizons) horizons[i] = p.N[i];
+        if (shooting) shooting[i] = p.ss[i];
+        if (reach_end) reach_end[i] = h->reach_end[i];
+    }
     return HSDDP_OK;
 }

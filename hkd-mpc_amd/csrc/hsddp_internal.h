@@ -56,6 +56,11 @@ struct Params {
     int AL_active, ReB_active, no_early_exit;
     int reb_uniform;  // every ReB (delta, eps) equals (grf_delta, grf_eps): per-knot arrays not read
     int fp32;         // fp32 Riccati mode (config C5): LQ records, sweep, gains and linear rollout in fp32
+    // shooting states per phase, SS_set = {0 .. ss-1} (SinglePhase::update_SS_config,
+    // SinglePhase.h:161-164): N_i + 1 except a new last phase of horizon <= 2 after a receding-
+    // horizon shift (HKDProblem.cpp:203-216); has_tail: some phase has non-shooting states
+    int ss[MAXP];
+    int has_tail;
 };
 
 struct ElemState {

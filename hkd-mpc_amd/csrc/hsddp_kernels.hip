@@ -201,6 +201,42 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
 }
 
 // ---------------------------------------------------------------------------------------------
+// Per-slot outputs of one rollout trial from the slot's state x = X[k], simulated state xs =
+// Xsim[k] and control u = U[k] (k < N): Defect, |Defect|^2, divergence flag, running or terminal
+// cost with its constraint violation and touchdown residuals (SinglePhase.cpp:196-232).
+DEV void finish_slot(const Params &p, const Bufs &d, int b, int s, int i, int k, const int *c, const int *cn,
+                     const double *x, const double *xs, const double *u)
+{
+    const size_t sb = (size_t)b * p.S;
+    double nrm = 0.0, fs = 0.0;
+    double *Dg = d.Defect + (sb + s) * NX;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+        nrm += xs[j] * xs[j];
+        const double df = xs[j] - x[j];
+        fs += df * df;
+        Dg[j] = df;
+    }
+    d.slot_feas[sb + s] = fs;
+    d.slot_div[sb + s] = (k > 0 && sqrt(nrm) > 1e6) ? 1 : 0;
+    const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
+    if (k == p.N[i]) {
+        double tv, h[4];
+        const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
+        d.slot_cost[sb + s] = terminal_cost(p, c, cn, x, xr, pf, sg, lm, tv, h);
+        d.slot_viol[sb + s] = tv;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) d.term_h[((size_t)b * p.P + i) * 4 + l] = h[l];
+    } else {
+        const int kc = p.k0[i] + k;
+        const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
+        const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
+        double viol;
+        d.slot_cost[sb + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
+        d.slot_viol[sb + s] = viol;
+    }
+}
+
 // k_rollout: one line-search trial (eps) per (element, state slot).  All knots are shooting states
 // (HKDProblem.cpp:104), so X[k] = Xbar[k] + eps dX[k] and the simulated state at k depends only on
 // knot k-1: the nonlinear rollout is knot-parallel.  U = Ubar + eps du with du = dU + K dX from the
@@ -282,7 +318,6 @@ __global__ __launch_bounds__(64) void k_rollout(Params p, Bufs d, double eps, in
     slot_phase(p, s, i, k);
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
-    const size_t sb = (size_t)b * p.S;
     const double *x = Xt + (gid - xr0) * RS;
     double xs[NX];
     if (k == 0) {
@@ -299,33 +334,68 @@ __global__ __launch_bounds__(64) void k_rollout(Params p, Bufs d, double eps, in
         double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
         hkd_step(x - RS, Ut + (kq - 1 - ur0) * RS, cd, p.dt, xs);
     }
-    double nrm = 0.0, fs = 0.0;
-    double *Dg = d.Defect + (sb + s) * NX;
-#pragma unroll
-    for (int j = 0; j < NX; ++j) {
-        nrm += xs[j] * xs[j];
-        const double df = xs[j] - x[j];
-        fs += df * df;
-        Dg[j] = df;
-    }
-    d.slot_feas[sb + s] = fs;
-    d.slot_div[sb + s] = (k > 0 && sqrt(nrm) > 1e6) ? 1 : 0;
-    const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
-    if (k == p.N[i]) {
-        double tv, h[4];
-        const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
-        d.slot_cost[sb + s] = terminal_cost(p, c, cn, x, xr, pf, sg, lm, tv, h);
-        d.slot_viol[sb + s] = tv;
-#pragma unroll
-        for (int l = 0; l < 4; ++l) d.term_h[((size_t)b * p.P + i) * 4 + l] = h[l];
-    } else {
-        const int kc = p.k0[i] + k;
-        const double *u = Ut + ((long)b * p.Kc + kc - ur0) * RS;
-        const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
-        const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
-        double viol;
-        d.slot_cost[sb + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
-        d.slot_viol[sb + s] = viol;
+    const double *u = k < p.N[i] ? Ut + ((long)b * p.Kc + p.k0[i] + k - ur0) * RS : nullptr;
+    finish_slot(p, d, b, s, i, k, c, cn, x, xs, u);
+}
+
+// k_rollout_tail: the non-shooting states of a phase (k >= ss; HKDProblem::update leaves a new
+// last phase of horizon <= 2 without shooting states) after k_rollout has handled the rest:
+// SinglePhase::hybrid_rollout's sequential branch (SinglePhase.cpp:185-222), X[k] = Xsim[k]
+// (X[0] = x_init when the set is empty) and U[k] = Ubar[k] + eps dU[k] + K[k] (X[k] - Xbar[k]),
+// then the slot outputs of those states.  One thread per element; rare (a few states per element).
+__global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double eps, int init)
+{
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= p.B) return;
+    const ElemState &E = d.el[b];
+    if (!(init ? !E.done : E.ls_active != 0)) return;
+    const size_t sb = (size_t)b * p.S, kb = (size_t)b * p.Kc;
+    for (int i = 0; i < p.P; ++i) {
+        const int N = p.N[i], ss = p.ss[i], s0 = p.s0[i], k0 = p.k0[i];
+        if (ss >= N + 1) continue;
+        int c[4], cn[4];
+        load_contacts(d, p, b, i, c, cn);
+        const double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
+        double x[NX], xs[NX], u[NU];
+        if (ss == 0) { // X[0] = Xsim[0] = x_init (MultiPhaseDDP.cpp:73-81)
+            if (i == 0) {
+                for (int j = 0; j < NX; ++j) xs[j] = d.x0[(size_t)b * NX + j];
+            } else {
+                int cp_[4], cpn[4];
+                load_contacts(d, p, b, i - 1, cp_, cpn);
+                hkd_resetmap(d.X + (sb + s0 - 1) * NX, cp_, cpn, xs);
+            }
+        } else { // Xsim[ss] from the last shooting state and its control (written by k_rollout)
+            const double *xg = d.X + (sb + s0 + ss - 1) * NX, *ug = d.U + (kb + k0 + ss - 1) * NU;
+            for (int j = 0; j < NX; ++j) x[j] = xg[j];
+            for (int j = 0; j < NU; ++j) u[j] = ug[j];
+            hkd_step(x, u, cd, p.dt, xs);
+        }
+        for (int k = ss; k <= N; ++k) {
+            const int s = s0 + k;
+            double *xg = d.X + (sb + s) * NX;
+            for (int j = 0; j < NX; ++j) { x[j] = xs[j]; xg[j] = xs[j]; }
+            const double *up = nullptr;
+            if (k < N) {
+                const int kc = k0 + k;
+                const double *xb = d.Xbar + (sb + s) * NX, *ub = d.Ubar + (kb + kc) * NU, *du = d.dU + (kb + kc) * NU;
+                double dx[NX];
+                for (int j = 0; j < NX; ++j) dx[j] = x[j] - xb[j];
+                for (int j = 0; j < NU; ++j) u[j] = 0.0;
+                // K (X - Xbar) from the 12 coupled gain rows (KCW layout; the other rows are zero)
+                for (int q = 0; q < 12; ++q) {
+                    const size_t kr = ((kb + kc) * 12 + q) * NX;
+                    double acc = 0.0;
+                    for (int j = 0; j < NX; ++j) acc += (p.fp32 ? (double)d.K32[kr + j] : d.K[kr + j]) * dx[j];
+                    u[c[q / 3] ? q : 12 + q] = acc;
+                }
+                double *ug = d.U + (kb + kc) * NU;
+                for (int j = 0; j < NU; ++j) { u[j] = ub[j] + eps * du[j] + u[j]; ug[j] = u[j]; }
+                up = u;
+            }
+            finish_slot(p, d, b, s, i, k, c, cn, x, xs, up);
+            if (k < N) hkd_step(x, u, cd, p.dt, xs);
+        }
     }
 }
 
@@ -558,6 +628,7 @@ static inline unsigned blocks_for(long n, int bs) { return (unsigned)((n + bs - 
 void launch_rollout(const Params &p, const Bufs &d, double eps, int init, hipStream_t st)
 {
     hipLaunchKernelGGL(k_rollout, dim3(blocks_for((long)p.B * p.S, 64)), dim3(64), 0, st, p, d, eps, init);
+    if (p.has_tail) hipLaunchKernelGGL(k_rollout_tail, dim3((p.B + 63) / 64), dim3(64), 0, st, p, d, eps, init);
 }
 void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, hipStream_t st)
 {

@@ -19,6 +19,15 @@ struct CmdArgs {
     float solve_time;
 };
 
+// receding-horizon gather: new slot <- old slot (labels as hsddp_api.cpp ShiftPhase)
+struct ShiftArgs {
+    int S_old, S_new, Kc;
+    const int *smap, *cmap;   // [S_new], [Kc] device
+    int fp32, zero_u0;
+};
+void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, double *Xbar_new, double *Ubar_new, void *K_new,
+                         hipStream_t st);
+
 void launch_extract_commands(const Params &p, const Bufs &d, const CmdArgs &a, hsddp_mpc_command *out,
                              hipStream_t st);
 

@@ -5,6 +5,10 @@
 //                        the first N_mpcsteps control knots of the solved trajectory into the
 //                        hkd_command_lcmt layout (lcmtypes/hkd_command_lcmt.lcm:1-11), one
 //                        workgroup per element, threads striding over the record's fields.
+//   k_shift_gather       HKDProblem::update's trajectory edits (HKDProblem.cpp:117-222): the
+//                        warm start (Xbar, Ubar, K) re-laid for the shifted phases — dropped
+//                        front knots / phases, pushed-back copies of X.back(), zero new phases —
+//                        as one gather over (element, new slot, entry) from host-built slot maps.
 #include "../../include/hsddp.h"
 #include "hsddp_mpc.h"
 
@@ -65,6 +69,48 @@ __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdA
         o.N_mpcsteps = a.n;
         o.solve_time = a.solve_time;
     }
+}
+
+// One thread per 2 doubles of the new Xbar / Ubar rows and compact K rows of every element.
+template <typename KT>
+__global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, const double *Xbar, const double *X,
+                                                      const double *Ubar, const KT *K, double *Xn, double *Un, KT *Kn)
+{
+    const long nx = (long)a.S_new * NX, nu = (long)a.Kc * NX, nk = (long)a.Kc * KCW, per = nx + nu + nk;
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)B * per) return;
+    const long b = gid / per;
+    long e = gid % per;
+    if (e < nx) {
+        const int s = (int)(e / NX), j = (int)(e % NX), lab = a.smap[s];
+        double v = 0.0;
+        if (lab >= 0) v = Xbar[(b * a.S_old + lab) * NX + j];
+        else if (lab <= -2) v = X[(b * a.S_old + (-2 - lab)) * NX + j];
+        Xn[b * nx + e] = v;
+        return;
+    }
+    e -= nx;
+    if (e < nu) {
+        const int k = (int)(e / NX), j = (int)(e % NX), lab = a.cmap[k];
+        Un[b * nu + e] = (lab >= 0 && !(a.zero_u0 && k == 0)) ? Ubar[(b * a.Kc + lab) * NX + j] : 0.0;
+        return;
+    }
+    e -= nu;
+    const int k = (int)(e / KCW), j = (int)(e % KCW), lab = a.cmap[k];
+    Kn[b * nk + e] = lab >= 0 ? K[((long)b * a.Kc + lab) * KCW + j] : (KT)0;
+}
+
+void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, double *Xbar_new, double *Ubar_new, void *K_new,
+                         hipStream_t st)
+{
+    const long n = (long)B * ((long)a.S_new * NX + (long)a.Kc * NX + (long)a.Kc * KCW);
+    const dim3 g((unsigned)((n + 255) / 256));
+    if (a.fp32)
+        hipLaunchKernelGGL(k_shift_gather<float>, g, dim3(256), 0, st, B, a, d.Xbar, d.X, d.Ubar, d.K32, Xbar_new,
+                           Ubar_new, (float *)K_new);
+    else
+        hipLaunchKernelGGL(k_shift_gather<double>, g, dim3(256), 0, st, B, a, d.Xbar, d.X, d.Ubar, d.K, Xbar_new,
+                           Ubar_new, (double *)K_new);
 }
 
 void launch_extract_commands(const Params &p, const Bufs &d, const CmdArgs &a, hsddp_mpc_command *out,

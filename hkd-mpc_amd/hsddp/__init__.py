@@ -153,6 +153,33 @@ class Solver:
             float(solve_time), out.ctypes.data))
         return out
 
+    # -- receding horizon (HKDProblem::update, HKDProblem.cpp:117-222) ------------------------
+    def layout(self) -> dict:
+        n = C.c_int()
+        hz, ss, re = (C.c_int * 16)(), (C.c_int * 16)(), (C.c_int * 16)()
+        check(lib().hsddp_get_layout(self._h, C.byref(n), hz, ss, re))
+        P = n.value
+        return {"horizons": list(hz[:P]), "shooting": list(ss[:P]), "reach_end": list(re[:P])}
+
+    def shift(self, contact_change) -> dict:
+        """len(contact_change) simulation steps of HKDProblem::update on the device-held warm start;
+        returns the new layout.  Call update_problem with inputs of that layout before solving."""
+        cc = np.ascontiguousarray(np.asarray(contact_change, dtype=np.int32).reshape(-1))
+        check(lib().hsddp_shift(self._h, int(cc.size), ip(cc)))
+        lay = self.layout()
+        self.P = len(lay["horizons"])
+        self.S = sum(n + 1 for n in lay["horizons"])
+        self.Kc = sum(lay["horizons"])
+        return lay
+
+    def update_problem(self, contacts, x0, ref_x, ref_u, ref_foot) -> None:
+        """Inputs of the current layout, keeping the warm start (hsddp_update_problem)."""
+        self._contacts = np.ascontiguousarray(contacts, dtype=np.int32)
+        check(lib().hsddp_update_problem(self._h, ip(self._contacts), dp(np.ascontiguousarray(x0, dtype=np.float64)),
+                                         dp(np.ascontiguousarray(ref_x, dtype=np.float64)),
+                                         dp(np.ascontiguousarray(ref_u, dtype=np.float64)),
+                                         dp(np.ascontiguousarray(ref_foot, dtype=np.float64))))
+
     def synchronize(self) -> None:
         check(lib().hsddp_synchronize(self._h))
 

@@ -90,6 +90,7 @@ EXPORTS = [
     "hsddp_hkd_dynamics_partial", "hsddp_hkd_foot_position", "hsddp_hkd_foot_jacobian",
     "hsddp_hkd_resetmap", "hsddp_hkd_resetmap_partial", "hsddp_device_alloc", "hsddp_device_free",
     "hsddp_memcpy_h2d", "hsddp_memcpy_d2h", "hsddp_device_synchronize", "hsddp_extract_commands",
+    "hsddp_shift", "hsddp_get_layout", "hsddp_update_problem",
 ]
 
 
@@ -133,6 +134,9 @@ def lib():
     L.hsddp_memcpy_h2d.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     L.hsddp_memcpy_d2h.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     L.hsddp_device_synchronize.argtypes = [C.c_int]
+    L.hsddp_shift.argtypes = [C.c_void_p, C.c_int, IP]
+    L.hsddp_get_layout.argtypes = [C.c_void_p, IP, IP, IP, IP]
+    L.hsddp_update_problem.argtypes = [C.c_void_p, IP, DP, DP, DP, DP]
     L.hsddp_extract_commands.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_void_p, C.c_int,
                                          C.c_void_p, C.c_int, C.c_float, C.c_void_p]
     _lib = L

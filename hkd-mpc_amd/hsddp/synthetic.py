@@ -95,18 +95,19 @@ def phase_schedule(gait: str, n_phases: int, offset: int = 0):
     return [cyc[(offset + i) % len(cyc)] for i in range(n_phases + 1)]
 
 
-def _reference_slots(contacts_ext, horizons, dt=DT):
+def _reference_slots(contacts_ext, horizons, dt=DT, t0=0):
     """Per-slot reference (x_r, u_r, foot_r) following HKDReference.cpp:24-57.
 
     The terminal slot of phase i sits at the start time of phase i+1, so its qdummy reference
-    uses the next phase's contact (the reference contact at that time)."""
+    uses the next phase's contact (the reference contact at that time).  t0: knot index of the
+    first slot (the window start after receding-horizon shifts)."""
     P = len(horizons)
     S = sum(n + 1 for n in horizons)
     ref_x = np.zeros((S, 24))
     ref_u = np.zeros((S, 24))
     ref_f = np.zeros((S, 12))
     s = 0
-    t_idx = 0
+    t_idx = t0
     for i in range(P):
         for k in range(horizons[i] + 1):
             t = (t_idx + k) * dt

@@ -19,6 +19,8 @@
  *   hsddp_solve_begin/_iterate/_end           the same loop split at its inner iterations (:257-303 / :304-381 / :383-408)
  *   hsddp_download_trajectory                 Trajectory fields read by the caller  HKDMPC.cpp:243-298
  *   hsddp_download_element_info               get_actual_cost / get_solver_info     MultiPhaseDDP.h:416; .cpp:532-541
+ *   hsddp_shift / hsddp_update_problem        HKDProblem::update + HKDMPCSolver::update's re-solve
+ *                                             setup (warm start reused)  HKDProblem.cpp:117-222; HKDMPC.cpp:96-143
  *   hsddp_extract_commands                    update_foot_placement + publish_mpc_cmd HKDMPC.cpp:207-298
  *   hsddp_hkd_dynamics                        HKD::Model::dynamics (hkinodyn)       HKDModel.h:33-45
  *   hsddp_hkd_dynamics_partial                HKD::Model::dynamics_partial          HKDModel.h:46-61
@@ -168,6 +170,26 @@ int hsddp_download_working(hsddp_handle h, double *X, double *U, double *Defect,
 int hsddp_download_element_info(hsddp_handle h, hsddp_element_info *info);
 int hsddp_synchronize(hsddp_handle h);
 size_t hsddp_device_bytes(hsddp_handle h);
+
+/* ---- receding-horizon update -----------------------------------------
+ * HKDProblem::update (HKDProblem.cpp:117-222) for n_steps simulation steps, on the warm start held
+ * on the device.  Per step: the first phase drops its first knot, or is removed when it has one
+ * knot left; the last phase grows by one knot holding a copy of X.back() with zero control and
+ * gain, or — when contact_change[j] (the contact at the new horizon end differs from the last
+ * phase's) and the last phase has already seen a change (is_phase_reach_end) — a new one-knot
+ * phase with a zero trajectory is appended.  Afterwards Ubar of the first knot is zeroed and every
+ * phase gets all its states as shooting states except a last phase of horizon <= 2, which keeps its
+ * set (empty for a new phase; its states are then simulated, SinglePhase.cpp:185-222).  The total
+ * number of control knots is unchanged.  The layout (phases, horizons) is shared by the batch.
+ * After a shift, hsddp_update_problem must upload contacts / x0 / references of the new layout
+ * before the next solve. */
+int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_change);
+/* current layout: n_phases, horizons[16], shooting states[16], is_phase_reach_end[16] (any NULL) */
+int hsddp_get_layout(hsddp_handle h, int *n_phases, int *horizons, int *shooting, int *reach_end);
+/* as hsddp_upload_problem, but keeps the warm start Xbar / Ubar / K (the MPC update's reuse of the
+ * previous solution); resets X = Xbar, U = Ubar and the ReB / AL parameters (reset_params) */
+int hsddp_update_problem(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
+                         const double *ref_u, const double *ref_foot);
 
 /* ---- MPC command extraction ------------------------------------------
  * Mirror of hkd_command_lcmt (lcmtypes/hkd_command_lcmt.lcm:1-11), field for field. */

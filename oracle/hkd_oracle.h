@@ -65,6 +65,8 @@ typedef struct {
     double td_sigma, td_sigma_max, td_lambda; /* constraint_params.info:15-19 */
     double ground_height;
     orc_weights w;
+    const int *shooting;      /* [P] shooting states per phase: SS_set = {0 .. n-1}
+                                 (SinglePhase::update_SS_config, SinglePhase.h:161-164); NULL = all */
 } orc_problem;
 
 typedef struct {

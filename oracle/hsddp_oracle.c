@@ -151,16 +151,23 @@ static const double GRF_ROW[5][3] = {{0, 0, 1}, {-1, 0, 1}, {1, 0, 1}, {0, -1, 1
 
 /* ---- phase-level routines ----------------------------------------------------------------- */
 
-/* SinglePhase::hybrid_rollout (SinglePhase.cpp:181-233) with all knots as shooting states */
+/* SinglePhase::hybrid_rollout (SinglePhase.cpp:181-233).  Shooting states SS_set = {0 .. ss-1}
+   (every state unless orc_problem.shooting says otherwise: HKDProblem::update leaves a new last
+   phase of horizon <= 2 with an empty set, HKDProblem.cpp:203-216): X = Xbar + eps dX there,
+   X = Xsim (X[0] = x_init) elsewhere. */
 static int phase_hybrid_rollout(ctx_t *C, int i, double eps, const double *x_init)
 {
     orc_element *e = C->e;
     const int N = C->N[i], s0 = C->s0[i], k0 = C->k0[i];
+    const int ss = C->p->shooting ? C->p->shooting[i] : N + 1;
     double cd[4];
     for (int l = 0; l < 4; ++l) cd[l] = C->c[i][l];
     double *X = e->X, *Xbar = e->Xbar, *U = e->U, *Ubar = e->Ubar;
     memcpy(C->Xsim + (size_t)s0 * NX, x_init, sizeof(double) * NX);
-    for (int j = 0; j < NX; ++j) X[s0 * NX + j] = Xbar[s0 * NX + j] + eps * e->dX[s0 * NX + j];
+    if (ss > 0)
+        for (int j = 0; j < NX; ++j) X[s0 * NX + j] = Xbar[s0 * NX + j] + eps * e->dX[s0 * NX + j];
+    else
+        memcpy(X + (size_t)s0 * NX, x_init, sizeof(double) * NX);
     double pv = 0;
     for (int k = 0; k < N; ++k) {
         int s = s0 + k, kc = k0 + k;
@@ -177,7 +184,10 @@ static int phase_hybrid_rollout(ctx_t *C, int i, double eps, const double *x_ini
         double nrm = 0;
         for (int j = 0; j < NX; ++j) nrm += xs[j] * xs[j];
         if (sqrt(nrm) > 1e6) return 0;
-        for (int j = 0; j < NX; ++j) X[(s + 1) * NX + j] = Xbar[(s + 1) * NX + j] + eps * e->dX[(s + 1) * NX + j];
+        if (k + 1 < ss && C->o->MS)
+            for (int j = 0; j < NX; ++j) X[(s + 1) * NX + j] = Xbar[(s + 1) * NX + j] + eps * e->dX[(s + 1) * NX + j];
+        else
+            memcpy(X + (size_t)(s + 1) * NX, xs, sizeof(double) * NX);
         /* GRFConstraint::compute_violation + update_max_violation(k) */
         if (n_stance(C->c[i])) {
             double mk = 0;

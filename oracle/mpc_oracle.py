@@ -65,3 +65,59 @@ def mpc_command(Xbar, Ubar, K, contacts, horizons, nsteps_between_mpc, mpc_time,
     cmd["foot_placement"] = foot_placement(Xbar, contacts, horizons, pf_current)
     cmd["solve_time"] = np.float32(solve_time)
     return cmd
+
+
+# ---- receding-horizon update ------------------------------------------------------------------
+def split_phases(arr, horizons, states):
+    """[S][..] (states) or [Kc][..] (controls) -> per-phase lists of rows"""
+    out, o = [], 0
+    for n in horizons:
+        m = n + 1 if states else n
+        out.append([np.array(arr[o + j], copy=True) for j in range(m)])
+        o += m
+    return out
+
+
+def shift(horizons, shooting, reach_end, Xbar, X, Ubar, K, contact_change):
+    """HKDProblem::update (HKDProblem.cpp:117-222) on one element's warm start, as deques of phases.
+
+    Per step: front — pop_front_phase (HKDProblem.h:56-66) when the first phase's end time is not
+    after the new start (one knot left), else SinglePhase::pop_front (SinglePhase.cpp:496-501:
+    Trajectory::pop_front drops X/Xbar/U/Ubar/K fronts, TrajectoryManagement.cpp:118-148); back — a
+    new phase (Trajectory::create_data: zeros, TrajectoryManagement.cpp:4-35; initialization()
+    clears SS_set) when the contact changes and is_phase_reach_end.back(), else push_back_default
+    (Trajectory::push_back_state(X.back()), TrajectoryManagement.cpp:178-208), marking
+    is_phase_reach_end on a change.  Then update_SS_config for all phases but a last one of horizon
+    <= 2 and Ubar[0] of the first phase zeroed.  Returns (horizons, shooting, reach_end, Xbar,
+    Ubar, K) in the flat slot layout."""
+    hz, ss, re = list(horizons), list(shooting), list(reach_end)
+    xb, xw = split_phases(Xbar, hz, True), split_phases(X, hz, True)
+    ub, kk = split_phases(Ubar, hz, False), split_phases(K, hz, False)
+    for cc in contact_change:
+        if hz[0] <= 1:                      # approx_leq(phase_end_times.front(), new_start_time)
+            for L in (hz, ss, re, xb, xw, ub, kk):
+                L.pop(0)
+        else:
+            for L in (xb[0], xw[0], ub[0], kk[0]):
+                L.pop(0)
+            hz[0] -= 1
+        if cc and re[-1]:
+            hz.append(1); ss.append(0); re.append(0)
+            xb.append([np.zeros_like(Xbar[0]) for _ in range(2)])
+            xw.append([np.zeros_like(Xbar[0]) for _ in range(2)])
+            ub.append([np.zeros_like(Ubar[0])])
+            kk.append([np.zeros_like(K[0])])
+        else:
+            last = np.array(xw[-1][-1], copy=True)   # X.back()
+            xb[-1].append(last); xw[-1].append(np.array(last, copy=True))
+            ub[-1].append(np.zeros_like(Ubar[0])); kk[-1].append(np.zeros_like(K[0]))
+            hz[-1] += 1
+            if cc:
+                re[-1] = 1
+    P = len(hz)
+    for i in range(P):
+        if i < P - 1 or hz[i] > 2:
+            ss[i] = hz[i] + 1
+    ub[0][0] = np.zeros_like(ub[0][0])
+    flat = lambda L: np.array([r for ph in L for r in ph])
+    return hz, ss, re, flat(xb), flat(ub), flat(kk)

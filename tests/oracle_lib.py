@@ -43,7 +43,7 @@ class OrcProblem(C.Structure):
     _fields_ = [("n_phases", C.c_int), ("horizons", IP), ("dt", C.c_double), ("mu_fric", C.c_double),
                 ("grf_delta", C.c_double), ("grf_delta_min", C.c_double), ("grf_eps", C.c_double),
                 ("td_sigma", C.c_double), ("td_sigma_max", C.c_double), ("td_lambda", C.c_double),
-                ("ground_height", C.c_double), ("w", OrcWeights)]
+                ("ground_height", C.c_double), ("w", OrcWeights), ("shooting", IP)]
 
 
 class OrcElement(C.Structure):
@@ -170,6 +170,10 @@ def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 
     n = len(idx)
     S, Kc, P = prob["S"], prob["Kc"], len(prob["horizons"])
     p, hz = default_problem(prob["horizons"], prob["dt"])
+    ss = None
+    if prob.get("shooting") is not None:  # shooting states per phase (after a receding-horizon shift)
+        ss = np.ascontiguousarray(prob["shooting"], dtype=np.int32)
+        p.shooting = ip(ss)
     st = {
         "Xbar": np.ascontiguousarray(prob["Xbar"][idx]).copy(),
         "X": np.ascontiguousarray(prob["Xbar"][idx]).copy(),
@@ -184,7 +188,7 @@ def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 
     x0 = np.ascontiguousarray(prob["x0"][idx])
     shared = prob["ref_x"].shape[0] == 1
     elems = (OrcElement * n)()
-    keep = [contacts, x0]
+    keep = [contacts, x0, hz, ss]
     for j, b in enumerate(idx):
         e = elems[j]
         rb = 0 if shared else b

@@ -44,3 +44,92 @@ def test_commands_match_oracle(P, N, mixed, fp32, nsteps):
             for f in ("N_mpcsteps", "mpc_times", "hkd_controls", "des_body_state", "contacts", "statusTimes",
                       "foot_placement", "feedback", "solve_time"):
                 assert np.array_equal(g[f], r[f]), (b, f)
+
+
+# ---- receding-horizon update (HKDProblem::update, HKDProblem.cpp:117-222) --------------------
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import oracle_lib as O  # noqa: E402
+from mpc_scenario import Scenario  # noqa: E402
+
+
+def _scenario_batch(B, P, N):
+    names = ["trot", "pace", "bound", "pronk"]
+    gaits = [names[b % 4] for b in range(B)]
+    sc = Scenario(gaits, P, N)
+    prob = syn.make_batch(B, P, N, "trot")
+    inp = sc.inputs(prob["x0"])
+    prob.update(inp)
+    prob["Xbar"] = inp["ref_x"].copy()
+    return sc, prob
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(1e-300, np.max(np.abs(b))))
+
+
+@pytest.mark.parametrize("steps", [[1, 1, 1, 1, 1, 1, 1], [3, 4, 2], [9]])
+def test_shift_matches_oracle(steps):
+    """The device gather reproduces the restated phase bookkeeping bit for bit: dropped front knots
+    and phases, X.back() copies, zero new phases, Ubar[0] zeroed; layout and shooting sets agree."""
+    B, P, N = 6, 4, 5
+    sc, prob = _scenario_batch(B, P, N)
+    s = hsddp.Solver(prob, hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=2))
+    s.solve()
+    for n in steps:
+        before = {**s.trajectory(), **s.working()}
+        lay0 = s.layout()
+        flags = sc.step(n)
+        lay = s.shift(flags)
+        assert lay["horizons"] == sc.horizons and lay["reach_end"] == sc.reach_end
+        ref = [M.shift(lay0["horizons"], lay0["shooting"], lay0["reach_end"], before["Xbar"][b], before["X"][b],
+                       before["Ubar"][b], before["K"][b], flags) for b in range(B)]
+        assert lay["shooting"] == ref[0][1]
+        with pytest.raises(hsddp.HSDDPError):
+            s.solve()  # inputs of the new layout are required first
+        inp = sc.inputs(np.stack([r[3][0] for r in ref]))
+        s.update_problem(inp["contacts"], inp["x0"], inp["ref_x"], inp["ref_u"], inp["ref_foot"])
+        tr = s.trajectory()
+        for b in range(B):
+            assert np.array_equal(tr["Xbar"][b], ref[b][3])
+            assert np.array_equal(tr["Ubar"][b], ref[b][4])
+            assert np.array_equal(tr["K"][b], ref[b][5])
+        s.solve()
+    s.close()
+
+
+def test_mpc_loop_matches_oracle():
+    """HKDMPCSolver::update's loop (HKDMPC.cpp:96-165): shift one step, new inputs with the warm
+    start kept, re-solve with max_AL_iter = 2, max_DDP_iter = 1 (quirk A17) — including the
+    updates whose new last phase has no shooting states — against the oracle doing the same."""
+    B, P, N = 8, 4, 5
+    sc, prob = _scenario_batch(B, P, N)
+    s = hsddp.Solver(prob, hsddp.load_settings())
+    s.solve()
+    r = O.solve_batch(prob, O.default_options(), n_threads=8)
+    g = {**s.trajectory(), **s.working(), **s.element_info()}
+    assert _rel(g["Xbar"], r["Xbar"]) < 1e-9
+    kw = dict(max_AL_iter=2, max_DDP_iter=1)
+    s.set_options(hsddp.load_settings(**kw))
+    tails = 0
+    for it in range(9):
+        lay0 = s.layout()
+        flags = sc.step(1)
+        lay = s.shift(flags)
+        tails += any(ss < n + 1 for ss, n in zip(lay["shooting"], lay["horizons"]))
+        sh = [M.shift(lay0["horizons"], lay0["shooting"], lay0["reach_end"], r["Xbar"][b], r["X"][b],
+                      r["Ubar"][b], r["K"][b], flags) for b in range(B)]
+        inp = sc.inputs(np.stack([q[3][0] for q in sh]))
+        s.update_problem(inp["contacts"], inp["x0"], inp["ref_x"], inp["ref_u"], inp["ref_foot"])
+        s.solve()
+        g = {**s.trajectory(), **s.working(), **s.element_info()}
+        p2 = {"batch": B, "horizons": lay["horizons"], "shooting": lay["shooting"], "dt": prob["dt"],
+              "S": sum(n + 1 for n in lay["horizons"]), "Kc": sum(lay["horizons"]), **inp,
+              "Xbar": np.stack([q[3] for q in sh]), "Ubar": np.stack([q[4] for q in sh]),
+              "K": np.stack([q[5] for q in sh])}
+        r = O.solve_batch(p2, O.default_options(**kw), n_threads=8)
+        for f in ("Xbar", "Ubar", "X", "K"):
+            assert _rel(g[f], r[f]) < 1e-8, (it, f)
+        assert np.array_equal(g["n_ls_trials"], r["n_ls_trials"]), it
+        assert _rel(g["cost"], r["cost"]) < 1e-9, it
+    assert tails >= 2  # the loop passed through last phases without shooting states
+    s.close()
