@@ -28,6 +28,8 @@ static int fail(int code, const std::string &msg)
     return code;
 }
 
+extern "C" int hsddp_ref_fail(int code, const char *msg) { return fail(code, msg); }
+
 #define HIPCHK(expr)                                                                                 \
     do {                                                                                             \
         hipError_t e_ = (expr);                                                                      \
@@ -220,6 +222,10 @@ struct hsddp_handle_t {
     double *spare_Xbar = nullptr, *spare_Ubar = nullptr;
     void *spare_K = nullptr;
     bool need_inputs = false;   // a shift changed the layout: update_problem before solving
+    double *ref_table = nullptr;  // reference samples [n][RT_W] (hsddp_set_reference_table)
+    int ref_n = 0;
+    float ref_dt = 0;
+    bool refs_on_device = false;  // references built by hsddp_build_references for this layout
 };
 
 // device staging area of at least `bytes` (contents not preserved when it grows)
@@ -369,6 +375,7 @@ extern "C" int hsddp_destroy(hsddp_handle h)
     if (h->stream) hipStreamSynchronize(h->stream);
     for (void *p : h->allocs) hipFree(p);
     if (h->scratch) hipFree(h->scratch);
+    if (h->ref_table) hipFree(h->ref_table);
 
     if (h->host_counter) hipHostFree(h->host_counter);
     if (h->stream) hipStreamDestroy(h->stream);
@@ -396,7 +403,11 @@ static int h2d(void *dst, const void *src, size_t bytes, hipStream_t st)
 static int upload_inputs(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
                          const double *ref_u, const double *ref_foot)
 {
-    if (!h || !contacts || !x0 || !ref_x || !ref_u || !ref_foot) return fail(HSDDP_ERR_ARG, "null argument");
+    if (!h || !contacts || !x0) return fail(HSDDP_ERR_ARG, "null argument");
+    const bool keep_refs = !ref_x && !ref_u && !ref_foot;
+    if (!keep_refs && (!ref_x || !ref_u || !ref_foot)) return fail(HSDDP_ERR_ARG, "references: all three or none");
+    if (keep_refs && !h->refs_on_device)
+        return fail(HSDDP_ERR_ARG, "no device references for this layout (hsddp_build_references)");
     HIPCHK(hipSetDevice(h->desc.device));
     const Params &p = h->p;
     const size_t B = p.B, S = p.S, P = p.P, Br = h->Bref;
@@ -404,11 +415,14 @@ static int upload_inputs(hsddp_handle h, const int *contacts, const double *x0, 
         if (contacts[q] != 0 && contacts[q] != 1) return fail(HSDDP_ERR_ARG, "contacts must be 0/1");
     int rc;
     if ((rc = h2d((void *)h->d.contacts, contacts, B * (P + 1) * 4 * sizeof(int), h->stream)) ||
-        (rc = h2d((void *)h->d.x0, x0, B * NX * sizeof(double), h->stream)) ||
-        (rc = h2d((void *)h->d.ref_x, ref_x, Br * S * NX * sizeof(double), h->stream)) ||
-        (rc = h2d((void *)h->d.ref_u, ref_u, Br * S * NX * sizeof(double), h->stream)) ||
-        (rc = h2d((void *)h->d.ref_foot, ref_foot, Br * S * 12 * sizeof(double), h->stream)))
+        (rc = h2d((void *)h->d.x0, x0, B * NX * sizeof(double), h->stream)))
         return rc;
+    if (!keep_refs &&
+        ((rc = h2d((void *)h->d.ref_x, ref_x, Br * S * NX * sizeof(double), h->stream)) ||
+         (rc = h2d((void *)h->d.ref_u, ref_u, Br * S * NX * sizeof(double), h->stream)) ||
+         (rc = h2d((void *)h->d.ref_foot, ref_foot, Br * S * 12 * sizeof(double), h->stream))))
+        return rc;
+    if (!keep_refs) h->refs_on_device = false;
     h->contacts.assign(contacts, contacts + B * (P + 1) * 4);
     return HSDDP_OK;
 }
@@ -764,6 +778,19 @@ extern "C" int hsddp_download_working(hsddp_handle h, double *X, double *U, doub
     return HSDDP_OK;
 }
 
+extern "C" int hsddp_download_references(hsddp_handle h, double *ref_x, double *ref_u, double *ref_foot)
+{
+    if (!h || !ref_x || !ref_u || !ref_foot) return fail(HSDDP_ERR_ARG, "null argument");
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const size_t Br = h->Bref, S = h->p.S;
+    int rc;
+    if ((rc = d2h(ref_x, h->d.ref_x, Br * S * NX * 8)) || (rc = d2h(ref_u, h->d.ref_u, Br * S * NX * 8)) ||
+        (rc = d2h(ref_foot, h->d.ref_foot, Br * S * 12 * 8)))
+        return rc;
+    return HSDDP_OK;
+}
+
 extern "C" int hsddp_download_element_info(hsddp_handle h, hsddp_element_info *info)
 {
     if (!h || !info) return fail(HSDDP_ERR_ARG, "null argument");
@@ -1030,6 +1057,7 @@ extern "C" int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_chang
     h->desc.n_phases = P;
     for (int i = 0; i < P; ++i) h->desc.horizons[i] = p.N[i];
     h->need_inputs = true;
+    h->refs_on_device = false;  // built for the old layout
     return HSDDP_OK;
 }
 
@@ -1043,5 +1071,77 @@ extern "C" int hsddp_get_layout(hsddp_handle h, int *n_phases, int *horizons, in
         if (shooting) shooting[i] = p.ss[i];
         if (reach_end) reach_end[i] = h->reach_end[i];
     }
+    return HSDDP_OK;
+}
+
+// ---- batched reference construction ------------------------------------------------------------
+extern "C" int hsddp_set_reference_table(hsddp_handle h, const hsddp_quad_state *table, int n, float dt_ref)
+{
+    if (!h || !table || n < 1) return fail(HSDDP_ERR_ARG, "null / empty table");
+    if (!(dt_ref > 0)) return fail(HSDDP_ERR_ARG, "dt_ref must be > 0");
+    HIPCHK(hipSetDevice(h->desc.device));
+    std::vector<double> t((size_t)n * RT_W, 0.0);
+    for (int i = 0; i < n; ++i) {
+        double *q = &t[(size_t)i * RT_W];
+        const hsddp_quad_state &s = table[i];
+        for (int j = 0; j < 12; ++j) {
+            q[RT_BODY + j] = s.body_state[j]; q[RT_QJ + j] = s.qJ[j]; q[RT_QJD + j] = s.qJd[j];
+            q[RT_FOOT + j] = s.foot_placements[j]; q[RT_GRF + j] = s.grf[j];
+        }
+        for (int l = 0; l < 4; ++l) q[RT_C + l] = s.contact[l];
+    }
+    if (h->ref_table) { hipFree(h->ref_table); h->ref_table = nullptr; }
+    HIPCHK(hipMalloc((void **)&h->ref_table, t.size() * sizeof(double)));
+    HIPCHK(hipMemcpy(h->ref_table, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+    h->ref_n = n;
+    h->ref_dt = dt_ref;
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_build_references(hsddp_handle h, const int *window_start, int window_len,
+                                      const float *phase_start_times, float dt_sim)
+{
+    if (!h || !window_start) return fail(HSDDP_ERR_ARG, "null argument");
+    if (!h->ref_table) return fail(HSDDP_ERR_ARG, "no reference table (hsddp_set_reference_table)");
+    if (window_len < 1 || !(dt_sim > 0)) return fail(HSDDP_ERR_ARG, "window_len >= 1 and dt_sim > 0 required");
+    const Params &p = h->p;
+    const int Br = h->Bref;
+    for (int b = 0; b < Br; ++b)
+        if (window_start[b] < 0 || window_start[b] >= h->ref_n) return fail(HSDDP_ERR_ARG, "window start outside the table");
+    // slot times as the reference forms them: t_offset (float, phase start relative to the first
+    // phase) + k dt (double), passed on as float (SinglePhase.cpp:243-287; set_time_offset,
+    // HKDProblem.cpp:103,208), snapped to a sample (QuadReference.cpp:60-76)
+    std::vector<float> start(p.P);
+    if (phase_start_times) {
+        for (int i = 0; i < p.P; ++i) start[i] = phase_start_times[i] - phase_start_times[0];
+    } else {  // the float clock of HKDProblem::initialization (t += dt_sim per knot)
+        float t = 0.0f;
+        for (int i = 0; i < p.P; ++i) {
+            start[i] = t;
+            for (int k = 0; k < p.N[i]; ++k) t += dt_sim;
+        }
+    }
+    std::vector<int> idx(p.S);
+    const int sz = window_len - 1;
+    for (int i = 0; i < p.P; ++i)
+        for (int k = 0; k <= p.N[i]; ++k) {
+            const float t = (float)((double)start[i] + k * (double)dt_sim);
+            int q = (int)std::floor(t / h->ref_dt);
+            if (t - q * h->ref_dt > 0.5 * h->ref_dt) q++;
+            idx[p.s0[i] + k] = q > sz ? sz : q;
+        }
+    HIPCHK(hipSetDevice(h->desc.device));
+    char *buf;
+    int rc;
+    if ((rc = scratch(h, (Br + p.S) * sizeof(int), &buf))) return rc;
+    int *dstart = (int *)buf, *didx = dstart + Br;
+    if ((rc = h2d(dstart, window_start, Br * sizeof(int), h->stream)) ||
+        (rc = h2d(didx, idx.data(), p.S * sizeof(int), h->stream)))
+        return rc;
+    RefArgs a{h->ref_table, h->ref_n, dstart, didx};
+    launch_build_refs(p, h->d, Br, a, h->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->refs_on_device = true;
     return HSDDP_OK;
 }

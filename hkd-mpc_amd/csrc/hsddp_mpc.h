@@ -28,6 +28,16 @@ struct ShiftArgs {
 void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, double *Xbar_new, double *Ubar_new, void *K_new,
                          hipStream_t st);
 
+// reference sample table on the device: [n][RT_W] doubles per sample
+constexpr int RT_BODY = 0, RT_QJ = 12, RT_QJD = 24, RT_FOOT = 36, RT_GRF = 48, RT_C = 60, RT_W = 64;
+struct RefArgs {
+    const double *table;   // [n][RT_W]
+    int n;
+    const int *start;      // [Bw] window start sample per element (Bw = Bref)
+    const int *slot_idx;   // [S] sample offset of each state slot within the window
+};
+void launch_build_refs(const Params &p, const Bufs &d, int Bref, const RefArgs &a, hipStream_t st);
+
 void launch_extract_commands(const Params &p, const Bufs &d, const CmdArgs &a, hsddp_mpc_command *out,
                              hipStream_t st);
 

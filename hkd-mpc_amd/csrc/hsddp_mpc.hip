@@ -5,6 +5,8 @@
 //                        the first N_mpcsteps control knots of the solved trajectory into the
 //                        hkd_command_lcmt layout (lcmtypes/hkd_command_lcmt.lcm:1-11), one
 //                        workgroup per element, threads striding over the record's fields.
+//   k_build_refs         HKDSinglePhaseReference::get_reference_at_t at every slot of every element
+//                        from a device-resident sample table (HKDReference.cpp:8-57).
 //   k_shift_gather       HKDProblem::update's trajectory edits (HKDProblem.cpp:117-222): the
 //                        warm start (Xbar, Ubar, K) re-laid for the shifted phases — dropped
 //                        front knots / phases, pushed-back copies of X.back(), zero new phases —
@@ -111,6 +113,35 @@ void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, double *Xbar_
     else
         hipLaunchKernelGGL(k_shift_gather<double>, g, dim3(256), 0, st, B, a, d.Xbar, d.X, d.Ubar, d.K, Xbar_new,
                            Ubar_new, (double *)K_new);
+}
+
+// HKDSinglePhaseReference::get_reference_at_t (HKDReference.cpp:8-57) at state slot s of reference
+// element b: one thread per (b, s); the slot -> sample offset map is shared (host-built with the
+// reference's float time rounding), the window start is per element.
+__global__ __launch_bounds__(256) void k_build_refs(Params p, Bufs d, int Bref, RefArgs a)
+{
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)Bref * p.S) return;
+    const int b = (int)(gid / p.S), s = (int)(gid % p.S);
+    int k = a.start[b] + a.slot_idx[s];
+    k = k < a.n ? k : a.n - 1;  // past the loaded data: its last sample
+    const double *q = a.table + (size_t)k * RT_W;
+    double *rx = (double *)d.ref_x + gid * NX, *ru = (double *)d.ref_u + gid * NX, *rf = (double *)d.ref_foot + gid * 12;
+    for (int j = 0; j < 12; ++j) rx[j] = q[RT_BODY + j];
+    for (int l = 0; l < 4; ++l)
+        for (int c = 0; c < 3; ++c)
+            rx[12 + 3 * l + c] = q[RT_C + l] > 0 ? q[RT_FOOT + 3 * l + c] : q[RT_QJ + 3 * l + c];
+    for (int j = 0; j < 12; ++j) {
+        ru[j] = q[RT_GRF + j];
+        ru[12 + j] = q[RT_QJD + j];
+        rf[j] = q[RT_FOOT + j];
+    }
+}
+
+void launch_build_refs(const Params &p, const Bufs &d, int Bref, const RefArgs &a, hipStream_t st)
+{
+    const long n = (long)Bref * p.S;
+    hipLaunchKernelGGL(k_build_refs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, d, Bref, a);
 }
 
 void launch_extract_commands(const Params &p, const Bufs &d, const CmdArgs &a, hsddp_mpc_command *out,

@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 from . import model, synthetic  # noqa: F401
-from ._lib import (MPC_COMMAND, ConstraintParams, ElementInfo, HSDDPError, Options, ProblemDesc, Stats, Weights,
+from ._lib import (MPC_COMMAND, PHASE_PLAN, QUAD_STATE, ConstraintParams, ElementInfo, HSDDPError, Options, ProblemDesc, Stats, Weights,
                    check, dp, ip, lib)
 
 SETTINGS_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "settings")
@@ -49,6 +49,55 @@ def load_constraint_params(path: str | None = None) -> ConstraintParams:
     return cp
 
 
+# -- reference construction (QuadReference / HKDProblem::initialization) ------------------------
+def load_quad_reference(path: str, reorder: bool = False):
+    """QuadReference::load_top_level_data (QuadReference.cpp:129-290): (samples [n] QUAD_STATE, dt)."""
+    L = lib()
+    dt = C.c_float()
+    n = L.hsddp_load_quad_reference(path.encode(), int(reorder), C.byref(dt), None, 0)
+    check(min(n, 0))
+    out = np.zeros(n, dtype=QUAD_STATE)
+    check(min(L.hsddp_load_quad_reference(path.encode(), int(reorder), C.byref(dt), out.ctypes.data, n), 0))
+    return out, float(dt.value)
+
+
+def plan_phases(window: np.ndarray, dt_ref: float, plan_duration: float = 0.6, dt_sim: float = 0.01,
+                dt_mpc: float = 0.01) -> dict:
+    """HKDProblem::initialization's phase segmentation (HKDProblem.cpp:15-68) of a reference window."""
+    w = np.ascontiguousarray(window, dtype=QUAD_STATE)
+    plan = np.zeros(1, dtype=PHASE_PLAN)
+    check(lib().hsddp_plan_phases(w.ctypes.data, int(w.size), dt_ref, plan_duration, dt_sim, dt_mpc, plan.ctypes.data))
+    P = int(plan["n_phases"][0])
+    return {"horizons": [int(v) for v in plan["horizons"][0][:P]], "contacts": plan["contacts"][0][:P + 1].copy(),
+            "durations": plan["durations"][0][:P].copy(), "start_times": plan["start_times"][0][:P].copy(),
+            "end_times": plan["end_times"][0][:P].copy()}
+
+
+def reference_problem(table: np.ndarray, dt_ref: float, window_start, x0: np.ndarray, plan_duration: float = 0.6,
+                      dt_sim: float = 0.01, dt_mpc: float = 0.01) -> dict:
+    """HKDProblem::initialization (HKDProblem.cpp:15-111) for a batch: the phase plan of the window
+    at table[window_start[0]] (the batch shares its layout; with per-element window starts every
+    element reads its own samples, e.g. windows into different gait files concatenated into one
+    table), contacts per element from its own window, and the inputs Solver needs to build the
+    references on the device.  Pass the result to Solver(prob)."""
+    ws = np.asarray(window_start, dtype=np.int32).reshape(-1)
+    x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(-1, 24)
+    B = x0.shape[0]
+    n_win = int(round(plan_duration / dt_ref)) + 2  # QuadReference::initialize: sz + 1 samples, sz = round(T/dt) + 1
+    plans = [plan_phases(table[w:w + n_win], dt_ref, plan_duration, dt_sim, dt_mpc) for w in ws]
+    hz = plans[0]["horizons"]
+    for q in plans[1:]:
+        if q["horizons"] != hz:
+            raise HSDDPError("per-element windows must share the phase layout")
+    contacts = np.stack([q["contacts"] for q in plans]).astype(np.int32)
+    if contacts.shape[0] == 1 and B > 1:
+        contacts = np.repeat(contacts, B, axis=0)
+    S, Kc = sum(n + 1 for n in hz), sum(hz)
+    return {"batch": B, "horizons": hz, "S": S, "Kc": Kc, "dt": dt_sim, "x0": x0, "contacts": contacts,
+            "shooting": [n + 1 for n in hz], "ref_table": table, "dt_ref": dt_ref, "window_start": ws,
+            "window_len": n_win, "phase_start_times": plans[0]["start_times"], "plan": plans[0]}
+
+
 class Solver:
     """B independent HKD trajectory optimisations on one GPU (one C-ABI handle)."""
 
@@ -69,7 +118,9 @@ class Solver:
         for i, n in enumerate(prob["horizons"]):
             desc.horizons[i] = int(n)
         desc.dt = float(prob["dt"])
-        desc.ref_per_element = 0 if prob["ref_x"].shape[0] == 1 else 1
+        from_table = "ref_x" not in prob  # references built on the device from prob["ref_table"]
+        self.ref_per_element = (np.size(prob["window_start"]) != 1) if from_table else (prob["ref_x"].shape[0] != 1)
+        desc.ref_per_element = int(self.ref_per_element)
         desc.riccati_fp32 = 1 if riccati_fp32 else 0
         if weights is None:
             L.hsddp_default_weights(C.byref(desc.weights))
@@ -84,12 +135,22 @@ class Solver:
         self._h = h
         self.options = options if options is not None else load_settings()
         check(L.hsddp_set_options(h, C.byref(self.options)))
-        self._contacts = np.ascontiguousarray(prob["contacts"], dtype=np.int32)
-        check(L.hsddp_upload_problem(h, ip(self._contacts), dp(np.ascontiguousarray(prob["x0"])),
-                                     dp(np.ascontiguousarray(prob["ref_x"])),
-                                     dp(np.ascontiguousarray(prob["ref_u"])),
-                                     dp(np.ascontiguousarray(prob["ref_foot"]))))
+        if from_table:
+            self.set_reference_table(prob["ref_table"], prob["dt_ref"])
+            self.build_references(prob["window_start"], prob["window_len"], prob.get("phase_start_times"),
+                                  prob["dt"])
+            self.upload_problem(prob["contacts"], prob["x0"])
+        else:
+            self.upload_problem(prob["contacts"], prob["x0"], prob["ref_x"], prob["ref_u"], prob["ref_foot"])
         self.warm_start(prob.get("Xbar"), prob.get("Ubar"), prob.get("K"))
+
+    def upload_problem(self, contacts, x0, ref_x=None, ref_u=None, ref_foot=None) -> None:
+        """Inputs with the default warm start Xbar = reference, Ubar = K = 0 (HKDProblem.cpp:84-90;
+        TrajectoryManagement.cpp:5-35).  References None: the ones hsddp_build_references made."""
+        self._contacts = np.ascontiguousarray(contacts, dtype=np.int32)
+        refs = [None if r is None else np.ascontiguousarray(r, dtype=np.float64) for r in (ref_x, ref_u, ref_foot)]
+        check(lib().hsddp_upload_problem(self._h, ip(self._contacts), dp(np.ascontiguousarray(x0, dtype=np.float64)),
+                                         *(None if r is None else dp(r) for r in refs)))
 
     # -- MultiPhaseDDP surface ---------------------------------------------------------------
     def set_options(self, options: Options) -> None:
@@ -153,6 +214,25 @@ class Solver:
             float(solve_time), out.ctypes.data))
         return out
 
+    def set_reference_table(self, table: np.ndarray, dt_ref: float) -> None:
+        t = np.ascontiguousarray(table, dtype=QUAD_STATE)
+        check(lib().hsddp_set_reference_table(self._h, t.ctypes.data, int(t.size), float(dt_ref)))
+
+    def build_references(self, window_start, window_len: int, phase_start_times=None, dt_sim: float = 0.01) -> None:
+        """get_reference_at_t at every slot of every element on the device (HKDReference.cpp:8-57);
+        then upload_problem / update_problem with ref_x = ref_u = ref_foot = None keep them."""
+        ws = np.ascontiguousarray(np.asarray(window_start, dtype=np.int32).reshape(-1))
+        ps = None if phase_start_times is None else np.ascontiguousarray(phase_start_times, dtype=np.float32)
+        check(lib().hsddp_build_references(self._h, ip(ws), int(window_len), None if ps is None else ps.ctypes.data,
+                                           float(dt_sim)))
+
+    def references(self) -> dict:
+        """The references the solve reads: ref_x, ref_u [Bref][S][24], ref_foot [Bref][S][12]."""
+        Br = self.B if self.ref_per_element else 1
+        rx = np.empty((Br, self.S, 24)); ru = np.empty((Br, self.S, 24)); rf = np.empty((Br, self.S, 12))
+        check(lib().hsddp_download_references(self._h, dp(rx), dp(ru), dp(rf)))
+        return {"ref_x": rx, "ref_u": ru, "ref_foot": rf}
+
     # -- receding horizon (HKDProblem::update, HKDProblem.cpp:117-222) ------------------------
     def layout(self) -> dict:
         n = C.c_int()
@@ -172,13 +252,13 @@ class Solver:
         self.Kc = sum(lay["horizons"])
         return lay
 
-    def update_problem(self, contacts, x0, ref_x, ref_u, ref_foot) -> None:
-        """Inputs of the current layout, keeping the warm start (hsddp_update_problem)."""
+    def update_problem(self, contacts, x0, ref_x=None, ref_u=None, ref_foot=None) -> None:
+        """Inputs of the current layout, keeping the warm start (hsddp_update_problem).  References
+        None: keep the ones hsddp_build_references made on the device for this layout."""
         self._contacts = np.ascontiguousarray(contacts, dtype=np.int32)
+        refs = [None if r is None else np.ascontiguousarray(r, dtype=np.float64) for r in (ref_x, ref_u, ref_foot)]
         check(lib().hsddp_update_problem(self._h, ip(self._contacts), dp(np.ascontiguousarray(x0, dtype=np.float64)),
-                                         dp(np.ascontiguousarray(ref_x, dtype=np.float64)),
-                                         dp(np.ascontiguousarray(ref_u, dtype=np.float64)),
-                                         dp(np.ascontiguousarray(ref_foot, dtype=np.float64))))
+                                         *(None if r is None else dp(r) for r in refs)))
 
     def synchronize(self) -> None:
         check(lib().hsddp_synchronize(self._h))

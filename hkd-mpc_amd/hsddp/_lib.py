@@ -74,6 +74,16 @@ MPC_COMMAND = np.dtype([("N_mpcsteps", np.int32), ("mpc_times", np.float64, (10,
                         ("solve_time", np.float32)], align=True)
 
 
+# hsddp_quad_state (QuadAugmentedState) and hsddp_phase_plan (include/hsddp.h) as C-aligned records
+QUAD_STATE = np.dtype([("body_state", np.float64, (12,)), ("qJ", np.float64, (12,)), ("qJd", np.float64, (12,)),
+                       ("foot_placements", np.float64, (12,)), ("grf", np.float64, (12,)),
+                       ("torque", np.float64, (12,)), ("contact", np.int32, (4,)), ("status_dur", np.float64, (4,))],
+                      align=True)
+PHASE_PLAN = np.dtype([("n_phases", np.int32), ("horizons", np.int32, (16,)), ("contacts", np.int32, (17, 4)),
+                       ("durations", np.float64, (16, 4)), ("start_times", np.float32, (16,)),
+                       ("end_times", np.float32, (16,))], align=True)
+
+
 class HSDDPError(RuntimeError):
     pass
 
@@ -90,7 +100,8 @@ EXPORTS = [
     "hsddp_hkd_dynamics_partial", "hsddp_hkd_foot_position", "hsddp_hkd_foot_jacobian",
     "hsddp_hkd_resetmap", "hsddp_hkd_resetmap_partial", "hsddp_device_alloc", "hsddp_device_free",
     "hsddp_memcpy_h2d", "hsddp_memcpy_d2h", "hsddp_device_synchronize", "hsddp_extract_commands",
-    "hsddp_shift", "hsddp_get_layout", "hsddp_update_problem",
+    "hsddp_shift", "hsddp_get_layout", "hsddp_update_problem", "hsddp_load_quad_reference",
+    "hsddp_plan_phases", "hsddp_set_reference_table", "hsddp_build_references", "hsddp_download_references",
 ]
 
 
@@ -135,6 +146,11 @@ def lib():
     L.hsddp_memcpy_d2h.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     L.hsddp_device_synchronize.argtypes = [C.c_int]
     L.hsddp_shift.argtypes = [C.c_void_p, C.c_int, IP]
+    L.hsddp_load_quad_reference.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_float), C.c_void_p, C.c_int]
+    L.hsddp_plan_phases.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_void_p]
+    L.hsddp_set_reference_table.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_float]
+    L.hsddp_build_references.argtypes = [C.c_void_p, IP, C.c_int, C.c_void_p, C.c_float]
+    L.hsddp_download_references.argtypes = [C.c_void_p, DP, DP, DP]
     L.hsddp_get_layout.argtypes = [C.c_void_p, IP, IP, IP, IP]
     L.hsddp_update_problem.argtypes = [C.c_void_p, IP, DP, DP, DP, DP]
     L.hsddp_extract_commands.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_void_p, C.c_int,

@@ -19,6 +19,9 @@
  *   hsddp_solve_begin/_iterate/_end           the same loop split at its inner iterations (:257-303 / :304-381 / :383-408)
  *   hsddp_download_trajectory                 Trajectory fields read by the caller  HKDMPC.cpp:243-298
  *   hsddp_download_element_info               get_actual_cost / get_solver_info     MultiPhaseDDP.h:416; .cpp:532-541
+ *   hsddp_load_quad_reference                 QuadReference::load_top_level_data   QuadReference.cpp:129-290
+ *   hsddp_plan_phases                         HKDProblem::initialization (segmentation) HKDProblem.cpp:15-68
+ *   hsddp_set_reference_table / _build_references  HKDSinglePhaseReference::get_reference_at_t HKDReference.cpp:8-57
  *   hsddp_shift / hsddp_update_problem        HKDProblem::update + HKDMPCSolver::update's re-solve
  *                                             setup (warm start reused)  HKDProblem.cpp:117-222; HKDMPC.cpp:96-143
  *   hsddp_extract_commands                    update_foot_placement + publish_mpc_cmd HKDMPC.cpp:207-298
@@ -170,6 +173,53 @@ int hsddp_download_working(hsddp_handle h, double *X, double *U, double *Defect,
 int hsddp_download_element_info(hsddp_handle h, hsddp_element_info *info);
 int hsddp_synchronize(hsddp_handle h);
 size_t hsddp_device_bytes(hsddp_handle h);
+
+/* ---- batched reference construction ----------------------------------
+ * One sample of a quad_reference.csv file (QuadAugmentedState, Reference/QuadReference.h:14-65). */
+typedef struct hsddp_quad_state {
+    double body_state[12];       /* eul, pos, omega, vWorld */
+    double qJ[12], qJd[12], foot_placements[12], grf[12], torque[12];
+    int contact[4];
+    double status_dur[4];
+} hsddp_quad_state;
+
+/* QuadReference::load_top_level_data (QuadReference.cpp:129-255, reorder_states :257-290): parse a
+ * quad_reference.csv (values rounded through float as std::stof / std::stoi).  Writes dt and up to
+ * `capacity` samples into out (out may be NULL to count); returns the number of samples (< 0 on
+ * error). */
+int hsddp_load_quad_reference(const char *path, int reorder, float *dt, hsddp_quad_state *out, int capacity);
+
+/* HKDProblem::initialization's phase segmentation (HKDProblem.cpp:15-68) on a reference window
+ * (QuadReference::initialize: window[0] = the current sample, n_window >= round(plan/dt_ref) + 2),
+ * with the float time arithmetic and sample rounding of QuadReference::get_contact_at_t
+ * (QuadReference.cpp:78-100): horizons, phase contacts (row n_phases = the contact at
+ * plan_duration + dt_mpc, add_tconstr_one_phase :272-276), contact durations, float start / end
+ * times. */
+typedef struct hsddp_phase_plan {
+    int n_phases;
+    int horizons[HSDDP_MAX_PHASES];
+    int contacts[HSDDP_MAX_PHASES + 1][4];
+    double durations[HSDDP_MAX_PHASES][4];
+    float start_times[HSDDP_MAX_PHASES], end_times[HSDDP_MAX_PHASES];
+} hsddp_phase_plan;
+int hsddp_plan_phases(const hsddp_quad_state *window, int n_window, float dt_ref, float plan_duration, float dt_sim,
+                      float dt_mpc, hsddp_phase_plan *plan);
+
+/* The reference sample table to the device (once per file): n samples, dt_ref. */
+int hsddp_set_reference_table(hsddp_handle h, const hsddp_quad_state *table, int n, float dt_ref);
+/* HKDSinglePhaseReference::get_reference_at_t (HKDReference.cpp:8-57) at every state slot of every
+ * element, on the device: slot k of phase i reads time t = start_i + k dt_sim (start_i =
+ * phase_start_times[i] - phase_start_times[0] as float, or the knot offset times dt_sim when
+ * phase_start_times is NULL), snapped to a sample as get_a_reference_ptr_at_t (QuadReference.cpp:
+ * 60-76, clamped to the window end window_len - 1) of element b's window, which starts at table
+ * sample window_start[b] (one value when the references are shared, ref_per_element = 0).
+ * ref_x = [body_state, foot_placements (stance) | qJ (swing)], ref_u = [grf, qJd], ref_foot =
+ * foot_placements.  Afterwards hsddp_upload_problem / hsddp_update_problem take NULL references
+ * and keep these. */
+int hsddp_build_references(hsddp_handle h, const int *window_start, int window_len, const float *phase_start_times,
+                           float dt_sim);
+/* The references the solve reads (uploaded or built): ref_x, ref_u [Bref][S][24], ref_foot [Bref][S][12]. */
+int hsddp_download_references(hsddp_handle h, double *ref_x, double *ref_u, double *ref_foot);
 
 /* ---- receding-horizon update -----------------------------------------
  * HKDProblem::update (HKDProblem.cpp:117-222) for n_steps simulation steps, on the warm start held

@@ -1,0 +1,212 @@
+"""ref_oracle.py — TEST INFRASTRUCTURE ONLY.
+
+CPU restatement (plain Python / numpy, small inputs) of the reference-construction steps that feed
+the solve in heli-sudoo/HKD-MPC, used by tests/ to check the product path
+(hkd-mpc_amd/csrc/hsddp_reference.cpp on the host, k_build_refs on the device):
+
+  * load_quad_reference   QuadReference::load_top_level_data (Reference/QuadReference.cpp:129-255)
+                          and reorder_states (:257-290): every number through std::stof, i.e.
+                          rounded once from its decimal text to float (restated here exactly, with
+                          rational arithmetic, so no double-rounding can hide a mismatch).
+  * sample_at             the sample index rule of get_a_reference_ptr_at_t / get_contact_at_t
+                          (QuadReference.cpp:65-100): floor(t / dt), +1 past the half step, clamped
+                          to the window end sz, in float arithmetic.
+  * plan_phases           HKDProblem::initialization's phase segmentation (HKD-TrajOpt/
+                          HKDProblem.cpp:26-68) and the last phase's next contact
+                          (add_tconstr_one_phase, :272-276), with the float clock of the reference.
+  * reference_slots       HKDSinglePhaseReference::get_reference_at_t (HKD-TrajOpt/
+                          HKDReference.cpp:8-57) at t_offset + k dt for every state slot, t_offset
+                          = phase_start_times[i] - phase_start_times[0] (HKDProblem.cpp:99,210) and
+                          the time formed as SinglePhase does (float + int * double, passed as
+                          float; SinglePhase.cpp:243-287).
+
+The product path never imports this module.
+"""
+import math
+import re
+from fractions import Fraction
+
+import numpy as np
+
+F32 = np.float32
+FIELDS12 = ("body_state", "qJ", "qJd", "foot_placements", "grf", "torque")
+
+
+def stof(word: str) -> np.float32:
+    """std::stof: the decimal text rounded once to the nearest float (ties to even)."""
+    w = word.strip()
+    if w.lower() in ("nan", "+nan", "-nan"):
+        return F32("nan")
+    if w.lower().lstrip("+-") in ("inf", "infinity"):
+        return F32(w)
+    exact = Fraction(w)
+    c = F32(float(w))  # within one ulp of the correctly rounded value
+    best = None
+    for cand in (np.nextafter(c, F32(-np.inf)), c, np.nextafter(c, F32(np.inf))):
+        if not np.isfinite(cand):
+            continue
+        err = abs(Fraction(float(cand)) - exact)
+        key = (err, int(cand.view(np.uint32)) & 1)  # ties: even mantissa
+        if best is None or key < best[0]:
+            best = (key, cand)
+    return best[1]
+
+
+def stoi(word: str) -> int:
+    return int(re.match(r"\s*([+-]?\d+)", word).group(1))
+
+
+def _empty_sample():
+    s = {f: np.zeros(12) for f in FIELDS12}
+    s["contact"] = np.zeros(4, np.int64)
+    s["status_dur"] = np.zeros(4)
+    return s
+
+
+def _words(line, n, conv):
+    out = []
+    for w in line.split():
+        if len(out) >= n:
+            break
+        out.append(conv(w))
+    return out
+
+
+def _reorder(s):
+    """QuadReference::reorder_states (QuadReference.cpp:257-290)."""
+    b = s["body_state"]
+    r = dict(s)
+    r["body_state"] = np.concatenate([b[3:6], b[0:3], b[9:12], b[6:9]])
+    r["body_state"][2] = 0.25
+    flip = lambda v: np.concatenate([v[3:6], v[0:3], v[9:12], v[6:9]])  # noqa: E731
+    r["qJ"] = flip(s["qJ"])
+    r["qJd"] = np.zeros(12)
+    r["foot_placements"] = flip(s["foot_placements"])
+    r["grf"] = flip(s["grf"])
+    r["torque"] = flip(s["torque"])
+    r["contact"] = s["contact"][[1, 0, 3, 2]]
+    r["status_dur"] = s["status_dur"][[1, 0, 3, 2]]
+    for leg in range(4):
+        for a in (1, 2):
+            r["qJ"][3 * leg + a] = -r["qJ"][3 * leg + a]
+            r["torque"][3 * leg + a] = -r["torque"][3 * leg + a]
+    return r
+
+
+def load_quad_reference(path: str, reorder: bool = False):
+    """QuadReference::load_top_level_data (QuadReference.cpp:129-255): (samples, dt)."""
+    with open(path) as f:
+        lines = f.read().split("\n")
+    if lines and lines[-1] == "":
+        lines.pop()  # getline yields no empty line after the final newline
+    dt = F32(0)
+    out = []
+    cur = _empty_sample()
+    i = 0
+    keys = [("body_state", 12), ("qJ", 12), ("foot_placements", 12), ("grf", 12), ("torque", 12),
+            ("contact", 4), ("status_dur", 4)]
+    while i < len(lines):
+        line = lines[i]
+        i += 1
+        if line == "dt":
+            if i < len(lines):
+                dt = stof(lines[i])
+                i += 1
+            continue
+        for key, n in keys:  # the reference's test order: the first header substring wins
+            if key in line:
+                nxt = lines[i] if i < len(lines) else ""
+                i += 1
+                if key == "body_state":
+                    cur = _empty_sample()  # quad_state.SetZero()
+                conv = stoi if key == "contact" else (lambda w: float(stof(w)))
+                vals = _words(nxt, n, conv)
+                cur[key][:len(vals)] = vals
+                if key == "status_dur":
+                    snap = {k: v.copy() for k, v in cur.items()}
+                    out.append(_reorder(snap) if reorder else snap)
+                break
+    return out, dt
+
+
+def sample_at(t, dt, sz):
+    """QuadReference.cpp:65-79 / 86-99, float t and dt."""
+    t, dt = F32(t), F32(dt)
+    k = int(math.floor(float(F32(t / dt))))
+    if float(F32(t - F32(k) * dt)) > 0.5 * float(dt):
+        k += 1
+    return min(k, sz)
+
+
+def _approx_eq(a, b):
+    return float(abs(F32(F32(a) - F32(b)))) <= float(F32(1e-6))
+
+
+def plan_phases(window, dt_ref, plan_duration=0.6, dt_sim=0.01, dt_mpc=0.01):
+    """HKDProblem::initialization (HKDProblem.cpp:26-68) on the window window[0..sz]."""
+    sz = len(window) - 1
+    dt_ref, plan_duration, dt_sim, dt_mpc = F32(dt_ref), F32(plan_duration), F32(dt_sim), F32(dt_mpc)
+    contact = lambda t: tuple(int(c) for c in window[sample_at(t, dt_ref, sz)]["contact"])  # noqa: E731
+    duration = lambda t: window[sample_at(t, dt_ref, sz)]["status_dur"].copy()  # noqa: E731
+    t = F32(0)
+    start = F32(0)
+    prev = contact(t)
+    dur = duration(t)
+    plan = {"horizons": [], "contacts": [], "durations": [], "start_times": [], "end_times": []}
+    while t < plan_duration or _approx_eq(t, plan_duration):
+        cur = contact(t)
+        if cur != prev or t > plan_duration or _approx_eq(t, plan_duration):
+            end = t
+            plan["start_times"].append(start)
+            plan["end_times"].append(end)
+            q = float(F32(F32(end - start) / dt_sim))
+            plan["horizons"].append(int(math.copysign(math.floor(abs(q) + 0.5), q)))  # std::round
+            plan["contacts"].append(prev)
+            plan["durations"].append(dur)
+            prev = cur
+            dur = duration(t)
+            start = end
+        t = F32(t + dt_sim)
+    plan["contacts"].append(contact(F32(plan_duration + dt_mpc)))
+    return plan
+
+
+def reference_at(sample):
+    """get_reference_at_t (HKDReference.cpp:8-57) of one sample: x_r, u_r, foot_r."""
+    x = np.zeros(24)
+    x[:12] = sample["body_state"]
+    for leg in range(4):
+        src = sample["foot_placements"] if sample["contact"][leg] > 0 else sample["qJ"]
+        x[12 + 3 * leg:15 + 3 * leg] = src[3 * leg:3 * leg + 3]
+    u = np.concatenate([sample["grf"], sample["qJd"]])
+    return x, u, sample["foot_placements"].copy()
+
+
+def slot_times(horizons, dt_sim, phase_start_times=None):
+    """t of every state slot: t_offset_i + k dt (SinglePhase.cpp:243-287)."""
+    dt_sim = F32(dt_sim)
+    if phase_start_times is None:  # the float clock of initialization
+        starts, t = [], F32(0)
+        for n in horizons:
+            starts.append(t)
+            for _ in range(n):
+                t = F32(t + dt_sim)
+    else:
+        starts = [F32(F32(s) - F32(phase_start_times[0])) for s in phase_start_times]
+    out = []
+    for i, n in enumerate(horizons):
+        for k in range(n + 1):
+            out.append(F32(float(starts[i]) + k * float(dt_sim)))
+    return out
+
+
+def reference_slots(table, window_start, window_len, dt_ref, horizons, dt_sim=0.01, phase_start_times=None):
+    """ref_x [S][24], ref_u [S][24], ref_foot [S][12] of one element whose window starts at
+    table[window_start] (samples past the table's end read its last sample)."""
+    sz = window_len - 1
+    ts = slot_times(horizons, dt_sim, phase_start_times)
+    rx, ru, rf = np.zeros((len(ts), 24)), np.zeros((len(ts), 24)), np.zeros((len(ts), 12))
+    for s, t in enumerate(ts):
+        k = min(window_start + sample_at(t, dt_ref, sz), len(table) - 1)
+        rx[s], ru[s], rf[s] = reference_at(table[k])
+    return rx, ru, rf

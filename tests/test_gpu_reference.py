@@ -1,0 +1,194 @@
+"""GPU checks of the batched reference construction through the C-ABI:
+HKDSinglePhaseReference::get_reference_at_t at every slot of every element, built on the device
+(k_build_refs) from a reference file's samples, against oracle/ref_oracle.py — bit-exact (data
+movement and float time rounding) — and the solve that reads them against the same solve with the
+oracle's references uploaded from the host (bit for bit) and against the oracle solver.
+
+Data: the first samples of the reference's own trot / flytrot files (tests/golden/ref_*.csv)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import hsddp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+sys.path.insert(0, HERE)
+import oracle_lib as O  # noqa: E402
+import ref_oracle as R  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(HERE, "golden")
+N_WIN = 62
+
+
+def _load(name, reorder=False):
+    p = os.path.join(GOLD, f"ref_{name}.csv")
+    tab, dt = hsddp.load_quad_reference(p, reorder)
+    ref, _ = R.load_quad_reference(p, reorder)
+    return tab, ref, dt
+
+
+def _x0(B, seed=3):
+    rng = np.random.default_rng(seed)
+    x0 = np.zeros((B, 24))
+    x0[:, 5] = 0.25
+    x0[:, 12:] = np.float32([.2, -.14, 0, .2, .14, 0, -.2, -.14, 0, -.2, .14, 0])
+    x0[:, :3] += rng.uniform(-.05, .05, (B, 3))
+    x0[:, 6:12] += rng.uniform(-.2, .2, (B, 6))
+    return x0
+
+
+def _oracle_refs(ref, starts, horizons, dt, pst=None):
+    out = [R.reference_slots(ref, int(w), N_WIN, dt, horizons, 0.01, pst) for w in starts]
+    return tuple(np.stack([o[q] for o in out]) for q in range(3))
+
+
+@pytest.mark.parametrize("start", [0, 7, 30])
+def test_build_references_match_oracle(start):
+    tab, ref, dt = _load("trot")
+    p = hsddp.reference_problem(tab, dt, [start], _x0(5))
+    s = hsddp.Solver(p)
+    got = s.references()
+    rx, ru, rf = _oracle_refs(ref, [start], p["horizons"], dt)
+    assert np.array_equal(got["ref_x"], rx) and np.array_equal(got["ref_u"], ru) and np.array_equal(got["ref_foot"], rf)
+    # explicit phase start times (HKDProblem::update's t_offset) give the same samples
+    s.build_references([start], N_WIN, p["phase_start_times"], 0.01)
+    again = s.references()
+    rx2, _, _ = _oracle_refs(ref, [start], p["horizons"], dt, p["phase_start_times"])
+    assert np.array_equal(again["ref_x"], rx2) and np.array_equal(again["ref_x"], rx)
+    # the default warm start is the reference (HKDProblem.cpp:84-90)
+    tr = s.trajectory()
+    assert np.array_equal(tr["Xbar"], np.repeat(rx, 5, axis=0))
+    s.close()
+
+
+def test_per_element_windows_match_oracle():
+    """Per-element references: one table holding two files (trot and its leg-reordered copy, whose
+    contact switches fall on the same knots), every element its own window start."""
+    t1, r1, dt = _load("trot")
+    t2, r2, _ = _load("trot", reorder=True)
+    tab = np.concatenate([t1, t2])
+    ref = r1 + r2
+    p0 = hsddp.plan_phases(tab[3:3 + N_WIN], dt)
+    starts = [3, 103, 3, 103, 3, 103]
+    p = hsddp.reference_problem(tab, dt, starts, _x0(6))
+    assert p["horizons"] == p0["horizons"]
+    s = hsddp.Solver(p)
+    got = s.references()
+    rx, ru, rf = _oracle_refs(ref, starts, p["horizons"], dt)
+    assert got["ref_x"].shape[0] == 6
+    assert np.array_equal(got["ref_x"], rx) and np.array_equal(got["ref_u"], ru) and np.array_equal(got["ref_foot"], rf)
+    # samples past the table's end read its last sample
+    s.build_references([150] * 6, N_WIN, None, 0.01)
+    rx3, _, _ = _oracle_refs(ref, [150] * 6, p["horizons"], dt)
+    assert np.array_equal(s.references()["ref_x"], rx3)
+    with pytest.raises(hsddp.HSDDPError):
+        s.build_references([400] * 6, N_WIN, None, 0.01)  # window outside the table
+    s.close()
+
+
+def _host_prob(p, ref, dt):
+    rx, ru, rf = _oracle_refs(ref, p["window_start"], p["horizons"], dt)
+    q = {k: v for k, v in p.items() if k not in ("ref_table", "window_start")}
+    q.update(ref_x=rx, ref_u=ru, ref_foot=rf, Xbar=np.repeat(rx, p["batch"], axis=0) if rx.shape[0] == 1 else rx,
+             Ubar=np.zeros((p["batch"], p["Kc"], 24)))
+    return q
+
+
+@pytest.mark.parametrize("name,start", [("trot", 0), ("flytrot", 11)])
+def test_solve_from_file_matches_host_refs_and_oracle(name, start):
+    tab, ref, dt = _load(name)
+    B = 6
+    p = hsddp.reference_problem(tab, dt, [start], _x0(B))
+    kw = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=2)
+    a = hsddp.Solver(p, hsddp.load_settings(**kw))
+    a.solve()
+    ga = {**a.trajectory(), **a.working(), **a.element_info()}
+    q = _host_prob(p, ref, dt)
+    b = hsddp.Solver(q, hsddp.load_settings(**kw))
+    b.solve()
+    gb = {**b.trajectory(), **b.working(), **b.element_info()}
+    for f in ("Xbar", "Ubar", "K", "X", "U", "cost", "n_ls_trials"):
+        assert np.array_equal(ga[f], gb[f]), f
+    r = O.solve_batch(q, O.default_options(**kw), n_threads=8)
+    for f in ("Xbar", "Ubar", "X", "U"):
+        assert np.max(np.abs(ga[f] - r[f])) <= 1e-9 * np.max(np.abs(r[f])), f
+    assert np.array_equal(ga["n_ls_trials"], r["n_ls_trials"])
+    a.close()
+    b.close()
+
+
+class _FileScenario:
+    """HKDProblem::update's caller-side bookkeeping (HKDProblem.cpp:117-222) over a reference
+    file with dt_ref = dt_sim: the window advances one sample per step; the contact at the new
+    horizon end (relative time 0.6 -> sample 60 of the window) decides the phase growth."""
+
+    def __init__(self, ref, start, plan):
+        self.ref, self.start = ref, start
+        self.horizons = list(plan["horizons"])
+        self.contacts = [tuple(int(v) for v in c) for c in plan["contacts"][:-1]]
+        self.reach_end = [0] * len(self.horizons)
+        self.next_contact = tuple(int(v) for v in plan["contacts"][-1])
+        self.initial = True
+
+    def contact(self, k):
+        return tuple(int(v) for v in self.ref[min(self.start + k, len(self.ref) - 1)]["contact"])
+
+    def step(self):
+        self.start += 1
+        self.initial = False
+        if self.horizons[0] <= 1:
+            self.horizons.pop(0); self.contacts.pop(0); self.reach_end.pop(0)
+        else:
+            self.horizons[0] -= 1
+        new = self.contact(60)
+        cc = new != self.contacts[-1]
+        if cc and self.reach_end[-1]:
+            self.horizons.append(1); self.contacts.append(new); self.reach_end.append(0)
+        else:
+            self.horizons[-1] += 1
+            if cc:
+                self.reach_end[-1] = 1
+        return int(cc)
+
+    def contact_rows(self, B):
+        last = self.contact(61) if self.reach_end[-1] else self.contacts[-1]
+        return np.repeat(np.array([self.contacts + [last]], np.int32), B, axis=0)
+
+
+def test_mpc_loop_from_file():
+    """Initialise from the trot file, then 12 receding-horizon updates: shift on the device, build
+    the next window's references on the device, re-solve; a twin solver fed the oracle's references
+    from the host stays bit-identical, and the built references equal the oracle's every step."""
+    tab, ref, dt = _load("trot")
+    B = 4
+    p = hsddp.reference_problem(tab, dt, [0], _x0(B))
+    kw = dict(max_AL_iter=2, max_DDP_iter=1)
+    dev = hsddp.Solver(p, hsddp.load_settings(**kw))
+    host = hsddp.Solver(_host_prob(p, ref, dt), hsddp.load_settings(**kw))
+    dev.solve(); host.solve()
+    sc = _FileScenario(ref, 0, p["plan"])
+    x0 = _x0(B, 9)
+    for it in range(12):
+        flag = sc.step()
+        la = dev.shift([flag]); lb = host.shift([flag])
+        assert la == lb and la["horizons"] == sc.horizons, it
+        contacts = sc.contact_rows(B)
+        dev.build_references([sc.start], N_WIN, None, 0.01)
+        dev.update_problem(contacts, x0)
+        rx, ru, rf = _oracle_refs(ref, [sc.start], sc.horizons, dt)
+        assert np.array_equal(dev.references()["ref_x"], rx), it
+        host.update_problem(contacts, x0, rx, ru, rf)
+        dev.solve(); host.solve()
+        ga, gb = dev.trajectory(), host.trajectory()
+        for f in ("Xbar", "Ubar", "K"):
+            assert np.array_equal(ga[f], gb[f]), (it, f)
+        assert np.all(np.isfinite(dev.element_info()["cost"]))
+    sc.step()
+    dev.shift([0])
+    with pytest.raises(hsddp.HSDDPError):
+        dev.update_problem(sc.contact_rows(B), x0)  # references of the old layout are not reused
+    dev.close(); host.close()

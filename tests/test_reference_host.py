@@ -1,0 +1,147 @@
+"""Reference construction on the host, no GPU: the quad_reference.csv
+reader and the phase segmentation of the C-ABI (hkd-mpc_amd/csrc/hsddp_reference.cpp) against
+oracle/ref_oracle.py, on samples of the reference's own data files (tests/golden/ref_*.csv, made
+by tests/golden/make_ref_fixtures.py).  Integer / float-rounding work: bit-exact.
+
+Pins: the values below are read off the reference's data files as text
+(Reference/Data/trot/quad_reference.csv:1-16; gaitLib/run_jump/quad_reference.csv:1-2 — its dt is
+NaN, quirk A16), and every window's phase horizons sum to the plan length round(0.6 / 0.01) = 60.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import hsddp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+import ref_oracle as R  # noqa: E402
+
+GOLD = os.path.join(HERE, "golden")
+FILES = {"trot": 100, "flytrot": 80, "run_jump": 40}
+
+
+def path(name):
+    return os.path.join(GOLD, f"ref_{name}.csv")
+
+
+@pytest.mark.parametrize("name", list(FILES))
+@pytest.mark.parametrize("reorder", [False, True])
+def test_reader_matches_oracle(name, reorder):
+    g, dt = hsddp.load_quad_reference(path(name), reorder)
+    r, dt_r = R.load_quad_reference(path(name), reorder)
+    assert len(g) == len(r) == FILES[name]
+    assert np.array_equal(np.float32(dt), dt_r, equal_nan=True)
+    for i, s in enumerate(r):
+        for k, v in s.items():
+            assert np.array_equal(g[k][i], v, equal_nan=True), (name, i, k)
+
+
+def test_reader_known_values():
+    g, dt = hsddp.load_quad_reference(path("trot"))
+    assert np.float32(dt) == np.float32(0.01)
+    s = g[0]
+    assert np.array_equal(s["body_state"], np.float32([0, 0, 0, 0, 0, .25, 0, 0, 0, .1, 0, 0]).astype(float))
+    assert np.array_equal(s["qJ"], np.float32([0, -.8, 1.6] * 4).astype(float))
+    assert np.array_equal(s["foot_placements"],
+                          np.float32([.2, -.14, 0, .2, .14, 0, -.2, -.14, 0, -.2, .14, 0]).astype(float))
+    assert np.array_equal(s["grf"], np.float32([0, 0, 22.5] * 4).astype(float))
+    assert list(s["contact"]) == [1, 1, 1, 1]
+    assert np.array_equal(s["status_dur"], np.float32([.31, .11, .11, .31]).astype(float))
+    assert not np.any(g["qJd"])  # the file has no qJd block
+    assert g[1]["body_state"][3] == np.float32(0.001)
+    # reorder_states: [pos, eul, vWorld, omega], z forced to 0.25, legs (FR, FL, HR, HL) swapped
+    # pairwise, knee / hip joint signs flipped (QuadReference.cpp:257-290)
+    q, _ = hsddp.load_quad_reference(path("trot"), reorder=True)
+    assert q[1]["body_state"][0] == np.float32(0.001) and q[1]["body_state"][2] == 0.25
+    assert np.array_equal(q[0]["qJ"], np.float32([0, .8, -1.6] * 4).astype(float))
+    assert np.array_equal(q[0]["status_dur"], np.float32([.11, .31, .31, .11]).astype(float))
+    _, dt_nan = hsddp.load_quad_reference(path("run_jump"))
+    assert np.isnan(dt_nan)
+
+
+def test_reader_errors(tmp_path):
+    with pytest.raises(hsddp.HSDDPError):
+        hsddp.load_quad_reference(str(tmp_path / "missing.csv"))
+    bad = tmp_path / "bad.csv"
+    bad.write_text("dt\n0.01\nbody_state\n 0.0 zz\n")
+    with pytest.raises(hsddp.HSDDPError):
+        hsddp.load_quad_reference(str(bad))
+    empty = tmp_path / "empty.csv"
+    empty.write_text("")
+    g, _ = hsddp.load_quad_reference(str(empty))
+    assert len(g) == 0
+
+
+def _windows(name, n_win=62):
+    tab, dt = hsddp.load_quad_reference(path(name))
+    ref, _ = R.load_quad_reference(path(name))
+    return tab, ref, dt, range(0, len(ref) - n_win + 1)
+
+
+@pytest.mark.parametrize("name", ["trot", "flytrot"])
+def test_plan_matches_oracle(name):
+    tab, ref, dt, starts = _windows(name)
+    n_win = 62
+    for st in starts:
+        g = hsddp.plan_phases(tab[st:st + n_win], dt)
+        r = R.plan_phases(ref[st:st + n_win], dt)
+        assert g["horizons"] == r["horizons"], st
+        assert sum(g["horizons"]) == 60, st
+        assert np.array_equal(g["contacts"], np.array(r["contacts"])), st
+        assert np.array_equal(g["durations"], np.array(r["durations"])), st
+        assert np.array_equal(g["start_times"], np.array(r["start_times"], np.float32)), st
+        assert np.array_equal(g["end_times"], np.array(r["end_times"], np.float32)), st
+
+
+def test_plan_known_answer_and_coarse_steps():
+    tab, ref, dt, _ = _windows("trot")
+    g = hsddp.plan_phases(tab[:62], dt)
+    assert g["horizons"] == [11, 20, 5, 19, 5]
+    assert [tuple(c) for c in g["contacts"]] == [(1, 1, 1, 1), (1, 0, 0, 1), (0, 0, 0, 0), (0, 1, 1, 0),
+                                                 (0, 0, 0, 0), (1, 0, 0, 1)]
+    # dt_sim = 2 dt_ref: every horizon counts 20 ms knots (the reference's round((end-start)/dt_sim))
+    g2 = hsddp.plan_phases(tab[:62], dt, dt_sim=0.02, dt_mpc=0.02)
+    r2 = R.plan_phases(ref[:62], dt, dt_sim=0.02, dt_mpc=0.02)
+    assert g2["horizons"] == r2["horizons"] and sum(g2["horizons"]) == 30
+
+
+def test_plan_errors():
+    tab, ref, dt, _ = _windows("trot")
+    rj, dt_nan = hsddp.load_quad_reference(path("run_jump"))
+    with pytest.raises(hsddp.HSDDPError):
+        hsddp.plan_phases(rj, dt_nan)  # quirk A16: NaN dt
+    with pytest.raises(hsddp.HSDDPError):
+        hsddp.plan_phases(tab[:0], dt)
+    with pytest.raises(hsddp.HSDDPError):
+        hsddp.plan_phases(tab[:62], dt, dt_sim=-0.01)
+
+
+def test_slot_times_float_clock_equals_phase_starts():
+    """Phase offsets from the initialization clock (knot counts x dt_sim accumulated in float) and
+    from the plan's own start times give the same sample at every slot; the Xbar initialisation's
+    float-only time (HKDProblem.cpp:87) lands on the same samples as the cost's
+    float + int * double time (SinglePhase.cpp:243)."""
+    tab, ref, dt, starts = _windows("trot")
+    for st in starts:
+        plan = R.plan_phases(ref[st:st + 62], dt)
+        a = R.slot_times(plan["horizons"], 0.01)
+        b = R.slot_times(plan["horizons"], 0.01, plan["start_times"])
+        ia = [R.sample_at(t, dt, 61) for t in a]
+        assert ia == [R.sample_at(t, dt, 61) for t in b]
+        init = [np.float32(plan["start_times"][i] + np.float32(np.float32(k) * np.float32(0.01)))
+                for i, n in enumerate(plan["horizons"]) for k in range(n + 1)]
+        assert ia == [R.sample_at(t, dt, 61) for t in init]
+
+
+def test_reference_problem_host_side():
+    tab, _ = hsddp.load_quad_reference(path("trot"))
+    x0 = np.zeros((3, 24))
+    p = hsddp.reference_problem(tab, 0.01, [4], x0)
+    assert p["batch"] == 3 and p["window_len"] == 62
+    assert p["S"] == sum(n + 1 for n in p["horizons"]) and p["Kc"] == 60
+    assert p["contacts"].shape == (3, len(p["horizons"]) + 1, 4)
+    with pytest.raises(hsddp.HSDDPError):  # per-element windows whose layouts differ
+        hsddp.reference_problem(tab, 0.01, [0, 1, 2], x0)
