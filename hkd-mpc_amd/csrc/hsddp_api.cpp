@@ -4,10 +4,14 @@
 // HKDProblem.h:70-90).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <array>
 #include <cctype>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <map>
 #include <sstream>
@@ -226,6 +230,15 @@ struct hsddp_handle_t {
     int ref_n = 0;
     float ref_dt = 0;
     bool refs_on_device = false;  // references built by hsddp_build_references for this layout
+    // reference-driven MPC state (hsddp_advance): the table's samples on the host (contacts and
+    // durations are read there), each reference element's window start, the window length and
+    // the simulation step of the last hsddp_build_references, QuadReference::t_cur, and the
+    // contact durations of every element's phases [B][P][4] (HKDProblemData::contact_durations)
+    std::vector<hsddp_quad_state> table_host;
+    std::vector<int> win_start;
+    int win_len = 0;
+    float dt_sim = 0, t_cur = 0;
+    std::vector<double> durations;
 };
 
 // device staging area of at least `bytes` (contents not preserved when it grows)
@@ -1095,11 +1108,33 @@ extern "C" int hsddp_set_reference_table(hsddp_handle h, const hsddp_quad_state 
     HIPCHK(hipMemcpy(h->ref_table, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
     h->ref_n = n;
     h->ref_dt = dt_ref;
+    h->table_host.assign(table, table + n);
+    h->win_start.clear();
     return HSDDP_OK;
 }
 
+// sample index of relative time t in a window of sz + 1 samples (QuadReference.cpp:65-79, 86-99)
+static int ref_sample(float t, float dt, int sz)
+{
+    int k = (int)std::floor(t / dt);
+    if (t - k * dt > 0.5 * dt) k++;
+    return k > sz ? sz : k;
+}
+
+static int build_refs(hsddp_handle h, const int *window_start, int window_len, const float *phase_start_times,
+                      float dt_sim, bool initial);
+
 extern "C" int hsddp_build_references(hsddp_handle h, const int *window_start, int window_len,
                                       const float *phase_start_times, float dt_sim)
+{
+    return build_refs(h, window_start, window_len, phase_start_times, dt_sim, true);
+}
+
+// initial: a new problem (not an hsddp_advance step): QuadReference's clock restarts and every
+// phase's contact duration is read at its start time, as HKDProblem::initialization does
+// (get_contact_duration_at_t at t = 0 and at each phase end, HKDProblem.cpp:38,63)
+static int build_refs(hsddp_handle h, const int *window_start, int window_len, const float *phase_start_times,
+                      float dt_sim, bool initial)
 {
     if (!h || !window_start) return fail(HSDDP_ERR_ARG, "null argument");
     if (!h->ref_table) return fail(HSDDP_ERR_ARG, "no reference table (hsddp_set_reference_table)");
@@ -1143,5 +1178,147 @@ extern "C" int hsddp_build_references(hsddp_handle h, const int *window_start, i
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(h->stream));
     h->refs_on_device = true;
+    h->win_start.assign(window_start, window_start + Br);
+    h->win_len = window_len;
+    h->dt_sim = dt_sim;
+    if (initial) {
+        h->t_cur = 0;
+        h->durations.assign((size_t)p.B * p.P * 4, 0.0);
+        for (int b = 0; b < p.B; ++b)
+            for (int i = 0; i < p.P; ++i) {
+                const int k = std::min(window_start[Br == 1 ? 0 : b] + ref_sample(start[i], h->ref_dt, sz), h->ref_n - 1);
+                for (int l = 0; l < 4; ++l) h->durations[((size_t)b * p.P + i) * 4 + l] = h->table_host[k].status_dur[l];
+            }
+    }
+    return HSDDP_OK;
+}
+
+// ---- reference-driven receding-horizon step -------------------------------------------------------
+// HKDProblem::update (HKDProblem.cpp:117-222) with the contacts read from the reference table:
+// per simulation step the window advances (QuadReference::step, QuadReference.cpp:33-47), the
+// contact at the new horizon end (get_contact_at_t(new_end - new_start)) decides whether the last
+// phase grows or a new phase starts, and a last phase that has reached its end gets the touchdown
+// constraint / reset map towards the contact at plan_duration + dt_mpc (add_tconstr_one_phase,
+// :199-202, 268-308).  Then the shifted warm start (hsddp_shift), the new layout's references
+// (build_refs) and the new contacts and x0 (hsddp_update_problem).
+extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, float dt_mpc, const double *x0,
+                             int *contact_change)
+{
+    if (!h || !x0) return fail(HSDDP_ERR_ARG, "null argument");
+    if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
+    if (h->win_start.empty() || h->table_host.empty())
+        return fail(HSDDP_ERR_ARG, "references not built from a table (hsddp_build_references)");
+    if (n_steps < 0) return fail(HSDDP_ERR_ARG, "n_steps must be >= 0");
+    const Params &p = h->p;
+    const int B = p.B, Br = h->Bref, sz = h->win_len - 1;
+    const float dt = h->ref_dt, dts = h->dt_sim;
+    auto leq = [](float a, float b) { return a < b || std::abs(a - b) <= 1e-6f; };
+    int adv = 0;  // samples per simulation step
+    for (int i = 1; leq(i * dt, dts); ++i) adv++;
+    // per element: phase contacts, the last phase's next contact (row P), phase durations
+    typedef std::array<int, 4> C4;
+    typedef std::array<double, 4> D4;
+    std::vector<std::deque<C4>> pc(B);
+    std::vector<std::deque<D4>> du(B);
+    std::vector<C4> next(B);
+    for (int b = 0; b < B; ++b) {
+        for (int i = 0; i <= p.P; ++i) {
+            C4 c;
+            for (int l = 0; l < 4; ++l) c[l] = h->contacts[((size_t)b * (p.P + 1) + i) * 4 + l];
+            if (i < p.P) pc[b].push_back(c); else next[b] = c;
+        }
+        for (int i = 0; i < p.P; ++i) {
+            D4 v;
+            for (int l = 0; l < 4; ++l) v[l] = h->durations[((size_t)b * p.P + i) * 4 + l];
+            du[b].push_back(v);
+        }
+    }
+    std::vector<int> hz(p.N, p.N + p.P), reach(h->reach_end), ws(h->win_start), flags(n_steps);
+    float t_cur = h->t_cur;
+    auto sample = [&](int b, float t) -> const hsddp_quad_state & {
+        const int k = ws[Br == 1 ? 0 : b] + ref_sample(t, dt, sz);
+        return h->table_host[std::min(k, h->ref_n - 1)];
+    };
+    for (int j = 0; j < n_steps; ++j) {
+        for (int a = 0; a < adv; ++a) {
+            t_cur += dt;
+            for (int &w : ws) w++;
+        }
+        for (int &w : ws)
+            if (w >= h->ref_n) return fail(HSDDP_ERR_ARG, "the reference window ran past the table");
+        if (hz.front() <= 1) {  // pop_front_phase (HKDProblem.h:56-66)
+            if (hz.size() == 1) return fail(HSDDP_ERR_ARG, "advance would remove the only phase");
+            hz.erase(hz.begin());
+            reach.erase(reach.begin());
+            for (int b = 0; b < B; ++b) { pc[b].pop_front(); du[b].pop_front(); }
+        } else {
+            hz.front()--;
+        }
+        const float rel = (t_cur + plan_duration) - t_cur;  // new_end_time - new_start_time
+        int cc = -1;
+        std::vector<C4> nc(B);
+        for (int b = 0; b < B; ++b) {
+            const hsddp_quad_state &q = sample(b, rel);
+            std::copy(q.contact, q.contact + 4, nc[b].begin());
+            const int cb = nc[b] != pc[b].back();
+            if (cc >= 0 && cb != cc)
+                return fail(HSDDP_ERR_UNSUPPORTED, "elements disagree on a contact change (the layout is shared)");
+            cc = cb;
+        }
+        if (cc && reach.back()) {
+            if ((int)hz.size() >= HSDDP_MAX_PHASES) return fail(HSDDP_ERR_ARG, "advance exceeds HSDDP_MAX_PHASES phases");
+            hz.push_back(1);
+            reach.push_back(0);
+            for (int b = 0; b < B; ++b) {
+                const hsddp_quad_state &q = sample(b, rel);
+                pc[b].push_back(nc[b]);
+                D4 v;
+                std::copy(q.status_dur, q.status_dur + 4, v.begin());
+                du[b].push_back(v);
+                next[b] = nc[b];  // a new phase carries no terminal constraint (identity reset)
+            }
+        } else {
+            hz.back()++;
+            if (cc) reach.back() = 1;
+        }
+        if (reach.back())
+            for (int b = 0; b < B; ++b) {
+                const hsddp_quad_state &q = sample(b, plan_duration + dt_mpc);
+                std::copy(q.contact, q.contact + 4, next[b].begin());
+            }
+        flags[j] = cc;
+    }
+    int rc;
+    if ((rc = hsddp_shift(h, n_steps, flags.data()))) return rc;
+    if (p.P != (int)hz.size() || !std::equal(hz.begin(), hz.end(), p.N) || h->reach_end != reach)
+        return fail(HSDDP_ERR_ARG, "internal: advance and shift disagree on the layout");
+    if ((rc = build_refs(h, ws.data(), h->win_len, nullptr, dts, false))) return rc;
+    const int P = p.P;
+    std::vector<int> contacts((size_t)B * (P + 1) * 4);
+    std::vector<double> dur((size_t)B * P * 4);
+    for (int b = 0; b < B; ++b) {
+        for (int i = 0; i <= P; ++i)
+            for (int l = 0; l < 4; ++l)
+                contacts[((size_t)b * (P + 1) + i) * 4 + l] = i < P ? pc[b][i][l] : next[b][l];
+        for (int i = 0; i < P; ++i)
+            for (int l = 0; l < 4; ++l) dur[((size_t)b * P + i) * 4 + l] = du[b][i][l];
+    }
+    if ((rc = hsddp_update_problem(h, contacts.data(), x0, nullptr, nullptr, nullptr))) return rc;
+    h->durations.swap(dur);
+    h->t_cur = t_cur;
+    if (contact_change) std::copy(flags.begin(), flags.end(), contact_change);
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_get_phase_info(hsddp_handle h, int *contacts, double *durations)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    const Params &p = h->p;
+    if (contacts) std::copy(h->contacts.begin(), h->contacts.end(), contacts);
+    if (durations) {
+        if (h->durations.size() != (size_t)p.B * p.P * 4)
+            return fail(HSDDP_ERR_ARG, "no phase durations (references not built from a table)");
+        std::copy(h->durations.begin(), h->durations.end(), durations);
+    }
     return HSDDP_OK;
 }

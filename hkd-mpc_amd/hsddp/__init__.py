@@ -260,6 +260,30 @@ class Solver:
         check(lib().hsddp_update_problem(self._h, ip(self._contacts), dp(np.ascontiguousarray(x0, dtype=np.float64)),
                                          *(None if r is None else dp(r) for r in refs)))
 
+    def advance(self, x0, n_steps: int = 1, plan_duration: float = 0.6, dt_mpc: float = 0.01) -> list:
+        """HKDProblem::update from the reference table (hsddp_advance): the window moves n_steps
+        simulation steps, the layout, warm start, references and contacts follow, x0 [B][24] is the
+        new initial state.  Returns the contact-change flag of every step."""
+        flags = np.zeros(max(1, n_steps), np.int32)
+        check(lib().hsddp_advance(self._h, int(n_steps), float(plan_duration), float(dt_mpc),
+                                  dp(np.ascontiguousarray(x0, dtype=np.float64)), ip(flags)))
+        lay = self.layout()
+        self.P = len(lay["horizons"])
+        self.S = sum(n + 1 for n in lay["horizons"])
+        return [int(f) for f in flags[:n_steps]]
+
+    def phase_info(self) -> dict:
+        """contacts [B][P+1][4] (row P: the last phase's next contact); durations [B][P][4] when the
+        references come from a table (else None)."""
+        c = np.zeros((self.B, self.P + 1, 4), np.int32)
+        d = np.zeros((self.B, self.P, 4))
+        try:
+            check(lib().hsddp_get_phase_info(self._h, ip(c), dp(d)))
+        except HSDDPError:
+            check(lib().hsddp_get_phase_info(self._h, ip(c), None))
+            d = None
+        return {"contacts": c, "durations": d}
+
     def synchronize(self) -> None:
         check(lib().hsddp_synchronize(self._h))
 

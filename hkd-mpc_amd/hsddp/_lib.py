@@ -101,7 +101,8 @@ EXPORTS = [
     "hsddp_hkd_resetmap", "hsddp_hkd_resetmap_partial", "hsddp_device_alloc", "hsddp_device_free",
     "hsddp_memcpy_h2d", "hsddp_memcpy_d2h", "hsddp_device_synchronize", "hsddp_extract_commands",
     "hsddp_shift", "hsddp_get_layout", "hsddp_update_problem", "hsddp_load_quad_reference",
-    "hsddp_plan_phases", "hsddp_set_reference_table", "hsddp_build_references", "hsddp_download_references",
+    "hsddp_plan_phases", "hsddp_set_reference_table", "hsddp_build_references", "hsddp_download_references", "hsddp_advance",
+    "hsddp_get_phase_info",
 ]
 
 
@@ -151,6 +152,8 @@ def lib():
     L.hsddp_set_reference_table.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_float]
     L.hsddp_build_references.argtypes = [C.c_void_p, IP, C.c_int, C.c_void_p, C.c_float]
     L.hsddp_download_references.argtypes = [C.c_void_p, DP, DP, DP]
+    L.hsddp_advance.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_float, DP, IP]
+    L.hsddp_get_phase_info.argtypes = [C.c_void_p, IP, DP]
     L.hsddp_get_layout.argtypes = [C.c_void_p, IP, IP, IP, IP]
     L.hsddp_update_problem.argtypes = [C.c_void_p, IP, DP, DP, DP, DP]
     L.hsddp_extract_commands.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_void_p, C.c_int,

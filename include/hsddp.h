@@ -22,6 +22,7 @@
  *   hsddp_load_quad_reference                 QuadReference::load_top_level_data   QuadReference.cpp:129-290
  *   hsddp_plan_phases                         HKDProblem::initialization (segmentation) HKDProblem.cpp:15-68
  *   hsddp_set_reference_table / _build_references  HKDSinglePhaseReference::get_reference_at_t HKDReference.cpp:8-57
+ *   hsddp_advance / hsddp_get_phase_info      HKDProblem::update from the reference table   HKDProblem.cpp:117-222
  *   hsddp_shift / hsddp_update_problem        HKDProblem::update + HKDMPCSolver::update's re-solve
  *                                             setup (warm start reused)  HKDProblem.cpp:117-222; HKDMPC.cpp:96-143
  *   hsddp_extract_commands                    update_foot_placement + publish_mpc_cmd HKDMPC.cpp:207-298
@@ -240,6 +241,20 @@ int hsddp_get_layout(hsddp_handle h, int *n_phases, int *horizons, int *shooting
  * previous solution); resets X = Xbar, U = Ubar and the ReB / AL parameters (reset_params) */
 int hsddp_update_problem(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
                          const double *ref_u, const double *ref_foot);
+
+/* HKDProblem::update (HKDProblem.cpp:117-222) driven by the reference table, for handles whose
+ * references were built by hsddp_build_references: n_steps simulation steps of the window
+ * (QuadReference::step), each with the contact at the new horizon end deciding the phase growth
+ * (the batch must agree on it), the last phase's next contact at plan_duration + dt_mpc once it
+ * has reached its end (add_tconstr_one_phase), new phases' contact durations; then hsddp_shift,
+ * the new layout's references and hsddp_update_problem with these contacts and x0 [B][24].
+ * contact_change [n_steps] (may be NULL) receives the step flags.  The caller's whole MPC tick is
+ * hsddp_advance + hsddp_solve + hsddp_extract_commands (HKDMPCSolver::update, HKDMPC.cpp:96-165). */
+int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, float dt_mpc, const double *x0,
+                  int *contact_change);
+/* The handle's phase bookkeeping: contacts [B][P+1][4] (row P: the last phase's next contact) and,
+ * for references built from a table, the phases' contact durations [B][P][4] (either may be NULL). */
+int hsddp_get_phase_info(hsddp_handle h, int *contacts, double *durations);
 
 /* ---- MPC command extraction ------------------------------------------
  * Mirror of hkd_command_lcmt (lcmtypes/hkd_command_lcmt.lcm:1-11), field for field. */

@@ -14,6 +14,9 @@ the solve in heli-sudoo/HKD-MPC, used by tests/ to chec
   * plan_phases           HKDProblem::initialization's phase segmentation (HKD-TrajOpt/
                           HKDProblem.cpp:26-68) and the last phase's next contact
                           (add_tconstr_one_phase, :272-276), with the float clock of the reference.
+  * ProblemTracker        HKDProblem::update's phase bookkeeping (HKDProblem.cpp:117-222) from the
+                          reference table: window step, contact changes at the horizon end, new
+                          phases, touchdown next contacts, contact durations.
   * reference_slots       HKDSinglePhaseReference::get_reference_at_t (HKD-TrajOpt/
                           HKDReference.cpp:8-57) at t_offset + k dt for every state slot, t_offset
                           = phase_start_times[i] - phase_start_times[0] (HKDProblem.cpp:99,210) and
@@ -169,6 +172,67 @@ def plan_phases(window, dt_ref, plan_duration=0.6, dt_sim=0.01, dt_mpc=0.01):
         t = F32(t + dt_sim)
     plan["contacts"].append(contact(F32(plan_duration + dt_mpc)))
     return plan
+
+
+class ProblemTracker:
+    """The phase bookkeeping of HKDProblem::initialization (HKDProblem.cpp:15-111) and
+    HKDProblem::update (:117-222) for one element whose reference window starts at table[start]:
+    horizons, is_phase_reach_end (quirk A15: all false at initialization), phase contacts, contact
+    durations, and the next contact of the last phase's touchdown constraint / reset map
+    (add_tconstr_one_phase, :268-308: at initialization for every phase; in update only once the
+    last phase has reached its end; a phase added by update carries none — its own contact)."""
+
+    def __init__(self, table, start, dt_ref, plan_duration=0.6, dt_sim=0.01, dt_mpc=0.01):
+        self.table, self.start = table, start
+        self.dt, self.T, self.dt_sim, self.dt_mpc = F32(dt_ref), F32(plan_duration), F32(dt_sim), F32(dt_mpc)
+        self.sz = int(round(float(self.T) / float(self.dt))) + 1  # QuadReference::initialize
+        plan = plan_phases(table[start:start + self.sz + 1], dt_ref, plan_duration, dt_sim, dt_mpc)
+        self.horizons = list(plan["horizons"])
+        self.contacts = [tuple(c) for c in plan["contacts"][:-1]]
+        self.next = tuple(plan["contacts"][-1])
+        self.durations = [np.asarray(d) for d in plan["durations"]]
+        self.reach_end = [0] * len(self.horizons)
+        self.t_cur = F32(0)
+
+    def _sample(self, t):
+        k = min(self.start + sample_at(t, self.dt, self.sz), len(self.table) - 1)
+        return self.table[k]
+
+    def step(self):
+        """one simulation step; returns the contact-change flag"""
+        i = 1
+        while True:  # QuadReference::step: samples while i dt <= dt_sim (approx)
+            t = F32(F32(i) * self.dt)
+            if not (t < self.dt_sim or _approx_eq(t, self.dt_sim)):
+                break
+            self.t_cur = F32(self.t_cur + self.dt)
+            self.start += 1
+            i += 1
+        if self.horizons[0] <= 1:
+            for a in (self.horizons, self.reach_end, self.contacts, self.durations):
+                a.pop(0)
+        else:
+            self.horizons[0] -= 1
+        rel = F32(F32(self.t_cur + self.T) - self.t_cur)
+        q = self._sample(rel)
+        new = tuple(int(v) for v in q["contact"])
+        cc = new != self.contacts[-1]
+        if cc and self.reach_end[-1]:
+            self.horizons.append(1)
+            self.reach_end.append(0)
+            self.contacts.append(new)
+            self.durations.append(q["status_dur"].copy())
+            self.next = new
+        else:
+            self.horizons[-1] += 1
+            if cc:
+                self.reach_end[-1] = 1
+        if self.reach_end[-1]:
+            self.next = tuple(int(v) for v in self._sample(F32(self.T + self.dt_mpc))["contact"])
+        return int(cc)
+
+    def contact_rows(self):
+        return np.array(self.contacts + [self.next], np.int32)
 
 
 def reference_at(sample):

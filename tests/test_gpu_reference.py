@@ -121,48 +121,11 @@ def test_solve_from_file_matches_host_refs_and_oracle(name, start):
     b.close()
 
 
-class _FileScenario:
-    """HKDProblem::update's caller-side bookkeeping (HKDProblem.cpp:117-222) over a reference
-    file with dt_ref = dt_sim: the window advances one sample per step; the contact at the new
-    horizon end (relative time 0.6 -> sample 60 of the window) decides the phase growth."""
-
-    def __init__(self, ref, start, plan):
-        self.ref, self.start = ref, start
-        self.horizons = list(plan["horizons"])
-        self.contacts = [tuple(int(v) for v in c) for c in plan["contacts"][:-1]]
-        self.reach_end = [0] * len(self.horizons)
-        self.next_contact = tuple(int(v) for v in plan["contacts"][-1])
-        self.initial = True
-
-    def contact(self, k):
-        return tuple(int(v) for v in self.ref[min(self.start + k, len(self.ref) - 1)]["contact"])
-
-    def step(self):
-        self.start += 1
-        self.initial = False
-        if self.horizons[0] <= 1:
-            self.horizons.pop(0); self.contacts.pop(0); self.reach_end.pop(0)
-        else:
-            self.horizons[0] -= 1
-        new = self.contact(60)
-        cc = new != self.contacts[-1]
-        if cc and self.reach_end[-1]:
-            self.horizons.append(1); self.contacts.append(new); self.reach_end.append(0)
-        else:
-            self.horizons[-1] += 1
-            if cc:
-                self.reach_end[-1] = 1
-        return int(cc)
-
-    def contact_rows(self, B):
-        last = self.contact(61) if self.reach_end[-1] else self.contacts[-1]
-        return np.repeat(np.array([self.contacts + [last]], np.int32), B, axis=0)
-
-
 def test_mpc_loop_from_file():
-    """Initialise from the trot file, then 12 receding-horizon updates: shift on the device, build
-    the next window's references on the device, re-solve; a twin solver fed the oracle's references
-    from the host stays bit-identical, and the built references equal the oracle's every step."""
+    """Initialise from the trot file, then 12 receding-horizon updates driven step by step: shift on
+    the device, build the next window's references on the device, re-solve; a twin solver fed the
+    oracle's references from the host stays bit-identical, and the built references equal the
+    oracle's every step."""
     tab, ref, dt = _load("trot")
     B = 4
     p = hsddp.reference_problem(tab, dt, [0], _x0(B))
@@ -170,16 +133,17 @@ def test_mpc_loop_from_file():
     dev = hsddp.Solver(p, hsddp.load_settings(**kw))
     host = hsddp.Solver(_host_prob(p, ref, dt), hsddp.load_settings(**kw))
     dev.solve(); host.solve()
-    sc = _FileScenario(ref, 0, p["plan"])
+    tk = R.ProblemTracker(ref, 0, dt)
+    assert tk.horizons == p["horizons"]
     x0 = _x0(B, 9)
     for it in range(12):
-        flag = sc.step()
+        flag = tk.step()
         la = dev.shift([flag]); lb = host.shift([flag])
-        assert la == lb and la["horizons"] == sc.horizons, it
-        contacts = sc.contact_rows(B)
-        dev.build_references([sc.start], N_WIN, None, 0.01)
+        assert la == lb and la["horizons"] == tk.horizons and la["reach_end"] == tk.reach_end, it
+        contacts = np.repeat(tk.contact_rows()[None], B, axis=0)
+        dev.build_references([tk.start], N_WIN, None, 0.01)
         dev.update_problem(contacts, x0)
-        rx, ru, rf = _oracle_refs(ref, [sc.start], sc.horizons, dt)
+        rx, ru, rf = _oracle_refs(ref, [tk.start], tk.horizons, dt)
         assert np.array_equal(dev.references()["ref_x"], rx), it
         host.update_problem(contacts, x0, rx, ru, rf)
         dev.solve(); host.solve()
@@ -187,8 +151,56 @@ def test_mpc_loop_from_file():
         for f in ("Xbar", "Ubar", "K"):
             assert np.array_equal(ga[f], gb[f]), (it, f)
         assert np.all(np.isfinite(dev.element_info()["cost"]))
-    sc.step()
+    tk.step()
     dev.shift([0])
     with pytest.raises(hsddp.HSDDPError):
-        dev.update_problem(sc.contact_rows(B), x0)  # references of the old layout are not reused
+        dev.update_problem(np.repeat(tk.contact_rows()[None], B, axis=0), x0)  # old layout's references
+    dev.close(); host.close()
+
+
+@pytest.mark.parametrize("name,start,steps,n", [("trot", 0, 36, 1), ("flytrot", 6, 8, 2), ("flytrot", 3, 12, 3)])
+def test_advance_matches_tracker(name, start, steps, n):
+    """hsddp_advance (HKDProblem::update from the table, the whole MPC tick's input side in one
+    call) against the oracle's ProblemTracker: step flags, layout, phase contacts (row P: the
+    touchdown target), contact durations and references equal; the re-solves bit-identical to a
+    twin driven through hsddp_shift / hsddp_update_problem with the oracle's inputs."""
+    tab, ref, dt = _load(name)
+    B = 3
+    p = hsddp.reference_problem(tab, dt, [start], _x0(B))
+    kw = dict(max_AL_iter=2, max_DDP_iter=1)
+    dev = hsddp.Solver(p, hsddp.load_settings(**kw))
+    host = hsddp.Solver(_host_prob(p, ref, dt), hsddp.load_settings(**kw))
+    tk = R.ProblemTracker(ref, start, dt)
+    info = dev.phase_info()
+    assert np.array_equal(info["contacts"][0], tk.contact_rows())
+    assert np.array_equal(info["durations"][0], np.array(tk.durations))
+    dev.solve(); host.solve()
+    rng = np.random.default_rng(5)
+    n_new = 0
+    for it in range(steps // n):
+        x0 = _x0(B, 100 + it)
+        flags = dev.advance(x0, n)
+        want = [tk.step() for _ in range(n)]
+        assert flags == want, it
+        lay = dev.layout()
+        assert lay["horizons"] == tk.horizons and lay["reach_end"] == tk.reach_end, it
+        n_new += sum(flags)
+        info = dev.phase_info()
+        rows = tk.contact_rows()
+        for b in range(B):
+            assert np.array_equal(info["contacts"][b], rows), it
+            assert np.array_equal(info["durations"][b], np.array(tk.durations)), it
+        rx, ru, rf = _oracle_refs(ref, [tk.start], tk.horizons, dt)
+        got = dev.references()
+        assert np.array_equal(got["ref_x"], rx) and np.array_equal(got["ref_u"], ru), it
+        host.shift(want)
+        host.update_problem(np.repeat(rows[None], B, axis=0), x0, rx, ru, rf)
+        dev.solve(); host.solve()
+        ga, gb = dev.trajectory(), host.trajectory()
+        for f in ("Xbar", "Ubar", "K"):
+            assert np.array_equal(ga[f], gb[f]), (it, f)
+        if it % 4 == 0:  # the commands of the tick, durations from the handle's bookkeeping
+            cmd = dev.extract_commands(1, 0.01 * it, 0.01, info["durations"], rng.standard_normal(12).astype(np.float32))
+            assert np.all(cmd["N_mpcsteps"] == 8)
+    assert n_new >= 2  # the window crossed contact switches
     dev.close(); host.close()

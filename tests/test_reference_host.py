@@ -145,3 +145,21 @@ def test_reference_problem_host_side():
     assert p["contacts"].shape == (3, len(p["horizons"]) + 1, 4)
     with pytest.raises(hsddp.HSDDPError):  # per-element windows whose layouts differ
         hsddp.reference_problem(tab, 0.01, [0, 1, 2], x0)
+
+
+def test_tracker_invariants():
+    """oracle ProblemTracker (HKDProblem::update bookkeeping): the horizon keeps 60 control knots,
+    phase lists stay aligned, adjacent phases differ in contact, and the 11-knot stance phase the
+    trot window opens with is gone after 11 steps."""
+    ref, dt = R.load_quad_reference(path("trot"))
+    tk = R.ProblemTracker(ref, 0, dt)
+    first = tk.contacts[0]
+    n_flags = 0
+    for j in range(38):
+        n_flags += tk.step()
+        assert sum(tk.horizons) == 60
+        assert len(tk.horizons) == len(tk.contacts) == len(tk.durations) == len(tk.reach_end) <= 16
+        assert all(a != b for a, b in zip(tk.contacts, tk.contacts[1:]))
+        if j == 10:
+            assert tk.contacts[0] != first
+    assert n_flags >= 2 and tk.start == 38
