@@ -216,6 +216,7 @@ struct hsddp_handle_t {
     int Bref = 1;
     bool have_problem = false;
     std::vector<int> contacts;  // host copy [B][P+1][4]: maps the compact K rows to controls
+    bool contacts_current = false;  // `contacts` belong to the current layout (not stale after a shift)
     void *scratch = nullptr;    // device staging for the MPC-side calls (grown on demand)
     size_t scratch_bytes = 0;
     // receding-horizon state (HKDProblemData, HKDProblem.h:20-66): is_phase_reach_end per phase,
@@ -416,7 +417,7 @@ static int h2d(void *dst, const void *src, size_t bytes, hipStream_t st)
 static int upload_inputs(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
                          const double *ref_u, const double *ref_foot)
 {
-    if (!h || !contacts || !x0) return fail(HSDDP_ERR_ARG, "null argument");
+    if (!h || !x0) return fail(HSDDP_ERR_ARG, "null argument");
     const bool keep_refs = !ref_x && !ref_u && !ref_foot;
     if (!keep_refs && (!ref_x || !ref_u || !ref_foot)) return fail(HSDDP_ERR_ARG, "references: all three or none");
     if (keep_refs && !h->refs_on_device)
@@ -424,6 +425,13 @@ static int upload_inputs(hsddp_handle h, const int *contacts, const double *x0, 
     HIPCHK(hipSetDevice(h->desc.device));
     const Params &p = h->p;
     const size_t B = p.B, S = p.S, P = p.P, Br = h->Bref;
+    // contacts NULL: the handle's own (those hsddp_advance derived for this layout)
+    const std::vector<int> own = contacts ? std::vector<int>() : h->contacts;
+    if (!contacts) {
+        if (!h->contacts_current || own.size() != B * (P + 1) * 4)
+            return fail(HSDDP_ERR_ARG, "no contacts of this layout on the handle");
+        contacts = own.data();
+    }
     for (size_t q = 0; q < B * (P + 1) * 4; ++q)
         if (contacts[q] != 0 && contacts[q] != 1) return fail(HSDDP_ERR_ARG, "contacts must be 0/1");
     int rc;
@@ -437,6 +445,7 @@ static int upload_inputs(hsddp_handle h, const int *contacts, const double *x0, 
         return rc;
     if (!keep_refs) h->refs_on_device = false;
     h->contacts.assign(contacts, contacts + B * (P + 1) * 4);
+    h->contacts_current = true;
     return HSDDP_OK;
 }
 
@@ -1071,6 +1080,7 @@ extern "C" int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_chang
     for (int i = 0; i < P; ++i) h->desc.horizons[i] = p.N[i];
     h->need_inputs = true;
     h->refs_on_device = false;  // built for the old layout
+    h->contacts_current = false;
     return HSDDP_OK;
 }
 
@@ -1204,8 +1214,9 @@ static int build_refs(hsddp_handle h, const int *window_start, int window_len, c
 extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, float dt_mpc, const double *x0,
                              int *contact_change)
 {
-    if (!h || !x0) return fail(HSDDP_ERR_ARG, "null argument");
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
+    if (h->need_inputs) return fail(HSDDP_ERR_ARG, "the previous shift awaits hsddp_update_problem");
     if (h->win_start.empty() || h->table_host.empty())
         return fail(HSDDP_ERR_ARG, "references not built from a table (hsddp_build_references)");
     if (n_steps < 0) return fail(HSDDP_ERR_ARG, "n_steps must be >= 0");
@@ -1303,7 +1314,12 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
         for (int i = 0; i < P; ++i)
             for (int l = 0; l < 4; ++l) dur[((size_t)b * P + i) * 4 + l] = du[b][i][l];
     }
-    if ((rc = hsddp_update_problem(h, contacts.data(), x0, nullptr, nullptr, nullptr))) return rc;
+    if (x0) {
+        if ((rc = hsddp_update_problem(h, contacts.data(), x0, nullptr, nullptr, nullptr))) return rc;
+    } else {  // x0 follows from the new first phase's contact: hsddp_update_problem(h, NULL, x0, NULL...)
+        h->contacts.swap(contacts);
+        h->contacts_current = true;
+    }
     h->durations.swap(dur);
     h->t_cur = t_cur;
     if (contact_change) std::copy(flags.begin(), flags.end(), contact_change);

@@ -93,7 +93,8 @@ def reference_problem(table: np.ndarray, dt_ref: float, window_start, x0: np.nda
     if contacts.shape[0] == 1 and B > 1:
         contacts = np.repeat(contacts, B, axis=0)
     S, Kc = sum(n + 1 for n in hz), sum(hz)
-    return {"batch": B, "horizons": hz, "S": S, "Kc": Kc, "dt": dt_sim, "x0": x0, "contacts": contacts,
+    # dt: HKDProblem's float dt_sim widened to double by Trajectory(dt_sim, N) (HKDProblem.cpp:81)
+    return {"batch": B, "horizons": hz, "S": S, "Kc": Kc, "dt": float(np.float32(dt_sim)), "x0": x0, "contacts": contacts,
             "shooting": [n + 1 for n in hz], "ref_table": table, "dt_ref": dt_ref, "window_start": ws,
             "window_len": n_win, "phase_start_times": plans[0]["start_times"], "plan": plans[0]}
 
@@ -255,18 +256,20 @@ class Solver:
     def update_problem(self, contacts, x0, ref_x=None, ref_u=None, ref_foot=None) -> None:
         """Inputs of the current layout, keeping the warm start (hsddp_update_problem).  References
         None: keep the ones hsddp_build_references made on the device for this layout."""
-        self._contacts = np.ascontiguousarray(contacts, dtype=np.int32)
+        self._contacts = None if contacts is None else np.ascontiguousarray(contacts, dtype=np.int32)
         refs = [None if r is None else np.ascontiguousarray(r, dtype=np.float64) for r in (ref_x, ref_u, ref_foot)]
-        check(lib().hsddp_update_problem(self._h, ip(self._contacts), dp(np.ascontiguousarray(x0, dtype=np.float64)),
+        check(lib().hsddp_update_problem(self._h, None if contacts is None else ip(self._contacts),
+                                         dp(np.ascontiguousarray(x0, dtype=np.float64)),
                                          *(None if r is None else dp(r) for r in refs)))
 
-    def advance(self, x0, n_steps: int = 1, plan_duration: float = 0.6, dt_mpc: float = 0.01) -> list:
+    def advance(self, x0=None, n_steps: int = 1, plan_duration: float = 0.6, dt_mpc: float = 0.01) -> list:
         """HKDProblem::update from the reference table (hsddp_advance): the window moves n_steps
         simulation steps, the layout, warm start, references and contacts follow, x0 [B][24] is the
-        new initial state.  Returns the contact-change flag of every step."""
+        new initial state (None: call update_problem(None, x0) next, e.g. with x0 formed from the
+        new first phase's contact).  Returns the contact-change flag of every step."""
         flags = np.zeros(max(1, n_steps), np.int32)
         check(lib().hsddp_advance(self._h, int(n_steps), float(plan_duration), float(dt_mpc),
-                                  dp(np.ascontiguousarray(x0, dtype=np.float64)), ip(flags)))
+                                  None if x0 is None else dp(np.ascontiguousarray(x0, dtype=np.float64)), ip(flags)))
         lay = self.layout()
         self.P = len(lay["horizons"])
         self.S = sum(n + 1 for n in lay["horizons"])

@@ -248,7 +248,10 @@ int hsddp_update_problem(hsddp_handle h, const int *contacts, const double *x0, 
  * (the batch must agree on it), the last phase's next contact at plan_duration + dt_mpc once it
  * has reached its end (add_tconstr_one_phase), new phases' contact durations; then hsddp_shift,
  * the new layout's references and hsddp_update_problem with these contacts and x0 [B][24].
- * contact_change [n_steps] (may be NULL) receives the step flags.  The caller's whole MPC tick is
+ * contact_change [n_steps] (may be NULL) receives the step flags.  x0 NULL: the inputs are left
+ * pending — read the new first phase's contact (hsddp_get_phase_info), form x0 from it
+ * (compute_hkd_state, HKDMPC.cpp:132-134) and call hsddp_update_problem(h, NULL, x0, NULL, NULL,
+ * NULL), where NULL contacts are the ones derived here.  The caller's whole MPC tick is
  * hsddp_advance + hsddp_solve + hsddp_extract_commands (HKDMPCSolver::update, HKDMPC.cpp:96-165). */
 int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, float dt_mpc, const double *x0,
                   int *contact_change);

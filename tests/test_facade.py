@@ -68,3 +68,76 @@ def test_facade_solve_matches_ctypes_path(tmp_path, gait, P, N):
     assert float(cost) == info["cost"][0]
     assert (int(iters), int(outer), int(status), int(nls)) == (
         info["iters"][0], info["outer_iters"][0], info["status"][0], info["n_ls_trials"][0])
+
+
+def _message(t, b):
+    """hkd_mpc_example's robot-state message of robot b at tick t (float32 arithmetic, same order)."""
+    f = np.float32
+    ft, fb = f(t), f(b)
+    p = np.array([f(0.001) * ft + f(0.002) * fb, f(0.0005) * fb, f(0.25)], np.float32)
+    v = np.array([0.1, 0, 0], np.float32)
+    rpy = np.array([f(0.002) * fb, f(0.001) * ft, 0], np.float32)
+    om = np.array([0, 0, f(0.01) * fb], np.float32)
+    dq = f(0.001) * f(t % 5)
+    qJ = np.array([[dq, f(-0.8) + dq, f(1.6) - dq]] * 4, np.float32).reshape(12)
+    pf = np.zeros(12, np.float32)
+    for leg in range(4):
+        pf[3 * leg] = (f(0.2) if leg < 2 else f(-0.2)) + f(0.001) * ft
+        pf[3 * leg + 1] = f(0.14) if leg % 2 else f(-0.14)
+    return p, v, rpy, om, qJ, pf
+
+
+def _hkd_state(hsddp, x, contact):
+    """compute_hkd_state (HKDModel.h:65-96): stance legs' qdummy = foot position (device FK)."""
+    B = x.shape[0]
+    xs = np.repeat(x, 4, axis=0)
+    pos = hsddp.model.foot_position(xs, np.tile(np.arange(4), B)).reshape(B, 4, 3)
+    out = x.copy()
+    for b in range(B):
+        for leg in range(4):
+            if contact[b][leg]:
+                out[b, 12 + 3 * leg:15 + 3 * leg] = pos[b, leg]
+    return out
+
+
+@pytest.mark.gpu
+def test_mpc_example_matches_python(tmp_path):
+    """The C++ HKDMPCSolver (hkd_mpc.hpp: initialize, mpcdata_lcm_handler -> update on the worker
+    thread, publish) against the same MPC loop written with the Python mirror (reference_problem,
+    advance, update_problem, solve, extract_commands): every command field of every tick equal
+    bit for bit (solve_time excepted: a wall-clock reading)."""
+    import hsddp
+    _make()
+    B, ticks = 3, 14
+    ref_csv = os.path.join(ROOT, "tests", "golden", "ref_trot.csv")
+    info_file = os.path.join(PKG, "settings", "ddp_setting.info")
+    r = subprocess.run([os.path.join(PKG, "hkd_mpc_example"), ref_csv, info_file, str(tmp_path), str(B), str(ticks)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(os.path.join(tmp_path, "commands.bin"), dtype=hsddp.MPC_COMMAND).reshape(ticks, B)
+
+    tab, dt = hsddp.load_quad_reference(ref_csv)
+    x0 = np.zeros((B, 24)); x0[:, 5] = 0.2486
+    x0[:, 12:] = np.tile([0.0, -0.8, 1.6], 4)
+    p = hsddp.reference_problem(tab, dt, [0], x0)
+    p["x0"] = _hkd_state(hsddp, x0, p["contacts"][:, 0])
+    s = hsddp.Solver(p, hsddp.load_settings(info_file))
+    s.solve()
+    dt_mpc = float(np.float32(0.01))
+    for t in range(1, ticks + 1):
+        s.set_options(hsddp.load_settings(info_file, max_AL_iter=2, max_DDP_iter=1))
+        s.advance(None, 1, 0.6, dt_mpc)
+        info = s.phase_info()
+        xs = np.zeros((B, 24)); pfs = np.zeros((B, 12), np.float32)
+        for b in range(B):
+            pp, v, rpy, om, qJ, pf = _message(t, b)
+            xs[b, 0:3] = rpy[::-1]; xs[b, 3:6] = pp; xs[b, 6:9] = om; xs[b, 9:12] = v; xs[b, 12:] = qJ
+            pfs[b] = pf
+        s.update_problem(None, _hkd_state(hsddp, xs, info["contacts"][:, 0]))
+        s.solve()
+        cmd = s.extract_commands(1, 0.01 * t, dt_mpc, info["durations"], pfs, 0.0)
+        for b in range(B):
+            for f in ("N_mpcsteps", "mpc_times", "hkd_controls", "des_body_state", "contacts", "statusTimes",
+                      "foot_placement", "feedback"):
+                assert np.array_equal(got[t - 1][b][f], cmd[b][f]), (t, b, f)
+    s.close()
