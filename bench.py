@@ -62,7 +62,7 @@ def cpu_baseline(args):
     n = float(np.sum(r["iters"]))
     return {"value": n / dt, "unit": UNIT, "cores": threads, "kind": "port",
             "sample": f"oracle/hsddp_oracle.c, {args.cpu_elements} elements x {args.cpu_iters} inner iterations "
-                      f"(+ initial rollout), same trot 4x50 workload, {threads} threads, {dt:.1f} s wall"}
+                      f"(+ initial rollout), same {args.gait} {args.phases}x{args.knots} workload, {threads} threads, {dt:.1f} s wall"}
 
 
 def main():
@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--phases", type=int, default=4)
     ap.add_argument("--knots", type=int, default=50)
     ap.add_argument("--gait", default="trot")
+    ap.add_argument("--mixed", action="store_true",
+                    help="config C4: per-element gait drawn from {trot, pace, bound, pronk} (per-element references)")
     ap.add_argument("--cpu-elements", type=int, default=2048)
     ap.add_argument("--cpu-iters", type=int, default=10)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -95,7 +97,7 @@ def main():
             dist.barrier()
 
     B = args.batch
-    prob = synthetic.make_batch(B, args.phases, args.knots, args.gait, first_element=rank * B)
+    prob = synthetic.make_batch(B, args.phases, args.knots, args.gait, mixed=args.mixed, first_element=rank * B)
     opt = hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=args.warmup + args.steps)
     solver = hsddp.Solver(prob, opt, device=local, riccati_fp32=args.riccati_fp32)
     solver.begin()
@@ -132,18 +134,22 @@ def main():
         # fp32 mode (C5) halves every term of the per-knot bytes
         bytes_launch = BWD_BYTES_PER_KNOT * Kc * B // (2 if args.riccati_fp32 else 1)
         achieved = bytes_launch / (avg_bwd_ms * 1e-3) / 1e9
-        cfg_key = f"{args.gait}_{args.phases}x{args.knots}_b{B}" + ("_fp32" if args.riccati_fp32 else "")
+        gait = "mixed" if args.mixed else args.gait
+        metric_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 4096)
+        label = ("config C5: fp32 Riccati" if args.riccati_fp32 else "BASELINE metric config" if metric_cfg
+                 else "config C3: jump with resets" if gait == "jump" else "config C4 shard: mixed gaits" if args.mixed
+                 else "custom")
+        cfg_key = f"{gait}_{args.phases}x{args.knots}_b{B}" + ("_fp32" if args.riccati_fp32 else "")
         traffic = load_traffic(cfg_key)
         out = {
             "metric": METRIC, "value": total_iters / elapsed, "unit": UNIT, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32 Riccati / f64 rollout" if args.riccati_fp32 else "f64",
-            "data": "synthetic: seeded random initial states (splitmix64), closed-form trot reference "
+            "data": f"synthetic: seeded random initial states (splitmix64), closed-form {gait} reference "
                     "(SURVEY.md §8d); no dataset or checkpoint",
-            "config": {"workload": f"HKD {args.gait}, {args.phases} phases x {args.knots} knots, "
-                                   f"batch={B} per GPU " + ("(config C5: fp32 Riccati)" if args.riccati_fp32
-                                                            else "(BASELINE metric config)"),
+            "config": {"workload": f"HKD {gait}, {args.phases} phases x {args.knots} knots, "
+                                   f"batch={B} per GPU ({label})",
                        "global_batch": B * world, "batch_per_gpu": B, "phases": args.phases,
                        "knots_per_phase": args.knots, "nx": 24, "nu": 24, "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_riccati", "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -158,7 +164,7 @@ def main():
                                              "forward_ls": st.ms_forward / args.steps},
                       "all_costs_finite": finite, "device_bytes": solver.device_bytes()},
         }
-        if world == 1 and not args.no_cpu_baseline and not args.riccati_fp32:
+        if world == 1 and not args.no_cpu_baseline and not args.riccati_fp32 and not args.mixed:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     solver.close()
