@@ -5,13 +5,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <array>
 #include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <deque>
 #include <fstream>
 #include <map>
 #include <sstream>
@@ -1226,29 +1224,23 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     auto leq = [](float a, float b) { return a < b || std::abs(a - b) <= 1e-6f; };
     int adv = 0;  // samples per simulation step
     for (int i = 1; leq(i * dt, dts); ++i) adv++;
-    // per element: phase contacts, the last phase's next contact (row P), phase durations
-    typedef std::array<int, 4> C4;
-    typedef std::array<double, 4> D4;
-    std::vector<std::deque<C4>> pc(B);
-    std::vector<std::deque<D4>> du(B);
-    std::vector<C4> next(B);
-    for (int b = 0; b < B; ++b) {
-        for (int i = 0; i <= p.P; ++i) {
-            C4 c;
-            for (int l = 0; l < 4; ++l) c[l] = h->contacts[((size_t)b * (p.P + 1) + i) * 4 + l];
-            if (i < p.P) pc[b].push_back(c); else next[b] = c;
-        }
-        for (int i = 0; i < p.P; ++i) {
-            D4 v;
-            for (int l = 0; l < 4; ++l) v[l] = h->durations[((size_t)b * p.P + i) * 4 + l];
-            du[b].push_back(v);
-        }
-    }
-    std::vector<int> hz(p.N, p.N + p.P), reach(h->reach_end), ws(h->win_start), flags(n_steps);
+    // The edits are the same for every element (the layout is shared), so they are tracked once as
+    // a source per phase: an old phase (index >= 0) or the sample a new phase starts from (step
+    // j: -1 - j); the next-contact row likewise.  Per-element values are read at the end.
+    const int P0 = p.P;
+    std::vector<int> hz(p.N, p.N + p.P), reach(h->reach_end), ws(h->win_start), flags(n_steps), src(P0);
+    for (int i = 0; i < P0; ++i) src[i] = i;
+    std::vector<std::vector<int>> wsj(n_steps);  // window starts at each step
+    std::vector<float> relj(n_steps);            // new_end - new_start at each step
+    int next_kind = 0, next_step = -1;           // row P: 0 old row, 1 contact at relj, 2 at plan + dt_mpc
     float t_cur = h->t_cur;
-    auto sample = [&](int b, float t) -> const hsddp_quad_state & {
-        const int k = ws[Br == 1 ? 0 : b] + ref_sample(t, dt, sz);
+    auto sample_w = [&](const std::vector<int> &w, int b, float t) -> const hsddp_quad_state & {
+        const int k = w[Br == 1 ? 0 : b] + ref_sample(t, dt, sz);
         return h->table_host[std::min(k, h->ref_n - 1)];
+    };
+    auto phase_contact = [&](int sc, int b, int l) {
+        return sc >= 0 ? h->contacts[((size_t)b * (P0 + 1) + sc) * 4 + l]
+                       : sample_w(wsj[-1 - sc], b, relj[-1 - sc]).contact[l];
     };
     for (int j = 0; j < n_steps; ++j) {
         for (int a = 0; a < adv; ++a) {
@@ -1257,21 +1249,21 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
         }
         for (int &w : ws)
             if (w >= h->ref_n) return fail(HSDDP_ERR_ARG, "the reference window ran past the table");
+        wsj[j] = ws;
         if (hz.front() <= 1) {  // pop_front_phase (HKDProblem.h:56-66)
             if (hz.size() == 1) return fail(HSDDP_ERR_ARG, "advance would remove the only phase");
             hz.erase(hz.begin());
             reach.erase(reach.begin());
-            for (int b = 0; b < B; ++b) { pc[b].pop_front(); du[b].pop_front(); }
+            src.erase(src.begin());
         } else {
             hz.front()--;
         }
-        const float rel = (t_cur + plan_duration) - t_cur;  // new_end_time - new_start_time
+        relj[j] = (t_cur + plan_duration) - t_cur;  // new_end_time - new_start_time
         int cc = -1;
-        std::vector<C4> nc(B);
         for (int b = 0; b < B; ++b) {
-            const hsddp_quad_state &q = sample(b, rel);
-            std::copy(q.contact, q.contact + 4, nc[b].begin());
-            const int cb = nc[b] != pc[b].back();
+            const int *nc = sample_w(ws, b, relj[j]).contact;
+            int cb = 0;
+            for (int l = 0; l < 4; ++l) cb |= nc[l] != phase_contact(src.back(), b, l);
             if (cc >= 0 && cb != cc)
                 return fail(HSDDP_ERR_UNSUPPORTED, "elements disagree on a contact change (the layout is shared)");
             cc = cb;
@@ -1280,23 +1272,14 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
             if ((int)hz.size() >= HSDDP_MAX_PHASES) return fail(HSDDP_ERR_ARG, "advance exceeds HSDDP_MAX_PHASES phases");
             hz.push_back(1);
             reach.push_back(0);
-            for (int b = 0; b < B; ++b) {
-                const hsddp_quad_state &q = sample(b, rel);
-                pc[b].push_back(nc[b]);
-                D4 v;
-                std::copy(q.status_dur, q.status_dur + 4, v.begin());
-                du[b].push_back(v);
-                next[b] = nc[b];  // a new phase carries no terminal constraint (identity reset)
-            }
+            src.push_back(-1 - j);
+            next_kind = 1;  // a new phase carries no terminal constraint (identity reset)
+            next_step = j;
         } else {
             hz.back()++;
             if (cc) reach.back() = 1;
         }
-        if (reach.back())
-            for (int b = 0; b < B; ++b) {
-                const hsddp_quad_state &q = sample(b, plan_duration + dt_mpc);
-                std::copy(q.contact, q.contact + 4, next[b].begin());
-            }
+        if (reach.back()) { next_kind = 2; next_step = j; }
         flags[j] = cc;
     }
     int rc;
@@ -1308,11 +1291,20 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     std::vector<int> contacts((size_t)B * (P + 1) * 4);
     std::vector<double> dur((size_t)B * P * 4);
     for (int b = 0; b < B; ++b) {
-        for (int i = 0; i <= P; ++i)
-            for (int l = 0; l < 4; ++l)
-                contacts[((size_t)b * (P + 1) + i) * 4 + l] = i < P ? pc[b][i][l] : next[b][l];
-        for (int i = 0; i < P; ++i)
-            for (int l = 0; l < 4; ++l) dur[((size_t)b * P + i) * 4 + l] = du[b][i][l];
+        for (int i = 0; i < P; ++i) {
+            const int sc = src[i];
+            const double *dv = sc >= 0 ? &h->durations[((size_t)b * P0 + sc) * 4]
+                                       : sample_w(wsj[-1 - sc], b, relj[-1 - sc]).status_dur;
+            for (int l = 0; l < 4; ++l) {
+                contacts[((size_t)b * (P + 1) + i) * 4 + l] = phase_contact(sc, b, l);
+                dur[((size_t)b * P + i) * 4 + l] = dv[l];
+            }
+        }
+        for (int l = 0; l < 4; ++l)
+            contacts[((size_t)b * (P + 1) + P) * 4 + l] =
+                next_kind == 0 ? h->contacts[((size_t)b * (P0 + 1) + P0) * 4 + l]
+                : next_kind == 1 ? sample_w(wsj[next_step], b, relj[next_step]).contact[l]
+                                 : sample_w(wsj[next_step], b, plan_duration + dt_mpc).contact[l];
     }
     if (x0) {
         if ((rc = hsddp_update_problem(h, contacts.data(), x0, nullptr, nullptr, nullptr))) return rc;

@@ -73,39 +73,48 @@ __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdA
     }
 }
 
-// One thread per 2 doubles of the new Xbar / Ubar rows and compact K rows of every element.
+// One thread per 16 bytes (two doubles / four floats, never straddling a row: NX and KCW are
+// multiples of 4) of the new Xbar / Ubar rows and compact K rows of every element; gathered reads,
+// contiguous writes.
 template <typename KT>
 __global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, const double *Xbar, const double *X,
                                                       const double *Ubar, const KT *K, double *Xn, double *Un, KT *Kn)
 {
-    const long nx = (long)a.S_new * NX, nu = (long)a.Kc * NX, nk = (long)a.Kc * KCW, per = nx + nu + nk;
+    constexpr int KV = 16 / sizeof(KT);  // K values per thread
+    const long nx = (long)a.S_new * NX / 2, nu = (long)a.Kc * NX / 2, nk = (long)a.Kc * KCW / KV, per = nx + nu + nk;
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long)B * per) return;
     const long b = gid / per;
     long e = gid % per;
     if (e < nx) {
-        const int s = (int)(e / NX), j = (int)(e % NX), lab = a.smap[s];
-        double v = 0.0;
-        if (lab >= 0) v = Xbar[(b * a.S_old + lab) * NX + j];
-        else if (lab <= -2) v = X[(b * a.S_old + (-2 - lab)) * NX + j];
-        Xn[b * nx + e] = v;
+        const int s = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = a.smap[s];
+        double2 v = {0.0, 0.0};
+        if (lab >= 0) v = *(const double2 *)&Xbar[(b * a.S_old + lab) * NX + j];
+        else if (lab <= -2) v = *(const double2 *)&X[(b * a.S_old + (-2 - lab)) * NX + j];
+        *(double2 *)&Xn[(b * nx + e) * 2] = v;
         return;
     }
     e -= nx;
     if (e < nu) {
-        const int k = (int)(e / NX), j = (int)(e % NX), lab = a.cmap[k];
-        Un[b * nu + e] = (lab >= 0 && !(a.zero_u0 && k == 0)) ? Ubar[(b * a.Kc + lab) * NX + j] : 0.0;
+        const int k = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = a.cmap[k];
+        double2 v = {0.0, 0.0};
+        if (lab >= 0 && !(a.zero_u0 && k == 0)) v = *(const double2 *)&Ubar[(b * a.Kc + lab) * NX + j];
+        *(double2 *)&Un[(b * nu + e) * 2] = v;
         return;
     }
     e -= nu;
-    const int k = (int)(e / KCW), j = (int)(e % KCW), lab = a.cmap[k];
-    Kn[b * nk + e] = lab >= 0 ? K[((long)b * a.Kc + lab) * KCW + j] : (KT)0;
+    const int k = (int)(KV * e / KCW), j = (int)(KV * e % KCW), lab = a.cmap[k];
+    float4 v = {0.f, 0.f, 0.f, 0.f};
+    if (lab >= 0) v = *(const float4 *)&K[((long)b * a.Kc + lab) * KCW + j];
+    *(float4 *)&Kn[(b * nk + e) * KV] = v;
 }
 
 void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, double *Xbar_new, double *Ubar_new, void *K_new,
                          hipStream_t st)
 {
-    const long n = (long)B * ((long)a.S_new * NX + (long)a.Kc * NX + (long)a.Kc * KCW);
+    static_assert(NX % 4 == 0 && KCW % 4 == 0, "16-byte pieces within rows");
+    const int KV = a.fp32 ? 4 : 2;
+    const long n = (long)B * ((long)a.S_new * NX / 2 + (long)a.Kc * NX / 2 + (long)a.Kc * KCW / KV);
     const dim3 g((unsigned)((n + 255) / 256));
     if (a.fp32)
         hipLaunchKernelGGL(k_shift_gather<float>, g, dim3(256), 0, st, B, a, d.Xbar, d.X, d.Ubar, d.K32, Xbar_new,
