@@ -1,0 +1,57 @@
+"""Sharded HIP solve: two ranks, each solving its disjoint shard of one
+global batch on the GPU, gathered to rank 0, equal bit for bit to one process solving the whole
+batch — per-element results do not depend on which elements share a launch.  Both ranks run on
+the box's one GPU (gloo carries the host-side gather); bench.py runs the same sharding with one GPU
+per rank and RCCL."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import hsddp
+from hsddp import synthetic as syn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from gpu_shard_worker import OPTS  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_gpu_shards_equal_single_process(tmp_path):
+    world, B = 2, 24
+    port = _free_port()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "gpu_shard_worker.py"), str(r), str(world),
+                               str(port), str(B), str(tmp_path)], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=150)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o
+    full = syn.make_batch(world * B, 4, 20, "trot", mixed=True)
+    s = hsddp.Solver(full, hsddp.load_settings(**OPTS))
+    s.solve()
+    info, tr = s.element_info(), s.trajectory()
+    s.close()
+    ref = np.stack([info["cost"], info["feas"], info["max_tconstr"], info["max_pconstr"]], 1)
+    assert np.array_equal(np.load(tmp_path / "summ.npy"), ref)
+    assert np.array_equal(np.load(tmp_path / "xbar.npy"), tr["Xbar"])
