@@ -238,6 +238,7 @@ struct hsddp_handle_t {
     int win_len = 0;
     float dt_sim = 0, t_cur = 0;
     std::vector<double> durations;
+    int retry_cap_alloc = 0, retry_m_alloc = 0;  // parallel regularisation retry scratch (k_riccati_retry)
 };
 
 // device staging area of at least `bytes` (contents not preserved when it grows)
@@ -307,6 +308,19 @@ static void fill_params(hsddp_handle h)
     // (delta, eps) at its initial value (ConstraintsBase.h:168-183): the kernels then read the two
     // scalars instead of the per-knot arrays.
     p.reb_uniform = o.update_ReB == 1.0 && o.update_relax == 1.0 && p.grf_delta >= p.grf_delta_min;
+    // attempts of backward_sweep_regularized after the first, at most (from mu = 0: 1e-3, then
+    // x update_regularization while <= 1e2); the parallel retry holds that many per deferred element
+    int M = 0;
+    if (o.update_regularization > 1) {
+        double mu = 0;
+        for (;;) {
+            mu = std::fmax(mu * o.update_regularization, 1e-03);
+            if (mu > 1e2) break;
+            if (++M > 64) { M = 0; break; }
+        }
+    }
+    p.retry_m = M;
+    p.retry_cap = (M > 0 && M <= h->retry_m_alloc) ? h->retry_cap_alloc : 0;
 }
 
 extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
@@ -365,6 +379,24 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         return rc;
     }
     d.contacts = contacts; d.x0 = x0; d.ref_x = rx; d.ref_u = ru; d.ref_foot = rf;
+    {   // parallel regularisation retries: up to 128 deferred elements per launch, p.retry_m attempts each
+        // (HSDDP_SEQUENTIAL_RETRY=1 keeps every retry inside k_riccati: a diagnostic for tests)
+        const char *seq = std::getenv("HSDDP_SEQUENTIAL_RETRY");
+        const size_t cap = std::min<size_t>(128, B), M = (seq && seq[0] == '1') ? 0 : p.retry_m, n = cap * M;
+        if (M > 0) {
+            void *rk;
+            if ((rc = dalloc(h, d.retry_list, cap)) || (rc = dalloc(h, d.retry_count, 1)) ||
+                (rc = dalloc(h, d.retry_flag, n)) || (rc = dalloc(h, d.retry_dU, n * Kc * NX)) ||
+                (rc = p.fp32 ? dalloc(h, (float *&)rk, n * Kc * KCW) : dalloc(h, (double *&)rk, n * Kc * KCW))) {
+                hsddp_destroy(h);
+                return rc;
+            }
+            d.retry_K = rk;
+            h->retry_cap_alloc = (int)cap;
+            h->retry_m_alloc = (int)M;
+            fill_params(h);
+        }
+    }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void **)&h->host_counter, 4 * sizeof(int), 0) != hipSuccess) {
         hsddp_destroy(h);

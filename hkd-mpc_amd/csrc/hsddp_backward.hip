@@ -456,7 +456,7 @@ DEV real half_sum(real v)
 // reference's 24-control solve reduces to a 12 x 12 one plus 12 divisions.
 template <typename real>
 DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem<real> &S, const PhaseConst<real> &pc, size_t b, int s, int kc,
-                  real reg, bool pre, bool more, bool &live, real &g, real &dV1, real &dV2)
+                  real *Kout, double *dUout, real reg, bool pre, bool more, bool &live, real &g, real &dV1, real &dV2)
 {
     // opaque per knot: keeps LICM from hoisting lane-dependent constants of the knot body
     // (regularised diagonals, lxx entries) out of the knot loop into long-lived VGPRs
@@ -686,7 +686,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem<real> &S, const PhaseC
 #pragma unroll
         for (int q = 0; q < HC; ++q) S.wqu[q] = w[q];
     // dU = -Quu^-1 Qu: coupled controls from lane 60, decoupled ones (Qu_z / Quu_zz) from the ql lanes
-    double *dUg = d.dU + kq * NX;
+    double *dUg = dUout + (size_t)kc * NX;
     if (ul)
         static_for<HC>([&](auto I) {
             constexpr int q = I;
@@ -714,7 +714,7 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem<real> &S, const PhaseC
             k1 = mfma16(a, b1, k1);
         }
         HSYNC();  // Quu^-1 is read; Kp takes its place
-        real *Kg = Prec<real>::K(d) + kq * KCW;
+        real *Kg = Kout + (size_t)kc * KCW;
         // rows 0..11 hold the result: registers 0..2 in the f64 layout, 0..3 (rows < 12) in the f32 one
 #pragma unroll
         for (int g = 0; g < (sizeof(real) == 8 ? 3 : 4); ++g) {
@@ -776,10 +776,13 @@ DEV void bwd_knot(const Params &p, const Bufs &d, BwdElem<real> &S, const PhaseC
     STAMP(9);
 }
 
-// MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229) with one regularisation value.
-// Returns false (and stops) at the first knot whose Quu fails the PSD test.
+// MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229) with one regularisation value; the
+// gains and dU rows of element b go to Kout / dUout (row kc at kc * KCW / kc * 24).
+// Returns -1, or (and stops at) the control slot of the first knot whose Quu fails the PSD test:
+// rows above it were written, it and the rows below were not.
 template <typename real>
-DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem<real> &S, size_t b, real reg, real &dV1, real &dV2)
+DEV int bwd_sweep(const Params &p, const Bufs &d, BwdElem<real> &S, size_t b, real *Kout, double *dUout, real reg,
+                  real &dV1, real &dV2)
 {
     const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5, cb = HC * hf;
     const bool rowl = r < NX;
@@ -838,10 +841,13 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem<real> &S, size_t b, r
         }
         HSYNC();
         const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
+        int k = N - 1;
 #pragma unroll 1
-        for (int k = N - 1; k >= 0 && live; --k)
-            bwd_knot(p, d, S, pc, b, s0 + k, k0 + k, reg, k < N - 1, k > 0, live, g, dV1, dV2);
-        if (!live) return false;
+        for (; k >= 0; --k) {
+            bwd_knot(p, d, S, pc, b, s0 + k, k0 + k, Kout, dUout, reg, k < N - 1, k > 0, live, g, dV1, dV2);
+            if (!live) break;
+        }
+        if (!live) return k0 + k;
         // G[0] += H[0] Defect[0] (SinglePhase.cpp:365)
         if (lane < NX) S.d[lane] = Prec<real>::def(d)[(b * p.S + s0) * NX + lane];
         HSYNC();
@@ -853,7 +859,7 @@ DEV bool bwd_sweep(const Params &p, const Bufs &d, BwdElem<real> &S, size_t b, r
         if (rowl) g += a;
         HSYNC();
     }
-    return true;
+    return -1;
 }
 
 template <typename real>
@@ -884,11 +890,29 @@ __global__ __launch_bounds__(64, 4) void k_riccati(Params p, Bufs d)
     HSYNC();
     const double cost = uniform(S.red[0]), feas = uniform(S.red[1]);
     double reg = uniform(E.reg);
-    bool ok = false;
     real dV1 = 0, dV2 = 0;
-    // backward_sweep_regularized (MultiPhaseDDP.cpp:141-181)
-    for (;;) {
-        if (bwd_sweep(p, d, S, b, (real)reg, dV1, dV2)) { ok = true; break; }
+    real *Ko = Prec<real>::K(d) + b * p.Kc * KCW;
+    double *dUo = d.dU + b * p.Kc * NX;
+    // backward_sweep_regularized (MultiPhaseDDP.cpp:141-181): the sweep with the element's mu,
+    // then mu = max(mu * update_regularization, 1e-3) until a sweep succeeds or mu > 1e2
+    bool ok = false;
+    for (bool first = true;; first = false) {  // one call site: the sweep is inlined once
+        if (bwd_sweep(p, d, S, b, Ko, dUo, (real)reg, dV1, dV2) < 0) { ok = true; break; }
+        if (first && p.retry_cap > 0) {
+            // the retries run in parallel in k_riccati_retry (the first retry_cap failures of
+            // this launch); k_riccati_select then takes the first mu that succeeds, as the loop
+            // would
+            if (lane == 0) {
+                const int f = atomicAdd(d.retry_count, 1);
+                if (f < p.retry_cap) d.retry_list[f] = RetryEntry{(int)b, 0, reg};
+                S.red[2] = f;
+            }
+            HSYNC();
+            if ((int)uniform(S.red[2]) < p.retry_cap) {
+                if (lane == 0) { E.iters += 1; E.cost = cost; E.feas = feas; E.accepted = 0; }
+                return;
+            }
+        }
         reg = fmax(reg * p.update_regularization, 1e-03);
         if (reg > 1e2) break;
     }
@@ -901,6 +925,87 @@ __global__ __launch_bounds__(64, 4) void k_riccati(Params p, Bufs d)
     if (lane == 0) {
         E.iters += 1; E.cost = cost; E.feas = feas; E.reg = reg; E.accepted = 0;
         if (!ok) { E.status = 1; E.done = 1; E.ls_active = 0; } // goto bad_solve
+    }
+}
+
+// The retries of backward_sweep_regularized for the elements k_riccati deferred, all at once:
+// block (f, a) sweeps deferred element f with the a-th next mu of the schedule (a = 1 ..
+// retry_m) into its own scratch rows.  Every attempt is the same deterministic sweep the
+// sequential loop would run with that mu, so taking the first success (k_riccati_select) gives
+// the loop's result; a straggler needing many retries costs one sweep instead of many.
+template <typename real>
+__global__ __launch_bounds__(64, 4) void k_riccati_retry(Params p, Bufs d)
+{
+    __shared__ BwdElem<real> S;
+    const int f = blockIdx.x / p.retry_m, a = blockIdx.x % p.retry_m + 1;
+    if (f >= min(*d.retry_count, p.retry_cap)) return;
+    const RetryEntry e = d.retry_list[f];
+    double reg = e.reg;
+    for (int t = 0; t < a; ++t) reg = fmax(reg * p.update_regularization, 1e-03);
+    int *flag = d.retry_flag + f * p.retry_m + (a - 1);
+    if (reg > 1e2) {  // past the loop's exit: never tried (the schedule is non-decreasing)
+        if (threadIdx.x == 0) *flag = 2;
+        return;
+    }
+    const size_t slot = (size_t)f * p.retry_m + (a - 1);
+    real dV1, dV2;
+    const int fk = bwd_sweep(p, d, S, e.b, (real *)d.retry_K + slot * p.Kc * KCW, d.retry_dU + slot * p.Kc * NX,
+                             (real)reg, dV1, dV2);
+    if (threadIdx.x == 0) *flag = fk < 0 ? 1 : -1 - fk;  // success, or -1 - (the failing control slot)
+}
+
+// The outcome of backward_sweep_regularized for each deferred element: the first attempt that
+// succeeded (its gains and dU rows copied to the element), mu / 20 (0 below 1e-6) as the next
+// regularisation; when none succeeds (mu passed 1e2: status 1, bad_solve) the element's rows are
+// left as the sequential loop leaves them: row kc from the last attempt that got past it.
+template <typename real>
+__global__ __launch_bounds__(64) void k_riccati_select(Params p, Bufs d)
+{
+    const int f = blockIdx.x, lane = threadIdx.x;
+    if (f >= min(*d.retry_count, p.retry_cap)) return;
+    const RetryEntry e = d.retry_list[f];
+    const size_t b = e.b;
+    double reg = e.reg;
+    int win = 0;
+    for (int a = 1; a <= p.retry_m; ++a) {
+        reg = fmax(reg * p.update_regularization, 1e-03);
+        if (reg > 1e2) break;
+        if (d.retry_flag[f * p.retry_m + a - 1] == 1) { win = a; break; }
+    }
+    real *Ko = Prec<real>::K(d) + b * p.Kc * KCW;
+    double *dUo = d.dU + b * p.Kc * NX;
+    if (win) {
+        const size_t slot = (size_t)f * p.retry_m + (win - 1);
+        const real *Ks = (const real *)d.retry_K + slot * p.Kc * KCW;
+        const double *Us = d.retry_dU + slot * p.Kc * NX;
+        for (size_t q = lane; q < (size_t)p.Kc * KCW; q += 64) Ko[q] = Ks[q];
+        for (size_t q = lane; q < (size_t)p.Kc * NX; q += 64) dUo[q] = Us[q];
+    } else {
+        const int *fl = d.retry_flag + f * p.retry_m;
+        // attempt a wrote the rows above its failing slot -1 - fl[a - 1]; attempts stop at flag 2
+        auto source = [&](int kc) {
+            int src = 0;
+            for (int a = 1; a <= p.retry_m && fl[a - 1] != 2; ++a)
+                if (-1 - fl[a - 1] < kc) src = a;
+            return src;
+        };
+        const real *K0 = (const real *)d.retry_K + (size_t)f * p.retry_m * p.Kc * KCW;
+        const double *U0 = d.retry_dU + (size_t)f * p.retry_m * p.Kc * NX;
+        for (size_t q = lane; q < (size_t)p.Kc * KCW; q += 64) {
+            const int a = source((int)(q / KCW));
+            if (a) Ko[q] = K0[(size_t)(a - 1) * p.Kc * KCW + q];
+        }
+        for (size_t q = lane; q < (size_t)p.Kc * NX; q += 64) {
+            const int a = source((int)(q / NX));
+            if (a) dUo[q] = U0[(size_t)(a - 1) * p.Kc * NX + q];
+        }
+    }
+    if (lane == 0) {
+        ElemState &E = d.el[b];
+        double rn = reg / 20;
+        if (rn < 1e-06) rn = 0;
+        E.reg = rn;
+        if (!win) { E.status = 1; E.done = 1; E.ls_active = 0; }  // goto bad_solve
     }
 }
 
@@ -1126,10 +1231,21 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
 
 void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
 {
+    if (p.retry_cap > 0) (void)hipMemsetAsync(d.retry_count, 0, sizeof(int), st);
     if (p.fp32)
         hipLaunchKernelGGL(k_riccati<float>, dim3(p.B), dim3(64), 0, st, p, d);
     else
         hipLaunchKernelGGL(k_riccati<double>, dim3(p.B), dim3(64), 0, st, p, d);
+    if (p.retry_cap > 0) {
+        const dim3 gr((unsigned)(p.retry_cap * p.retry_m)), gs((unsigned)p.retry_cap);
+        if (p.fp32) {
+            hipLaunchKernelGGL(k_riccati_retry<float>, gr, dim3(64), 0, st, p, d);
+            hipLaunchKernelGGL(k_riccati_select<float>, gs, dim3(64), 0, st, p, d);
+        } else {
+            hipLaunchKernelGGL(k_riccati_retry<double>, gr, dim3(64), 0, st, p, d);
+            hipLaunchKernelGGL(k_riccati_select<double>, gs, dim3(64), 0, st, p, d);
+        }
+    }
 }
 
 void launch_lin_rollout(const Params &p, const Bufs &d, hipStream_t st)

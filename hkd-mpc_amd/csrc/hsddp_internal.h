@@ -61,6 +61,16 @@ struct Params {
     // horizon shift (HKDProblem.cpp:203-216); has_tail: some phase has non-shooting states
     int ss[MAXP];
     int has_tail;
+    // parallel regularisation retries (k_riccati_retry): elements whose first sweep fails the PSD
+    // test, up to retry_cap of them per launch, evaluate the next retry_m values of the mu schedule
+    // of backward_sweep_regularized (MultiPhaseDDP.cpp:141-181) at once; 0 = sequential only
+    int retry_cap, retry_m;
+};
+
+// one element deferred to the parallel retry: its index and the regularisation of its failed sweep
+struct RetryEntry {
+    int b, pad;
+    double reg;
 };
 
 struct ElemState {
@@ -83,6 +93,12 @@ struct Bufs {
     float *lq32, *K32, *def32;
     ElemState *el;
     int *counter;                          // [4] host-visible activity counters
+    // parallel regularisation retries: deferred elements [retry_cap], their count, per attempt a
+    // success flag [retry_cap][retry_m] and the attempt's gains / dU rows [retry_cap][retry_m][Kc][..]
+    RetryEntry *retry_list;
+    int *retry_count, *retry_flag;
+    void *retry_K;                         // real (fp64, or fp32 in the C5 mode) [..][KCW]
+    double *retry_dU;                      // [..][24]
     unsigned long long *dbg;               // [B][16] diagnostic builds only (in-kernel stamps)
 };
 

@@ -198,3 +198,29 @@ def test_single_shooting_rejected():
     with pytest.raises(hsddp.HSDDPError, match="single shooting"):
         s.solve()
     s.close()
+
+
+def _stack(idx, P, N, gait):
+    ps = [syn.make_batch(1, P, N, gait, first_element=i) for i in idx]
+    q = dict(ps[0]); q["batch"] = len(idx)
+    for k in ("contacts", "x0", "Xbar", "Ubar"):
+        q[k] = np.concatenate([p[k] for p in ps])
+    return q
+
+
+def test_parallel_retry_equals_sequential(monkeypatch):
+    """Regularisation retries (backward_sweep_regularized, MultiPhaseDDP.cpp:141-181) evaluated in
+    parallel (k_riccati_retry / k_riccati_select) give the sequential loop's result bit for bit.
+    Jump elements 377, 760, 656 of the synthetic batch need 4 and 9, 18 (all failing: status 1,
+    replayed) and 2 sweeps in inner iterations 9-12 (counted on the oracle); the oracle agrees on
+    every status and line-search trial count."""
+    prob = _stack([377, 760, 656, 321, 0], 8, 25, "jump")
+    kw = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=12)
+    g = _run(prob, **kw)
+    monkeypatch.setenv("HSDDP_SEQUENTIAL_RETRY", "1")
+    q = _run(prob, **kw)
+    for f in ("Xbar", "Ubar", "K", "X", "U", "dU", "dX", "cost", "feas", "iters", "status", "n_ls_trials"):
+        assert np.array_equal(g[f], q[f]), f
+    r = O.solve_batch(prob, O.default_options(**kw), n_threads=8)
+    assert np.array_equal(g["status"], r["status"]) and g["status"][1] == 1
+    assert np.array_equal(g["n_ls_trials"], r["n_ls_trials"])
