@@ -26,12 +26,54 @@ using namespace hkd;
 #endif
 
 // ---------------------------------------------------------------------------------------------
+// Record stores of k_lq.  One lane computes one knot's record, so direct stores from the lanes hit
+// 64 records (64 cache lines) per instruction.  For the gradient pieces (lx, lu, ReB Hessian) each
+// wave instead stages the piece of its records in LDS (lane-major, odd stride) and the lanes still
+// active write it back record by record: consecutive lanes write consecutive 2-value pairs of one
+// record, so an instruction covers ~1 KB of contiguous records.  Pieces are even-sized at even
+// offsets, so every pair is aligned in HBM.  Lanes that returned early (past the batch, finished
+// element, phase-end slot) left ridx = -1 and their records are skipped.
+constexpr int LQ_STG = 25; // LDS stride per lane (pieces of 24, +1)
+
+template <typename T, int OFF, int N>
+DEV void lq_stage_store(T *wl, const long *ridx, const double *v, T *lq, int ldw, int lane)
+{
+#pragma unroll
+    for (int j = 0; j < N; ++j) wl[lane * LQ_STG + j] = (T)v[j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    using T2 = std::conditional_t<std::is_same_v<T, float>, float2, double2>;
+    const unsigned long long m = __ballot(1);
+    const int na = __popcll(m), rank = __popcll(m & ((1ull << lane) - 1));
+    for (int q = rank; q < 64 * (N / 2); q += na) {
+        const int r = q / (N / 2), jp = q % (N / 2);
+        const long rr = ridx[r];
+        if (rr >= 0) {
+            T2 w;
+            w.x = wl[r * LQ_STG + 2 * jp];
+            w.y = wl[r * LQ_STG + 2 * jp + 1];
+            *reinterpret_cast<T2 *>(lq + rr * ldw + OFF + 2 * jp) = w;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_lq: per (element, state slot): cost and |Defect|^2 at the current (X, U); compact LQ model at
 // control slots (SinglePhase::compute_cost + LQ_approximation, SinglePhase.cpp:235-296).
 // F32: config C5's fp32 Riccati mode (records in fp32 plus an fp32 copy of Defect for the sweep)
+// The A - I / B pieces go out by direct stores (staging them would keep all 102 values live).
 template <bool F32>
 __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 {
+    using T = std::conditional_t<F32, float, double>;
+    __shared__ T stage[4][64 * LQ_STG];
+    __shared__ long sridx[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    sridx[w][lane] = -1; // before any early return: lanes without a record stay -1
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long)p.B * p.S) return;
     const int b = (int)(gid / p.S), s = (int)(gid % p.S);
@@ -63,6 +105,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
         return;
     }
     const int kc = p.k0[i] + k;
+    sridx[w][lane] = (long)b * p.Kc + kc;
     double u[NU];
     const double *ug = d.U + ((size_t)b * p.Kc + kc) * NU;
 #pragma unroll
@@ -98,8 +141,9 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
         lx[3 + j % 3] += -v;
         lx[12 + j] += v;
     }
-#pragma unroll
-    for (int j = 0; j < NX; ++j) rec.set(LQ_LX + j, lx[j]);
+    T *lqT = F32 ? (T *)d.lq32 : (T *)d.lq;
+    const int ldw = F32 ? LQW32 : LQW;
+    lq_stage_store<T, LQ_LX, NX>(stage[w], sridx[w], lx, lqT, ldw, lane);
     // lu + ReB gradient / Hessian (SinglePhase.cpp:380-394)
     double lu[NU], rb[24];
 #pragma unroll
@@ -127,10 +171,8 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
             for (int a = 0; a < 6; ++a) rb[6 * lg + a] = p.dt * hu[a];
         }
     }
-#pragma unroll
-    for (int j = 0; j < NU; ++j) rec.set(LQ_LU + j, lu[j]);
-#pragma unroll
-    for (int j = 0; j < 24; ++j) rec.set(LQ_RB + j, rb[j]);
+    lq_stage_store<T, LQ_LU, NU>(stage[w], sridx[w], lu, lqT, ldw, lane);
+    lq_stage_store<T, LQ_RB, 24>(stage[w], sridx[w], rb, lqT, ldw, lane);
 }
 
 // k_terminal: one wave per (element, phase): Phix, Phixx (+AL, quirk A4) and reset-map Jacobian Px.
