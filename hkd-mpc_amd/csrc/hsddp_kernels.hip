@@ -235,10 +235,15 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
         for (int l = 0; l < 4; ++l) v += scoef[l][1] * (shx[l][r] * shx[l][cidx]);
         rec[TM_PHIXX + e] = v;
     }
-    if (i < p.P - 1 && t < NX) { // Px rows at X_i[N]
-        double row[NX];
-        hkd_resetmap_partial_row(sx, sc, scn, t, row);
-        for (int j = 0; j < NX; ++j) rec[TM_PX + t * NX + j] = row[j];
+    if (i < p.P - 1) { // Px rows at X_i[N]: one row per lane, staged in LDS, stored coalesced by the wave
+        __shared__ double spx[NX * (NX + 1)];
+        if (t < NX) {
+            double row[NX];
+            hkd_resetmap_partial_row(sx, sc, scn, t, row);
+            for (int j = 0; j < NX; ++j) spx[t * (NX + 1) + j] = row[j];
+        }
+        __syncthreads();
+        for (int e = t; e < NN; e += 64) rec[TM_PX + e] = spx[(e / NX) * (NX + 1) + e % NX];
     }
 }
 
