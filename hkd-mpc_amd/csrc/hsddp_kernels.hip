@@ -507,18 +507,19 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
 // Trajectory::update_nominal_vals for accepted elements (copy X->Xbar, U->Ubar, Defect->Defect_bar)
 __global__ __launch_bounds__(256) void k_update_nominal(Params p, Bufs d, int init)
 {
+    // one thread per 16-byte pair (rows of 24 doubles: X, Defect [B][S][24], U [B][Kc][24])
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long per = (long)p.S * NX;
+    const long per = (long)p.S * (NX / 2);
     if (gid >= (long)p.B * per) return;
     const int b = (int)(gid / per);
     const ElemState &E = d.el[b];
     if (!E.accepted || (init && E.done)) return;
-    d.Xbar[gid] = d.X[gid];
-    d.Defect_bar[gid] = d.Defect[gid];
+    reinterpret_cast<double2 *>(d.Xbar)[gid] = reinterpret_cast<const double2 *>(d.X)[gid];
+    reinterpret_cast<double2 *>(d.Defect_bar)[gid] = reinterpret_cast<const double2 *>(d.Defect)[gid];
     const long r = gid % per;
-    if (r < (long)p.Kc * NU) {
-        const long ug = (long)b * p.Kc * NU + r;
-        d.Ubar[ug] = d.U[ug];
+    if (r < (long)p.Kc * (NU / 2)) {
+        const long ug = (long)b * p.Kc * (NU / 2) + r;
+        reinterpret_cast<double2 *>(d.Ubar)[ug] = reinterpret_cast<const double2 *>(d.U)[ug];
     }
 }
 
@@ -683,7 +684,7 @@ void launch_decide(const Params &p, const Bufs &d, double eps, int last, int ini
 }
 void launch_update_nominal(const Params &p, const Bufs &d, int init, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_update_nominal, dim3(blocks_for((long)p.B * p.S * NX, 256)), dim3(256), 0, st, p, d, init);
+    hipLaunchKernelGGL(k_update_nominal, dim3(blocks_for((long)p.B * p.S * (NX / 2), 256)), dim3(256), 0, st, p, d, init);
 }
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
 {
