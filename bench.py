@@ -6,13 +6,24 @@ linear rollout, line search, nominal update; MultiPhaseDDP.cpp:304-381) over the
 of B = 4096 independent 4-phase x 50-knot HKD trot problems per GPU, fp64, inputs resident in HBM.
 value = trajectory-iterations/s over all ranks (sum of per-element inner iterations / max rank
 time).  N GPUs: one process per GPU, disjoint shards (weak scaling), no collective on the data
-path; a final gather of per-element summaries to rank 0 after the timed region.
+path; a final RCCL gather of per-element summaries to rank 0 after the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+
+`--gpus N` with N > 1 outside a torch.distributed launch starts the N ranks itself (a child
+`torch.distributed.run`, before this process touches the GPU) and exits with its status.
+
+Roofline: `achieved` = the dominant kernel's (k_riccati) algorithmic bytes per launch
+in this design's compact layout (hsddp/traffic.py) / its average launch time from HIP events on
+the solver's stream.  `traffic` = HBM bytes per launch measured by rocprofv3 PMC passes
+(profiles/pmc_summary.json, tools/pmc.sh).  The sweep is fp64-issue-bound, so its fp64 FLOP rate
+against the vector peak is reported next to it, and the whole step's algorithmic bytes / step time.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,36 +35,51 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hkd-mpc_amd"))
 
 import hsddp  # noqa: E402
-from hsddp import synthetic  # noqa: E402
+from hsddp import synthetic, traffic  # noqa: E402
 
 METRIC = "batched DDP iters/sec (fwd+bwd), 4-phase 200-knot HKD fp64, batch=4096"
 UNIT = "trajectory-iterations/s"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector (= fp64 matrix) peak, spec; 60-75 measured (tools/micro/rates.hip)
 
 
-# algorithmic bytes per knot per DDP iteration of the BWD pass (r A, B, l*, Defect
-# 2952 fp64; w K, dU 600 fp64) — the per-unit figure the roofline is quoted on.  One k_riccati
-# launch processes every control knot of every element once.
-BWD_BYTES_PER_KNOT = 8 * (2952 + 600)
-
-
-def load_traffic(cfg_key: str):
-    """Measured HBM bytes per k_riccati launch from the committed rocprofv3 PMC summary (or None)."""
+def load_traffic(cfg_key: str, kernel: str = "k_riccati"):
+    """Measured HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             data = json.load(f)
-        return data.get(cfg_key, {}).get("k_riccati", {}).get("hbm_bytes_per_launch")
+        return data.get(cfg_key, {}).get(kernel, {}).get("hbm_bytes_per_launch"), data.get("_source", "profiles/pmc_summary.json")
     except (OSError, ValueError):
-        return None
+        return None, None
+
+
+def host_cpu():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, affinity
 
 
 def cpu_baseline(args):
     """The oracle (CPU restatement of the reference solver, C, one trajectory per thread) timed on a
-    bounded sample of the same workload on this host."""
+    bounded sample of the same workload on this host's cores: every core this process may run on,
+    limited by the job's CPU share where the launcher sets one (OMP_NUM_THREADS; 16 on the GPU box)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    model, nproc, affinity = host_cpu()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = args.cpu_threads or (min(affinity, share) if share > 0 else affinity)
     prob = synthetic.make_batch(args.cpu_elements, args.phases, args.knots, args.gait)
     opt = O.default_options(no_early_exit=1, max_AL_iter=1, max_DDP_iter=args.cpu_iters)
     t0 = time.perf_counter()
@@ -61,8 +87,20 @@ def cpu_baseline(args):
     dt = time.perf_counter() - t0
     n = float(np.sum(r["iters"]))
     return {"value": n / dt, "unit": UNIT, "cores": threads, "kind": "port",
-            "sample": f"oracle/hsddp_oracle.c, {args.cpu_elements} elements x {args.cpu_iters} inner iterations "
-                      f"(+ initial rollout), same {args.gait} {args.phases}x{args.knots} workload, {threads} threads, {dt:.1f} s wall"}
+            "host": {"cpu_model": model, "nproc": nproc, "affinity_cpus": affinity, "job_cpu_share": share or None},
+            "sample": f"oracle/hsddp_oracle.c (-O2, fp64), {args.cpu_elements} elements x {args.cpu_iters} inner iterations "
+                      f"(+ initial rollout), same {args.gait} {args.phases}x{args.knots} workload, one trajectory per thread, "
+                      f"{threads} threads, {dt:.1f} s wall"}
+
+
+def spawn_ranks(args) -> int:
+    """Run this script as N torch.distributed ranks (one per GPU) in a child launcher."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -75,14 +113,17 @@ def main():
     ap.add_argument("--knots", type=int, default=50)
     ap.add_argument("--gait", default="trot")
     ap.add_argument("--mixed", action="store_true",
-                    help="config C4: per-element gait drawn from {trot, pace, bound, pronk} (per-element references)")
+                    help="config C4: per-element gait drawn from {trot, pace, bound, pronk, jump} (per-element references)")
     ap.add_argument("--cpu-elements", type=int, default=2048)
     ap.add_argument("--cpu-iters", type=int, default=10)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core of this process's share")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--riccati-fp32", action="store_true",
                     help="config C5: fp32 LQ records / Riccati sweep / linear rollout (fp64 rollout, costs, outer loop)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))  # nothing above touched the GPU
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -113,37 +154,56 @@ def main():
     elem_iters = float(info["iters"].sum() - it0)
 
     red = torch.tensor([t1 - t0, elem_iters, float(st.ls_trials)], dtype=torch.float64, device=dev)
+    rank_ms = [(t1 - t0) / args.steps * 1e3]
     if world > 1:
-        tmax = red[0:1].clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = red[1:3].clone(); dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed, total_iters, total_ls = float(tmax[0]), float(tsum[0]), float(tsum[1])
-        # final gather of per-element summaries to rank 0 (outside the timed region)
-        summ = torch.from_numpy(np.stack([info["cost"], info["feas"], info["max_tconstr"],
-                                          info["max_pconstr"]], 1)).to(dev)
+        allr = [torch.zeros_like(red) for _ in range(world)]
+        dist.all_gather(allr, red)
+        rank_ms = [float(r[0]) / args.steps * 1e3 for r in allr]
+        elapsed = max(float(r[0]) for r in allr)
+        total_iters = sum(float(r[1]) for r in allr)
+        total_ls = sum(float(r[2]) for r in allr)
+        # final gather of per-element summaries to rank 0 (outside the timed region; RCCL)
+        summ = torch.from_numpy(np.stack([info["cost"], info["feas"], info["max_tconstr"], info["max_pconstr"],
+                                          info["iters"].astype(np.float64), info["status"].astype(np.float64)], 1)).to(dev)
         gathered = [torch.empty_like(summ) for _ in range(world)] if rank == 0 else None
         dist.gather(summ, gathered, dst=0)
         finite = bool(torch.isfinite(torch.cat(gathered)).all()) if rank == 0 else True
+        gathered_rows = int(sum(g.shape[0] for g in gathered)) if rank == 0 else 0
     else:
         elapsed, total_iters, total_ls = t1 - t0, elem_iters, float(st.ls_trials)
         finite = bool(np.isfinite(info["cost"]).all())
+        gathered_rows = B
 
     if rank == 0:
         S, Kc, P = prob["S"], prob["Kc"], len(prob["horizons"])
+        ms_step = elapsed / args.steps * 1e3
+        mean_ls = total_ls / max(1.0, total_iters)
+        kb = traffic.kernel_bytes(B, S, Kc, P, fp32=args.riccati_fp32, ref_per_element=args.mixed)
         # k_riccati time from HIP events recorded around its launches on the solver's stream
         avg_bwd_ms = st.ms_backward / max(1, st.n_backward_launches)
-        # fp32 mode (C5) halves every term of the per-knot bytes
-        bytes_launch = BWD_BYTES_PER_KNOT * Kc * B // (2 if args.riccati_fp32 else 1)
+        bytes_launch = kb["k_riccati"]
         achieved = bytes_launch / (avg_bwd_ms * 1e-3) / 1e9
+        flop_launch = traffic.RICCATI_FLOP_PER_KNOT * Kc * B
+        tflops = flop_launch / (avg_bwd_ms * 1e-3) / 1e12
+        step_b = traffic.step_bytes(B, S, Kc, P, mean_ls, fp32=args.riccati_fp32, ref_per_element=args.mixed)
         gait = "mixed" if args.mixed else args.gait
         metric_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 4096)
         label = ("config C5: fp32 Riccati" if args.riccati_fp32 else "BASELINE metric config" if metric_cfg
                  else "config C3: jump with resets" if gait == "jump" else "config C4 shard: mixed gaits" if args.mixed
                  else "custom")
         cfg_key = f"{gait}_{args.phases}x{args.knots}_b{B}" + ("_fp32" if args.riccati_fp32 else "")
-        traffic = load_traffic(cfg_key)
+        meas, meas_src = load_traffic(cfg_key)
+        n = max(1, args.steps)
+        dms = {"total": st.ms_total / n, "lq+terminal": st.ms_lq / n, "backward": st.ms_backward / n,
+               "linear_rollout": st.ms_linear / n, "forward_ls+update": st.ms_forward / n}
+        gbs = {"k_lq+k_terminal": (kb["k_lq"] + kb["k_terminal"]) / (dms["lq+terminal"] * 1e6),
+               "k_riccati": achieved,
+               "k_lin_rollout": kb["k_lin_rollout"] / (dms["linear_rollout"] * 1e6),
+               "k_rollout x trials + k_update_nominal": (mean_ls * kb["k_rollout"] + kb["k_update_nominal"]) /
+                                                         (dms["forward_ls+update"] * 1e6)}
         out = {
             "metric": METRIC, "value": total_iters / elapsed, "unit": UNIT, "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32 Riccati / f64 rollout" if args.riccati_fp32 else "f64",
             "data": f"synthetic: seeded random initial states (splitmix64), closed-form {gait} reference "
@@ -153,15 +213,19 @@ def main():
                        "global_batch": B * world, "batch_per_gpu": B, "phases": args.phases,
                        "knots_per_phase": args.knots, "nx": 24, "nu": 24, "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_riccati", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch,
-                         "avg_launch_ms": avg_bwd_ms},
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": meas,
+                         "traffic_source": meas_src if meas is not None else None,
+                         "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": avg_bwd_ms,
+                         "bytes_model": "compact layout, hsddp/traffic.py (DESIGN.md §3)",
+                         "limiter": "fp64 issue (the sweep's dependent per-knot chain), see fp64",
+                         "fp64": {"flop_per_launch": flop_launch, "achieved_tflops": tflops,
+                                  "peak_tflops": FP64_PEAK_TFLOPS, "frac": tflops / FP64_PEAK_TFLOPS},
+                         "step": {"algorithmic_bytes": step_b, "achieved": step_b / (ms_step * 1e6),
+                                  "frac": step_b / (ms_step * 1e6) / HBM_PEAK_GBS,
+                                  "kernel_GBps": gbs}},
             "extra": {"batch_iterations_per_s": total_iters / elapsed / (B * world),
-                      "mean_ls_trials": total_ls / max(1.0, total_iters),
-                      "device_ms_per_step": {"total": st.ms_total / args.steps, "lq": st.ms_lq / args.steps,
-                                             "backward": st.ms_backward / args.steps,
-                                             "linear_rollout": st.ms_linear / args.steps,
-                                             "forward_ls": st.ms_forward / args.steps},
+                      "mean_ls_trials": mean_ls, "device_ms_per_step": dms,
+                      "rank_ms_per_step": rank_ms, "rccl_world_size": world, "gathered_elements": gathered_rows,
                       "all_costs_finite": finite, "device_bytes": solver.device_bytes()},
         }
         if world == 1 and not args.no_cpu_baseline and not args.riccati_fp32 and not args.mixed:

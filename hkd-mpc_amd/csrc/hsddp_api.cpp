@@ -427,11 +427,33 @@ extern "C" int hsddp_destroy(hsddp_handle h)
     return HSDDP_OK;
 }
 
+extern "C" int hsddp_validate_options(const hsddp_options *o)
+{
+    if (!o) return fail(HSDDP_ERR_ARG, "null argument");
+    if (!(o->alpha > 0 && o->alpha < 1)) return fail(HSDDP_ERR_ARG, "alpha must lie in (0, 1)");
+    if (o->max_AL_iter < 0 || o->max_DDP_iter < 0) return fail(HSDDP_ERR_ARG, "negative iteration budget");
+    // backward_sweep_regularized (MultiPhaseDDP.cpp:150-167) raises mu = max(mu * factor, 1e-3)
+    // until a sweep succeeds or mu > 1e2.  A factor <= 1 never gets there (the reference spins
+    // forever on the first failed sweep) and a factor barely above 1 takes thousands of sweeps per
+    // failure; both are refused rather than left to hang a GPU wave.
+    if (!(o->update_regularization > 1))
+        return fail(HSDDP_ERR_ARG, "update_regularization must exceed 1 (the regularisation schedule would never end)");
+    int m = 0;
+    for (double mu = 0;; ++m) {
+        mu = std::fmax(mu * o->update_regularization, 1e-03);
+        if (mu > 1e2) break;
+        if (m >= HSDDP_MAX_REG_ATTEMPTS)
+            return fail(HSDDP_ERR_ARG, "update_regularization too close to 1: more than HSDDP_MAX_REG_ATTEMPTS "
+                                       "regularisation retries per failed sweep");
+    }
+    return HSDDP_OK;
+}
+
 extern "C" int hsddp_set_options(hsddp_handle h, const hsddp_options *o)
 {
     if (!h || !o) return fail(HSDDP_ERR_ARG, "null argument");
-    if (!(o->alpha > 0 && o->alpha < 1)) return fail(HSDDP_ERR_ARG, "alpha must lie in (0, 1)");
-    if (o->max_AL_iter < 0 || o->max_DDP_iter < 0) return fail(HSDDP_ERR_ARG, "negative iteration budget");
+    int rc = hsddp_validate_options(o);
+    if (rc) return rc;
     h->opt = *o;
     fill_params(h);
     return HSDDP_OK;

@@ -94,7 +94,7 @@ _lib = None
 EXPORTS = [
     "hsddp_last_error", "hsddp_version", "hsddp_default_options", "hsddp_default_weights",
     "hsddp_default_constraint_params", "hsddp_load_settings", "hsddp_load_constraint_params",
-    "hsddp_create", "hsddp_destroy", "hsddp_set_options", "hsddp_upload_problem",
+    "hsddp_create", "hsddp_destroy", "hsddp_set_options", "hsddp_validate_options", "hsddp_upload_problem",
     "hsddp_upload_warm_start", "hsddp_solve", "hsddp_solve_begin", "hsddp_iterate", "hsddp_solve_end", "hsddp_download_trajectory", "hsddp_download_working",
     "hsddp_download_element_info", "hsddp_synchronize", "hsddp_device_bytes", "hsddp_hkd_dynamics",
     "hsddp_hkd_dynamics_partial", "hsddp_hkd_foot_position", "hsddp_hkd_foot_jacobian",
@@ -120,6 +120,7 @@ def lib():
     L.hsddp_create.argtypes = [C.POINTER(ProblemDesc), C.POINTER(C.c_void_p)]
     L.hsddp_destroy.argtypes = [C.c_void_p]
     L.hsddp_set_options.argtypes = [C.c_void_p, C.POINTER(Options)]
+    L.hsddp_validate_options.argtypes = [C.POINTER(Options)]
     L.hsddp_upload_problem.argtypes = [C.c_void_p, IP, DP, DP, DP, DP]
     L.hsddp_upload_warm_start.argtypes = [C.c_void_p, DP, DP, DP]
     L.hsddp_solve.argtypes = [C.c_void_p, C.POINTER(Stats)]

@@ -154,7 +154,9 @@ def make_batch(batch: int, n_phases: int = 4, knots: int = 50, gait: str = "trot
     S = sum(n + 1 for n in horizons)
     Kc = sum(horizons)
     if mixed:
-        names = ["trot", "pace", "bound", "pronk"]
+        # every gait of SURVEY.md §8(d)'s C4 set; jump runs the first n_phases phases of its cycle
+        # (for 4 phases: stance, rear stance, flight, front stance, then flight after the horizon)
+        names = ["trot", "pace", "bound", "pronk", "jump"]
         pick = (uniform_stream(seed ^ 0x5A5A, first_element + batch)[first_element:] * len(names)).astype(int)
         gaits = [names[i] for i in pick]
     else:

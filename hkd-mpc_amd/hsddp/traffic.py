@@ -1,0 +1,76 @@
+"""Algorithmic HBM bytes and fp64 FLOPs of one DDP inner iteration, per kernel.
+
+These are the bytes each kernel must move in THIS design's compact layout (hsddp_internal.h): a
+knot's LQ model is the 174-value record (A - I and B non-zeros, lx, lu, dt * ReB Hessian), the
+gains are the 12 coupled rows (12 x 24), lxx and luu's diagonal are rebuilt from parameters.  They
+replace SURVEY.md §8(d)'s dense per-knot model (A, B, lxx, luu, lux materialised as 24 x 24
+matrices, 88 KB per knot), which prices traffic this design never generates.
+
+Every figure counts each byte a kernel reads or writes in HBM once per launch (reads of the same
+row by neighbouring lanes or knots are one read).  Per-handle constants (contacts, the shared
+reference of a common gait, Params) are < 0.1 % and left out; per-element references (mixed
+gaits) are counted.
+
+    B  elements, S state slots (sum N_i + 1), Kc control slots (sum N_i), P phases.
+"""
+from __future__ import annotations
+
+NX = 24
+LQW, LQW32 = 174, 176   # compact LQ record (fp64 / fp32 stride), hsddp_internal.h
+KCW = 12 * 24           # compact gain rows
+TW_PHI = 24 + 576       # Phix + Phixx per phase end
+TW_PX = 576             # reset-map Jacobian per phase boundary
+
+
+def kernel_bytes(B: int, S: int, Kc: int, P: int, fp32: bool = False, ref_per_element: bool = False) -> dict:
+    """Algorithmic bytes per launch of each kernel of one inner iteration."""
+    d = 8                              # fp64
+    f = 4 if fp32 else 8               # Riccati precision: LQ record, gains, Defect copy (C5)
+    rec = (LQW32 * 4) if fp32 else (LQW * 8)
+    ref = (S * (24 + 12) + Kc * 24) * d if ref_per_element else 0   # ref_x, ref_foot per slot, ref_u per knot
+    term = (P * TW_PHI + (P - 1) * TW_PX) * d                      # Phix, Phixx (every phase end), Px (boundaries)
+    out = {}
+    # k_lq: per slot X, Defect read, slot cost / feasibility written (+ fp32 Defect copy); per control
+    # knot U read and the record written
+    out["k_lq"] = B * (S * (2 * NX * d + 2 * d + (NX * 4 if fp32 else 0)) + Kc * (NX * d + rec) + ref)
+    # k_terminal: per phase end X read (+ AL sigma, lambda), Phix, Phixx, Px written
+    out["k_terminal"] = B * (P * (NX + 8) * d + term)
+    # k_riccati: per control knot the record and Defect[k+1] read, gain rows and dU written; per
+    # element the terminal records and the slot cost / feasibility partial sums read
+    out["k_riccati"] = B * (Kc * (rec + NX * f + KCW * f + NX * d) + term + 2 * S * d)
+    # k_lin_rollout: per control knot gains, record, Defect, dU read, du and dX written; terminal
+    # records read per phase
+    out["k_lin_rollout"] = B * (Kc * (KCW * f + rec + NX * f + NX * d + 2 * NX * d) + term)
+    # k_rollout (one line-search trial): per slot Xbar, dX read, X, Defect written, cost /
+    # feasibility / violation / divergence written; per control knot Ubar, du read, U written
+    out["k_rollout"] = B * (S * (4 * NX * d + 4 * d) + Kc * 3 * NX * d + ref)
+    # k_update_nominal: X -> Xbar, Defect -> Defect_bar per slot, U -> Ubar per control knot
+    out["k_update_nominal"] = B * (S * 2 * NX * d * 2 + Kc * NX * d * 2)
+    return out
+
+
+def step_bytes(B: int, S: int, Kc: int, P: int, n_trials: float, fp32: bool = False,
+               ref_per_element: bool = False) -> float:
+    """Algorithmic bytes of one inner iteration: every kernel once, k_rollout n_trials times
+    (the measured mean number of line-search trials)."""
+    kb = kernel_bytes(B, S, Kc, P, fp32, ref_per_element)
+    return sum(v for k, v in kb.items() if k != "k_rollout") + n_trials * kb["k_rollout"]
+
+
+# fp64 FMAs of one knot of the backward sweep as k_riccati evaluates it (structure exploited:
+# A = I + S with 69 non-zeros of S, B_c with 48 non-zeros, 12 coupled controls, symmetric value
+# update).  Each term is the product's multiply-add count.
+RICCATI_FMA_PER_KNOT = {
+    "Gn = G + H d": 24 * 24,
+    "T = H B_c": 24 * 48,
+    "M = H A (S part)": 24 * 69,
+    "Qx = lx + A^T Gn": 69,
+    "Qu_c = lu + B_c^T Gn": 48,
+    "Qxx = lxx + A^T M (S part)": 24 * 69,
+    "Qux_c = B_c^T M": 12 * 24 * 4,
+    "Quu_cc = luu + B_c^T T": 12 * 48,
+    "[Quu_cc | Qux_c | Qu_c] elimination": 12 * 11 * 37,
+    "P = Qux_c^T Kp": 24 * 24 * 12,
+    "G = Qx - Qux_c^T k": 24 * 12,
+}
+RICCATI_FLOP_PER_KNOT = 2 * sum(RICCATI_FMA_PER_KNOT.values())

@@ -57,6 +57,9 @@ extern "C" {
 #define HSDDP_NX 24
 #define HSDDP_NU 24
 #define HSDDP_MAX_PHASES 16
+/* longest regularisation schedule accepted: mu = max(mu * update_regularization, 1e-3) retries
+ * of one failed backward sweep until mu > 1e2 (MultiPhaseDDP.cpp:150-167) */
+#define HSDDP_MAX_REG_ATTEMPTS 64
 
 enum {
     HSDDP_OK = 0,
@@ -150,6 +153,10 @@ int hsddp_load_constraint_params(const char *path, hsddp_constraint_params *cp);
 int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out);
 int hsddp_destroy(hsddp_handle h);
 int hsddp_set_options(hsddp_handle h, const hsddp_options *opt);
+/* The checks hsddp_set_options applies (host only, no device needed): alpha in (0, 1), non-negative
+ * iteration budgets, update_regularization > 1 with at most HSDDP_MAX_REG_ATTEMPTS retries from
+ * mu = 0 to mu > 1e2.  The reference accepts any factor and spins forever on a factor <= 1. */
+int hsddp_validate_options(const hsddp_options *opt);
 
 /* contacts int32 [B][P+1][4] (row P: contact after the horizon, for the last phase's touchdown
  * constraint); x0 [B][24]; ref_x, ref_u [Bref][S][24]; ref_foot [Bref][S][12]. */

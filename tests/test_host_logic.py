@@ -102,3 +102,20 @@ def test_splitmix64_known_values():
     assert v == 0xE220A8397B1DCDAF
     s, v = syn.splitmix64(s)
     assert v == 0x6E789E6AA1B965F4
+
+
+def test_validate_options_refuses_unending_regularisation_schedule():
+    """backward_sweep_regularized (MultiPhaseDDP.cpp:150-167) never reaches mu > 1e2 with a factor
+    <= 1; the C-ABI refuses such options (hsddp_set_options applies the same check) instead of
+    leaving a GPU wave spinning."""
+    L = _lib.lib()
+    ok = hsddp.default_options()
+    assert L.hsddp_validate_options(C.byref(ok)) == 0
+    for f in (1.0, 0.5, -2.0, float("nan"), 1.01):  # 1.01: > HSDDP_MAX_REG_ATTEMPTS retries
+        o = hsddp.default_options(update_regularization=f)
+        assert L.hsddp_validate_options(C.byref(o)) == -1, f  # HSDDP_ERR_ARG
+        assert b"update_regularization" in L.hsddp_last_error()
+    o = hsddp.default_options(update_regularization=1.5)   # 30 retries: accepted
+    assert L.hsddp_validate_options(C.byref(o)) == 0
+    o = hsddp.default_options(alpha=1.0)
+    assert L.hsddp_validate_options(C.byref(o)) == -1
