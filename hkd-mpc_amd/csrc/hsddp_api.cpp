@@ -381,8 +381,14 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
     d.contacts = contacts; d.x0 = x0; d.ref_x = rx; d.ref_u = ru; d.ref_foot = rf;
     {   // parallel regularisation retries: up to 128 deferred elements per launch, p.retry_m attempts each
         // (HSDDP_SEQUENTIAL_RETRY=1 keeps every retry inside k_riccati: a diagnostic for tests)
+        // Scratch: cap x M attempts x (Kc gain rows + Kc dU rows), e.g. 128 x 17 x 200 x 312 x 8 B = 1.1 GB
+        // at the metric's horizon in fp64 (device_bytes counts it).  HSDDP_RETRY_CAP=n lowers the cap
+        // (a diagnostic: tests use it to send deferrals past the cap into the in-kernel loop).
         const char *seq = std::getenv("HSDDP_SEQUENTIAL_RETRY");
-        const size_t cap = std::min<size_t>(128, B), M = (seq && seq[0] == '1') ? 0 : p.retry_m, n = cap * M;
+        const char *capenv = std::getenv("HSDDP_RETRY_CAP");
+        size_t cap = std::min<size_t>(128, B);
+        if (capenv && std::atoi(capenv) > 0) cap = std::min<size_t>(cap, (size_t)std::atoi(capenv));
+        const size_t M = (seq && seq[0] == '1') ? 0 : p.retry_m, n = cap * M;
         if (M > 0) {
             void *rk;
             if ((rc = dalloc(h, d.retry_list, cap)) || (rc = dalloc(h, d.retry_count, 1)) ||

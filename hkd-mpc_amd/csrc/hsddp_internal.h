@@ -28,15 +28,22 @@ constexpr int MAXP = 16;
 // download.
 constexpr int KCW = 12 * 24;
 
-// compact LQ record per control slot
-constexpr int LQ_SE = 0;                 // 15  A - I, eul rows
-constexpr int LQ_SW = LQ_SE + 15;        // 51  A - I, omega rows
-constexpr int LQ_BW = LQ_SW + 51;        // 36  B, omega rows x GRF cols
-constexpr int LQ_LX = LQ_BW + 36;        // 24
-constexpr int LQ_LU = LQ_LX + 24;        // 24
-constexpr int LQ_RB = LQ_LU + 24;        // 24  dt * ReB Hessian, 4 legs x sym 3x3 (00,01,02,11,12,22)
-constexpr int LQW = LQ_RB + 24;          // 174
-constexpr int LQW32 = 176;               // fp32 record stride: LQW padded to 16-byte pieces
+// compact LQ record per control slot.  Every piece starts at an even index (16-byte aligned in
+// fp64); the slot after SE and after SW is an exact zero (written by k_lq) that the sweep's
+// lane-indexed reads use for structurally absent entries.
+constexpr int LQ_SE = 0;                 // 15  A - I, eul rows (+1 zero)
+constexpr int LQ_SW = 16;                // 51  A - I, omega rows (+1 zero)
+constexpr int LQ_BW = 68;                // 36  B, omega rows x GRF cols
+constexpr int LQ_LX = 104;               // 24
+constexpr int LQ_LU = 128;               // 24
+constexpr int LQ_RB = 152;               // 24  dt * ReB Hessian, 4 legs x sym 3x3 (00,01,02,11,12,22)
+constexpr int LQW = 176;
+constexpr int LQW32 = 176;               // fp32 record stride (16-byte pieces)
+static_assert(LQ_SE + 15 < LQ_SW && LQ_SW + 51 < LQ_BW && LQ_BW + 36 == LQ_LX && LQ_LX + 24 == LQ_LU &&
+              LQ_LU + 24 == LQ_RB && LQ_RB + 24 == LQW, "record layout");
+
+// longest regularisation schedule of one failed sweep (HSDDP_MAX_REG_ATTEMPTS, include/hsddp.h)
+constexpr int MAX_REG_ATTEMPTS = 64;
 
 constexpr int TM_PHIX = 0;
 constexpr int TM_PHIXX = 24;

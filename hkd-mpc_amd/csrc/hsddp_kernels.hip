@@ -130,6 +130,8 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     for (int j = 0; j < SW_N; ++j) rec.set(LQ_SW + j, Sw[j]);
 #pragma unroll
     for (int j = 0; j < BW_N; ++j) rec.set(LQ_BW + j, Bw[j]);
+    rec.set(LQ_SE + SE_N, 0.0);  // the record's two zero slots (hsddp_internal.h)
+    rec.set(LQ_SW + SW_N, 0.0);
     // lx: tracking + foot regularisation (HKDCost.cpp:22-37)
     double lx[NX];
 #pragma unroll

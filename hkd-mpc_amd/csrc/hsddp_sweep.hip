@@ -1,0 +1,796 @@
+// hsddp_sweep.hip — the regularised backward Riccati sweep, two elements per wave (gfx950).
+//
+// MultiPhaseDDP::backward_sweep_regularized / backward_sweep (HSDDPSolver/source/
+// MultiPhaseDDP.cpp:141-229) over SinglePhase::backward_sweep (SinglePhase.cpp:298-367), with the
+// impact-aware value transfer (MultiPhaseDDP.cpp:480-484), for B independent elements.
+//
+// Mapping.  One 64-lane wave sweeps two elements ("items"), one per half-wave: lane L works on
+// item e = L >> 5 at position p = L & 31.  Both halves run the same instruction stream on their
+// own data, so nothing branches on the half.  Position p < 24 owns row p of the value Hessian H
+// (24 doubles in registers, carried from knot to knot) and, after the column exchange through
+// LDS, column p of M = H A and of Qux; position 24 carries the vector terms (S^T Gn, Qu).
+//
+// Coefficients.  A knot's LQ record and Defect[k+1] arrive in LDS by LDS-DMA (requested during
+// the previous knot's elimination).  The 128 values every lane multiplies by — A - I (69
+// non-zeros), B's omega rows (36), Defect (24) — are spread over the 16 lanes of each DPP row,
+// eight registers per lane, and enter the multiply-adds through row_newbcast broadcasts
+// (v_fmac_f64_dpp): a broadcast coefficient costs no instruction, and the sparsity of A and B is
+// compile-time, so each product issues exactly its non-zero multiply-adds.
+//
+// Per knot (row r of the element on each lane, all sums over the structural non-zeros):
+//   Gn = G + H d;  T = H B_c;  M = H A                         (rows in registers)
+//   M, T rows -> LDS; lane c reads column c of M
+//   Z = M + (S^T M)^T (row c);  Qux_c column c = B_c^T M[:, c];  position 24: S^T Gn, Qu_c
+//   Qxx = lxx + reg I + (Z + Z^T) / 2  (lxx, reg added in LDS by ds_add_f64, transposed read)
+//   Quu_cc column q = luu + reg + B_c^T T[:, q]    (T columns from LDS)
+//   Gauss-Jordan on [Quu_cc | Qux_c | Qu_c]: 12 pivot steps, columns in lanes, pivots by DPP
+//   K = -Quu_cc^-1 Qux_c, dU, G = Qx - Qux_c^T Quu_cc^-1 Qu_c, dV
+//   H = Qxx - Qux_c^T Quu_cc^-1 Qux_c on the matrix cores (v_mfma_f64_16x16x4_f64, symmetric tiles)
+// Only the 12 coupled controls (those whose B column is non-zero, hsddp_backward.hip notes) enter
+// the elimination; the other 12 are decoupled: K row 0, dU = -lu / (dt R + reg), exactly as the
+// reference's dense 24-control solve gives them.  PSD test: every elimination pivot of Quu_cc and
+// every decoupled diagonal must exceed 1e-9 (the reference's LDLT of Quu - 1e-9 I).
+//
+// Templates on `real`: double (the reference's T = double) and float (config C5's fp32 mode).
+#include "hsddp_wave.h"
+
+namespace hsddp {
+
+using namespace hkd;
+
+namespace sweep {
+
+// stage boundary: LDS accesses stay in their stage and the scheduler does not interleave stages
+// (which would keep both stages' operands live)
+#define SSYNC()                              \
+    do {                                     \
+        asm volatile("" ::: "memory");       \
+        __builtin_amdgcn_sched_barrier(0);   \
+    } while (0)
+
+constexpr int HC = 12;        // coupled controls per knot
+constexpr int MS = 26;        // M / Z / P image row stride (reals): conflict-free rows and columns
+constexpr int TS = 14;        // T / Qux^T / Kp^T image row stride
+constexpr int WS = 25;        // W image row stride (phase boundary)
+// coefficient vector V of a knot image: record [0, 104) = SE | SW | BW, then Defect[k+1] (24), then
+// record [104, 176) = LX | LU | RB
+constexpr int V_SE = LQ_SE, V_SW = LQ_SW, V_BW = LQ_BW, V_D = 104, V_LX = 128, V_LU = 152, V_RB = 176, VW = 200;
+static_assert(LQ_BW + 36 == V_D && LQ_LX + 24 == V_LX && LQ_LU + 24 == V_LU && LQ_RB + 24 == V_RB, "image layout");
+
+template <typename real>
+struct alignas(16) Lds {
+    real img[2][VW];               // knot images of the two items (one DMA target)
+    real zero[32];                 // exact zeros: reads standing for structurally absent entries
+    struct alignas(16) Item {
+        real TI[24 * TS];          // T rows, then Qux^T rows (25: row 24 = Qu_c)
+        real MI[25 * MS];          // M rows (col 24 = Gn) -> Z rows (row 24 = S^T Gn) -> Kp^T rows -> P rows; W at phase ends
+        real du[24];
+        real pc[8];                // bv[4], bq[4] of the phase
+    } it[2];
+};
+static_assert(sizeof(Lds<double>) <= 20480, "two waves per SIMD on 160 KB of LDS need <= 20 KB per wave");
+
+// knot image pieces (16 bytes) of one item: the record's coefficient part, Defect[k+1], the rest
+template <typename real>
+struct Pieces {
+    static constexpr int E = 16 / sizeof(real);
+    static constexpr int NA = V_D / E, ND = NX / E, NR = (LQW - V_D) / E, NP = NA + ND + NR;
+    static constexpr int NI = (2 * NP + 63) / 64;  // DMA instructions per wave
+    static_assert(NP * E == VW && V_D % E == 0, "16-byte pieces");
+};
+
+template <typename real> struct Prec;
+template <> struct Prec<double> {
+    static DEV const double *lq(const Bufs &d) { return d.lq; }
+    static DEV double *K(const Bufs &d) { return d.K; }
+    static DEV const double *def(const Bufs &d) { return d.Defect; }
+    static constexpr int LQS = LQW;
+};
+template <> struct Prec<float> {
+    static DEV const float *lq(const Bufs &d) { return d.lq32; }
+    static DEV float *K(const Bufs &d) { return d.K32; }
+    static DEV const float *def(const Bufs &d) { return d.def32; }
+    static constexpr int LQS = LQW32;
+};
+
+// One sweep item: element, regularisation, outputs (gain rows, dU rows) and whether it runs.
+template <typename real>
+struct Item {
+    int b;          // element (valid even when inactive: its rows are read, never written)
+    bool act;       // this half sweeps
+    real reg;
+    real *K;        // [Kc][12][24]
+    double *dU;     // [Kc][24]
+};
+
+// Per-lane constants of a phase (contacts of the lane's item); the B entries of the contacts
+// (bv, bq) live in LDS (Lds::Item::pc), read where they are used.
+template <typename real>
+struct Phase {
+    int cmask;      // bit l: leg l in stance
+    int xmask;      // row pp's lxx cross terms present (bit t; see Lane::xc0)
+    real lxd;       // row pp < 24: lxx diagonal
+    real xw;        // row pp: magnitude of its lxx cross terms (each is -xw)
+    real dtr;       // Quu column lane: dt R of its coupled control (stance: GRF, swing: qJd)
+    real dtrz;      // position pp < 12: dt R of its decoupled control
+};
+
+// Phase layout entries with a runtime phase index, read from the kernel-argument segment (scalar
+// loads): indexing the by-value Params directly makes the compiler copy it to scratch.
+DEV const __attribute__((address_space(4))) Params *kparams()
+{
+    return (const __attribute__((address_space(4))) Params *)__builtin_amdgcn_kernarg_segment_ptr();
+}
+DEV int phase_N(int i) { return kparams()->N[i]; }
+DEV int phase_s0(int i) { return kparams()->s0[i]; }
+DEV int phase_k0(int i) { return kparams()->k0[i]; }
+
+template <typename real>
+DEV void load_phase(const Params &p, const Bufs &d, typename Lds<real>::Item &I, int b, int i, int pp, Phase<real> &ph)
+{
+    const int *cs = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
+    int c[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) c[l] = cs[l];
+    ph.cmask = 0;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) ph.cmask |= (c[l] != 0) << l;
+    SSYNC();
+    if (pp < 8) {  // B rows 9..11 (dt c_l / m) and 12..23 (dt (1 - c_l)) of leg pp % 4
+        const int cl = (ph.cmask >> (pp & 3)) & 1;
+        I.pc[pp] = pp < 4 ? (cl ? (real)p.dt_m : (real)0) : (cl ? (real)0 : (real)p.dt);
+    }
+    SSYNC();
+    const int pos = pp & 15, cq = (ph.cmask >> ((pos / 3) & 3)) & 1;
+    ph.dtr = (real)(p.dt * (cq ? p.r_grf : p.r_qJd));
+    const int cz = (ph.cmask >> ((pp < HC ? pp : 0) / 3)) & 1;
+    ph.dtrz = (real)(p.dt * (cz ? p.r_qJd : p.r_grf));
+    // lxx row pp (HKDCost.cpp:32: dt Q + dt D^T Qfoot D)
+    const int r = pp < NX ? pp : 0;
+    double dg = p.dt * (r < 12 ? kparams()->qbase[r] : p.q_qJ * (1 - ((ph.cmask >> ((r - 12) / 3)) & 1)));
+    ph.xmask = 0;
+    ph.xw = 0;
+    if (r >= 3 && r < 6) {
+        const double fw = p.dt * (p.foot_gain * kparams()->foot_w[r - 3]);
+#pragma unroll
+        for (int l = 0; l < 4; ++l) dg += c[l] ? fw : 0.0;
+        ph.xmask = ph.cmask;
+        ph.xw = (real)fw;
+    } else if (r >= 12) {
+        const int m = r - 12;
+        const double w = ((ph.cmask >> (m / 3)) & 1) ? p.dt * (p.foot_gain * kparams()->foot_w[m % 3]) : 0.0;
+        dg += w;
+        ph.xmask = 1;
+        ph.xw = (real)w;
+    }
+    ph.lxd = (real)dg;
+}
+
+// Request the knot images (record + Defect[s+1]) of both items into S.img by LDS-DMA.  The leading
+// lgkmcnt(0) retires every LDS read of the old images first.
+template <typename real>
+DEV void fetch(Lds<real> &S, const real *rec0, const real *def0, const real *rec1, const real *def1, int lane)
+{
+    using PC = Pieces<real>;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < PC::NI; ++t) {
+        const int n = 64 * t + lane;
+        if (n < 2 * PC::NP) {
+            const int e = n >= PC::NP, q = n - e * PC::NP;
+            const real *rec = e ? rec1 : rec0, *def = e ? def1 : def0;
+            const real *src = q < PC::NA ? rec + PC::E * q : q < PC::NA + PC::ND ? def + PC::E * (q - PC::NA)
+                                                                                 : rec + PC::E * (q - PC::ND);
+            lds_dma16(src, (unsigned)(size_t)(&S.img[0][0]) + 1024u * t);
+        }
+    }
+}
+
+// RB (sym 3x3, stored 00,01,02,11,12,22) index of entry (a, b)
+DEV constexpr int rb_index(int a, int b)
+{
+    return (a < b ? a : b) == 0 ? (a > b ? a : b) : (a < b ? a : b) == 1 ? 2 + (a > b ? a : b) : 5;
+}
+
+// Per-lane constants of the whole sweep (lane roles, LDS addresses)
+struct Lane {
+    int lane, e, pp, pos;
+    bool row;       // pp < 24
+    bool qlane;     // a Quu_cc column lane (pos < 12)
+    int rb[3];      // image index of this Quu column's ReB row (leg pos / 3, axis pos % 3)
+    int rbdiag;
+    int xc0, xkind;  // lxx cross terms of row pp: kind 1 (rows 3..5): columns xc0 + 3 t; kind 2 (rows >= 12): xc0
+};
+
+// One knot of SinglePhase::backward_sweep for the wave's two items.  h / g: H[k+1] row pp and
+// G[k+1][pp] on entry, H[k], G[k] on exit.  live: this half's item is still sweeping (turns false
+// at a failed PSD test: nothing of this knot or below is written).  more: the next knot's images
+// are requested into S.img during the elimination (nrec*/ndef*).
+template <typename real>
+DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &ph, const Item<real> &it, int kc,
+              real (&h)[NX], real &g, bool &live, real &dV1, real &dV2, bool more, const real *nrec0,
+              const real *ndef0, const real *nrec1, const real *ndef1)
+{
+    typename Lds<real>::Item &I = S.it[L.e];
+    const real *img = S.img[L.e];
+    const int pp = L.pp, pos = L.pos;
+    const real dt = (real)p.dt;
+    real reg = it.reg;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this knot's images (and the last knot's stores)
+    // coefficient registers: V[16 k + pos] on register k of every DPP row
+    real cf[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cf[k] = img[16 * k + pos];
+    // ---- Gn = G + H d (SinglePhase.cpp:320), T = H B_c, M = H A (rows) ------------------------
+    real gn = g;
+    static_for<NX>([&](auto C) { vfma<V_D + C>(gn, cf, h[C]); });
+    real bv[4], bq[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) { bv[l] = I.pc[l]; bq[l] = I.pc[4 + l]; }
+    real t[HC];
+    static_for<HC>([&](auto Q) {
+        constexpr int q = Q;
+        real a = h[9 + q % 3] * bv[q / 3];
+        a = __builtin_fma(h[12 + q], bq[q / 3], a);
+        vfma<V_BW + q>(a, cf, h[6]);
+        vfma<V_BW + 12 + q>(a, cf, h[7]);
+        vfma<V_BW + 24 + q>(a, cf, h[8]);
+        t[q] = a;
+    });
+    real m[NX];
+    static_for<NX>([&](auto Cc) {
+        constexpr int c = Cc, qe = se_index(c), qw = sw_index(c);
+        real a = h[c];
+        if constexpr (qe >= 0) {
+            vfma<V_SE + qe>(a, cf, h[0]);
+            vfma<V_SE + 5 + qe>(a, cf, h[1]);
+            vfma<V_SE + 10 + qe>(a, cf, h[2]);
+        }
+        if constexpr (c >= 9 && c < 12) a = __builtin_fma(h[c - 6], dt, a);
+        if constexpr (qw >= 0) {
+            vfma<V_SW + qw>(a, cf, h[6]);
+            vfma<V_SW + 17 + qw>(a, cf, h[7]);
+            vfma<V_SW + 34 + qw>(a, cf, h[8]);
+        }
+        m[c] = a;
+    });
+    pin(t);
+    pin(m);
+    if (L.row) {
+#pragma unroll
+        for (int c = 0; c < NX; ++c) I.MI[pp * MS + c] = m[c];
+        I.MI[pp * MS + NX] = gn;
+#pragma unroll
+        for (int q = 0; q < HC; ++q) I.TI[pp * TS + q] = t[q];
+    }
+    SSYNC();
+    // ---- column pp of M (position 24: Gn); Z row, Qux_c column, Qu_c ---------------------------
+    const int pc = pp < MS - 1 ? pp : MS - 1;
+    real mc[NX];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) mc[j] = I.MI[j * MS + pc];
+    // Z[pp][i] = M[pp][i] + sum_k M[k][pp] S[k][i] (S^T M transposed); position 24: (S^T Gn)[i]
+    static_for<NX>([&](auto Ii) {
+        constexpr int i = Ii, qe = se_index(i), qw = sw_index(i);
+        real a = m[i];
+        if constexpr (qe >= 0) {
+            vfma<V_SE + qe>(a, cf, mc[0]);
+            vfma<V_SE + 5 + qe>(a, cf, mc[1]);
+            vfma<V_SE + 10 + qe>(a, cf, mc[2]);
+        }
+        if constexpr (i >= 9 && i < 12) a = __builtin_fma(mc[i - 6], dt, a);
+        if constexpr (qw >= 0) {
+            vfma<V_SW + qw>(a, cf, mc[6]);
+            vfma<V_SW + 17 + qw>(a, cf, mc[7]);
+            vfma<V_SW + 34 + qw>(a, cf, mc[8]);
+        }
+        m[i] = a;  // Z row
+    });
+    // Qux_c[q][pp] = (B_c^T M)[q][pp] (lux = 0); position 24: Qu_c = lu_c + B_c^T Gn
+    const real *lcp[4];  // lu of each leg's coupled controls on position 24, zeros elsewhere
+#pragma unroll
+    for (int l = 0; l < 4; ++l) lcp[l] = pp == NX ? img + V_LU + (((ph.cmask >> l) & 1) ? 3 * l : 12 + 3 * l) : S.zero;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) { bv[l] = I.pc[l]; bq[l] = I.pc[4 + l]; }
+    real w2[HC];
+    static_for<HC>([&](auto Q) {
+        constexpr int q = Q;
+        real a = lcp[q / 3][q % 3];
+        a = __builtin_fma(mc[9 + q % 3], bv[q / 3], a);
+        a = __builtin_fma(mc[12 + q], bq[q / 3], a);
+        vfma<V_BW + q>(a, cf, mc[6]);
+        vfma<V_BW + 12 + q>(a, cf, mc[7]);
+        vfma<V_BW + 24 + q>(a, cf, mc[8]);
+        w2[q] = a;
+    });
+    pin(m);
+    pin(w2);
+    // ---- Qxx = lxx + reg I + (Z + Z^T) / 2 (SinglePhase.cpp:323-352) ---------------------------
+    if (pp <= NX) {  // Z rows (two zero columns: the column reads of positions > 24 see zeros)
+#pragma unroll
+        for (int c = 0; c < NX; ++c) I.MI[pp * MS + c] = m[c];
+        I.MI[pp * MS + NX] = 0;
+        I.MI[pp * MS + NX + 1] = 0;
+    }
+    SSYNC();
+    if (L.row) {
+        atomicAdd(&I.MI[pp * MS + pp], ph.lxd + reg);
+#pragma unroll
+        for (int t2 = 0; t2 < 4; ++t2) {
+            const int col = L.xkind == 1 ? L.xc0 + 3 * t2 : (L.xkind == 2 && t2 == 0) ? L.xc0 : MS - 1;
+            atomicAdd(&I.MI[pp * MS + col], ((ph.xmask >> t2) & 1) ? -ph.xw : (real)0);
+        }
+    }
+    SSYNC();
+    const real *zrow = L.row ? I.MI + pp * MS : S.zero;
+    real qxx[NX];
+#pragma unroll
+    for (int c = 0; c < NX; ++c) qxx[c] = zrow[c];
+#pragma unroll
+    for (int c = 0; c < NX; ++c) qxx[c] = (qxx[c] + I.MI[c * MS + pc]) * (real)0.5;
+    pin(qxx);  // materialised here, not sunk to the value update (twice the registers across the elimination)
+    // Qx = lx + A^T Gn = lx + Gn + S^T Gn
+    const real qx = img[V_LX + (L.row ? pp : 0)] + (gn + I.MI[NX * MS + pc]);
+    // ---- Quu_cc column pos = luu + reg + B_c^T T[:, pos] (SinglePhase.cpp:324, MultiPhaseDDP.cpp:160)
+    if (L.qlane && pp < HC) atomicAdd((real *)&img[L.rbdiag], ph.dtr + reg);  // dt R + reg on the diagonal
+    SSYNC();
+    real tcol[18];
+#pragma unroll
+    for (int j = 0; j < 18; ++j) tcol[j] = I.TI[(6 + j) * TS + pos];
+    real lbr[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) lbr[a] = (L.qlane ? img + L.rb[a] : S.zero + a)[0];
+    const int lq = pos / 3;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) { bv[l] = I.pc[l]; bq[l] = I.pc[4 + l]; }
+    real w[HC];
+    static_for<HC>([&](auto Q) {
+        constexpr int q = Q;
+        real a = (L.qlane && lq == q / 3) ? lbr[q % 3] : (real)0;
+        a = __builtin_fma(tcol[3 + q % 3], bv[q / 3], a);
+        a = __builtin_fma(tcol[6 + q], bq[q / 3], a);
+        vfma<V_BW + q>(a, cf, tcol[0]);
+        vfma<V_BW + 12 + q>(a, cf, tcol[1]);
+        vfma<V_BW + 24 + q>(a, cf, tcol[2]);
+        w[q] = a;
+    });
+    pin(w);
+    // decoupled controls on positions 0..11: Qu_z = lu_z, Quu_zz = dt R_z + reg
+    const bool zl = pp < HC;
+    const int du_z = ((ph.cmask >> ((zl ? pp : 0) / 3)) & 1) ? 12 + pp : pp;  // the decoupled control of pp < 12
+    const real quz = img[zl ? V_LU + du_z : V_LU];
+    const real qzz = ph.dtrz + reg;
+    // the images are read: the next knot's are requested now (in flight during the elimination)
+    if (more) fetch(S, nrec0, ndef0, nrec1, ndef1, L.lane);
+    // ---- PSD test + Gauss-Jordan on [Quu_cc | Qux_c | Qu_c] --------------------------------------
+    real quxs[HC];  // Qux_c column pp (position 24: Qu_c), kept for G, dV and the value update
+#pragma unroll
+    for (int q = 0; q < HC; ++q) quxs[q] = w2[q];
+    pin(quxs);
+    unsigned long long bad = __builtin_amdgcn_ballot_w64(zl && !(qzz > (real)1e-9));
+    // Step j takes column j of Quu_cc from DPP position j (both DPP rows of an item hold Quu_cc).
+    // Rows already used as pivots are kept negated, so at the end w2 = -Quu_cc^-1 [Qux_c | Qu_c]
+    // = [K_c | dU_c] (the reference's explicit inverse, SinglePhase.cpp:351-356, as a solve).
+    static_for<HC>([&](auto J) {
+        constexpr int j = J;
+        const real piv = row_bcast<j>(w[j]);
+        bad |= __builtin_amdgcn_ballot_w64(!(piv > (real)1e-9));
+        const real inv = recip(piv);
+        const real nf = -(w[j] * inv), nf2 = -(w2[j] * inv);
+        // the right-hand sides first: they read the pivot column (w[i] on lane j) before it changes
+        static_for<HC>([&](auto Ii) {
+            constexpr int i = Ii;
+            if constexpr (i != j) bfma<j>(w2[i], w[i], nf2);
+        });
+        static_for<HC>([&](auto Ii) {
+            constexpr int i = Ii;
+            if constexpr (i != j) fmac_row_bcast<j, false>(w[i], nf);
+        });
+        w[j] = nf;
+        w2[j] = nf2;
+    });
+    const bool okh = L.e ? (bad >> 32) == 0 : (bad & 0xffffffffull) == 0;
+    live = live && okh;
+    const bool st = live;  // this half writes the knot's outputs
+    // ---- outputs: K_c rows, dU, dV (SinglePhase.cpp:354-362) -----------------------------------
+    real *Kg = it.K + (size_t)kc * KCW;
+    if (st && L.row)
+#pragma unroll
+        for (int q = 0; q < HC; ++q) Kg[q * NX + pp] = w2[q];
+    if (pp == NX)  // coupled dU from position 24
+#pragma unroll
+        for (int q = 0; q < HC; ++q) I.du[(((ph.cmask >> (q / 3)) & 1) ? 0 : 12) + q] = w2[q];
+    const real duz = -(quz / qzz);
+    if (zl) I.du[du_z] = duz;
+    // expected cost change Qu^T Quu^-1 Qu: position 24 (coupled) + positions 0..11 (decoupled)
+    real dvp = 0;
+#pragma unroll
+    for (int q = 0; q < HC; ++q) dvp = __builtin_fma(quxs[q], w2[q], dvp);  // -Qu_c^T Quu_cc^-1 Qu_c
+    dvp = pp == NX ? dvp : zl ? quz * duz : (real)0;
+    const real dvk = -half_sum(dvp);
+    if (st) { dV1 -= dvk; dV2 += dvk; }
+    // Kp^T rows (negated: K_c^T) for the value update; Qux_c^T rows
+    if (pp <= NX)
+#pragma unroll
+        for (int q = 0; q < HC; ++q) I.MI[pp * TS + q] = w2[q];
+    if (L.row)
+#pragma unroll
+        for (int q = 0; q < HC; ++q) I.TI[pp * TS + q] = quxs[q];
+    SSYNC();
+    if (st && L.row) it.dU[(size_t)kc * NX + pp] = I.du[pp];
+    // G = Qx - Qux_c^T Quu_cc^-1 Qu_c = Qx + Qux_c^T dU_c (row 24 of the K^T image holds dU_c)
+    real gq = qx;
+#pragma unroll
+    for (int q = 0; q < HC; ++q) gq = __builtin_fma(quxs[q], I.MI[NX * TS + q], gq);
+    // ---- H = Qxx - Qux_c^T Quu_cc^-1 Qux_c = Qxx + Qux_c^T K_c on the matrix cores ------------------
+    // (tiles (0,0), (0,1), (1,1) of the symmetric 24 x 24 product, K = 12; rows / columns 24..31
+    // only feed discarded outputs).  One item after the other, every lane on the item's tiles.
+    const int li = L.lane & 15, lk = L.lane >> 4;
+#pragma unroll
+    for (int ei = 0; ei < 2; ++ei) {
+        typename Lds<real>::Item &J = S.it[ei];
+        real a0[3], a1[3], b0[3], b1[3];
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+            const int q = 4 * ks + lk;
+            a0[ks] = J.TI[li * TS + q];
+            a1[ks] = J.TI[(16 + li) * TS + q];
+            b0[ks] = J.MI[li * TS + q];
+            b1[ks] = J.MI[(16 + li) * TS + q];
+        }
+        acc4<real> t00 = {0, 0, 0, 0}, t01 = t00, t11 = t00;
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+            t00 = mfma16(a0[ks], b0[ks], t00);
+            t01 = mfma16(a0[ks], b1[ks], t01);
+            t11 = mfma16(a1[ks], b1[ks], t11);
+        }
+        SSYNC();  // the operands are in registers: the product overwrites the K^T image
+#pragma unroll
+        for (int gi = 0; gi < 4; ++gi) {
+            const int r0 = mfma_row<real>(lk, gi), r1 = 16 + r0, c1 = 16 + li;
+            J.MI[r0 * MS + li] = t00[gi];
+            if (c1 < NX) {
+                J.MI[r0 * MS + c1] = t01[gi];
+                J.MI[c1 * MS + r0] = t01[gi];
+            }
+            if (r1 < NX && c1 < NX) J.MI[r1 * MS + c1] = t11[gi];
+        }
+    }
+    SSYNC();
+    const real *prow = L.row ? I.MI + pp * MS : S.zero;
+#pragma unroll
+    for (int c = 0; c < NX; ++c) h[c] = qxx[c] + prow[c];
+    g = L.row ? gq : (real)0;
+    SSYNC();
+}
+
+// MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229) for the wave's two items with their
+// own regularisation.  Returns, per half, -1 (success) or the control slot of the first knot whose
+// Quu fails the PSD test (that knot and the ones below it are not written).
+template <typename real>
+DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, const Item<real> &it, real &dV1,
+                   real &dV2)
+{
+    const int pp = L.pp;
+    const real *lqg = Prec<real>::lq(d), *defg = Prec<real>::def(d);
+    // the other item of the wave (its element's records feed the DMA even when this half is idle)
+    const int b = it.b, bo = __shfl_xor(it.b, 32);
+    const int b0 = L.e ? bo : b, b1 = L.e ? b : bo;
+    bool live = it.act;
+    int fail = -1;
+    real h[NX], g = 0;
+    dV1 = 0; dV2 = 0;
+    for (int i = p.P - 1; i >= 0; --i) {
+        Phase<real> ph;
+        load_phase<real>(p, d, S.it[L.e], b, i, pp, ph);
+        const double *rec = d.term + ((size_t)b * p.P + i) * TW;
+        if (i == p.P - 1) {
+#pragma unroll
+            for (int c = 0; c < NX; ++c) h[c] = L.row ? (real)rec[TM_PHIXX + pp * NX + c] : (real)0;
+            g = L.row ? (real)rec[TM_PHIX + pp] : (real)0;
+        } else {
+            // impact-aware step G' = Phix + Px^T G0, H' = Phixx + Px^T H0 Px (MultiPhaseDDP.cpp:480-484):
+            // W = H0 Px by rows (Px by DPP broadcast), then row pp of W^T Px from column pp of W
+            typename Lds<real>::Item &I = S.it[L.e];
+            const double *Px = rec + TM_PX;
+            // W = H0 Px by rows: Px in three 8-row chunks of DPP-broadcast coefficients
+            real wr[NX];
+#pragma unroll
+            for (int c = 0; c < NX; ++c) wr[c] = 0;
+            static_for<3>([&](auto Kc) {
+                real px[12];
+#pragma unroll
+                for (int k = 0; k < 12; ++k) px[k] = (real)Px[192 * Kc + 16 * k + L.pos];
+                static_for<8>([&](auto Kk) {
+                    static_for<NX>([&](auto Cc) { vfma<NX * Kk + Cc>(wr[Cc], px, h[8 * Kc + Kk]); });
+                });
+            });
+            SSYNC();
+            if (L.row) {
+#pragma unroll
+                for (int c = 0; c < NX; ++c) I.MI[pp * WS + c] = wr[c];
+                I.MI[pp * WS + NX] = g;  // column 24: G0
+            }
+            SSYNC();
+            const int pc = pp < NX ? pp : NX;
+            real wc[NX];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) wc[j] = I.MI[j * WS + pc];
+            real vr[NX];
+#pragma unroll
+            for (int c = 0; c < NX; ++c) vr[c] = 0;
+            static_for<3>([&](auto Kc) {
+                real px[12];
+#pragma unroll
+                for (int k = 0; k < 12; ++k) px[k] = (real)Px[192 * Kc + 16 * k + L.pos];
+                static_for<8>([&](auto Jj) {
+                    static_for<NX>([&](auto Cc) { vfma<NX * Jj + Cc>(vr[Cc], px, wc[8 * Kc + Jj]); });
+                });
+            });
+            SSYNC();
+            if (pp == NX)
+#pragma unroll
+                for (int c = 0; c < NX; ++c) I.MI[NX * WS + c] = vr[c];  // Px^T G0
+            SSYNC();
+            const real gp = I.MI[NX * WS + (L.row ? pp : 0)];
+#pragma unroll
+            for (int c = 0; c < NX; ++c) h[c] = L.row ? (real)rec[TM_PHIXX + pp * NX + c] + vr[c] : (real)0;
+            g = L.row ? (real)rec[TM_PHIX + pp] + gp : (real)0;
+            SSYNC();
+        }
+        const int N = phase_N(i), s0 = phase_s0(i), k0 = phase_k0(i);
+        auto recp = [&](int bb, int k) { return lqg + ((size_t)bb * p.Kc + k0 + k) * Prec<real>::LQS; };
+        auto defp = [&](int bb, int k) { return defg + ((size_t)bb * p.S + s0 + k + 1) * NX; };
+        fetch(S, recp(b0, N - 1), defp(b0, N - 1), recp(b1, N - 1), defp(b1, N - 1), L.lane);
+        int k = N - 1;
+#pragma unroll 1
+        for (; k >= 0; --k) {
+            const bool more = k > 0;
+            const int kn = more ? k - 1 : 0;
+            const bool was = live;
+            knot(p, S, L, ph, it, k0 + k, h, g, live, dV1, dV2, more, recp(b0, kn), defp(b0, kn), recp(b1, kn),
+                 defp(b1, kn));
+            if (was && !live) fail = k0 + k;
+            if (!__builtin_amdgcn_ballot_w64(live)) break;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA left in flight
+        if (!__builtin_amdgcn_ballot_w64(live)) break;
+        // G[0] += H[0] Defect[0] (SinglePhase.cpp:365)
+        const real *d0 = defg + ((size_t)b * p.S + s0) * NX;
+        real dc[2] = {d0[L.pos], L.pos < NX - 16 ? d0[16 + L.pos] : (real)0};
+        real a = 0;
+        static_for<NX>([&](auto Cc) { vfma<Cc>(a, dc, h[Cc]); });
+        if (L.row) g += a;
+    }
+    return it.act ? fail : -1;
+}
+
+// ElemState cost / feasibility of element b at the start of the inner iteration
+// (MultiPhaseDDP.cpp:306-307; the reference's summation order)
+DEV void element_cost(const Params &p, const Bufs &d, int b, double &cost, double &feas)
+{
+    cost = 0.0; feas = 0.0;
+    for (int i = 0; i < p.P; ++i) {
+        double ci = 0.0, fi = 0.0;
+        const int N = phase_N(i), s0 = phase_s0(i);
+        for (int k = 0; k < N; ++k) ci += d.slot_cost[(size_t)b * p.S + s0 + k];
+        ci += d.slot_cost[(size_t)b * p.S + s0 + N];
+        for (int k = 0; k <= N; ++k) fi += d.slot_feas[(size_t)b * p.S + s0 + k];
+        cost += ci;
+        feas += fi;
+    }
+    feas = sqrt(feas);
+}
+
+DEV Lane make_lane()
+{
+    Lane L;
+    L.lane = threadIdx.x;
+    L.e = L.lane >> 5;
+    L.pp = L.lane & 31;
+    L.pos = L.lane & 15;
+    L.row = L.pp < NX;
+    L.qlane = L.pos < HC;
+    const int lq = (L.qlane ? L.pos : 0) / 3, aq = L.pos % 3;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) L.rb[a] = V_RB + 6 * lq + rb_index(aq, a);
+    L.rbdiag = V_RB + 6 * lq + rb_index(aq, aq);
+    L.xkind = (L.pp >= 3 && L.pp < 6) ? 1 : (L.pp >= 12 && L.pp < NX) ? 2 : 0;
+    L.xc0 = L.xkind == 1 ? 12 + (L.pp - 3) : L.xkind == 2 ? 3 + (L.pp - 12) % 3 : MS - 1;
+    return L;
+}
+
+template <typename real>
+DEV void zero_init(Lds<real> &S, int lane)
+{
+    if (lane < 32) S.zero[lane] = 0;
+    SSYNC();
+}
+
+}  // namespace sweep
+
+using namespace sweep;
+
+// backward_sweep_regularized (MultiPhaseDDP.cpp:141-181) for elements 2 blockIdx and 2 blockIdx + 1:
+// the sweep with each element's mu, then (for an element whose first sweep fails and that the
+// parallel retry cannot take) mu = max(mu * update_regularization, 1e-3) until a sweep succeeds or
+// mu > 1e2, then mu / 20 (0 below 1e-6) as the next regularisation.
+template <typename real>
+__global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
+{
+    __shared__ Lds<real> S;
+    const Lane L = make_lane();
+    zero_init(S, L.lane);
+    const int b = 2 * blockIdx.x + L.e;
+    const bool valid = b < p.B;
+    const int bv = valid ? b : p.B - 1;
+    ElemState &E = d.el[bv];
+    bool act = valid && !E.done && !E.inner_done;
+    if (!__builtin_amdgcn_ballot_w64(act)) return;
+    double reg = E.reg;
+    Item<real> it;
+    it.b = bv;
+    it.K = Prec<real>::K(d) + (size_t)bv * p.Kc * KCW;
+    it.dU = d.dU + (size_t)bv * p.Kc * NX;
+    bool need = act, ok = false;
+    real dV1 = 0, dV2 = 0;
+    for (int attempt = 0; __builtin_amdgcn_ballot_w64(need); ++attempt) {
+        it.act = need;
+        it.reg = (real)reg;
+        const int fk = sweep_pair(p, d, S, L, it, dV1, dV2);
+        if (need) {
+            if (fk < 0) {
+                ok = true;
+                need = false;
+            } else {
+                bool deferred = false;
+                if (attempt == 0 && p.retry_cap > 0) {
+                    // the retries run in parallel in k_riccati_retry (the first retry_cap failures
+                    // of this launch); k_riccati_select takes the first mu that succeeds
+                    int f = 0;
+                    if (L.pp == 0) {
+                        f = atomicAdd(d.retry_count, 1);
+                        if (f < p.retry_cap) d.retry_list[f] = RetryEntry{bv, 0, reg};
+                    }
+                    f = __shfl(f, L.lane & 32);
+                    deferred = f < p.retry_cap;
+                }
+                if (deferred) {
+                    need = false;
+                    if (L.pp == 0) {
+                        double cost, feas;
+                        element_cost(p, d, bv, cost, feas);
+                        E.iters += 1; E.cost = cost; E.feas = feas; E.accepted = 0;
+                    }
+                    act = false;  // finished by k_riccati_select
+                } else {
+                    reg = fmax(reg * p.update_regularization, 1e-03);
+                    if (reg > 1e2 || attempt >= MAX_REG_ATTEMPTS) need = false;  // goto bad_solve
+                }
+            }
+        }
+    }
+    if (act && L.pp == 0) {
+        double cost, feas;
+        element_cost(p, d, bv, cost, feas);
+        double rn = reg / 20;
+        if (rn < 1e-06) rn = 0;
+        E.iters += 1; E.cost = cost; E.feas = feas; E.accepted = 0;
+        if (ok) E.reg = rn;
+        else { E.reg = rn; E.status = 1; E.done = 1; E.ls_active = 0; }
+    }
+}
+
+// The retries of backward_sweep_regularized for the elements k_riccati deferred, all at once:
+// item (f, a) sweeps deferred element f with the a-th next mu of the schedule into its own scratch
+// rows, two items per wave.  Every attempt is the sweep the sequential loop would run with that mu,
+// so taking the first success (k_riccati_select) gives the loop's result.
+template <typename real>
+__global__ __launch_bounds__(64, 2) void k_riccati_retry(Params p, Bufs d)
+{
+    __shared__ Lds<real> S;
+    const Lane L = make_lane();
+    zero_init(S, L.lane);
+    const int n = min(*d.retry_count, p.retry_cap);
+    const int item = 2 * blockIdx.x + L.e, f = item / p.retry_m, a = item % p.retry_m + 1;
+    bool act = f < n;
+    if (!__builtin_amdgcn_ballot_w64(act)) return;
+    const int fv = act ? f : 0;
+    const RetryEntry e = d.retry_list[fv];
+    double reg = e.reg;
+    for (int t = 0; t < a; ++t) reg = fmax(reg * p.update_regularization, 1e-03);
+    int *flag = d.retry_flag + fv * p.retry_m + (a - 1);
+    if (act && reg > 1e2) {  // past the loop's exit: never tried (the schedule is non-decreasing)
+        if (L.pp == 0) *flag = 2;
+        act = false;
+    }
+    if (!__builtin_amdgcn_ballot_w64(act)) return;
+    const size_t slot = (size_t)fv * p.retry_m + (a - 1);
+    Item<real> it;
+    it.b = e.b;
+    it.act = act;
+    it.reg = (real)reg;
+    it.K = (real *)d.retry_K + slot * p.Kc * KCW;
+    it.dU = d.retry_dU + slot * p.Kc * NX;
+    real dV1, dV2;
+    const int fk = sweep_pair(p, d, S, L, it, dV1, dV2);
+    if (act && L.pp == 0) *flag = fk < 0 ? 1 : -1 - fk;  // success, or -1 - (the failing control slot)
+}
+
+// The outcome of backward_sweep_regularized for each deferred element: the first attempt that
+// succeeded (its gains and dU rows copied to the element), mu / 20 (0 below 1e-6) as the next
+// regularisation; when none succeeds (mu passed 1e2: status 1, bad_solve) the element's rows are
+// left as the sequential loop leaves them: row kc from the last attempt that got past it.
+template <typename real>
+__global__ __launch_bounds__(64) void k_riccati_select(Params p, Bufs d)
+{
+    const int f = blockIdx.x, lane = threadIdx.x;
+    if (f >= min(*d.retry_count, p.retry_cap)) return;
+    const RetryEntry e = d.retry_list[f];
+    const size_t b = e.b;
+    double reg = e.reg;
+    int win = 0;
+    for (int a = 1; a <= p.retry_m; ++a) {
+        reg = fmax(reg * p.update_regularization, 1e-03);
+        if (reg > 1e2) break;
+        if (d.retry_flag[f * p.retry_m + a - 1] == 1) { win = a; break; }
+    }
+    real *Ko = Prec<real>::K(d) + b * p.Kc * KCW;
+    double *dUo = d.dU + b * p.Kc * NX;
+    if (win) {
+        const size_t slot = (size_t)f * p.retry_m + (win - 1);
+        const real *Ks = (const real *)d.retry_K + slot * p.Kc * KCW;
+        const double *Us = d.retry_dU + slot * p.Kc * NX;
+        for (size_t q = lane; q < (size_t)p.Kc * KCW; q += 64) Ko[q] = Ks[q];
+        for (size_t q = lane; q < (size_t)p.Kc * NX; q += 64) dUo[q] = Us[q];
+    } else {
+        const int *fl = d.retry_flag + f * p.retry_m;
+        // attempt a wrote the rows above its failing slot -1 - fl[a - 1]; attempts stop at flag 2
+        auto source = [&](int kc) {
+            int src = 0;
+            for (int a = 1; a <= p.retry_m && fl[a - 1] != 2; ++a)
+                if (-1 - fl[a - 1] < kc) src = a;
+            return src;
+        };
+        const real *K0 = (const real *)d.retry_K + (size_t)f * p.retry_m * p.Kc * KCW;
+        const double *U0 = d.retry_dU + (size_t)f * p.retry_m * p.Kc * NX;
+        for (size_t q = lane; q < (size_t)p.Kc * KCW; q += 64) {
+            const int a = source((int)(q / KCW));
+            if (a) Ko[q] = K0[(size_t)(a - 1) * p.Kc * KCW + q];
+        }
+        for (size_t q = lane; q < (size_t)p.Kc * NX; q += 64) {
+            const int a = source((int)(q / NX));
+            if (a) dUo[q] = U0[(size_t)(a - 1) * p.Kc * NX + q];
+        }
+    }
+    if (lane == 0) {
+        ElemState &E = d.el[b];
+        double rn = reg / 20;
+        if (rn < 1e-06) rn = 0;
+        E.reg = rn;
+        if (!win) { E.status = 1; E.done = 1; E.ls_active = 0; }  // goto bad_solve
+    }
+}
+
+void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
+{
+    if (p.retry_cap > 0) (void)hipMemsetAsync(d.retry_count, 0, sizeof(int), st);
+    const dim3 g1((unsigned)((p.B + 1) / 2));
+    if (p.fp32)
+        hipLaunchKernelGGL(k_riccati<float>, g1, dim3(64), 0, st, p, d);
+    else
+        hipLaunchKernelGGL(k_riccati<double>, g1, dim3(64), 0, st, p, d);
+    if (p.retry_cap > 0) {
+        const dim3 gr((unsigned)((p.retry_cap * p.retry_m + 1) / 2)), gs((unsigned)p.retry_cap);
+        if (p.fp32) {
+            hipLaunchKernelGGL(k_riccati_retry<float>, gr, dim3(64), 0, st, p, d);
+            hipLaunchKernelGGL(k_riccati_select<float>, gs, dim3(64), 0, st, p, d);
+        } else {
+            hipLaunchKernelGGL(k_riccati_retry<double>, gr, dim3(64), 0, st, p, d);
+            hipLaunchKernelGGL(k_riccati_select<double>, gs, dim3(64), 0, st, p, d);
+        }
+    }
+}
+
+}  // namespace hsddp

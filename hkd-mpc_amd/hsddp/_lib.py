@@ -120,7 +120,8 @@ def lib():
     L.hsddp_create.argtypes = [C.POINTER(ProblemDesc), C.POINTER(C.c_void_p)]
     L.hsddp_destroy.argtypes = [C.c_void_p]
     L.hsddp_set_options.argtypes = [C.c_void_p, C.POINTER(Options)]
-    L.hsddp_validate_options.argtypes = [C.POINTER(Options)]
+    if hasattr(L, "hsddp_validate_options"):  # (older A/B builds lack it)
+        L.hsddp_validate_options.argtypes = [C.POINTER(Options)]
     L.hsddp_upload_problem.argtypes = [C.c_void_p, IP, DP, DP, DP, DP]
     L.hsddp_upload_warm_start.argtypes = [C.c_void_p, DP, DP, DP]
     L.hsddp_solve.argtypes = [C.c_void_p, C.POINTER(Stats)]

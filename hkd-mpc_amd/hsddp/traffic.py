@@ -1,7 +1,7 @@
 """Algorithmic HBM bytes and fp64 FLOPs of one DDP inner iteration, per kernel.
 
 These are the bytes each kernel must move in THIS design's compact layout (hsddp_internal.h): a
-knot's LQ model is the 174-value record (A - I and B non-zeros, lx, lu, dt * ReB Hessian), the
+knot's LQ model is the 176-value record (A - I and B non-zeros, lx, lu, dt * ReB Hessian), the
 gains are the 12 coupled rows (12 x 24), lxx and luu's diagonal are rebuilt from parameters.  They
 replace SURVEY.md §8(d)'s dense per-knot model (A, B, lxx, luu, lux materialised as 24 x 24
 matrices, 88 KB per knot), which prices traffic this design never generates.
@@ -16,7 +16,7 @@ gaits) are counted.
 from __future__ import annotations
 
 NX = 24
-LQW, LQW32 = 174, 176   # compact LQ record (fp64 / fp32 stride), hsddp_internal.h
+LQW, LQW32 = 176, 176   # compact LQ record (fp64 / fp32 stride), hsddp_internal.h
 KCW = 12 * 24           # compact gain rows
 TW_PHI = 24 + 576       # Phix + Phixx per phase end
 TW_PX = 576             # reset-map Jacobian per phase boundary

@@ -162,14 +162,17 @@ def resetmap_partial(x, c, cn):
 
 # ---- solver -----------------------------------------------------------------------------------
 def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 1,
-                elements=None) -> dict:
-    """Run the oracle solve on (a subset of) a synthetic batch; returns per-element outputs."""
+                elements=None, weights: dict | None = None) -> dict:
+    """Run the oracle solve on (a subset of) a synthetic batch; returns per-element outputs.
+    weights: HKD cost-weight overrides by field name (e.g. {"r_qJd": -0.5})."""
     options = options or default_options()
     B = prob["batch"]
     idx = list(range(B)) if elements is None else list(elements)
     n = len(idx)
     S, Kc, P = prob["S"], prob["Kc"], len(prob["horizons"])
     p, hz = default_problem(prob["horizons"], prob["dt"])
+    for k, v in (weights or {}).items():
+        setattr(p.w, k, v)
     ss = None
     if prob.get("shooting") is not None:  # shooting states per phase (after a receding-horizon shift)
         ss = np.ascontiguousarray(prob["shooting"], dtype=np.int32)

@@ -19,6 +19,27 @@ __global__ void k_fma(double *out, double s)
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
 }
 
+// v_fmac_f64 with a DPP row_newbcast source (the sweep's broadcast-coefficient form)
+__global__ void k_fma_dpp(double *out, double s)
+{
+    double a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    double c = s * threadIdx.x;
+    asm volatile("s_nop 4" ::: "memory");
+    for (int i = 0; i < ITER; ++i) {
+        asm volatile("v_fmac_f64_dpp %0, %8, %9 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_fmac_f64_dpp %1, %8, %9 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_fmac_f64_dpp %2, %8, %9 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_fmac_f64_dpp %3, %8, %9 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_fmac_f64_dpp %4, %8, %9 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_fmac_f64_dpp %5, %8, %9 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_fmac_f64_dpp %6, %8, %9 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_fmac_f64_dpp %7, %8, %9 row_newbcast:8 row_mask:0xf bank_mask:0xf"
+                     : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                     : "v"(c), "v"(s));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+}
+
 __global__ void k_add32(double *out, double s)
 {
     unsigned a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
@@ -131,6 +152,9 @@ int main()
         float ms;
         ms = run(k_fma, blocks, 256, out);
         printf("wpcu %2d fma_f64   : %.2f wave-instr/cycle/CU  (%.1f TF)\n", wps, waves * ITER * 8 / (ms * 1e-3 * ghz * 1e9) / cu,
+               waves * 64 * ITER * 8 * 2 / (ms * 1e-3) / 1e12);
+        ms = run(k_fma_dpp, blocks, 256, out);
+        printf("wpcu %2d fma_f64_dpp: %.2f wave-instr/cycle/CU  (%.1f TF)\n", wps, waves * ITER * 8 / (ms * 1e-3 * ghz * 1e9) / cu,
                waves * 64 * ITER * 8 * 2 / (ms * 1e-3) / 1e12);
         ms = run(k_add32, blocks, 256, out);
         printf("wpcu %2d add_u32   : %.2f wave-instr/cycle/CU\n", wps, waves * ITER * 8 / (ms * 1e-3 * ghz * 1e9) / cu);
