@@ -40,6 +40,30 @@ using namespace hkd;
 
 namespace sweep {
 
+#ifndef HSDDP_STAMPS
+#define HSDDP_STAMPS 0
+#endif
+// In-kernel stamps (diagnostic build only, make stamps): s_memtime at the stage boundaries of a
+// knot (each after a full LDS drain, so stages do not overlap), differences summed per stage into
+// LDS and written to Bufs::dbg of the wave's first element (tools/stamps.py).
+#if HSDDP_STAMPS
+#define STAMP(n)                                                                              \
+    do {                                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        unsigned long long t_;                                                                \
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        if (threadIdx.x == 0) {                                                               \
+            if ((n) > 0) S.st[n] += t_ - S.tprev;                                             \
+            S.tprev = t_;                                                                     \
+        }                                                                                     \
+    } while (0)
+#else
+#define STAMP(n) \
+    do {         \
+    } while (0)
+#endif
+
 // stage boundary: LDS accesses stay in their stage and the scheduler does not interleave stages
 // (which would keep both stages' operands live)
 #define SSYNC()                              \
@@ -67,6 +91,9 @@ struct alignas(16) Lds {
         real du[24];
         real pc[8];                // bv[4], bq[4] of the phase
     } it[2];
+#if HSDDP_STAMPS
+    unsigned long long st[12], tprev;  // diagnostic build: cycles per knot stage
+#endif
 };
 static_assert(sizeof(Lds<double>) <= 20480, "two waves per SIMD on 160 KB of LDS need <= 20 KB per wave");
 
@@ -198,62 +225,147 @@ struct Lane {
     bool row;       // pp < 24
     bool qlane;     // a Quu_cc column lane (pos < 12)
     int rb[3];      // image index of this Quu column's ReB row (leg pos / 3, axis pos % 3)
-    int rbdiag;
     int xc0, xkind;  // lxx cross terms of row pp: kind 1 (rows 3..5): columns xc0 + 3 t; kind 2 (rows >= 12): xc0
 };
+
+// acc[c] += sum_j x[j] S[j][c] (S = A - I: rows 0..2 eul, 3..5 the dt entries, 6..8 omega) in
+// source order: consecutive multiply-adds feed different accumulators
+template <typename real>
+DEV void emit_SA(real (&acc)[NX], const real (&x)[NX], const real (&cf)[8], real dt)
+{
+    auto sw_row = [&](auto I) {
+        constexpr int i = I;
+        static_for<17>([&](auto Q) { vfma<V_SW + 17 * i + Q>(acc[sw_col(Q)], cf, x[6 + i]); });
+    };
+    auto se_row = [&](auto I) {
+        constexpr int i = I;
+        static_for<5>([&](auto Q) { vfma<V_SE + 5 * i + Q>(acc[se_col(Q)], cf, x[i]); });
+    };
+    sw_row(std::integral_constant<int, 0>{});
+    se_row(std::integral_constant<int, 0>{});
+    sw_row(std::integral_constant<int, 1>{});
+    se_row(std::integral_constant<int, 1>{});
+    sw_row(std::integral_constant<int, 2>{});
+    se_row(std::integral_constant<int, 2>{});
+#pragma unroll
+    for (int a = 0; a < 3; ++a) acc[9 + a] = __builtin_fma(x[3 + a], dt, acc[9 + a]);
+}
+
+// acc[q] += (B_c^T y)[q] for the 12 coupled controls, y = (y6, y7, y8) on B's omega rows (BW, DPP
+// broadcast), y9[a] on row 9 + a (bv: dt c / m), y12[q] on row 12 + q (bq: dt (1 - c)); the
+// structurally absent half of the last two is an exact zero
+template <typename real>
+DEV void emit_Bc(real (&acc)[HC], real y6, real y7, real y8, const real *y9, const real *y12, const real (&bv)[4],
+                 const real (&bq)[4], const real (&cf)[8])
+{
+#pragma unroll
+    for (int q = 0; q < HC; ++q) acc[q] = __builtin_fma(y12[q], bq[q / 3], acc[q]);
+#pragma unroll
+    for (int q = 0; q < HC; ++q) acc[q] = __builtin_fma(y9[q % 3], bv[q / 3], acc[q]);
+    static_for<HC>([&](auto Q) { vfma<V_BW + Q>(acc[Q], cf, y6); });
+    static_for<HC>([&](auto Q) { vfma<V_BW + 12 + Q>(acc[Q], cf, y7); });
+    static_for<HC>([&](auto Q) { vfma<V_BW + 24 + Q>(acc[Q], cf, y8); });
+}
+
+// Gauss-Jordan without pivoting on the columns held in lanes: w = Quu_cc columns (DPP positions
+// 0..11 of both DPP rows of an item), w2 = right-hand sides.  Step j takes column j from DPP
+// position j.  Rows already used as pivots are kept negated, so at the end w2 = -Quu_cc^-1 (rhs).
+// The next step's pivot chain (DPP broadcast, reciprocal, two Newton steps, the two factors) is
+// threaded through this step's independent multiply-adds, its operand row updated first.
+// bad: ballot of pivots <= 1e-9 (the PSD test).
+template <typename real>
+DEV void gauss_jordan(real (&w)[HC], real (&w2)[HC], unsigned long long &bad)
+{
+    constexpr bool F64 = sizeof(real) == 8;
+    real r, e, nf, nf2;
+    {
+        const real piv = row_bcast<0>(w[0]);
+        bad |= __builtin_amdgcn_ballot_w64(!(piv > (real)1e-9));
+        asm_rcp(r, piv);
+        asm volatile("s_nop 1" ::: "memory");
+        asm_nfma1(e, piv, r);
+        asm_newton(r, e);
+        if constexpr (F64) {
+            asm_nfma1(e, piv, r);
+            asm_newton(r, e);
+        }
+        asm_nmul(nf, w[0], r);
+        asm_nmul(nf2, w2[0], r);
+    }
+    static_for<HC>([&](auto J) {
+        constexpr int j = J, jn = j + 1;
+        constexpr bool nx = jn < HC;
+        real pivn = 0, rn = 0, en = 0, nfn = 0, nf2n = 0;
+        if constexpr (nx) {  // the next pivot's row first (right-hand side before its multiplier changes)
+            bfma<j>(w2[jn], w[jn], nf2);
+            fmac_row_bcast<j, false>(w[jn], nf);
+        }
+        constexpr int NO = nx ? HC - 2 : HC - 1;
+        static_for<2 * NO>([&](auto T) {
+            constexpr int t = T, k = t / 2;
+            constexpr int i = nx ? (j + 2 + k) % HC : k;
+            if constexpr (t % 2 == 0)
+                bfma<j>(w2[i], w[i], nf2);
+            else
+                fmac_row_bcast<j, false>(w[i], nf);
+            if constexpr (nx) {
+                if constexpr (t == 1) pivn = row_bcast<(nx ? jn : 0)>(w[jn]);
+                if constexpr (t == 3) asm_rcp(rn, pivn);
+                if constexpr (t == 5) asm_nfma1(en, pivn, rn);
+                if constexpr (t == 7) asm_newton(rn, en);
+                if constexpr (F64 && t == 9) asm_nfma1(en, pivn, rn);
+                if constexpr (F64 && t == 11) asm_newton(rn, en);
+                if constexpr (t == (F64 ? 13 : 9)) {
+                    asm_nmul(nfn, w[jn], rn);
+                    asm_nmul(nf2n, w2[jn], rn);
+                }
+            }
+        });
+        w[j] = nf;
+        w2[j] = nf2;
+        if constexpr (nx) {
+            bad |= __builtin_amdgcn_ballot_w64(!(pivn > (real)1e-9));
+            nf = nfn;
+            nf2 = nf2n;
+        }
+    });
+}
 
 // One knot of SinglePhase::backward_sweep for the wave's two items.  h / g: H[k+1] row pp and
 // G[k+1][pp] on entry, H[k], G[k] on exit.  live: this half's item is still sweeping (turns false
 // at a failed PSD test: nothing of this knot or below is written).  more: the next knot's images
-// are requested into S.img during the elimination (nrec*/ndef*).
+// are requested into S.img during the elimination (nrec*/ndef*).  The expected cost change of the
+// sweep (SinglePhase.cpp:357-358) is not formed: the MS linear rollout replaces it (quirk A3).
 template <typename real>
 DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &ph, const Item<real> &it, int kc,
-              real (&h)[NX], real &g, bool &live, real &dV1, real &dV2, bool more, const real *nrec0,
-              const real *ndef0, const real *nrec1, const real *ndef1)
+              real (&h)[NX], real &g, bool &live, bool more, const real *nrec0, const real *ndef0, const real *nrec1,
+              const real *ndef1)
 {
     typename Lds<real>::Item &I = S.it[L.e];
     const real *img = S.img[L.e];
     const int pp = L.pp, pos = L.pos;
     const real dt = (real)p.dt;
     real reg = it.reg;
+    STAMP(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this knot's images (and the last knot's stores)
     // coefficient registers: V[16 k + pos] on register k of every DPP row
     real cf[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) cf[k] = img[16 * k + pos];
-    // ---- Gn = G + H d (SinglePhase.cpp:320), T = H B_c, M = H A (rows) ------------------------
-    real gn = g;
-    static_for<NX>([&](auto C) { vfma<V_D + C>(gn, cf, h[C]); });
     real bv[4], bq[4];
 #pragma unroll
     for (int l = 0; l < 4; ++l) { bv[l] = I.pc[l]; bq[l] = I.pc[4 + l]; }
-    real t[HC];
-    static_for<HC>([&](auto Q) {
-        constexpr int q = Q;
-        real a = h[9 + q % 3] * bv[q / 3];
-        a = __builtin_fma(h[12 + q], bq[q / 3], a);
-        vfma<V_BW + q>(a, cf, h[6]);
-        vfma<V_BW + 12 + q>(a, cf, h[7]);
-        vfma<V_BW + 24 + q>(a, cf, h[8]);
-        t[q] = a;
-    });
-    real m[NX];
-    static_for<NX>([&](auto Cc) {
-        constexpr int c = Cc, qe = se_index(c), qw = sw_index(c);
-        real a = h[c];
-        if constexpr (qe >= 0) {
-            vfma<V_SE + qe>(a, cf, h[0]);
-            vfma<V_SE + 5 + qe>(a, cf, h[1]);
-            vfma<V_SE + 10 + qe>(a, cf, h[2]);
-        }
-        if constexpr (c >= 9 && c < 12) a = __builtin_fma(h[c - 6], dt, a);
-        if constexpr (qw >= 0) {
-            vfma<V_SW + qw>(a, cf, h[6]);
-            vfma<V_SW + 17 + qw>(a, cf, h[7]);
-            vfma<V_SW + 34 + qw>(a, cf, h[8]);
-        }
-        m[c] = a;
-    });
+    STAMP(1);
+    // ---- Gn = G + H d (SinglePhase.cpp:320), T = H B_c, M = H A (row pp) ----------------------
+    real m[NX], t[HC], ga[4] = {g, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < NX; ++c) m[c] = h[c];
+#pragma unroll
+    for (int q = 0; q < HC; ++q) t[q] = 0;
+    emit_SA(m, h, cf, dt);
+    emit_Bc(t, h[6], h[7], h[8], h + 9, h + 12, bv, bq, cf);
+    static_for<NX>([&](auto C) { vfma<V_D + C>(ga[C & 3], cf, h[C]); });
+    const real gn = (ga[0] + ga[1]) + (ga[2] + ga[3]);
     pin(t);
     pin(m);
     if (L.row) {
@@ -264,47 +376,26 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
         for (int q = 0; q < HC; ++q) I.TI[pp * TS + q] = t[q];
     }
     SSYNC();
+    STAMP(2);
     // ---- column pp of M (position 24: Gn); Z row, Qux_c column, Qu_c ---------------------------
     const int pc = pp < MS - 1 ? pp : MS - 1;
     real mc[NX];
 #pragma unroll
     for (int j = 0; j < NX; ++j) mc[j] = I.MI[j * MS + pc];
-    // Z[pp][i] = M[pp][i] + sum_k M[k][pp] S[k][i] (S^T M transposed); position 24: (S^T Gn)[i]
-    static_for<NX>([&](auto Ii) {
-        constexpr int i = Ii, qe = se_index(i), qw = sw_index(i);
-        real a = m[i];
-        if constexpr (qe >= 0) {
-            vfma<V_SE + qe>(a, cf, mc[0]);
-            vfma<V_SE + 5 + qe>(a, cf, mc[1]);
-            vfma<V_SE + 10 + qe>(a, cf, mc[2]);
-        }
-        if constexpr (i >= 9 && i < 12) a = __builtin_fma(mc[i - 6], dt, a);
-        if constexpr (qw >= 0) {
-            vfma<V_SW + qw>(a, cf, mc[6]);
-            vfma<V_SW + 17 + qw>(a, cf, mc[7]);
-            vfma<V_SW + 34 + qw>(a, cf, mc[8]);
-        }
-        m[i] = a;  // Z row
-    });
     // Qux_c[q][pp] = (B_c^T M)[q][pp] (lux = 0); position 24: Qu_c = lu_c + B_c^T Gn
-    const real *lcp[4];  // lu of each leg's coupled controls on position 24, zeros elsewhere
-#pragma unroll
-    for (int l = 0; l < 4; ++l) lcp[l] = pp == NX ? img + V_LU + (((ph.cmask >> l) & 1) ? 3 * l : 12 + 3 * l) : S.zero;
-#pragma unroll
-    for (int l = 0; l < 4; ++l) { bv[l] = I.pc[l]; bq[l] = I.pc[4 + l]; }
     real w2[HC];
-    static_for<HC>([&](auto Q) {
-        constexpr int q = Q;
-        real a = lcp[q / 3][q % 3];
-        a = __builtin_fma(mc[9 + q % 3], bv[q / 3], a);
-        a = __builtin_fma(mc[12 + q], bq[q / 3], a);
-        vfma<V_BW + q>(a, cf, mc[6]);
-        vfma<V_BW + 12 + q>(a, cf, mc[7]);
-        vfma<V_BW + 24 + q>(a, cf, mc[8]);
-        w2[q] = a;
-    });
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        const real *lcp = pp == NX ? img + V_LU + (((ph.cmask >> l) & 1) ? 3 * l : 12 + 3 * l) : S.zero;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) w2[3 * l + a] = lcp[a];
+    }
+    // Z[pp][i] = M[pp][i] + sum_k M[k][pp] S[k][i] (S^T M transposed); position 24: (S^T Gn)[i]
+    emit_SA(m, mc, cf, dt);
+    emit_Bc(w2, mc[6], mc[7], mc[8], mc + 9, mc + 12, bv, bq, cf);
     pin(m);
     pin(w2);
+    STAMP(3);
     // ---- Qxx = lxx + reg I + (Z + Z^T) / 2 (SinglePhase.cpp:323-352) ---------------------------
     if (pp <= NX) {  // Z rows (two zero columns: the column reads of positions > 24 see zeros)
 #pragma unroll
@@ -313,13 +404,23 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
         I.MI[pp * MS + NX + 1] = 0;
     }
     SSYNC();
+    // lxx + reg I into the Z image: each row lane adds its diagonal and lxx cross terms to its own
+    // row (read, add, write back: no two lanes touch one entry; absent terms add 0 to column 25)
     if (L.row) {
-        atomicAdd(&I.MI[pp * MS + pp], ph.lxd + reg);
+        real *zr = I.MI + pp * MS;
+        int col[4];
 #pragma unroll
-        for (int t2 = 0; t2 < 4; ++t2) {
-            const int col = L.xkind == 1 ? L.xc0 + 3 * t2 : (L.xkind == 2 && t2 == 0) ? L.xc0 : MS - 1;
-            atomicAdd(&I.MI[pp * MS + col], ((ph.xmask >> t2) & 1) ? -ph.xw : (real)0);
-        }
+        for (int t2 = 0; t2 < 4; ++t2) col[t2] = L.xkind == 1 ? L.xc0 + 3 * t2 : (L.xkind == 2 && t2 == 0) ? L.xc0 : MS - 1;
+        real v[5];
+        v[0] = zr[pp];
+#pragma unroll
+        for (int t2 = 0; t2 < 4; ++t2) v[1 + t2] = zr[col[t2]];
+        v[0] += ph.lxd + reg;
+#pragma unroll
+        for (int t2 = 0; t2 < 4; ++t2) v[1 + t2] += ((ph.xmask >> t2) & 1) ? -ph.xw : (real)0;
+        zr[pp] = v[0];
+#pragma unroll
+        for (int t2 = 0; t2 < 4; ++t2) zr[col[t2]] = v[1 + t2];
     }
     SSYNC();
     const real *zrow = L.row ? I.MI + pp * MS : S.zero;
@@ -331,29 +432,20 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     pin(qxx);  // materialised here, not sunk to the value update (twice the registers across the elimination)
     // Qx = lx + A^T Gn = lx + Gn + S^T Gn
     const real qx = img[V_LX + (L.row ? pp : 0)] + (gn + I.MI[NX * MS + pc]);
+    STAMP(4);
     // ---- Quu_cc column pos = luu + reg + B_c^T T[:, pos] (SinglePhase.cpp:324, MultiPhaseDDP.cpp:160)
-    if (L.qlane && pp < HC) atomicAdd((real *)&img[L.rbdiag], ph.dtr + reg);  // dt R + reg on the diagonal
-    SSYNC();
     real tcol[18];
 #pragma unroll
     for (int j = 0; j < 18; ++j) tcol[j] = I.TI[(6 + j) * TS + pos];
-    real lbr[3];
+    real lbr[3];  // row pos % 3 of the leg's ReB block, dt R + reg on its diagonal
+    const int aq = pos % 3;
 #pragma unroll
-    for (int a = 0; a < 3; ++a) lbr[a] = (L.qlane ? img + L.rb[a] : S.zero + a)[0];
+    for (int a = 0; a < 3; ++a) lbr[a] = (L.qlane ? img + L.rb[a] : S.zero + a)[0] + (a == aq ? ph.dtr + reg : (real)0);
     const int lq = pos / 3;
-#pragma unroll
-    for (int l = 0; l < 4; ++l) { bv[l] = I.pc[l]; bq[l] = I.pc[4 + l]; }
     real w[HC];
-    static_for<HC>([&](auto Q) {
-        constexpr int q = Q;
-        real a = (L.qlane && lq == q / 3) ? lbr[q % 3] : (real)0;
-        a = __builtin_fma(tcol[3 + q % 3], bv[q / 3], a);
-        a = __builtin_fma(tcol[6 + q], bq[q / 3], a);
-        vfma<V_BW + q>(a, cf, tcol[0]);
-        vfma<V_BW + 12 + q>(a, cf, tcol[1]);
-        vfma<V_BW + 24 + q>(a, cf, tcol[2]);
-        w[q] = a;
-    });
+#pragma unroll
+    for (int q = 0; q < HC; ++q) w[q] = (L.qlane && lq == q / 3) ? lbr[q % 3] : (real)0;
+    emit_Bc(w, tcol[0], tcol[1], tcol[2], tcol + 3, tcol + 6, bv, bq, cf);
     pin(w);
     // decoupled controls on positions 0..11: Qu_z = lu_z, Quu_zz = dt R_z + reg
     const bool zl = pp < HC;
@@ -362,37 +454,21 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     const real qzz = ph.dtrz + reg;
     // the images are read: the next knot's are requested now (in flight during the elimination)
     if (more) fetch(S, nrec0, ndef0, nrec1, ndef1, L.lane);
+    STAMP(5);
     // ---- PSD test + Gauss-Jordan on [Quu_cc | Qux_c | Qu_c] --------------------------------------
-    real quxs[HC];  // Qux_c column pp (position 24: Qu_c), kept for G, dV and the value update
+    real quxs[HC];  // Qux_c column pp (position 24: Qu_c), kept for G and the value update
 #pragma unroll
     for (int q = 0; q < HC; ++q) quxs[q] = w2[q];
     pin(quxs);
     unsigned long long bad = __builtin_amdgcn_ballot_w64(zl && !(qzz > (real)1e-9));
-    // Step j takes column j of Quu_cc from DPP position j (both DPP rows of an item hold Quu_cc).
-    // Rows already used as pivots are kept negated, so at the end w2 = -Quu_cc^-1 [Qux_c | Qu_c]
-    // = [K_c | dU_c] (the reference's explicit inverse, SinglePhase.cpp:351-356, as a solve).
-    static_for<HC>([&](auto J) {
-        constexpr int j = J;
-        const real piv = row_bcast<j>(w[j]);
-        bad |= __builtin_amdgcn_ballot_w64(!(piv > (real)1e-9));
-        const real inv = recip(piv);
-        const real nf = -(w[j] * inv), nf2 = -(w2[j] * inv);
-        // the right-hand sides first: they read the pivot column (w[i] on lane j) before it changes
-        static_for<HC>([&](auto Ii) {
-            constexpr int i = Ii;
-            if constexpr (i != j) bfma<j>(w2[i], w[i], nf2);
-        });
-        static_for<HC>([&](auto Ii) {
-            constexpr int i = Ii;
-            if constexpr (i != j) fmac_row_bcast<j, false>(w[i], nf);
-        });
-        w[j] = nf;
-        w2[j] = nf2;
-    });
+    // w2 becomes -Quu_cc^-1 [Qux_c | Qu_c] = [K_c | dU_c] (the reference's explicit inverse,
+    // SinglePhase.cpp:351-356, as a solve)
+    gauss_jordan(w, w2, bad);
     const bool okh = L.e ? (bad >> 32) == 0 : (bad & 0xffffffffull) == 0;
     live = live && okh;
     const bool st = live;  // this half writes the knot's outputs
-    // ---- outputs: K_c rows, dU, dV (SinglePhase.cpp:354-362) -----------------------------------
+    STAMP(6);
+    // ---- outputs: K_c rows, dU (SinglePhase.cpp:354-356) ----------------------------------------
     real *Kg = it.K + (size_t)kc * KCW;
     if (st && L.row)
 #pragma unroll
@@ -400,16 +476,8 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     if (pp == NX)  // coupled dU from position 24
 #pragma unroll
         for (int q = 0; q < HC; ++q) I.du[(((ph.cmask >> (q / 3)) & 1) ? 0 : 12) + q] = w2[q];
-    const real duz = -(quz / qzz);
-    if (zl) I.du[du_z] = duz;
-    // expected cost change Qu^T Quu^-1 Qu: position 24 (coupled) + positions 0..11 (decoupled)
-    real dvp = 0;
-#pragma unroll
-    for (int q = 0; q < HC; ++q) dvp = __builtin_fma(quxs[q], w2[q], dvp);  // -Qu_c^T Quu_cc^-1 Qu_c
-    dvp = pp == NX ? dvp : zl ? quz * duz : (real)0;
-    const real dvk = -half_sum(dvp);
-    if (st) { dV1 -= dvk; dV2 += dvk; }
-    // Kp^T rows (negated: K_c^T) for the value update; Qux_c^T rows
+    if (zl) I.du[du_z] = -(quz / qzz);
+    // K_c^T rows (row 24: dU_c) and Qux_c^T rows for the value update
     if (pp <= NX)
 #pragma unroll
         for (int q = 0; q < HC; ++q) I.MI[pp * TS + q] = w2[q];
@@ -418,59 +486,68 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
         for (int q = 0; q < HC; ++q) I.TI[pp * TS + q] = quxs[q];
     SSYNC();
     if (st && L.row) it.dU[(size_t)kc * NX + pp] = I.du[pp];
-    // G = Qx - Qux_c^T Quu_cc^-1 Qu_c = Qx + Qux_c^T dU_c (row 24 of the K^T image holds dU_c)
-    real gq = qx;
+    // G = Qx - Qux_c^T Quu_cc^-1 Qu_c = Qx + Qux_c^T dU_c (SinglePhase.cpp:359)
+    real gq4[4] = {qx, 0, 0, 0};
 #pragma unroll
-    for (int q = 0; q < HC; ++q) gq = __builtin_fma(quxs[q], I.MI[NX * TS + q], gq);
+    for (int q = 0; q < HC; ++q) gq4[q & 3] = __builtin_fma(quxs[q], I.MI[NX * TS + q], gq4[q & 3]);
+    const real gq = (gq4[0] + gq4[1]) + (gq4[2] + gq4[3]);
+    STAMP(7);
     // ---- H = Qxx - Qux_c^T Quu_cc^-1 Qux_c = Qxx + Qux_c^T K_c on the matrix cores ------------------
-    // (tiles (0,0), (0,1), (1,1) of the symmetric 24 x 24 product, K = 12; rows / columns 24..31
-    // only feed discarded outputs).  One item after the other, every lane on the item's tiles.
+    // (tiles (0,0), (0,1), (1,1) of the symmetric 24 x 24 product, K = 12, for both items at once;
+    // rows / columns 24..31 only feed discarded outputs; SinglePhase.cpp:360)
     const int li = L.lane & 15, lk = L.lane >> 4;
+    real a0[2][3], a1[2][3], b0[2][3], b1[2][3];
 #pragma unroll
-    for (int ei = 0; ei < 2; ++ei) {
-        typename Lds<real>::Item &J = S.it[ei];
-        real a0[3], a1[3], b0[3], b1[3];
+    for (int ei = 0; ei < 2; ++ei)
 #pragma unroll
         for (int ks = 0; ks < 3; ++ks) {
             const int q = 4 * ks + lk;
-            a0[ks] = J.TI[li * TS + q];
-            a1[ks] = J.TI[(16 + li) * TS + q];
-            b0[ks] = J.MI[li * TS + q];
-            b1[ks] = J.MI[(16 + li) * TS + q];
+            a0[ei][ks] = S.it[ei].TI[li * TS + q];
+            a1[ei][ks] = S.it[ei].TI[(16 + li) * TS + q];
+            b0[ei][ks] = S.it[ei].MI[li * TS + q];
+            b1[ei][ks] = S.it[ei].MI[(16 + li) * TS + q];
         }
-        acc4<real> t00 = {0, 0, 0, 0}, t01 = t00, t11 = t00;
+    acc4<real> t00[2], t01[2], t11[2];
 #pragma unroll
-        for (int ks = 0; ks < 3; ++ks) {
-            t00 = mfma16(a0[ks], b0[ks], t00);
-            t01 = mfma16(a0[ks], b1[ks], t01);
-            t11 = mfma16(a1[ks], b1[ks], t11);
+    for (int ei = 0; ei < 2; ++ei) t00[ei] = t01[ei] = t11[ei] = acc4<real>{0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+        for (int ei = 0; ei < 2; ++ei) {
+            t00[ei] = mfma16(a0[ei][ks], b0[ei][ks], t00[ei]);
+            t01[ei] = mfma16(a0[ei][ks], b1[ei][ks], t01[ei]);
+            t11[ei] = mfma16(a1[ei][ks], b1[ei][ks], t11[ei]);
         }
-        SSYNC();  // the operands are in registers: the product overwrites the K^T image
+    SSYNC();  // the operands are in registers: the product overwrites the K^T images
+#pragma unroll
+    for (int ei = 0; ei < 2; ++ei) {
+        real *P = S.it[ei].MI;
 #pragma unroll
         for (int gi = 0; gi < 4; ++gi) {
             const int r0 = mfma_row<real>(lk, gi), r1 = 16 + r0, c1 = 16 + li;
-            J.MI[r0 * MS + li] = t00[gi];
+            P[r0 * MS + li] = t00[ei][gi];
             if (c1 < NX) {
-                J.MI[r0 * MS + c1] = t01[gi];
-                J.MI[c1 * MS + r0] = t01[gi];
+                P[r0 * MS + c1] = t01[ei][gi];
+                P[c1 * MS + r0] = t01[ei][gi];
             }
-            if (r1 < NX && c1 < NX) J.MI[r1 * MS + c1] = t11[gi];
+            if (r1 < NX && c1 < NX) P[r1 * MS + c1] = t11[ei][gi];
         }
     }
     SSYNC();
+    STAMP(8);
     const real *prow = L.row ? I.MI + pp * MS : S.zero;
 #pragma unroll
     for (int c = 0; c < NX; ++c) h[c] = qxx[c] + prow[c];
     g = L.row ? gq : (real)0;
     SSYNC();
+    STAMP(9);
 }
 
 // MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229) for the wave's two items with their
 // own regularisation.  Returns, per half, -1 (success) or the control slot of the first knot whose
 // Quu fails the PSD test (that knot and the ones below it are not written).
 template <typename real>
-DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, const Item<real> &it, real &dV1,
-                   real &dV2)
+DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, const Item<real> &it)
 {
     const int pp = L.pp;
     const real *lqg = Prec<real>::lq(d), *defg = Prec<real>::def(d);
@@ -480,7 +557,6 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
     bool live = it.act;
     int fail = -1;
     real h[NX], g = 0;
-    dV1 = 0; dV2 = 0;
     for (int i = p.P - 1; i >= 0; --i) {
         Phase<real> ph;
         load_phase<real>(p, d, S.it[L.e], b, i, pp, ph);
@@ -549,8 +625,7 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
             const bool more = k > 0;
             const int kn = more ? k - 1 : 0;
             const bool was = live;
-            knot(p, S, L, ph, it, k0 + k, h, g, live, dV1, dV2, more, recp(b0, kn), defp(b0, kn), recp(b1, kn),
-                 defp(b1, kn));
+            knot(p, S, L, ph, it, k0 + k, h, g, live, more, recp(b0, kn), defp(b0, kn), recp(b1, kn), defp(b1, kn));
             if (was && !live) fail = k0 + k;
             if (!__builtin_amdgcn_ballot_w64(live)) break;
         }
@@ -595,7 +670,6 @@ DEV Lane make_lane()
     const int lq = (L.qlane ? L.pos : 0) / 3, aq = L.pos % 3;
 #pragma unroll
     for (int a = 0; a < 3; ++a) L.rb[a] = V_RB + 6 * lq + rb_index(aq, a);
-    L.rbdiag = V_RB + 6 * lq + rb_index(aq, aq);
     L.xkind = (L.pp >= 3 && L.pp < 6) ? 1 : (L.pp >= 12 && L.pp < NX) ? 2 : 0;
     L.xc0 = L.xkind == 1 ? 12 + (L.pp - 3) : L.xkind == 2 ? 3 + (L.pp - 12) % 3 : MS - 1;
     return L;
@@ -622,6 +696,9 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
     __shared__ Lds<real> S;
     const Lane L = make_lane();
     zero_init(S, L.lane);
+#if HSDDP_STAMPS
+    if (L.lane < 12) S.st[L.lane] = 0;
+#endif
     const int b = 2 * blockIdx.x + L.e;
     const bool valid = b < p.B;
     const int bv = valid ? b : p.B - 1;
@@ -634,11 +711,10 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
     it.K = Prec<real>::K(d) + (size_t)bv * p.Kc * KCW;
     it.dU = d.dU + (size_t)bv * p.Kc * NX;
     bool need = act, ok = false;
-    real dV1 = 0, dV2 = 0;
     for (int attempt = 0; __builtin_amdgcn_ballot_w64(need); ++attempt) {
         it.act = need;
         it.reg = (real)reg;
-        const int fk = sweep_pair(p, d, S, L, it, dV1, dV2);
+        const int fk = sweep_pair(p, d, S, L, it);
         if (need) {
             if (fk < 0) {
                 ok = true;
@@ -671,6 +747,10 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
             }
         }
     }
+#if HSDDP_STAMPS
+    SSYNC();
+    if (L.lane < 12) d.dbg[(size_t)(2 * blockIdx.x) * 16 + L.lane] += S.st[L.lane];
+#endif
     if (act && L.pp == 0) {
         double cost, feas;
         element_cost(p, d, bv, cost, feas);
@@ -713,8 +793,7 @@ __global__ __launch_bounds__(64, 2) void k_riccati_retry(Params p, Bufs d)
     it.reg = (real)reg;
     it.K = (real *)d.retry_K + slot * p.Kc * KCW;
     it.dU = d.retry_dU + slot * p.Kc * NX;
-    real dV1, dV2;
-    const int fk = sweep_pair(p, d, S, L, it, dV1, dV2);
+    const int fk = sweep_pair(p, d, S, L, it);
     if (act && L.pp == 0) *flag = fk < 0 ? 1 : -1 - fk;  // success, or -1 - (the failing control slot)
 }
 

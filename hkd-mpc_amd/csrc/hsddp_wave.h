@@ -172,3 +172,22 @@ DEV void lds_dma16(const void *src, unsigned m0)
 }
 
 }  // namespace hsddp
+
+namespace hsddp {
+
+// Scalar f64 / f32 VALU operations as inline asm: emitted exactly where written among the
+// (equally volatile) DPP multiply-adds, so a dependent chain can be threaded between independent
+// instructions by hand (the Gauss-Jordan pivot chain, hsddp_sweep.hip).
+DEV void asm_rcp(double &r, double x) { asm volatile("v_rcp_f64 %0, %1" : "=v"(r) : "v"(x)); }
+DEV void asm_rcp(float &r, float x) { asm volatile("v_rcp_f32 %0, %1" : "=v"(r) : "v"(x)); }
+// e = 1 - x r
+DEV void asm_nfma1(double &e, double x, double r) { asm volatile("v_fma_f64 %0, -%1, %2, 1.0" : "=v"(e) : "v"(x), "v"(r)); }
+DEV void asm_nfma1(float &e, float x, float r) { asm volatile("v_fma_f32 %0, -%1, %2, 1.0" : "=v"(e) : "v"(x), "v"(r)); }
+// r = r + r e
+DEV void asm_newton(double &r, double e) { asm volatile("v_fma_f64 %0, %0, %1, %0" : "+v"(r) : "v"(e)); }
+DEV void asm_newton(float &r, float e) { asm volatile("v_fma_f32 %0, %0, %1, %0" : "+v"(r) : "v"(e)); }
+// y = -(a b)
+DEV void asm_nmul(double &y, double a, double b) { asm volatile("v_mul_f64 %0, -%1, %2" : "=v"(y) : "v"(a), "v"(b)); }
+DEV void asm_nmul(float &y, float a, float b) { asm volatile("v_mul_f32 %0, -%1, %2" : "=v"(y) : "v"(a), "v"(b)); }
+
+}  // namespace hsddp

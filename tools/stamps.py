@@ -17,9 +17,9 @@ sys.path.insert(0, os.path.join(ROOT, "hkd-mpc_amd"))
 import hsddp  # noqa: E402
 from hsddp import synthetic  # noqa: E402
 
-STAGES = ["stage inputs -> LDS", "M, T_c rows (stage A)", "Qx, Qu_c, Z", "Z rows, Qux_c",
-          "symmetrise Qxx", "Quu_cc rows (operand)", "Gauss-Jordan (12 steps)", "Quu^-1, dU, Kp/K (MFMA)",
-          "dV, G, value update (MFMA)"]
+STAGES = ["wait DMA, coefficients", "Gn, T, M rows", "M columns, Z, Qux_c, Qu_c", "Qxx (symmetrise)",
+          "Quu_cc columns", "Gauss-Jordan (12 steps)", "K, dU, dV, G, images", "value update (MFMA)",
+          "H rows"]
 
 
 def main():
@@ -34,7 +34,7 @@ def main():
     rc = L.hsddp_debug_stamps(s._h, out.ctypes.data)
     s.close()
     assert rc == 0, rc
-    cyc = out[:, 1:10].astype(np.float64).mean(0)
+    cyc = out[0::2, 1:10].astype(np.float64).mean(0)  # one stamp record per wave (its first element)
     tot = cyc.sum()
     for name, c in zip(STAGES, cyc):
         print(f"{name:28s} {c / (3 * 200):10.0f} cycles/knot  {100 * c / tot:5.1f} %")
