@@ -267,16 +267,18 @@ DEV void emit_Bc(real (&acc)[HC], real y6, real y7, real y8, const real *y9, con
     static_for<HC>([&](auto Q) { vfma<V_BW + 24 + Q>(acc[Q], cf, y8); });
 }
 
-// Gauss-Jordan without pivoting on the columns held in lanes: w = Quu_cc columns (DPP positions
-// 0..11 of both DPP rows of an item), w2 = right-hand sides.  Step j takes column j from DPP
-// position j.  Rows already used as pivots are kept negated, so at the end w2 = -Quu_cc^-1 (rhs).
-// The next step's pivot chain (DPP broadcast, reciprocal, two Newton steps, the two factors) is
-// threaded through this step's independent multiply-adds, its operand row updated first.
-// bad: ballot of pivots <= 1e-9 (the PSD test).
+// Gaussian elimination without pivoting on the columns held in lanes, then back substitution:
+// w = Quu_cc columns (DPP positions 0..11 of both DPP rows of an item), w2 = right-hand sides.
+// Forward step j takes column j from DPP position j and eliminates it from the rows below; pivot
+// rows are kept scaled by 1 / pivot and negated, so after the back substitution w2 =
+// -Quu_cc^-1 (rhs).  The next step's pivot chain (DPP broadcast, reciprocal, Newton steps, the two
+// factors) is threaded through this step's independent multiply-adds, its operand row first.  The
+// pivots are those of the LDL^T factorisation of Quu_cc; bad: ballot of pivots <= 1e-9 (PSD test).
 template <typename real>
-DEV void gauss_jordan(real (&w)[HC], real (&w2)[HC], unsigned long long &bad)
+DEV void eliminate(real (&w)[HC], real (&w2)[HC], unsigned long long &bad)
 {
     constexpr bool F64 = sizeof(real) == 8;
+    constexpr int CH = F64 ? 13 : 9;  // slot of the last chain operation
     real r, e, nf, nf2;
     {
         const real piv = row_bcast<0>(w[0]);
@@ -300,22 +302,25 @@ DEV void gauss_jordan(real (&w)[HC], real (&w2)[HC], unsigned long long &bad)
             bfma<j>(w2[jn], w[jn], nf2);
             fmac_row_bcast<j, false>(w[jn], nf);
         }
-        constexpr int NO = nx ? HC - 2 : HC - 1;
-        static_for<2 * NO>([&](auto T) {
-            constexpr int t = T, k = t / 2;
-            constexpr int i = nx ? (j + 2 + k) % HC : k;
-            if constexpr (t % 2 == 0)
-                bfma<j>(w2[i], w[i], nf2);
-            else
-                fmac_row_bcast<j, false>(w[i], nf);
+        constexpr int NO = nx ? HC - 2 - j : 0;        // rows below jn
+        constexpr int NT = (2 * NO > CH + 1) ? 2 * NO : CH + 1;
+        static_for<NT>([&](auto T) {
+            constexpr int t = T, i = jn + 1 + t / 2;
+            if constexpr (t < 2 * NO) {
+                if constexpr (t % 2 == 0)
+                    bfma<j>(w2[i], w[i], nf2);
+                else
+                    fmac_row_bcast<j, false>(w[i], nf);
+            }
             if constexpr (nx) {
                 if constexpr (t == 1) pivn = row_bcast<(nx ? jn : 0)>(w[jn]);
                 if constexpr (t == 3) asm_rcp(rn, pivn);
+                if constexpr (t == 4 && 2 * NO <= 4) asm volatile("s_nop 1" ::: "memory");
                 if constexpr (t == 5) asm_nfma1(en, pivn, rn);
                 if constexpr (t == 7) asm_newton(rn, en);
                 if constexpr (F64 && t == 9) asm_nfma1(en, pivn, rn);
                 if constexpr (F64 && t == 11) asm_newton(rn, en);
-                if constexpr (t == (F64 ? 13 : 9)) {
+                if constexpr (t == CH) {
                     asm_nmul(nfn, w[jn], rn);
                     asm_nmul(nf2n, w2[jn], rn);
                 }
@@ -328,6 +333,15 @@ DEV void gauss_jordan(real (&w)[HC], real (&w2)[HC], unsigned long long &bad)
             nf = nfn;
             nf2 = nf2n;
         }
+    });
+    // back substitution: x_j = w2[j] (negated), rows i < j lose U[i][j] x_j (U[i][j] = w[i] on lane j,
+    // negated too: the product's sign is right), the next row first
+    static_for<HC - 1>([&](auto Jr) {
+        constexpr int j = HC - 1 - Jr;
+        static_for<j>([&](auto Ii) {
+            constexpr int i = j - 1 - Ii;
+            bfma<j>(w2[i], w[i], w2[j]);
+        });
     });
 }
 
@@ -463,7 +477,7 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     unsigned long long bad = __builtin_amdgcn_ballot_w64(zl && !(qzz > (real)1e-9));
     // w2 becomes -Quu_cc^-1 [Qux_c | Qu_c] = [K_c | dU_c] (the reference's explicit inverse,
     // SinglePhase.cpp:351-356, as a solve)
-    gauss_jordan(w, w2, bad);
+    eliminate(w, w2, bad);
     const bool okh = L.e ? (bad >> 32) == 0 : (bad & 0xffffffffull) == 0;
     live = live && okh;
     const bool st = live;  // this half writes the knot's outputs
