@@ -43,6 +43,11 @@ namespace sweep {
 #ifndef HSDDP_STAMPS
 #define HSDDP_STAMPS 0
 #endif
+// value update on the matrix cores (1) or by DPP-broadcast multiply-adds from the lanes holding
+// K_c (0, no LDS round trip)
+#ifndef HSDDP_VALUE_MFMA
+#define HSDDP_VALUE_MFMA 0
+#endif
 // In-kernel stamps (diagnostic build only, make stamps): s_memtime at the stage boundaries of a
 // knot (each after a full LDS drain, so stages do not overlap), differences summed per stage into
 // LDS and written to Bufs::dbg of the wave's first element (tools/stamps.py).
@@ -491,6 +496,7 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
 #pragma unroll
         for (int q = 0; q < HC; ++q) I.du[(((ph.cmask >> (q / 3)) & 1) ? 0 : 12) + q] = w2[q];
     if (zl) I.du[du_z] = -(quz / qzz);
+#if HSDDP_VALUE_MFMA
     // K_c^T rows (row 24: dU_c) and Qux_c^T rows for the value update
     if (pp <= NX)
 #pragma unroll
@@ -552,6 +558,36 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     const real *prow = L.row ? I.MI + pp * MS : S.zero;
 #pragma unroll
     for (int c = 0; c < NX; ++c) h[c] = qxx[c] + prow[c];
+#else
+    SSYNC();
+    if (st && L.row) it.dU[(size_t)kc * NX + pp] = I.du[pp];
+    // K_c columns of both DPP rows at every DPP position (column c of the item on position c & 15
+    // of ka (c < 16) or kb (c >= 16)); the coupled dU_c is position 24's: kb at position 8
+    real ka[HC], kb[HC];
+#pragma unroll
+    for (int q = 0; q < HC; ++q) row_pair(w2[q], ka[q], kb[q]);
+#pragma unroll
+    for (int q = 0; q < HC; ++q) quxs[q] = L.row ? quxs[q] : (real)0;  // positions >= 24 keep H = 0
+    // G = Qx - Qux_c^T Quu_cc^-1 Qu_c = Qx + Qux_c^T dU_c (SinglePhase.cpp:359)
+    real gq4[4] = {qx, 0, 0, 0};
+    static_for<HC>([&](auto Q) { bfma<8>(gq4[Q & 3], kb[Q], quxs[Q]); });
+    const real gq = (gq4[0] + gq4[1]) + (gq4[2] + gq4[3]);
+    STAMP(7);
+    // ---- H = Qxx - Qux_c^T Quu_cc^-1 Qux_c = Qxx + Qux_c^T K_c (SinglePhase.cpp:360): row pp,
+    // K_c by DPP broadcast from the lanes that hold its columns
+#pragma unroll
+    for (int c = 0; c < NX; ++c) h[c] = qxx[c];
+    static_for<HC>([&](auto Q) {
+        static_for<NX>([&](auto C) {
+            constexpr int c = C;
+            if constexpr (c < 16)
+                bfma<c & 15>(h[c], ka[Q], quxs[Q]);
+            else
+                bfma<c & 15>(h[c], kb[Q], quxs[Q]);
+        });
+    });
+    STAMP(8);
+#endif
     g = L.row ? gq : (real)0;
     SSYNC();
     STAMP(9);

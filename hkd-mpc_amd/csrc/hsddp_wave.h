@@ -190,4 +190,23 @@ DEV void asm_newton(float &r, float e) { asm volatile("v_fma_f32 %0, %0, %1, %0"
 DEV void asm_nmul(double &y, double a, double b) { asm volatile("v_mul_f64 %0, -%1, %2" : "=v"(y) : "v"(a), "v"(b)); }
 DEV void asm_nmul(float &y, float a, float b) { asm volatile("v_mul_f32 %0, -%1, %2" : "=v"(y) : "v"(a), "v"(b)); }
 
+
+// The values of x on the two 16-lane DPP rows of this lane's half-wave, at this lane's DPP
+// position: ka from the first row (lanes 0..15 / 32..47), kb from the second (v_permlane16_swap).
+DEV void row_pair(double x, double &ka, double &kb)
+{
+    const unsigned lo = __double2loint(x), hi = __double2hiint(x);
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    ka = __hiloint2double(b[0], a[0]);
+    kb = __hiloint2double(b[1], a[1]);
+}
+DEV void row_pair(float x, float &ka, float &kb)
+{
+    const unsigned u = __float_as_uint(x);
+    const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    ka = __uint_as_float(a[0]);
+    kb = __uint_as_float(a[1]);
+}
+
 }  // namespace hsddp
