@@ -602,8 +602,8 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
     const int pp = L.pp;
     const real *lqg = Prec<real>::lq(d), *defg = Prec<real>::def(d);
     // the other item of the wave (its element's records feed the DMA even when this half is idle)
-    const int b = it.b, bo = __shfl_xor(it.b, 32);
-    const int b0 = L.e ? bo : b, b1 = L.e ? b : bo;
+    const int b = it.b;
+    const int b0 = __builtin_amdgcn_readlane(b, 0), b1 = __builtin_amdgcn_readlane(b, 32);  // wave-uniform (SGPRs)
     bool live = it.act;
     int fail = -1;
     real h[NX], g = 0;
