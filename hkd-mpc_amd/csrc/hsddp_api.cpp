@@ -239,6 +239,8 @@ struct hsddp_handle_t {
     float dt_sim = 0, t_cur = 0;
     std::vector<double> durations;
     int retry_cap_alloc = 0, retry_m_alloc = 0;  // parallel regularisation retry scratch (k_riccati_retry)
+    float *hist = nullptr;  // solver-info history [B][p.hcap][4] (grown by ensure_history)
+    double *value0 = nullptr;  // G[0], H[0] per phase [B][16][600] (hsddp_set_value_export)
 };
 
 // device staging area of at least `bytes` (contents not preserved when it grows)
@@ -320,7 +322,30 @@ static void fill_params(hsddp_handle h)
         }
     }
     p.retry_m = M;
-    p.retry_cap = (M > 0 && M <= h->retry_m_alloc) ? h->retry_cap_alloc : 0;
+    // value export writes G[0], H[0] from the sweep that succeeds: the in-kernel retry loop only
+    p.retry_cap = (M > 0 && M <= h->retry_m_alloc && !p.store_value) ? h->retry_cap_alloc : 0;
+}
+
+// the solver-info history holds every entry one solve with the handle's options can push: the
+// initial one and one per inner iteration (MultiPhaseDDP.cpp:277-280, 368-371)
+static int ensure_history(hsddp_handle h)
+{
+    const long need = 1 + (long)std::max(0, h->opt.max_AL_iter) * std::max(0, h->opt.max_DDP_iter);
+    if (h->hist && need <= h->p.hcap) return HSDDP_OK;
+    const int cap = (int)std::min<long>(std::max<long>(need, 16), 1 << 20);
+    float *nh = nullptr;
+    HIPCHK(hipMalloc(&nh, (size_t)h->p.B * cap * 4 * sizeof(float)));
+    HIPCHK(hipMemset(nh, 0, (size_t)h->p.B * cap * 4 * sizeof(float)));
+    if (h->hist) {
+        HIPCHK(hipStreamSynchronize(h->stream));
+        hipFree(h->hist);
+        h->bytes -= (size_t)h->p.B * h->p.hcap * 4 * sizeof(float);
+    }
+    h->hist = nh;
+    h->d.hist = nh;
+    h->p.hcap = cap;
+    h->bytes += (size_t)h->p.B * cap * 4 * sizeof(float);
+    return HSDDP_OK;
 }
 
 extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
@@ -408,6 +433,10 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         hsddp_destroy(h);
         return fail(HSDDP_ERR_DEVICE, "stream / pinned allocation failed");
     }
+    if ((rc = ensure_history(h))) {
+        hsddp_destroy(h);
+        return rc;
+    }
     launch_init_params(p, d, h->stream);
     launch_reset_elements(p, d, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess) {
@@ -426,6 +455,8 @@ extern "C" int hsddp_destroy(hsddp_handle h)
     for (void *p : h->allocs) hipFree(p);
     if (h->scratch) hipFree(h->scratch);
     if (h->ref_table) hipFree(h->ref_table);
+    if (h->hist) hipFree(h->hist);
+    if (h->value0) hipFree(h->value0);
 
     if (h->host_counter) hipHostFree(h->host_counter);
     if (h->stream) hipStreamDestroy(h->stream);
@@ -462,7 +493,7 @@ extern "C" int hsddp_set_options(hsddp_handle h, const hsddp_options *o)
     if (rc) return rc;
     h->opt = *o;
     fill_params(h);
-    return HSDDP_OK;
+    return ensure_history(h);
 }
 
 static int h2d(void *dst, const void *src, size_t bytes, hipStream_t st)
@@ -884,6 +915,174 @@ extern "C" int hsddp_download_element_info(hsddp_handle h, hsddp_element_info *i
         info[b].max_tconstr = e.max_t; info[b].max_pconstr = e.max_p;
         info[b].iters = e.iters; info[b].outer_iters = e.outer_iters; info[b].status = e.status;
         info[b].n_ls_trials = e.n_ls;
+    }
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_download_solver_info(hsddp_handle h, int capacity, float *cost, float *dyn_feas,
+                                          float *eqn_feas, float *ineq_feas, int *count)
+{
+    if (!h || capacity < 0) return fail(HSDDP_ERR_ARG, "null handle or negative capacity");
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const int B = h->p.B, hc = h->p.hcap;
+    std::vector<ElemState> el(B);
+    HIPCHK(hipMemcpy(el.data(), h->d.el, B * sizeof(ElemState), hipMemcpyDeviceToHost));
+    std::vector<float> hv((size_t)B * hc * 4);
+    HIPCHK(hipMemcpy(hv.data(), h->d.hist, hv.size() * sizeof(float), hipMemcpyDeviceToHost));
+    float *outs[4] = {cost, dyn_feas, eqn_feas, ineq_feas};
+    for (int b = 0; b < B; ++b) {
+        const int n = std::min(el[b].hist_n, std::min(hc, capacity));
+        if (count) count[b] = n;
+        for (int f = 0; f < 4; ++f) {
+            if (!outs[f]) continue;
+            float *o = outs[f] + (size_t)b * capacity;
+            for (int k = 0; k < capacity; ++k) o[k] = k < n ? hv[((size_t)b * hc + k) * 4 + f] : 0.0f;
+        }
+    }
+    return HSDDP_OK;
+}
+
+// ---- the reference Trajectory's derived fields (TrajectoryManagement.h:49-81) ---------------
+// The device keeps the LQ model of a knot in the compact record (hsddp_internal.h); these host
+// routines expand it to the reference's dense blocks for callers that read them.
+
+// phase of control slot kc and of state slot s
+static int phase_of_control(const Params &p, int kc)
+{
+    int i = 0;
+    while (i + 1 < p.P && kc >= p.k0[i + 1]) ++i;
+    return i;
+}
+
+extern "C" int hsddp_download_lq(hsddp_handle h, double *A, double *Bm, double *l, double *lx, double *lu,
+                                 double *lxx, double *luu)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const Params &p = h->p;
+    const size_t B = p.B, Kc = p.Kc, S = p.S, W = p.fp32 ? LQW32 : LQW;
+    std::vector<double> rec(B * Kc * W), cost(B * S);
+    if (p.fp32) {
+        std::vector<float> r32(B * Kc * W);
+        HIPCHK(hipMemcpy(r32.data(), h->d.lq32, r32.size() * sizeof(float), hipMemcpyDeviceToHost));
+        for (size_t q = 0; q < rec.size(); ++q) rec[q] = r32[q];
+    } else {
+        HIPCHK(hipMemcpy(rec.data(), h->d.lq, rec.size() * sizeof(double), hipMemcpyDeviceToHost));
+    }
+    if (l) HIPCHK(hipMemcpy(cost.data(), h->d.slot_cost, cost.size() * sizeof(double), hipMemcpyDeviceToHost));
+    const double dt = p.dt;
+    for (size_t b = 0; b < B; ++b)
+        for (size_t kc = 0; kc < Kc; ++kc) {
+            const double *r = rec.data() + (b * Kc + kc) * W;
+            const int i = phase_of_control(p, (int)kc);
+            const int *c = h->contacts.data() + (b * (p.P + 1) + i) * 4;
+            const size_t o = (b * Kc + kc);
+            if (A) {  // A = I + S (hkd_model.h: Se, Sw, dt at (3 + a, 9 + a))
+                double *a = A + o * NN;
+                std::fill(a, a + NN, 0.0);
+                for (int j = 0; j < NX; ++j) a[j * NX + j] = 1.0;
+                for (int rr = 0; rr < 3; ++rr)
+                    for (int q = 0; q < 5; ++q) a[rr * NX + hkd::se_col(q)] += r[LQ_SE + 5 * rr + q];
+                for (int q = 0; q < 3; ++q) a[(3 + q) * NX + 9 + q] += dt;
+                for (int rr = 0; rr < 3; ++rr)
+                    for (int q = 0; q < 17; ++q) a[(6 + rr) * NX + hkd::sw_col(q)] += r[LQ_SW + 17 * rr + q];
+            }
+            if (Bm) {
+                double *bb = Bm + o * NN;
+                std::fill(bb, bb + NN, 0.0);
+                for (int rr = 0; rr < 3; ++rr)
+                    for (int q = 0; q < 12; ++q) bb[(6 + rr) * NX + q] = r[LQ_BW + 12 * rr + q];
+                for (int lg = 0; lg < 4; ++lg)
+                    for (int a = 0; a < 3; ++a) {
+                        bb[(9 + a) * NX + 3 * lg + a] = dt * c[lg] / hkd::kMass;
+                        bb[(12 + 3 * lg + a) * NX + 12 + 3 * lg + a] = dt * (1.0 - c[lg]);
+                    }
+            }
+            if (l) l[o] = cost[b * S + kc + i];
+            if (lx) for (int j = 0; j < NX; ++j) lx[o * NX + j] = r[LQ_LX + j];
+            if (lu) for (int j = 0; j < NX; ++j) lu[o * NX + j] = r[LQ_LU + j];
+            if (lxx) {  // dt Q + dt D^T Qfoot D (HKDCost.cpp:22-37; constant per phase)
+                double *m = lxx + o * NN;
+                std::fill(m, m + NN, 0.0);
+                for (int j = 0; j < NX; ++j)
+                    m[j * NX + j] = dt * (j < 12 ? p.qbase[j] : p.q_qJ * (1 - c[(j - 12) / 3]));
+                for (int lg = 0; lg < 4; ++lg)
+                    for (int a = 0; a < 3; ++a) {
+                        const double w = c[lg] ? dt * (p.foot_gain * p.foot_w[a]) : 0.0;
+                        const int pa = 3 + a, qa = 12 + 3 * lg + a;
+                        m[pa * NX + pa] += w; m[qa * NX + qa] += w;
+                        m[pa * NX + qa] -= w; m[qa * NX + pa] -= w;
+                    }
+            }
+            if (luu) {  // dt R + dt ReB Hessian of the stance legs' GRF rows (SinglePhase.cpp:380-394)
+                double *m = luu + o * NN;
+                std::fill(m, m + NN, 0.0);
+                for (int j = 0; j < NX; ++j) m[j * NX + j] = dt * (j < 12 ? p.r_grf : p.r_qJd);
+                static const int ix[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+                for (int lg = 0; lg < 4; ++lg)
+                    for (int a = 0; a < 3; ++a)
+                        for (int e = 0; e < 3; ++e) m[(3 * lg + a) * NX + 3 * lg + e] += r[LQ_RB + 6 * lg + ix[a][e]];
+            }
+        }
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_download_terminal(hsddp_handle h, double *Phi, double *Phix, double *Phixx, double *Px)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const Params &p = h->p;
+    const size_t B = p.B, P = p.P;
+    std::vector<double> term(B * P * TW), cost(B * p.S);
+    HIPCHK(hipMemcpy(term.data(), h->d.term, term.size() * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cost.data(), h->d.slot_cost, cost.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (size_t b = 0; b < B; ++b)
+        for (size_t i = 0; i < P; ++i) {
+            const double *t = term.data() + (b * P + i) * TW;
+            const size_t o = b * P + i;
+            if (Phi) Phi[o] = cost[b * p.S + p.s0[i] + p.N[i]];
+            if (Phix) std::copy(t + TM_PHIX, t + TM_PHIX + NX, Phix + o * NX);
+            if (Phixx) std::copy(t + TM_PHIXX, t + TM_PHIXX + NN, Phixx + o * NN);
+            if (Px) {
+                if (i + 1 < P) std::copy(t + TM_PX, t + TM_PX + NN, Px + o * NN);
+                else std::fill(Px + o * NN, Px + (o + 1) * NN, 0.0);  // no reset after the last phase
+            }
+        }
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_set_value_export(hsddp_handle h, int on)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    HIPCHK(hipSetDevice(h->desc.device));
+    if (on && !h->value0) {
+        const size_t n = (size_t)h->p.B * HSDDP_MAX_PHASES * (NX + NN);
+        HIPCHK(hipMalloc(&h->value0, n * sizeof(double)));
+        HIPCHK(hipMemset(h->value0, 0, n * sizeof(double)));
+        h->bytes += n * sizeof(double);
+        h->d.value0 = h->value0;
+    }
+    h->p.store_value = on ? 1 : 0;
+    fill_params(h);
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_download_value(hsddp_handle h, double *G, double *H)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    if (!h->value0) return fail(HSDDP_ERR_ARG, "value export is off (hsddp_set_value_export)");
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const size_t B = h->p.B, P = h->p.P;
+    std::vector<double> v(B * P * (NX + NN));
+    HIPCHK(hipMemcpy(v.data(), h->value0, v.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (size_t o = 0; o < B * P; ++o) {
+        const double *s = v.data() + o * (NX + NN);
+        if (G) std::copy(s, s + NX, G + o * NX);
+        if (H) std::copy(s + NX, s + NX + NN, H + o * NN);
     }
     return HSDDP_OK;
 }

@@ -72,6 +72,8 @@ struct Params {
     // test, up to retry_cap of them per launch, evaluate the next retry_m values of the mu schedule
     // of backward_sweep_regularized (MultiPhaseDDP.cpp:141-181) at once; 0 = sequential only
     int retry_cap, retry_m;
+    int hcap;  // solver-info history entries per element (Bufs::hist)
+    int store_value;  // the sweep writes G[0], H[0] of every phase (Bufs::value0)
 };
 
 // one element deferred to the parallel retry: its index and the regularisation of its failed sweep
@@ -84,6 +86,7 @@ struct ElemState {
     double cost, feas, merit, merit_rho, dV1, dV2, reg;
     double max_t, max_p, max_t_prev, max_p_prev, cost_prev, merit_prev, feas_prev;
     int done, inner_done, ls_active, accepted, status, iters, outer_iters, n_ls;
+    int hist_n;  // entries pushed to the solver-info history (MultiPhaseDDP.cpp:277-280, 368-371)
 };
 
 struct Bufs {
@@ -107,6 +110,10 @@ struct Bufs {
     void *retry_K;                         // real (fp64, or fp32 in the C5 mode) [..][KCW]
     double *retry_dU;                      // [..][24]
     unsigned long long *dbg;               // [B][16] diagnostic builds only (in-kernel stamps)
+    // get_solver_info buffers (MultiPhaseDDP.cpp:532-541): per element hcap entries of
+    // (actual_cost, dynamics feasibility, max terminal violation, max path violation)
+    float *hist;                           // [B][hcap][4]
+    double *value0;                        // [B][P][24 + 576]: G[0], H[0] per phase (store_value)
 };
 
 // kernel launchers (hsddp_kernels.hip)

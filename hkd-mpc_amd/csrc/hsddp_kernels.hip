@@ -486,8 +486,18 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
     feas = sqrt(feas);
     E.max_p = max_p;
     E.max_t = max_t;
+    // one entry of the solver-info buffers (cost_buffer, dyn_feas_buffer, eqn_feas_buffer,
+    // ineq_feas_buffer; MultiPhaseDDP.cpp:277-280, 368-371), float as the reference's vectors
+    auto push_info = [&]() {
+        if (E.hist_n < p.hcap) {
+            float *hv = d.hist + ((size_t)b * p.hcap + E.hist_n) * 4;
+            hv[0] = (float)E.cost; hv[1] = (float)E.feas; hv[2] = (float)E.max_t; hv[3] = (float)E.max_p;
+        }
+        E.hist_n += 1;
+    };
     if (init) {
         E.cost = cost; E.feas = feas; E.accepted = 1;
+        push_info();  // the initial information (:277-280)
         return;
     }
     E.n_ls += 1;
@@ -501,9 +511,13 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
     } else if (last) {
         E.accepted = 0; E.ls_active = 0; E.cost = E.cost_prev; E.merit = E.merit_prev; fin = true;
     }
-    if (fin && !p.no_early_exit && fabs((E.cost_prev - E.cost) / E.cost_prev) < p.cost_thresh &&
-        E.feas <= p.feas_thresh)
-        E.inner_done = 1;
+    if (fin) {
+        // the later-termination test breaks before the iteration's entry is buffered (:358-371)
+        if (!p.no_early_exit && fabs((E.cost_prev - E.cost) / E.cost_prev) < p.cost_thresh && E.feas <= p.feas_thresh)
+            E.inner_done = 1;
+        else
+            push_info();
+    }
 }
 
 // Trajectory::update_nominal_vals for accepted elements (copy X->Xbar, U->Ubar, Defect->Defect_bar)

@@ -687,6 +687,14 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
         real a = 0;
         static_for<NX>([&](auto Cc) { vfma<Cc>(a, dc, h[Cc]); });
         if (L.row) g += a;
+        // SinglePhase::get_value_approx (G[0], H[0] of the phase, SinglePhase.cpp:365) for callers
+        // that read the value function (hsddp_set_value_export)
+        if (p.store_value && live && L.row) {
+            double *V = d.value0 + ((size_t)b * p.P + i) * (NX + NN);
+#pragma unroll
+            for (int c = 0; c < NX; ++c) V[NX + pp * NX + c] = (double)h[c];
+            V[pp] = (double)g;
+        }
     }
     return it.act ? fail : -1;
 }

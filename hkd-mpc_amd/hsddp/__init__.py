@@ -200,6 +200,17 @@ class Solver:
             out[f] = np.array([getattr(info[b], f) for b in range(self.B)])
         return out
 
+    def solver_info(self, capacity: int | None = None) -> dict:
+        """MultiPhaseDDP::get_solver_info (MultiPhaseDDP.cpp:532-541) for every element: the
+        per-iteration buffers of the last solve as lists of float32 arrays (cost, dyn_feas,
+        eqn_feas, ineq_feas), the initial entry first."""
+        cap = capacity or (1 + self.options.max_AL_iter * self.options.max_DDP_iter)
+        arrs = [np.zeros((self.B, cap), np.float32) for _ in range(4)]
+        cnt = np.zeros(self.B, np.int32)
+        check(lib().hsddp_download_solver_info(self._h, cap, *(a.ctypes.data for a in arrs), cnt.ctypes.data))
+        names = ("cost", "dyn_feas", "eqn_feas", "ineq_feas")
+        return {n: [a[b, :cnt[b]].copy() for b in range(self.B)] for n, a in zip(names, arrs)}
+
     def extract_commands(self, nsteps_between_mpc: int = 1, mpc_time: float = 0.0, dt_mpc: float = 0.01,
                          status_durations=None, foot_placements=None, solve_time: float = 0.0) -> np.ndarray:
         """HKDMPCSolver::update_foot_placement + publish_mpc_cmd (HKDMPC.cpp:207-298) for every

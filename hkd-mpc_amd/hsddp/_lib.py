@@ -96,7 +96,8 @@ EXPORTS = [
     "hsddp_default_constraint_params", "hsddp_load_settings", "hsddp_load_constraint_params",
     "hsddp_create", "hsddp_destroy", "hsddp_set_options", "hsddp_validate_options", "hsddp_upload_problem",
     "hsddp_upload_warm_start", "hsddp_solve", "hsddp_solve_begin", "hsddp_iterate", "hsddp_solve_end", "hsddp_download_trajectory", "hsddp_download_working",
-    "hsddp_download_element_info", "hsddp_synchronize", "hsddp_device_bytes", "hsddp_hkd_dynamics",
+    "hsddp_download_element_info", "hsddp_download_solver_info", "hsddp_download_lq",
+    "hsddp_download_terminal", "hsddp_set_value_export", "hsddp_download_value", "hsddp_synchronize", "hsddp_device_bytes", "hsddp_hkd_dynamics",
     "hsddp_hkd_dynamics_partial", "hsddp_hkd_foot_position", "hsddp_hkd_foot_jacobian",
     "hsddp_hkd_resetmap", "hsddp_hkd_resetmap_partial", "hsddp_device_alloc", "hsddp_device_free",
     "hsddp_memcpy_h2d", "hsddp_memcpy_d2h", "hsddp_device_synchronize", "hsddp_extract_commands",
@@ -120,6 +121,13 @@ def lib():
     L.hsddp_create.argtypes = [C.POINTER(ProblemDesc), C.POINTER(C.c_void_p)]
     L.hsddp_destroy.argtypes = [C.c_void_p]
     L.hsddp_set_options.argtypes = [C.c_void_p, C.POINTER(Options)]
+    if hasattr(L, "hsddp_download_lq"):
+        L.hsddp_download_lq.argtypes = [C.c_void_p] + [C.c_void_p] * 7
+        L.hsddp_download_terminal.argtypes = [C.c_void_p] + [C.c_void_p] * 4
+        L.hsddp_set_value_export.argtypes = [C.c_void_p, C.c_int]
+        L.hsddp_download_value.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    if hasattr(L, "hsddp_download_solver_info"):
+        L.hsddp_download_solver_info.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 5
     if hasattr(L, "hsddp_validate_options"):  # (older A/B builds lack it)
         L.hsddp_validate_options.argtypes = [C.POINTER(Options)]
     L.hsddp_upload_problem.argtypes = [C.c_void_p, IP, DP, DP, DP, DP]

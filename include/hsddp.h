@@ -18,7 +18,8 @@
  *   hsddp_solve                               MultiPhaseDDP::solve                  MultiPhaseDDP.cpp:232-428
  *   hsddp_solve_begin/_iterate/_end           the same loop split at its inner iterations (:257-303 / :304-381 / :383-408)
  *   hsddp_download_trajectory                 Trajectory fields read by the caller  HKDMPC.cpp:243-298
- *   hsddp_download_element_info               get_actual_cost / get_solver_info     MultiPhaseDDP.h:416; .cpp:532-541
+ *   hsddp_download_element_info               get_actual_cost                       MultiPhaseDDP.h:416
+ *   hsddp_download_solver_info                get_solver_info (per-iteration buffers) MultiPhaseDDP.cpp:532-541
  *   hsddp_load_quad_reference                 QuadReference::load_top_level_data   QuadReference.cpp:129-290
  *   hsddp_plan_phases                         HKDProblem::initialization (segmentation) HKDProblem.cpp:15-68
  *   hsddp_set_reference_table / _build_references  HKDSinglePhaseReference::get_reference_at_t HKDReference.cpp:8-57
@@ -179,6 +180,33 @@ int hsddp_download_trajectory(hsddp_handle h, double *Xbar, double *Ubar, double
 /* X, U, Defect, dX, dU (any may be NULL) — the working trajectory (quirk A2 state). */
 int hsddp_download_working(hsddp_handle h, double *X, double *U, double *Defect, double *dX, double *dU);
 int hsddp_download_element_info(hsddp_handle h, hsddp_element_info *info);
+/* MultiPhaseDDP::get_solver_info (MultiPhaseDDP.cpp:532-541): per element, the buffered
+ * (actual cost, dynamics feasibility, max terminal-constraint violation, max path-constraint
+ * violation) of the last solve — the initial entry after the first rollout and one per inner
+ * iteration that passed the later-termination test (:277-280, :368-371).  Arrays [B][capacity]
+ * (any may be NULL); count [B] receives the entries stored (at most capacity; the rest are 0).
+ * The handle keeps 1 + max_AL_iter * max_DDP_iter entries of its current options. */
+int hsddp_download_solver_info(hsddp_handle h, int capacity, float *cost, float *dyn_feas, float *eqn_feas,
+                               float *ineq_feas, int *count);
+/* The LQ model of the last LQ_approximation (SinglePhase.cpp:264-296; the working point X, U of
+ * the last inner iteration, quirk A2), expanded from the device's compact record into the
+ * reference Trajectory's dense blocks (TrajectoryManagement.h:65-81, RCostData
+ * HSDDP_CompoundTypes.h:91-122): A, B [B][Kc][24][24] (row-major, discrete dynamics Jacobians),
+ * l [B][Kc] running cost, lx, lu [B][Kc][24], lxx, luu [B][Kc][24][24] (lux = 0, no outputs).
+ * Any pointer may be NULL. */
+int hsddp_download_lq(hsddp_handle h, double *A, double *B, double *l, double *lx, double *lu, double *lxx,
+                      double *luu);
+/* The terminal data of every phase (TCostData, HSDDP_CompoundTypes.h:125-150, with AL terms;
+ * SinglePhase.cpp:286-295) and the reset-map Jacobian at its end (HKDReset.h:78-136; zero after
+ * the last phase): Phi [B][P], Phix [B][P][24], Phixx, Px [B][P][24][24]; any may be NULL. */
+int hsddp_download_terminal(hsddp_handle h, double *Phi, double *Phix, double *Phixx, double *Px);
+/* Value-function export (SinglePhase::get_value_approx, SinglePhaseBase.h:45): when on, every
+ * sweep stores G[0], H[0] of each phase (with the Defect[0] term, SinglePhase.cpp:365); regularisation
+ * retries then run in the sweep kernel itself.  hsddp_download_value: G [B][P][24], H [B][P][24][24]
+ * of the last successful sweep.  Off by default (the solver itself needs only the phase-boundary
+ * transfer it does in registers). */
+int hsddp_set_value_export(hsddp_handle h, int on);
+int hsddp_download_value(hsddp_handle h, double *G, double *H);
 int hsddp_synchronize(hsddp_handle h);
 size_t hsddp_device_bytes(hsddp_handle h);
 

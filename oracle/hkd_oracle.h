@@ -85,10 +85,19 @@ typedef struct {
     /* outputs */
     double cost, feas, merit, max_tconstr, max_pconstr;
     int iters, outer_iters, status, n_ls_trials;
+    /* get_solver_info buffers (MultiPhaseDDP.cpp:277-280, 368-371, 532-541): hist_cap entries of
+       (cost, feas, max_tconstr, max_pconstr) as float; NULL = not recorded.  hist_n: entries pushed */
+    float *hist;
+    int hist_cap, hist_n;
 } orc_element;
 
 void orc_default_options(orc_options *o);
 void orc_default_weights(orc_weights *w);
+/* One knot + phase end alone: l, Phi, lx, lu, lxx, luu, lux, Phix, Phixx, A, B (see the .c) */
+void orc_knot_eval(const orc_problem *p, const orc_options *o, const int *c, const int *cn, const double *x,
+                   const double *u, const double *xr, const double *ur, const double *pf, const double *x_end,
+                   const double *xr_end, const double *pf_end, const double *reb_delta, const double *reb_eps,
+                   const double *sigma, const double *lambda, double *out);
 /* Full MultiPhaseDDP::solve restatement (MultiPhaseDDP.cpp:232-428) on one element. */
 int orc_solve(const orc_problem *p, const orc_options *o, orc_element *e);
 /* Batch driver: threads over elements (CPU baseline). */

@@ -771,6 +771,84 @@ void orc_init_element(const orc_problem *p, orc_element *e)
     for (int q = 0; q < P * 4; ++q) { e->al_sigma[q] = p->td_sigma; e->al_lambda[q] = p->td_lambda; }
 }
 
+/* One knot and one phase end, evaluated alone (test infrastructure for the known-answer and
+ * finite-difference tests): a one-phase, one-knot problem whose running slot holds (x, u) with
+ * references (xr, ur, pf) and whose terminal slot holds x_end (references xr_end, pf_end), phase
+ * contact c and next contact cn.  The constraint values come from GRFConstraint::compute_violation
+ * (HKDConstraints.cpp:7-66) and TouchDownConstraint::compute_violation (:69-118), then
+ * SinglePhase::compute_cost (SinglePhase.cpp:235-262) and LQ_approximation (:264-296) run as in the
+ * solve.  out: l, Phi (2) | lx, lu (48) | lxx, luu, lux (3 x 576) | Phix (24) | Phixx (576) |
+ * A, B (2 x 576). */
+void orc_knot_eval(const orc_problem *p, const orc_options *o, const int *c, const int *cn, const double *x,
+                   const double *u, const double *xr, const double *ur, const double *pf, const double *x_end,
+                   const double *xr_end, const double *pf_end, const double *reb_delta, const double *reb_eps,
+                   const double *sigma, const double *lambda, double *out)
+{
+    orc_problem p1 = *p;
+    const int hz[1] = {1};
+    p1.n_phases = 1;
+    p1.horizons = hz;
+    p1.shooting = NULL;
+    double X[2 * NX], Xbar[2 * NX], U[NX], Ubar[NX], D[2 * NX], Db[2 * NX], dX[2 * NX], dU[NX], K[NN];
+    double RX[2 * NX], RU[2 * NX], RF[24], rd[20], re[20], as[4], al[4];
+    int cc[8];
+    memcpy(X, x, sizeof(double) * NX); memcpy(X + NX, x_end, sizeof(double) * NX);
+    memcpy(U, u, sizeof(double) * NX);
+    memcpy(RX, xr, sizeof(double) * NX); memcpy(RX + NX, xr_end, sizeof(double) * NX);
+    memcpy(RU, ur, sizeof(double) * NX); memset(RU + NX, 0, sizeof(double) * NX);
+    memcpy(RF, pf, sizeof(double) * 12); memcpy(RF + 12, pf_end, sizeof(double) * 12);
+    memcpy(rd, reb_delta, sizeof rd); memcpy(re, reb_eps, sizeof re);
+    memcpy(as, sigma, sizeof as); memcpy(al, lambda, sizeof al);
+    for (int l = 0; l < 4; ++l) { cc[l] = c[l]; cc[4 + l] = cn[l]; }
+    orc_element e;
+    memset(&e, 0, sizeof e);
+    e.contacts = cc; e.x0 = x; e.ref_x = RX; e.ref_u = RU; e.ref_foot = RF;
+    e.X = X; e.Xbar = Xbar; e.U = U; e.Ubar = Ubar; e.Defect = D; e.Defect_bar = Db; e.dX = dX; e.dU = dU; e.K = K;
+    e.reb_delta = rd; e.reb_eps = re; e.al_sigma = as; e.al_lambda = al;
+    ctx_t *C = (ctx_t *)calloc(1, sizeof(ctx_t));
+    double *pool = (double *)calloc(8 * NN + 4 * NX + 64, sizeof(double));
+    C->p = &p1; C->o = o; C->e = &e; C->P = 1; C->S = 2; C->Kc = 1;
+    C->N[0] = 1; C->s0[0] = 0; C->k0[0] = 0;
+    for (int l = 0; l < 4; ++l) { C->c[0][l] = c[l]; C->c[1][l] = cn[l]; }
+    setup_costs(C);
+    double *q = pool;
+    C->A = q; q += NN; C->B = q; q += NN; C->lxx = q; q += NN; C->luu = q; q += NN; C->lux = q; q += NN;
+    C->l = q; q += 1; C->lx = q; q += NX; C->lu = q; q += NX;
+    C->Phi = q; q += 1; C->Phix = q; q += NX; C->Phixx = q; q += NN; C->g = q; q += 20;
+    for (int l = 0; l < 4; ++l)
+        if (c[l]) grf_rows(p1.mu_fric, u + 3 * l, C->g + 5 * l);
+    for (int l = 0; l < 4; ++l) {
+        if (!(c[l] == 0 && cn[l] == 1)) continue;
+        double pfz[3];
+        orc_foot_position(l, x_end + 3, x_end, x_end + 12 + 3 * l, pfz);
+        C->h[0][l] = pfz[2] - p1.ground_height;
+    }
+    phase_compute_cost(C, 0);
+    phase_LQ(C, 0);
+    out[0] = C->l[0]; out[1] = C->Phi[0];
+    memcpy(out + 2, C->lx, sizeof(double) * NX); memcpy(out + 2 + NX, C->lu, sizeof(double) * NX);
+    memcpy(out + 2 + 2 * NX, C->lxx, sizeof(double) * NN); memcpy(out + 2 + 2 * NX + NN, C->luu, sizeof(double) * NN);
+    memcpy(out + 2 + 2 * NX + 2 * NN, C->lux, sizeof(double) * NN);
+    memcpy(out + 2 + 2 * NX + 3 * NN, C->Phix, sizeof(double) * NX);
+    memcpy(out + 2 + 3 * NX + 3 * NN, C->Phixx, sizeof(double) * NN);
+    memcpy(out + 2 + 3 * NX + 4 * NN, C->A, sizeof(double) * NN);
+    memcpy(out + 2 + 3 * NX + 5 * NN, C->B, sizeof(double) * NN);
+    free(pool);
+    free(C);
+}
+
+/* cost_buffer / dyn_feas_buffer / eqn_feas_buffer / ineq_feas_buffer .push_back (float vectors) */
+static void push_info(ctx_t *C)
+{
+    orc_element *e = C->e;
+    if (e->hist && e->hist_n < e->hist_cap) {
+        float *h = e->hist + 4 * (size_t)e->hist_n;
+        h[0] = (float)C->actual_cost; h[1] = (float)C->feas;
+        h[2] = (float)C->max_tconstr; h[3] = (float)C->max_pconstr;
+    }
+    e->hist_n++;
+}
+
 /* MultiPhaseDDP::solve (MultiPhaseDDP.cpp:232-428) */
 int orc_solve(const orc_problem *p, const orc_options *o, orc_element *e)
 {
@@ -807,6 +885,8 @@ int orc_solve(const orc_problem *p, const orc_options *o, orc_element *e)
     mp_update_nominal(C);
     mp_compute_cost(C);
     C->feas = mp_feas(C);
+    e->hist_n = 0;
+    push_info(C);  /* the initial information (MultiPhaseDDP.cpp:277-280) */
 
     while (iter_ou < o->max_AL_iter) {
         iter_ou++;
@@ -835,6 +915,7 @@ int orc_solve(const orc_problem *p, const orc_options *o, orc_element *e)
             if (!o->no_early_exit && (fabs((cost_prev - C->actual_cost) / cost_prev) < o->cost_thresh) &&
                 (C->feas <= o->dynamics_feas_thresh))
                 break;
+            push_info(C);  /* MultiPhaseDDP.cpp:368-371 */
         }
         if (o->AL_active) mp_update_AL(C);
         if (o->ReB_active) mp_update_ReB(C);

@@ -54,7 +54,8 @@ class OrcElement(C.Structure):
                 ("cost", C.c_double), ("feas", C.c_double), ("merit", C.c_double),
                 ("max_tconstr", C.c_double), ("max_pconstr", C.c_double),
                 ("iters", C.c_int), ("outer_iters", C.c_int), ("status", C.c_int),
-                ("n_ls_trials", C.c_int)]
+                ("n_ls_trials", C.c_int), ("hist", C.POINTER(C.c_float)), ("hist_cap", C.c_int),
+                ("hist_n", C.c_int)]
 
 
 def build(quiet: bool = True) -> None:
@@ -84,6 +85,7 @@ def lib():
         _lib.orc_foot_jacobian.argtypes = [C.c_int, DP, DP, DP, DP]
         _lib.orc_resetmap.argtypes = [DP, IP, IP, DP]
         _lib.orc_resetmap_partial.argtypes = [DP, IP, IP, DP]
+        _lib.orc_knot_eval.argtypes = [C.POINTER(OrcProblem), C.POINTER(OrcOptions), IP, IP] + [DP] * 13
     return _lib
 
 
@@ -160,6 +162,33 @@ def resetmap_partial(x, c, cn):
     return o
 
 
+def knot_eval(c, cn, x, u, xr, ur, pf, x_end=None, xr_end=None, pf_end=None, reb_delta=None, reb_eps=None,
+              sigma=None, lam=None, options=None, dt=0.01, weights=None) -> dict:
+    """orc_knot_eval: one knot's cost and LQ model, and one phase end's terminal data, alone."""
+    p, _hz = default_problem([1], dt)
+    for k, v in (weights or {}).items():
+        setattr(p.w, k, v)
+    o = options or default_options()
+    f = lambda a, n: np.ascontiguousarray(np.zeros(n) if a is None else a, dtype=np.float64)
+    args = [f(x, 24), f(u, 24), f(xr, 24), f(ur, 24), f(pf, 12), f(x if x_end is None else x_end, 24),
+            f(xr if xr_end is None else xr_end, 24), f(pf if pf_end is None else pf_end, 12),
+            f(np.full(20, p.grf_delta) if reb_delta is None else reb_delta, 20),
+            f(np.full(20, p.grf_eps) if reb_eps is None else reb_eps, 20),
+            f(np.full(4, p.td_sigma) if sigma is None else sigma, 4), f(np.full(4, p.td_lambda) if lam is None else lam, 4)]
+    out = np.zeros(2 + 3 * 24 + 6 * 576)
+    ci = np.asarray(c, np.int32); cni = np.asarray(cn, np.int32)
+    lib().orc_knot_eval(C.byref(p), C.byref(o), ip(ci), ip(cni), *[dp(a) for a in args], dp(out))
+    N = 576
+    r = {"l": out[0], "Phi": out[1], "lx": out[2:26], "lu": out[26:50]}
+    q = 50
+    for k in ("lxx", "luu", "lux"):
+        r[k] = out[q:q + N].reshape(24, 24); q += N
+    r["Phix"] = out[q:q + 24]; q += 24
+    for k in ("Phixx", "A", "B"):
+        r[k] = out[q:q + N].reshape(24, 24); q += N
+    return r
+
+
 # ---- solver -----------------------------------------------------------------------------------
 def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 1,
                 elements=None, weights: dict | None = None) -> dict:
@@ -204,9 +233,16 @@ def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 
         for k in st:
             setattr(e, k, dp(st[k][j]))
         lib().orc_init_element(C.byref(p), C.byref(e))
+    hcap = 1 + options.max_AL_iter * options.max_DDP_iter
+    hist = np.zeros((n, hcap, 4), np.float32)
+    for j in range(n):
+        elems[j].hist = hist[j].ctypes.data_as(C.POINTER(C.c_float))
+        elems[j].hist_cap = hcap
     lib().orc_solve_batch(C.byref(p), C.byref(options), elems, n, n_threads)
     out = dict(st)
     for f in ("cost", "feas", "merit", "max_tconstr", "max_pconstr", "iters", "outer_iters", "status",
               "n_ls_trials"):
         out[f] = np.array([getattr(elems[j], f) for j in range(n)])
+    # get_solver_info buffers per element: [n_j][4] (cost, dyn_feas, eqn_feas, ineq_feas)
+    out["solver_info"] = [hist[j, :min(elems[j].hist_n, hcap)].copy() for j in range(n)]
     return out

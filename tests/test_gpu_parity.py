@@ -264,3 +264,22 @@ def test_retries_match_oracle(monkeypatch, B, cap):
     assert np.array_equal(g["n_ls_trials"][sample], r["n_ls_trials"])
     for f in ("Xbar", "Ubar", "K", "dU"):
         assert rel(g[f][sample], r[f]) < 1e-9, f
+
+
+def test_solver_info_history_matches_oracle():
+    """get_solver_info (MultiPhaseDDP.cpp:532-541): the per-element buffers of a full solve with
+    early exits — the initial entry and one per inner iteration that passes the later-termination
+    test (:277-280, :358-371) — equal the oracle's entry for entry (float32 values)."""
+    prob = syn.make_batch(6, 4, 20, "trot")
+    s = hsddp.Solver(prob, hsddp.load_settings())
+    s.solve()
+    h = s.solver_info()
+    info = s.element_info()
+    s.close()
+    r = O.solve_batch(prob, O.default_options(), n_threads=8)
+    assert np.array_equal(info["iters"], r["iters"])
+    for b in range(6):
+        ref = r["solver_info"][b]
+        assert len(h["cost"][b]) == len(ref) > 1, b
+        got = np.stack([h[k][b] for k in ("cost", "dyn_feas", "eqn_feas", "ineq_feas")], 1)
+        assert np.allclose(got, ref, rtol=1e-6, atol=1e-9), b
