@@ -628,6 +628,7 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
                 real px[12];
 #pragma unroll
                 for (int k = 0; k < 12; ++k) px[k] = (real)Px[192 * Kc + 16 * k + L.pos];
+                if constexpr (sizeof(real) == 4) dpp_ready(px);  // converted by VALU: DPP sources
                 static_for<8>([&](auto Kk) {
                     static_for<NX>([&](auto Cc) { vfma<NX * Kk + Cc>(wr[Cc], px, h[8 * Kc + Kk]); });
                 });
@@ -650,6 +651,7 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
                 real px[12];
 #pragma unroll
                 for (int k = 0; k < 12; ++k) px[k] = (real)Px[192 * Kc + 16 * k + L.pos];
+                if constexpr (sizeof(real) == 4) dpp_ready(px);  // converted by VALU: DPP sources
                 static_for<8>([&](auto Jj) {
                     static_for<NX>([&](auto Cc) { vfma<NX * Jj + Cc>(vr[Cc], px, wc[8 * Kc + Jj]); });
                 });

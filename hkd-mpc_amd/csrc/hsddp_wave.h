@@ -139,6 +139,18 @@ DEV void bfma(T &acc, T coef, T x)
         asm volatile("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(coef), "v"(x), "i"(j));
 }
 
+// DPP sources that VALU instructions produce (e.g. values converted to fp32): every value exists
+// before the s_nop, which gives the last of them its two wait states before the first DPP read
+// (the inline-asm DPP instructions are invisible to the compiler's hazard recognizer;
+// tools/dpp_hazards.py checks the emitted code)
+template <typename T, int N>
+DEV void dpp_ready(T (&a)[N])
+{
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(a[i]));
+    asm volatile("s_nop 1");
+}
+
 // acc += V[n] * x, where the coefficient vector V is spread over the DPP row: V[16 k + j] is held
 // by register cf[k] of position j (compile-time n)
 template <int n, typename T, int NC>

@@ -211,6 +211,35 @@ class Solver:
         names = ("cost", "dyn_feas", "eqn_feas", "ineq_feas")
         return {n: [a[b, :cnt[b]].copy() for b in range(self.B)] for n, a in zip(names, arrs)}
 
+    def lq(self) -> dict:
+        """The LQ model of the last LQ_approximation (SinglePhase.cpp:264-296) as the reference
+        Trajectory's dense blocks (TrajectoryManagement.h:65-81): A, B, lxx, luu [B][Kc][24][24],
+        lx, lu [B][Kc][24], l [B][Kc] (lux = 0)."""
+        B, Kc = self.B, self.Kc
+        out = {k: np.empty((B, Kc, 24, 24)) for k in ("A", "B", "lxx", "luu")}
+        out.update(lx=np.empty((B, Kc, 24)), lu=np.empty((B, Kc, 24)), l=np.empty((B, Kc)))
+        check(lib().hsddp_download_lq(self._h, *(out[k].ctypes.data for k in ("A", "B", "l", "lx", "lu", "lxx", "luu"))))
+        return out
+
+    def terminal(self) -> dict:
+        """Terminal data of every phase (TCostData + AL terms, reset-map Jacobian Px; zero after the
+        last phase): Phi [B][P], Phix [B][P][24], Phixx, Px [B][P][24][24]."""
+        P = self.P
+        out = {"Phi": np.empty((self.B, P)), "Phix": np.empty((self.B, P, 24)),
+               "Phixx": np.empty((self.B, P, 24, 24)), "Px": np.empty((self.B, P, 24, 24))}
+        check(lib().hsddp_download_terminal(self._h, *(out[k].ctypes.data for k in ("Phi", "Phix", "Phixx", "Px"))))
+        return out
+
+    def set_value_export(self, on: bool = True) -> None:
+        """Store G[0], H[0] of every phase in each sweep (SinglePhase::get_value_approx)."""
+        check(lib().hsddp_set_value_export(self._h, int(bool(on))))
+
+    def value(self) -> dict:
+        P = self.P
+        G = np.empty((self.B, P, 24)); H = np.empty((self.B, P, 24, 24))
+        check(lib().hsddp_download_value(self._h, G.ctypes.data, H.ctypes.data))
+        return {"G": G, "H": H}
+
     def extract_commands(self, nsteps_between_mpc: int = 1, mpc_time: float = 0.0, dt_mpc: float = 0.01,
                          status_durations=None, foot_placements=None, solve_time: float = 0.0) -> np.ndarray:
         """HKDMPCSolver::update_foot_placement + publish_mpc_cmd (HKDMPC.cpp:207-298) for every

@@ -192,7 +192,8 @@ int hsddp_download_solver_info(hsddp_handle h, int capacity, float *cost, float 
  * the last inner iteration, quirk A2), expanded from the device's compact record into the
  * reference Trajectory's dense blocks (TrajectoryManagement.h:65-81, RCostData
  * HSDDP_CompoundTypes.h:91-122): A, B [B][Kc][24][24] (row-major, discrete dynamics Jacobians),
- * l [B][Kc] running cost, lx, lu [B][Kc][24], lxx, luu [B][Kc][24][24] (lux = 0, no outputs).
+ * l [B][Kc] running cost of the last compute_cost (the last rollout's trajectory, SinglePhase.cpp:
+ * 235-262), lx, lu [B][Kc][24], lxx, luu [B][Kc][24][24] (lux = 0, no outputs).
  * Any pointer may be NULL. */
 int hsddp_download_lq(hsddp_handle h, double *A, double *B, double *l, double *lx, double *lu, double *lxx,
                       double *luu);

@@ -95,6 +95,7 @@ def sweep(prob, b, X, U, Defect, reg=0.0, delta=0.1, eps=0.1, sigma=50.0, lam=0.
         lq.append((ks, Phix, Phixx, Px))
     K = [None] * k0[-1]; dU = [None] * k0[-1]
     G0 = H0 = None
+    V0 = [None] * P  # (G[0], H[0]) per phase, SinglePhase.cpp:365
     for i in reversed(range(P)):
         ks, Phix, Phixx, _ = lq[i]
         if i == P - 1:
@@ -115,6 +116,7 @@ def sweep(prob, b, X, U, Defect, reg=0.0, delta=0.1, eps=0.1, sigma=50.0, lam=0.
             G = Qx - Qux.T @ Qi @ Qu
             H = Qxx - Qux.T @ Qi @ Qux
         G0, H0 = G + H @ Defect[s0[i]], H
+        V0[i] = (G0, H0)
     # linear rollout (eps = 1)
     dX = np.zeros_like(X); du_all = np.zeros_like(U)
     dV1 = dV2 = 0.0
@@ -134,7 +136,8 @@ def sweep(prob, b, X, U, Defect, reg=0.0, delta=0.1, eps=0.1, sigma=50.0, lam=0.
             dV2 += dX[s] @ lxx @ dX[s] + du @ luu @ du
         xe = dX[s0[i] + hz[i]]
         dV1 += Phix @ xe; dV2 += xe @ Phixx @ xe
-    return {"K": np.array(K), "dU": np.array(dU), "dX": dX, "du": du_all, "dV1": dV1, "dV2": dV2}
+    return {"K": np.array(K), "dU": np.array(dU), "dX": dX, "du": du_all, "dV1": dV1, "dV2": dV2,
+            "lq": lq, "G0": np.array([v[0] for v in V0]), "H0": np.array([v[1] for v in V0])}
 
 
 def initial_rollout(prob, b):

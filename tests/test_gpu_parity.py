@@ -283,3 +283,42 @@ def test_solver_info_history_matches_oracle():
         assert len(h["cost"][b]) == len(ref) > 1, b
         got = np.stack([h[k][b] for k in ("cost", "dyn_feas", "eqn_feas", "ineq_feas")], 1)
         assert np.allclose(got, ref, rtol=1e-6, atol=1e-9), b
+
+
+@pytest.mark.parametrize("gait,P,N", [("trot", 2, 8), ("jump", 8, 4)])
+def test_trajectory_exports_match_numpy_restatement(gait, P, N):
+    """The dense Trajectory fields a reference caller reads (TrajectoryManagement.h:49-81): the LQ
+    model A, B, lx, lu, lxx, luu of the first LQ_approximation (SinglePhase.cpp:264-296), the
+    terminal Phix, Phixx (+ AL) and reset-map Jacobian Px per phase, and the value function G[0],
+    H[0] per phase of the first sweep (SinglePhase.cpp:365) — against the independent dense numpy
+    restatement (tests/numpy_riccati.py) at the initial rollout.  l and Phi are those of the last
+    compute_cost (the last line-search trial, SinglePhase.cpp:235-262): they sum to the accepted cost."""
+    import numpy_riccati as NR
+    B = 3
+    prob = syn.make_batch(B, P, N, gait)
+    s = hsddp.Solver(prob, hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=1))
+    s.set_value_export(True)
+    s.solve()
+    lq, tm, v, info = s.lq(), s.terminal(), s.value(), s.element_info()
+    s.close()
+    k0 = np.cumsum([0] + list(prob["horizons"]))
+    for b in range(B):
+        X, U, D = NR.initial_rollout(prob, b)
+        ref = NR.sweep(prob, b, X, U, D)
+        for i in range(P):
+            ks, Phix, Phixx, Px = ref["lq"][i]
+            for k in range(prob["horizons"][i]):
+                kc = k0[i] + k
+                for name, want in zip(("A", "B", "lx", "lu", "lxx", "luu"), ks[k]):
+                    assert rel(lq[name][b, kc], want) < 1e-12, (b, kc, name)
+            assert rel(tm["Phix"][b, i], Phix) < 1e-12, (b, i)
+            assert rel(tm["Phixx"][b, i], Phixx) < 1e-12, (b, i)
+            if Px is None:
+                assert np.all(tm["Px"][b, i] == 0)
+            else:
+                assert rel(tm["Px"][b, i], Px) < 1e-12, (b, i)
+        assert rel(v["G"][b], ref["G0"]) < 1e-9, b
+        assert rel(v["H"][b], ref["H0"]) < 1e-9, b
+        if info["n_ls_trials"][b] < 4:  # accepted: the last trial's slot costs are the element's cost
+            total = lq["l"][b].sum() + tm["Phi"][b].sum()
+            assert abs(total - info["cost"][b]) <= 1e-12 * abs(total), b
