@@ -24,7 +24,7 @@ constexpr int NN = 576;
 constexpr int MAXP = 16;
 // Gains are stored for the 12 controls whose B column is non-zero: row q (0..11) is control
 // u = q when leg q/3 is in stance, u = 12 + q when it swings.  The other 12 rows of the
-// reference's 24 x 24 K are exactly zero (hsddp_backward.hip, bwd_knot) and are expanded on
+// reference's 24 x 24 K are exactly zero (hsddp_sweep.hip) and are expanded on
 // download.
 constexpr int KCW = 12 * 24;
 

@@ -4,9 +4,9 @@
 // for B trajectories is:
 //   k_lq        knot-parallel  cost at (X, U) + compact LQ model   SinglePhase::compute_cost/LQ_approximation
 //   k_terminal  (elem, phase)  Phix, Phixx (+AL), reset Jacobian   SinglePhase.cpp:286-295; HKDReset.h:78-136
-//   k_riccati   one wave/elem  regularised Riccati sweep over all phases     (hsddp_backward.hip)
+//   k_riccati   one wave/2 elems regularised Riccati sweep over all phases   (hsddp_sweep.hip)
 //                              MultiPhaseDDP.cpp:141-229; SinglePhase.cpp:298-367
-//   k_lin_rollout one wave/elem  MS linear rollout + merit                    (hsddp_backward.hip)
+//   k_lin_rollout one wave/elem  MS linear rollout + merit                    (hsddp_linear.hip)
 //                              MultiPhaseDDP.cpp:20-50, 309-318; SinglePhase.cpp:144-178
 //   k_rollout   knot-parallel  one line-search trial (all knots are shooting states)  SinglePhase.cpp:181-233
 //   k_decide    per element    merit acceptance (MultiPhaseDDP.cpp:113-133) + inner-loop exit tests

@@ -26,7 +26,7 @@
 //   Gauss-Jordan on [Quu_cc | Qux_c | Qu_c]: 12 pivot steps, columns in lanes, pivots by DPP
 //   K = -Quu_cc^-1 Qux_c, dU, G = Qx - Qux_c^T Quu_cc^-1 Qu_c, dV
 //   H = Qxx - Qux_c^T Quu_cc^-1 Qux_c on the matrix cores (v_mfma_f64_16x16x4_f64, symmetric tiles)
-// Only the 12 coupled controls (those whose B column is non-zero, hsddp_backward.hip notes) enter
+// Only the 12 coupled controls (those whose B column is non-zero, DESIGN.md §3.1 "Decoupled controls") enter
 // the elimination; the other 12 are decoupled: K row 0, dU = -lu / (dt R + reg), exactly as the
 // reference's dense 24-control solve gives them.  PSD test: every elimination pivot of Quu_cc and
 // every decoupled diagonal must exceed 1e-9 (the reference's LDLT of Quu - 1e-9 I).
