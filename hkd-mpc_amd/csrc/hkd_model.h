@@ -311,6 +311,22 @@ HKD_FN double hkd_foot_height_grad(int l, const double *x, double *hx)
     return x[5] + R.r[2][0] * pb[0] + R.r[2][1] * pb[1] + R.r[2][2] * pb[2];
 }
 
+// hkd_foot_height_grad's non-zeros only (no runtime-indexed local array): ge = d h / d eul (state
+// 0..2), gq = d h / d foot position of leg l (states 12 + 3 l + k); d h / d state 5 is 1
+HKD_FN double hkd_foot_height_grad_sparse(int l, const double *x, double *ge, double *gq)
+{
+    Rot R, Dy, Dp, Dr;
+    rot_zyx(x, R);
+    rot_zyx_grad(x, Dy, Dp, Dr);
+    double pb[3], dpb[3][3];
+    foot_body(l, x + 12 + 3 * l, pb, dpb);
+    ge[0] = Dy.r[2][0] * pb[0] + Dy.r[2][1] * pb[1] + Dy.r[2][2] * pb[2];
+    ge[1] = Dp.r[2][0] * pb[0] + Dp.r[2][1] * pb[1] + Dp.r[2][2] * pb[2];
+    ge[2] = Dr.r[2][0] * pb[0] + Dr.r[2][1] * pb[1] + Dr.r[2][2] * pb[2];
+    for (int k = 0; k < 3; ++k) gq[k] = R.r[2][0] * dpb[0][k] + R.r[2][1] * dpb[1][k] + R.r[2][2] * dpb[2][k];
+    return x[5] + R.r[2][0] * pb[0] + R.r[2][1] * pb[1] + R.r[2][2] * pb[2];
+}
+
 // HKDReset::resetmap
 HKD_FN void hkd_resetmap(const double *x, const int *c, const int *cn, double *xn)
 {

@@ -27,9 +27,18 @@ DEV void pin(T (&a)[N])
 
 // ---------------------------------------------------------------------------------------------
 // cost model helpers (HKDCost.h / HKDCost.cpp / SinglePhaseInterface.cpp:55-118)
-DEV double q_diag(const Params &p, const int *c, int j) { return j < 12 ? p.qbase[j] : p.q_qJ * (1 - c[(j - 12) / 3]); }
+// Params read in place from the kernel-argument segment (scalar loads).  Every kernel takes Params
+// first, so it sits at offset 0; indexing the by-value copy with a runtime index makes the compiler
+// copy the whole struct to scratch, per lane.
+typedef const __attribute__((address_space(4))) Params KParams;
+DEV KParams *kparams() { return (KParams *)__builtin_amdgcn_kernarg_segment_ptr(); }
+
+// PT: Params (compile-time indices) or KParams (runtime indices)
+template <typename PT>
+DEV double q_diag(const PT &p, const int *c, int j) { return j < 12 ? p.qbase[j] : p.q_qJ * (1 - c[(j - 12) / 3]); }
 DEV double r_diag(const Params &p, int j) { return j < 12 ? p.r_grf : p.r_qJd; }
-DEV double foot_weight(const Params &p, const int *c, int j) { return p.foot_gain * p.foot_w[j % 3] * c[j / 3]; }
+template <typename PT>
+DEV double foot_weight(const PT &p, const int *c, int j) { return p.foot_gain * p.foot_w[j % 3] * c[j / 3]; }
 DEV bool touchdown(const int *c, const int *cn, int l) { return c[l] == 0 && cn[l] == 1; }
 
 DEV void slot_phase(const Params &p, int s, int &i, int &k)

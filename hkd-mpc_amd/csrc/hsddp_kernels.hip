@@ -192,44 +192,49 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
         sc[t] = cc[t]; scn[t] = cc[4 + t];
     }
     __syncthreads();
-    if (t < 4) {
+    for (int e = t; e < 4 * NX; e += 64) (&shx[0][0])[e] = 0.0;
+    __syncthreads();
+    if (t < 4) {  // touchdown legs: h and its gradient (non-zeros at 0..2, 5, 12 + 3 l + k)
         const int l = t;
-        double hx[NX];
-        double h = 0.0;
-        bool td = touchdown(sc, scn, l);
-        if (td) h = hkd_foot_height_grad(l, sx, hx) - p.ground;
-        for (int j = 0; j < NX; ++j) shx[l][j] = td ? hx[j] : 0.0;
+        const bool td = touchdown(sc, scn, l);
+        double h = 0.0, ge[3], gq[3];
+        if (td) {
+            h = hkd_foot_height_grad_sparse(l, sx, ge, gq) - p.ground;
+            for (int k = 0; k < 3; ++k) { shx[l][k] = ge[k]; shx[l][12 + 3 * l + k] = gq[k]; }
+            shx[l][5] = 1.0;
+        }
         double sg = d.al_sigma[((size_t)b * p.P + i) * 4 + l], lm = d.al_lambda[((size_t)b * p.P + i) * 4 + l];
         scoef[l][0] = (td && p.AL_active) ? sg * h + lm : 0.0;
         scoef[l][1] = (td && p.AL_active) ? sg * (1 + h) + lm : 0.0;
     }
     __syncthreads();
+    KParams &kp = *kparams();  // runtime-indexed weights
     double *rec = d.term + ((size_t)b * p.P + i) * TW;
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
     if (t < NX) { // Phix
         const int j = t;
-        double v = p.qf_gain * p.qf_scale[j] * q_diag(p, sc, j) * (sx[j] - xr[j]);
+        double v = kp.qf_gain * kp.qf_scale[j] * q_diag(kp, sc, j) * (sx[j] - xr[j]);
         if (j >= 3 && j < 6) {
             for (int l = 0; l < 4; ++l) {
                 int m = 3 * l + (j - 3);
                 double e = (sx[12 + m] - sx[j]) - (pf[m] - xr[j]);
-                v += -(p.foot_term_grad * sc[l] * foot_weight(p, sc, m) * e);
+                v += -(p.foot_term_grad * sc[l] * foot_weight(kp, sc, m) * e);
             }
         } else if (j >= 12) {
             int m = j - 12, l = m / 3;
             double e = (sx[j] - sx[3 + m % 3]) - (pf[m] - xr[3 + m % 3]);
-            v += p.foot_term_grad * sc[l] * foot_weight(p, sc, m) * e;
+            v += p.foot_term_grad * sc[l] * foot_weight(kp, sc, m) * e;
         }
         for (int l = 0; l < 4; ++l) v += scoef[l][0] * shx[l][j];
         rec[TM_PHIX + j] = v;
     }
     for (int e = t; e < NN; e += 64) { // Phixx
         const int r = e / NX, cidx = e % NX;
-        double v = (r == cidx) ? p.qf_gain * p.qf_scale[r] * q_diag(p, sc, r) : 0.0;
+        double v = (r == cidx) ? kp.qf_gain * kp.qf_scale[r] * q_diag(kp, sc, r) : 0.0;
         // foot Hessian 20 D^T Qfoot D
         for (int l = 0; l < 4; ++l)
             for (int j = 0; j < 3; ++j) {
-                double w = p.foot_term_grad * sc[l] * sc[l] * foot_weight(p, sc, 3 * l + j);
+                double w = p.foot_term_grad * sc[l] * sc[l] * foot_weight(kp, sc, 3 * l + j);
                 int a = 3 + j, bb = 12 + 3 * l + j;
                 if ((r == a && cidx == a) || (r == bb && cidx == bb)) v += w;
                 if ((r == a && cidx == bb) || (r == bb && cidx == a)) v -= w;
@@ -237,12 +242,34 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
         for (int l = 0; l < 4; ++l) v += scoef[l][1] * (shx[l][r] * shx[l][cidx]);
         rec[TM_PHIXX + e] = v;
     }
-    if (i < p.P - 1) { // Px rows at X_i[N]: one row per lane, staged in LDS, stored coalesced by the wave
+    if (i < p.P - 1) { // Px at X_i[N] (HKDReset.h:78-136), staged in LDS, stored coalesced by the wave
         __shared__ double spx[NX * (NX + 1)];
-        if (t < NX) {
-            double row[NX];
-            hkd_resetmap_partial_row(sx, sc, scn, t, row);
-            for (int j = 0; j < NX; ++j) spx[t * (NX + 1) + j] = row[j];
+        for (int e = t; e < NX * (NX + 1); e += 64) spx[e] = (e / (NX + 1) == e % (NX + 1)) ? 1.0 : 0.0;
+        __syncthreads();
+        if (t < 4) {  // rows 12 + 3 l + k of leg l: zero at lift-off, foot Jacobian rows at touchdown
+            const int l = t;
+            if (sc[l] && !scn[l]) {
+                for (int k = 0; k < 3; ++k) spx[(12 + 3 * l + k) * (NX + 2)] = 0.0;
+            } else if (!sc[l] && scn[l]) {  // rows k < 2: the foot Jacobian's rows (hkd_foot_jacobian)
+                Rot R, Dy, Dp, Dr;
+                rot_zyx(sx, R);
+                rot_zyx_grad(sx, Dy, Dp, Dr);
+                double pb[3], dpb[3][3];
+                foot_body(l, sx + 12 + 3 * l, pb, dpb);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    double *row = spx + (12 + 3 * l + k) * (NX + 1);
+                    row[12 + 3 * l + k] = 0.0;
+                    if (k == 2) continue;
+                    row[0] = Dy.r[k][0] * pb[0] + Dy.r[k][1] * pb[1] + Dy.r[k][2] * pb[2];
+                    row[1] = Dp.r[k][0] * pb[0] + Dp.r[k][1] * pb[1] + Dp.r[k][2] * pb[2];
+                    row[2] = Dr.r[k][0] * pb[0] + Dr.r[k][1] * pb[1] + Dr.r[k][2] * pb[2];
+                    row[3 + k] = 1.0;
+#pragma unroll
+                    for (int m = 0; m < 3; ++m)
+                        row[12 + 3 * l + m] = R.r[k][0] * dpb[0][m] + R.r[k][1] * dpb[1][m] + R.r[k][2] * dpb[2][m];
+                }
+            }
         }
         __syncthreads();
         for (int e = t; e < NN; e += 64) rec[TM_PX + e] = spx[(e / NX) * (NX + 1) + e % NX];
@@ -291,22 +318,11 @@ DEV void finish_slot(const Params &p, const Bufs &d, int b, int s, int i, int k,
 // knot k-1: the nonlinear rollout is knot-parallel.  U = Ubar + eps du with du = dU + K dX from the
 // linear rollout (equal to the reference's Ubar + eps dU + K (X - Xbar) up to rounding of X - Xbar).
 //
-// One wave per 64 consecutive slots.  The trial rows it needs (states of its slots and the one
-// before, their controls and the one before) are formed with coalesced 16-byte loads (lanes over
-// row entries, not rows) into LDS — the output X and U rows are stored from the same pass — and
-// each lane then reads its rows from LDS: the row-per-lane global accesses this replaces touched
-// 64 cache lines per instruction.
+// One wave per 64 consecutive slots.  The trial state rows it needs (its slots and the one before)
+// are formed with coalesced 16-byte loads (lanes over row entries, not rows) into LDS — the output
+// X rows are stored from the same pass — and each lane then reads its rows from LDS.
 constexpr int RS = NX + 1;  // LDS row stride (doubles): conflict-free row-per-lane reads
 constexpr int RW = 65;      // rows per wave: 64 slots and the one before
-
-// control row (b Kc + kc) of slot g; terminal slots map to the next phase's first control
-DEV long slot_kq(const Params &p, long g)
-{
-    const int b = (int)(g / p.S), s = (int)(g % p.S);
-    int i, k;
-    slot_phase(p, s, i, k);
-    return (long)b * p.Kc + s - i;
-}
 
 // X_t = Xbar + eps dX (or U_t = Ubar + eps du) for rows r0 .. r0 + RW - 1 of an [rows][24] pair
 // into LDS; rows of inactive elements are skipped, own rows (own(r)) are stored to `out`
@@ -331,14 +347,33 @@ DEV void stage_trial(double *L, const double *bar, const double *del, double *ou
     }
 }
 
-__global__ __launch_bounds__(64) void k_rollout(Params p, Bufs d, double eps, int init)
+#ifndef HSDDP_ROLLOUT_WAVES
+#define HSDDP_ROLLOUT_WAVES 2  // measured: 2 (256 VGPRs, no spills) 0.93 ms/step forward vs 3: 1.23, 4: 1.07
+#endif
+
+// trial control row r: U = Ubar + eps du, straight from global memory (the wave's 64 rows are one
+// contiguous 12 KB range, so the row-per-lane loads are served by the vector L1 / L2)
+DEV void trial_row(const Bufs &d, long r, double eps, double *u)
 {
-    __shared__ double Xt[RW * RS], Ut[RW * RS];
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const d2 *ub = (const d2 *)(d.Ubar + r * NU), *du = (const d2 *)(d.du + r * NU);
+#pragma unroll
+    for (int j = 0; j < NU / 2; ++j) {
+        const d2 a = ub[j], e = du[j];
+        u[2 * j] = a.x + eps * e.x;
+        u[2 * j + 1] = a.y + eps * e.y;
+    }
+}
+
+// Only the state rows go through LDS (13 KB per wave); the control rows are read per lane
+// (trial_row), the slot's own control row stored from registers.  With both row sets in LDS
+// (26 KB per wave) only 6 waves fit a CU: 1.25 ms/step of line search vs 0.93 here.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOUT_WAVES))) void k_rollout(Params p, Bufs d, double eps, int init)
+{
+    __shared__ double Xt[RW * RS];
     const int lane = threadIdx.x;
     const long total = (long)p.B * p.S, g0 = (long)blockIdx.x * 64, gid = g0 + lane;
     const long gl = min(g0 + 63, total - 1);
-    // the wave's slots span elements bA .. bB: two when S >= 64 (the metric's 204), more for short
-    // horizons; the first and last flags are kept in registers, any between are read again
     const int bA = (int)(g0 / p.S), bB = (int)(gl / p.S);
     auto act = [&](int b) { const ElemState &E = d.el[b]; return init ? !E.done : E.ls_active != 0; };
     const bool aA = act(bA), aB = act(bB);
@@ -349,16 +384,6 @@ __global__ __launch_bounds__(64) void k_rollout(Params p, Bufs d, double eps, in
     const long xr0 = g0 - 1;
     stage_trial(Xt, d.Xbar, d.dX, d.X, xr0, total, p.S, eps, lane, active,
                 [&](long r) { return r >= g0; });
-    const long ur0 = slot_kq(p, g0) - 1, nk = (long)p.B * p.Kc;
-    // own control rows: the controls of this wave's non-terminal slots
-    stage_trial(Ut, d.Ubar, d.du, d.U, ur0, nk, p.Kc, eps, lane, active, [&](long r) {
-        const int b = (int)(r / p.Kc), kc = (int)(r % p.Kc);
-        int i = 0;
-        for (int j = 1; j < p.P; ++j)
-            if (kc >= p.k0[j]) i = j;
-        const long g = (long)b * p.S + kc + i;
-        return g >= g0 && g <= gl;
-    });
     __syncthreads();
     if (gid >= total) return;
     const int b = (int)(gid / p.S), s = (int)(gid % p.S);
@@ -368,6 +393,7 @@ __global__ __launch_bounds__(64) void k_rollout(Params p, Bufs d, double eps, in
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     const double *x = Xt + (gid - xr0) * RS;
+    const long kq = (long)b * p.Kc + s - i;  // the slot's control row (k < N)
     double xs[NX];
     if (k == 0) {
         if (i == 0) {
@@ -379,11 +405,19 @@ __global__ __launch_bounds__(64) void k_rollout(Params p, Bufs d, double eps, in
             hkd_resetmap(x - RS, cp_, cpn, xs);
         }
     } else {
-        const long kq = (long)b * p.Kc + s - i;
+        double up[NU];
+        trial_row(d, kq - 1, eps, up);
         double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
-        hkd_step(x - RS, Ut + (kq - 1 - ur0) * RS, cd, p.dt, xs);
+        hkd_step(x - RS, up, cd, p.dt, xs);
     }
-    const double *u = k < p.N[i] ? Ut + ((long)b * p.Kc + p.k0[i] + k - ur0) * RS : nullptr;
+    double u[NU];  // read by finish_slot only when k < N
+    if (k < p.N[i]) {
+        trial_row(d, kq, eps, u);
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        d2 *ug = (d2 *)(d.U + kq * NU);
+#pragma unroll
+        for (int j = 0; j < NU / 2; ++j) ug[j] = d2{u[2 * j], u[2 * j + 1]};
+    }
     finish_slot(p, d, b, s, i, k, c, cn, x, xs, u);
 }
 

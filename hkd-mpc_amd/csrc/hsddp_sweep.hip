@@ -149,10 +149,6 @@ struct Phase {
 
 // Phase layout entries with a runtime phase index, read from the kernel-argument segment (scalar
 // loads): indexing the by-value Params directly makes the compiler copy it to scratch.
-DEV const __attribute__((address_space(4))) Params *kparams()
-{
-    return (const __attribute__((address_space(4))) Params *)__builtin_amdgcn_kernarg_segment_ptr();
-}
 DEV int phase_N(int i) { return kparams()->N[i]; }
 DEV int phase_s0(int i) { return kparams()->s0[i]; }
 DEV int phase_k0(int i) { return kparams()->k0[i]; }
