@@ -1143,6 +1143,53 @@ extern "C" int hsddp_hkd_resetmap_partial(const double *x, const int *c, const i
     return check_launch();
 }
 
+// weights / dt of a plugin primitive in the solver's parameter block (the kernels share the
+// solver's cost helpers)
+static Params plugin_params(const hsddp_hkd_weights &w, double dt)
+{
+    Params p{};
+    p.dt = dt;
+    for (int j = 0; j < 3; ++j) { p.qbase[j] = w.q_eul[j]; p.qbase[3 + j] = w.q_pos[j]; p.qbase[6 + j] = w.q_omega[j]; p.qbase[9 + j] = w.q_v[j]; }
+    p.q_qJ = w.q_qJ;
+    for (int j = 0; j < 24; ++j) p.qf_scale[j] = w.qf_scale[j];
+    p.qf_gain = w.qf_gain; p.r_grf = w.r_grf; p.r_qJd = w.r_qJd;
+    for (int j = 0; j < 3; ++j) p.foot_w[j] = w.foot_w[j];
+    p.foot_gain = w.foot_gain; p.foot_term_cost = w.foot_term_cost; p.foot_term_grad = w.foot_term_grad;
+    return p;
+}
+extern "C" int hsddp_hkd_running_cost(const double *x, const double *u, const int *c, const double *xr, const double *ur,
+                                      const double *pf, const hsddp_hkd_weights *w, double dt, int terms, double *l,
+                                      double *lx, double *lu, double *lxx, double *luu, int n, void *stream)
+{
+    if (!x || !u || !c || !xr || !ur || !pf || !w || n < 0 || (terms & ~3)) return fail(HSDDP_ERR_ARG, "bad argument");
+    if (n) launch_model_running_cost(plugin_params(*w, dt), x, u, c, xr, ur, pf, terms, l, lx, lu, lxx, luu, n,
+                                     (hipStream_t)stream);
+    return check_launch();
+}
+extern "C" int hsddp_hkd_terminal_cost(const double *x, const int *c, const double *xr, const double *pf,
+                                       const hsddp_hkd_weights *w, int terms, double *Phi, double *Phix, double *Phixx,
+                                       int n, void *stream)
+{
+    if (!x || !c || !xr || !pf || !w || n < 0 || (terms & ~3)) return fail(HSDDP_ERR_ARG, "bad argument");
+    if (n) launch_model_terminal_cost(plugin_params(*w, 0.0), x, c, xr, pf, terms, Phi, Phix, Phixx, n,
+                                      (hipStream_t)stream);
+    return check_launch();
+}
+extern "C" int hsddp_hkd_grf_constraint(const double *u, const int *c, double mu, double *g, double *gu, int n,
+                                        void *stream)
+{
+    if (!u || !c || n < 0) return fail(HSDDP_ERR_ARG, "bad argument");
+    if (n) launch_model_grf(u, c, mu, g, gu, n, (hipStream_t)stream);
+    return check_launch();
+}
+extern "C" int hsddp_hkd_touchdown_constraint(const double *x, const int *c, const int *cn, double ground, double *h,
+                                              double *hx, int n, void *stream)
+{
+    if (!x || !c || !cn || n < 0) return fail(HSDDP_ERR_ARG, "bad argument");
+    if (n) launch_model_touchdown(x, c, cn, ground, h, hx, n, (hipStream_t)stream);
+    return check_launch();
+}
+
 extern "C" void *hsddp_device_alloc(size_t bytes, int device)
 {
     if (hipSetDevice(device) != hipSuccess) { g_err = "hipSetDevice failed"; return nullptr; }

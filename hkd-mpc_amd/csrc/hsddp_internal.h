@@ -140,5 +140,13 @@ void launch_model_partial(const double *x, const double *u, const double *c, dou
 void launch_model_foot(const double *x, const int *leg, double *p, double *J, int n, hipStream_t st);
 void launch_model_reset(const double *x, const int *c, const int *cn, double *xn, double *Px, int n,
                         hipStream_t st);
+void launch_model_running_cost(const Params &p, const double *x, const double *u, const int *c, const double *xr,
+                               const double *ur, const double *pf, int terms, double *l, double *lx, double *lu,
+                               double *lxx, double *luu, int n, hipStream_t st);
+void launch_model_terminal_cost(const Params &p, const double *x, const int *c, const double *xr, const double *pf,
+                                int terms, double *Phi, double *Phix, double *Phixx, int n, hipStream_t st);
+void launch_model_grf(const double *u, const int *c, double mu, double *g, double *gu, int n, hipStream_t st);
+void launch_model_touchdown(const double *x, const int *c, const int *cn, double ground, double *h, double *hx, int n,
+                            hipStream_t st);
 
 }  // namespace hsddp

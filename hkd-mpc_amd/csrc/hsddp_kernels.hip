@@ -706,6 +706,174 @@ __global__ void k_model_foot(const double *x, const int *leg, double *p, double 
     }
 }
 
+// ---- cost / constraint plugin primitives (the facade's hkd:: plugin bodies) ------------------
+// One thread per point.  Params carries the weights (hsddp_hkd_weights via fill_weights) and dt;
+// every index below is compile-time, so the by-value Params stays in SGPRs.
+struct PluginOut {
+    double *l, *lx, *lu, *lxx, *luu;  // running: RCostData (matrices column-major, = row-major: symmetric)
+};
+__global__ void k_model_running_cost(Params p, const double *x, const double *u, const int *cc, const double *xr,
+                                     const double *ur, const double *pf, int terms, PluginOut o, int n)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const double *xq = x + (size_t)q * NX, *uq = u + (size_t)q * NU, *rq = xr + (size_t)q * NX,
+                 *vq = ur + (size_t)q * NU, *fq = pf + (size_t)q * 12;
+    int c[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) c[l] = cc[(size_t)q * 4 + l];
+    double L = 0.0, gx[NX], gu[NU];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) { gx[j] = 0.0; gu[j] = 0.0; }
+    if (terms & 1) {  // HKDTrackingCost (HKDCost.h:8-38): .5 dt (e' Q e + eu' R eu)
+        double lt = 0.0, lu = 0.0;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) { const double e = xq[j] - rq[j]; lt += e * q_diag(p, c, j) * e; gx[j] = p.dt * q_diag(p, c, j) * e; }
+#pragma unroll
+        for (int j = 0; j < NU; ++j) { const double e = uq[j] - vq[j]; lu += e * r_diag(p, j) * e; gu[j] = p.dt * r_diag(p, j) * e; }
+        L += p.dt * (0.5 * lt + 0.5 * lu);
+    }
+    if (terms & 2) {  // HKDFootPlaceReg (HKDCost.cpp:5-33): .5 dt d' Qfoot d, d = prel - prel_r
+        double lf = 0.0;
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const double e = (xq[12 + j] - xq[3 + j % 3]) - (fq[j] - rq[3 + j % 3]);
+            const double w = foot_weight(p, c, j);
+            lf += e * w * e;
+            gx[3 + j % 3] += -(p.dt * w * e);
+            gx[12 + j] += p.dt * w * e;
+        }
+        L += p.dt * (.5 * lf);
+    }
+    if (o.l) o.l[q] = L;
+    if (o.lx) for (int j = 0; j < NX; ++j) o.lx[(size_t)q * NX + j] = gx[j];
+    if (o.lu) for (int j = 0; j < NU; ++j) o.lu[(size_t)q * NU + j] = gu[j];
+    if (o.lxx) {
+        double *m = o.lxx + (size_t)q * NN;
+        for (int e = 0; e < NN; ++e) m[e] = 0.0;
+        if (terms & 1)
+#pragma unroll
+            for (int j = 0; j < NX; ++j) m[j * NX + j] = p.dt * q_diag(p, c, j);
+        if (terms & 2)
+#pragma unroll
+            for (int j = 0; j < 12; ++j) {
+                const double w = p.dt * foot_weight(p, c, j);
+                const int a = 3 + j % 3, bb = 12 + j;
+                m[a * NX + a] += w; m[bb * NX + bb] += w; m[a * NX + bb] -= w; m[bb * NX + a] -= w;
+            }
+    }
+    if (o.luu) {
+        double *m = o.luu + (size_t)q * NN;
+        for (int e = 0; e < NN; ++e) m[e] = 0.0;
+        if (terms & 1)
+#pragma unroll
+            for (int j = 0; j < NU; ++j) m[j * NU + j] = p.dt * r_diag(p, j);
+    }
+}
+
+__global__ void k_model_terminal_cost(Params p, const double *x, const int *cc, const double *xr, const double *pf,
+                                      int terms, double *Phi, double *Phix, double *Phixx, int n)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const double *xq = x + (size_t)q * NX, *rq = xr + (size_t)q * NX, *fq = pf + (size_t)q * 12;
+    int c[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) c[l] = cc[(size_t)q * 4 + l];
+    double F = 0.0, g[NX];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) g[j] = 0.0;
+    if (terms & 1) {  // HKDTrackingCost::terminal_cost(_par): .5 e' Qf e
+        double phi = 0.0;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) {
+            const double e = xq[j] - rq[j], w = p.qf_gain * p.qf_scale[j] * q_diag(p, c, j);
+            phi += e * w * e;
+            g[j] = w * e;
+        }
+        F += 0.5 * phi;
+    }
+    if (terms & 2) {  // HKDFootPlaceReg::terminal_cost(_par) (HKDCost.cpp:35-63): 10 d' Qfoot d, 20 D' Qfoot d
+        double fc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const double e = (xq[12 + j] - xq[3 + j % 3]) - (fq[j] - rq[3 + j % 3]);
+            const double w = foot_weight(p, c, j);
+            fc += e * w * e;
+            g[3 + j % 3] += -(p.foot_term_grad * w * e);
+            g[12 + j] += p.foot_term_grad * w * e;
+        }
+        F += p.foot_term_cost * fc;
+    }
+    if (Phi) Phi[q] = F;
+    if (Phix) for (int j = 0; j < NX; ++j) Phix[(size_t)q * NX + j] = g[j];
+    if (Phixx) {
+        double *m = Phixx + (size_t)q * NN;
+        for (int e = 0; e < NN; ++e) m[e] = 0.0;
+        if (terms & 1)
+#pragma unroll
+            for (int j = 0; j < NX; ++j) m[j * NX + j] = p.qf_gain * p.qf_scale[j] * q_diag(p, c, j);
+        if (terms & 2)
+#pragma unroll
+            for (int j = 0; j < 12; ++j) {
+                const double w = p.foot_term_grad * foot_weight(p, c, j);
+                const int a = 3 + j % 3, bb = 12 + j;
+                m[a * NX + a] += w; m[bb * NX + bb] += w; m[a * NX + bb] -= w; m[bb * NX + a] -= w;
+            }
+    }
+}
+
+// GRFConstraint (HKDConstraints.cpp:7-66): 5 friction-pyramid rows per stance leg, in leg order;
+// g [n][20] and gu [n][20][24] (rows past 5 x stance legs are zero)
+__global__ void k_model_grf(const double *u, const int *cc, double mu, double *g, double *gu, int n)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    int row = 0;
+    for (int e = 0; e < 20; ++e) {
+        if (g) g[(size_t)q * 20 + e] = 0.0;
+        if (gu) for (int j = 0; j < NU; ++j) gu[((size_t)q * 20 + e) * NU + j] = 0.0;
+    }
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        if (!cc[(size_t)q * 4 + l]) continue;
+#pragma unroll
+        for (int r = 0; r < 5; ++r, ++row) {
+            double a[3];
+            grf_row(mu, r, a);
+            if (g) g[(size_t)q * 20 + row] = grf_value(mu, r, u + (size_t)q * NU + 3 * l);
+            if (gu) for (int k = 0; k < 3; ++k) gu[((size_t)q * 20 + row) * NU + 3 * l + k] = a[k];
+        }
+    }
+}
+
+// TouchDownConstraint (HKDConstraints.cpp:69-171): h = foot height - ground for each leg touching
+// down (c = 0, next c = 1), in leg order; h [n][4], hx [n][4][24] (unused rows zero)
+__global__ void k_model_touchdown(const double *x, const int *cc, const int *cn, double ground, double *h, double *hx,
+                                  int n)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const double *xq = x + (size_t)q * NX;
+    for (int e = 0; e < 4; ++e) {
+        if (h) h[(size_t)q * 4 + e] = 0.0;
+        if (hx) for (int j = 0; j < NX; ++j) hx[((size_t)q * 4 + e) * NX + j] = 0.0;
+    }
+    int row = 0;
+    for (int l = 0; l < 4; ++l) {
+        if (!(cc[(size_t)q * 4 + l] == 0 && cn[(size_t)q * 4 + l] == 1)) continue;
+        double ge[3], gq[3];
+        const double hv = hkd_foot_height_grad_sparse(l, xq, ge, gq) - ground;
+        if (h) h[(size_t)q * 4 + row] = hv;
+        if (hx) {
+            double *r = hx + ((size_t)q * 4 + row) * NX;
+            for (int k = 0; k < 3; ++k) { r[k] = ge[k]; r[12 + 3 * l + k] = gq[k]; }
+            r[5] = 1.0;
+        }
+        ++row;
+    }
+}
+
 __global__ void k_model_reset(const double *x, const int *c, const int *cn, double *xn, double *Px, int n)
 {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -795,6 +963,28 @@ void launch_model_partial(const double *x, const double *u, const double *c, dou
 void launch_model_foot(const double *x, const int *leg, double *p, double *J, int n, hipStream_t st)
 {
     hipLaunchKernelGGL(k_model_foot, dim3(blocks_for(n, 64)), dim3(64), 0, st, x, leg, p, J, n);
+}
+void launch_model_running_cost(const Params &p, const double *x, const double *u, const int *c, const double *xr,
+                               const double *ur, const double *pf, int terms, double *l, double *lx, double *lu,
+                               double *lxx, double *luu, int n, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_model_running_cost, dim3(blocks_for(n, 64)), dim3(64), 0, st, p, x, u, c, xr, ur, pf, terms,
+                       PluginOut{l, lx, lu, lxx, luu}, n);
+}
+void launch_model_terminal_cost(const Params &p, const double *x, const int *c, const double *xr, const double *pf,
+                                int terms, double *Phi, double *Phix, double *Phixx, int n, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_model_terminal_cost, dim3(blocks_for(n, 64)), dim3(64), 0, st, p, x, c, xr, pf, terms, Phi,
+                       Phix, Phixx, n);
+}
+void launch_model_grf(const double *u, const int *c, double mu, double *g, double *gu, int n, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_model_grf, dim3(blocks_for(n, 64)), dim3(64), 0, st, u, c, mu, g, gu, n);
+}
+void launch_model_touchdown(const double *x, const int *c, const int *cn, double ground, double *h, double *hx, int n,
+                            hipStream_t st)
+{
+    hipLaunchKernelGGL(k_model_touchdown, dim3(blocks_for(n, 64)), dim3(64), 0, st, x, c, cn, ground, h, hx, n);
 }
 void launch_model_reset(const double *x, const int *c, const int *cn, double *xn, double *Px, int n,
                         hipStream_t st)

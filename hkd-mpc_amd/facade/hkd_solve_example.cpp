@@ -6,7 +6,10 @@
 //   hkd_solve_example <dir> [max_AL_iter max_DDP_iter [ddp_setting.info]]
 //   <dir>/problem.txt : P dt N_0 .. N_{P-1}
 //   <dir>/contacts.i32 [(P+1)][4], x0.f64 [24], ref_x.f64 [S][24], ref_u.f64 [S][24], ref_foot.f64 [S][12]
-//   writes <dir>/Xbar.f64 [S][24], Ubar.f64 [Kc][24], K.f64 [Kc][24][24] (row-major), info.txt
+//   writes <dir>/Xbar.f64 [S][24], Ubar.f64 [Kc][24], K.f64 [Kc][24][24] (row-major), info.txt, and
+//   the Trajectory exports: Xsim.f64 [S][24], A.f64 [Kc][24][24], l.f64 / lx.f64 / luu.f64 (rcostData),
+//   Phix.f64 [P][24] (tcostData), G0.f64 [P][24], H0.f64 [P][24][24] (get_value_approx),
+//   phase_cost.f64 [P], solver_info.f32 [n][4] (get_solver_info)
 #include <cstdio>
 #include <fstream>
 #include <iostream>
@@ -117,15 +120,48 @@ int main(int argc, char **argv)
                     for (int b = 0; b < 24; ++b) K.push_back(tr.K[k](a, b));
             }
         }
+        std::vector<double> Xsim, A, l, lx, luu, Phix, G0, H0, pc;
+        for (int i = 0; i < P; ++i) {
+            auto &tr = *trajs[i];
+            for (int k = 0; k <= N[i]; ++k)
+                for (int j = 0; j < 24; ++j) Xsim.push_back(tr.Xsim[k][j]);
+            for (int k = 0; k < N[i]; ++k) {
+                l.push_back(tr.rcostData[k].l);
+                for (int a = 0; a < 24; ++a) {
+                    lx.push_back(tr.rcostData[k].lx[a]);
+                    for (int b = 0; b < 24; ++b) { A.push_back(tr.A[k](a, b)); luu.push_back(tr.rcostData[k].luu(a, b)); }
+                }
+            }
+            DVec<double> G;
+            DMat<double> H;
+            phases[i]->get_value_approx(G, H);
+            for (int a = 0; a < 24; ++a) {
+                Phix.push_back(tr.tcostData.Phix[a]);
+                G0.push_back(G[a]);
+                for (int b = 0; b < 24; ++b) H0.push_back(H(a, b));
+            }
+            pc.push_back(phases[i]->get_actual_cost());
+        }
+        write_bin(dir + "/Xsim.f64", Xsim);
+        write_bin(dir + "/A.f64", A);
+        write_bin(dir + "/l.f64", l);
+        write_bin(dir + "/lx.f64", lx);
+        write_bin(dir + "/luu.f64", luu);
+        write_bin(dir + "/Phix.f64", Phix);
+        write_bin(dir + "/G0.f64", G0);
+        write_bin(dir + "/H0.f64", H0);
+        write_bin(dir + "/phase_cost.f64", pc);
         write_bin(dir + "/Xbar.f64", Xb);
         write_bin(dir + "/Ubar.f64", Ub);
         write_bin(dir + "/K.f64", K);
-        std::vector<float> c, f, e, q;
+        std::vector<float> c, f, e, q, hist;
         solver.get_solver_info(c, f, e, q);
+        for (size_t n = 0; n < c.size(); ++n) hist.insert(hist.end(), {c[n], f[n], e[n], q[n]});
+        write_bin(dir + "/solver_info.f32", hist);
         const hsddp_element_info &info = solver.element_info();
         std::ofstream out(dir + "/info.txt");
         out.precision(17);
-        out << solver.get_actual_cost() << " " << f[0] << " " << info.iters << " " << info.outer_iters << " "
+        out << solver.get_actual_cost() << " " << solver.measure_dynamics_feasibility() << " " << info.iters << " " << info.outer_iters << " "
             << info.status << " " << info.n_ls_trials << "\n";
         std::printf("facade solve ok: cost %.17g iters %d\n", solver.get_actual_cost(), info.iters);
     } catch (const std::exception &ex) {

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cmath>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -32,13 +33,18 @@
 #include <vector>
 
 #include "../../include/hsddp.h"
+#include "hsddp_pack.hpp"
 
 // ---- dense containers (Eigen-style access, column-major) -------------------------------------
+template <typename T, size_t n>
+class VecM;
 template <typename T>
 class DVec {
 public:
     DVec() = default;
     explicit DVec(size_t n) : v_(n, T(0)) {}
+    template <size_t n>
+    DVec(const VecM<T, n> &v) : v_(v.data(), v.data() + n) {}  // VecM -> DVec, as Eigen assigns
     size_t size() const { return v_.size(); }
     T &operator()(size_t i) { return v_[i]; }
     const T &operator()(size_t i) const { return v_[i]; }
@@ -76,7 +82,10 @@ template <typename T, size_t n>
 class VecM {
 public:
     VecM() { a_.fill(T(0)); }
+    VecM(const DVec<T> &v) { for (size_t i = 0; i < n; ++i) a_[i] = i < v.size() ? v[i] : T(0); }  // Eigen's DVec -> VecM
+    static VecM Zero() { return VecM(); }
     static constexpr size_t size() { return n; }
+    VecM &operator+=(const VecM &o) { for (size_t i = 0; i < n; ++i) a_[i] += o.a_[i]; return *this; }
     T &operator()(size_t i) { return a_[i]; }
     const T &operator()(size_t i) const { return a_[i]; }
     T &operator[](size_t i) { return a_[i]; }
@@ -93,7 +102,10 @@ template <typename T, size_t m, size_t n>
 class MatMN {
 public:
     MatMN() { a_.fill(T(0)); }
+    static MatMN Zero() { return MatMN(); }
     static constexpr size_t rows() { return m; }
+    MatMN &operator+=(const MatMN &o) { for (size_t i = 0; i < m * n; ++i) a_[i] += o.a_[i]; return *this; }
+    void setIdentity() { a_.fill(T(0)); for (size_t i = 0; i < (m < n ? m : n); ++i) (*this)(i, i) = T(1); }
     static constexpr size_t cols() { return n; }
     T &operator()(size_t i, size_t j) { return a_[j * m + i]; }
     const T &operator()(size_t i, size_t j) const { return a_[j * m + i]; }
@@ -156,7 +168,80 @@ inline void loadHSDDPSetting(const std::string &filename, HSDDP_OPTION &option)
     option.from_c(o);
 }
 
-// ---- Trajectory (TrajectoryManagement.h:20-80), the fields the solver reads and writes --------
+template <typename> class MultiPhaseDDP;
+
+// ---- cost / constraint data (HSDDP_CompoundTypes.h:89-150, ConstraintsBase.h:12-86) -----------
+template <typename T, size_t xs_, size_t us_, size_t ys_>
+struct RCostData {
+    T l;
+    VecM<T, xs_> lx;
+    VecM<T, us_> lu;
+    VecM<T, ys_> ly;
+    MatMN<T, xs_, xs_> lxx;
+    MatMN<T, us_, xs_> lux;
+    MatMN<T, us_, us_> luu;
+    MatMN<T, ys_, ys_> lyy;
+    RCostData() { Zeros(); }
+    void Zeros()
+    {
+        l = 0;
+        lx.setZero(); lu.setZero(); ly.setZero(); lxx.setZero(); luu.setZero(); lux.setZero(); lyy.setZero();
+    }
+    void add(const RCostData &c)
+    {
+        l += c.l;
+        lx += c.lx; lu += c.lu; ly += c.ly; lxx += c.lxx; luu += c.luu; lux += c.lux; lyy += c.lyy;
+    }
+};
+
+template <typename T, size_t xs_>
+struct TCostData {
+    T Phi;
+    VecM<T, xs_> Phix;
+    MatMN<T, xs_, xs_> Phixx;
+    TCostData() { Zeros(); }
+    void Zeros() { Phi = 0; Phix.setZero(); Phixx.setZero(); }
+    void add(const TCostData &c) { Phi += c.Phi; Phix += c.Phix; Phixx += c.Phixx; }
+};
+
+template <typename T, size_t xs, size_t us, size_t ys>
+struct IneqConstrData {
+    T g = 0;
+    VecM<T, xs> gx;
+    VecM<T, us> gu;
+    VecM<T, ys> gy;
+    MatMN<T, xs, xs> gxx;
+    MatMN<T, us, us> guu;
+    MatMN<T, ys, ys> gyy;
+    static IneqConstrData Zero() { return IneqConstrData(); }
+};
+
+template <typename T, size_t xs>
+struct TConstrData {
+    T h = 0;
+    VecM<T, xs> hx;
+    MatMN<T, xs, xs> hxx;
+};
+
+template <typename T>
+struct AL_Param_Struct {
+    T lambda = 0, sigma = 0, sigma_max = 0;
+    void update_penalty(T beta) { sigma *= beta; }
+    void update_Lagrange(T h) { lambda += h * sigma; }
+};
+
+template <typename T>
+struct REB_Param_Struct {
+    T delta = 0.1, delta_min = 0.01, eps = 1;
+    void update_relax(T beta) { delta *= beta; delta = std::fmax(delta, delta_min); }
+    void update_weight(T beta) { eps *= beta; }
+};
+
+// ---- Trajectory (TrajectoryManagement.h:20-82 / .cpp) ----------------------------------------
+// After MultiPhaseDDP::solve: Xbar, Ubar, K, X, U, Defect, Defect_bar, dX, dU, Xsim (= X + Defect),
+// A, B and rcostData (the LQ model of the last LQ_approximation), tcostData, G[0] and H[0] (the
+// value function at the phase start, get_value_approx).  V, dV and G/H past the first knot are not
+// kept by the device solve and stay zero.
 template <typename T, size_t xs, size_t us, size_t ys>
 class Trajectory {
 public:
@@ -167,48 +252,345 @@ public:
         timeStep = timeStep_;
         horizon = horizon_;
         duration = timeStep * horizon;
-        Xbar.assign(horizon + 1, VecM<T, xs>()); X = Xbar; Defect = Xbar; Defect_bar = Xbar; dX = Xbar;
-        Ubar.assign(horizon, VecM<T, us>()); U = Ubar; dU = Ubar;
-        K.assign(horizon, MatMN<T, us, xs>());
+        const size_t n1 = horizon + 1, n = horizon;
+        Xbar.assign(n1, VecM<T, xs>()); X = Xbar; Xsim = Xbar; Defect_bar = Xbar; Defect = Xbar; dX = Xbar; G = Xbar;
+        Ubar.assign(n, VecM<T, us>()); U = Ubar; dU = Ubar;
+        Y.assign(n, VecM<T, ys>());
+        A.assign(n1, MatMN<T, xs, xs>()); H = A;
+        B.assign(n, MatMN<T, xs, us>());
+        C.assign(n, MatMN<T, ys, xs>());
+        D.assign(n, MatMN<T, ys, us>());
+        V.assign(n1, T(0)); dV = V;
+        K.assign(n1, MatMN<T, us, xs>());
+        rcostData.assign(n, RCostData<T, xs, us, ys>());
+    }
+    void zero_all() { create_data(timeStep, horizon); }
+    void clear()
+    {
+        Xbar.clear(); X.clear(); Ubar.clear(); U.clear(); Y.clear(); Xsim.clear(); Defect_bar.clear(); Defect.clear();
+        A.clear(); B.clear(); C.clear(); D.clear(); V.clear(); dV.clear(); dU.clear(); G.clear(); H.clear();
+        K.clear(); dX.clear(); rcostData.clear();
+    }
+    void update_nominal_vals()  // TrajectoryManagement.cpp:110-115
+    {
+        std::copy(X.begin(), X.end(), Xbar.begin());
+        std::copy(U.begin(), U.end(), Ubar.begin());
+        std::copy(Defect.begin(), Defect.end(), Defect_bar.begin());
+    }
+    void pop_front()  // :118-141
+    {
+        Xbar.pop_front(); X.pop_front(); Ubar.pop_front(); U.pop_front(); Y.pop_front(); Xsim.pop_front();
+        Defect.pop_front(); Defect_bar.pop_front(); A.pop_front(); B.pop_front(); C.pop_front(); D.pop_front();
+        V.pop_front(); dV.pop_front(); dU.pop_front(); G.pop_front(); H.pop_front(); K.pop_front(); dX.pop_front();
+        rcostData.pop_front();
+        horizon--;
+    }
+    void push_back_zero() { push_back_state(DVec<T>(VecM<T, xs>())); }  // :143-166
+    void push_back_state(const DVec<T> &state_to_add)                  // :168-191
+    {
+        Xbar.push_back(VecM<T, xs>(state_to_add)); X.push_back(VecM<T, xs>(state_to_add));
+        Ubar.push_back(VecM<T, us>()); U.push_back(VecM<T, us>()); Y.push_back(VecM<T, ys>());
+        Xsim.push_back(VecM<T, xs>()); Defect.push_back(VecM<T, xs>()); Defect_bar.push_back(VecM<T, xs>());
+        A.push_back(MatMN<T, xs, xs>()); B.push_back(MatMN<T, xs, us>()); C.push_back(MatMN<T, ys, xs>());
+        D.push_back(MatMN<T, ys, us>()); V.push_back(T(0)); dV.push_back(T(0)); dU.push_back(VecM<T, us>());
+        G.push_back(VecM<T, xs>()); H.push_back(MatMN<T, xs, xs>()); K.push_back(MatMN<T, us, xs>());
+        dX.push_back(VecM<T, xs>()); rcostData.push_back(RCostData<T, xs, us, ys>());
+        horizon++;
     }
     int size() { return (int)Xbar.size(); }
+    void compute_defect()  // :193-199
+    {
+        for (int k = 0; k <= horizon; ++k)
+            for (size_t j = 0; j < xs; ++j) Defect[k][j] = Xsim[k][j] - X[k][j];
+    }
+    T measure_dynamics_feasibility(int norm_id = 2)  // :201-208 (2-norm of the stacked defects)
+    {
+        T s = 0, mx = 0;
+        for (auto &d : Defect)
+            for (size_t j = 0; j < xs; ++j) { s += d[j] * d[j]; mx = std::max(mx, std::fabs(d[j])); }
+        return norm_id == 2 ? std::sqrt(s) : mx;
+    }
 
     T duration = 0, timeStep = 0;
     int horizon = 0;
-    std::deque<VecM<T, xs>> Xbar, X, Defect, Defect_bar, dX;
-    std::deque<VecM<T, us>> Ubar, U, dU;
+    std::deque<VecM<T, xs>> Xbar, X;
+    std::deque<VecM<T, us>> Ubar, U;
+    std::deque<VecM<T, ys>> Y;
+    std::deque<VecM<T, xs>> Xsim, Defect_bar, Defect;
+    std::deque<MatMN<T, xs, xs>> A;
+    std::deque<MatMN<T, xs, us>> B;
+    std::deque<MatMN<T, ys, xs>> C;
+    std::deque<MatMN<T, ys, us>> D;
+    std::deque<T> V, dV;
+    std::deque<VecM<T, us>> dU;
+    std::deque<VecM<T, xs>> G;
+    std::deque<MatMN<T, xs, xs>> H;
     std::deque<MatMN<T, us, xs>> K;
+    std::deque<VecM<T, xs>> dX;
+    std::deque<RCostData<T, xs, us, ys>> rcostData;
+    TCostData<T, xs> tcostData;
 };
 
-// ---- plugin bases (SinglePhaseInterface.h:47-53, ConstraintsBase.h:267-268, 401-402) ----------
-template <typename T, size_t xs, size_t us, size_t ys>
+// ---- plugin bases with the reference's signatures ---------------------------------------------
+// CostBase (SinglePhaseInterface.h:35-57).  The solver evaluates costs on the device; a cost runs
+// there only when it is one of the hkd:: registrations below (their virtuals evaluate the same
+// terms on the device for callers that use them point by point).
+template <typename T, size_t xs_, size_t us_, size_t ys_>
 class CostBase {
 public:
+    typedef VecM<T, xs_> State;
+    typedef VecM<T, us_> Contrl;
+    typedef VecM<T, ys_> Output;
+    typedef RCostData<T, xs_, us_, ys_> RCost;
+    typedef TCostData<T, xs_> TCost;
+
+    CostBase(const std::string &cost_name_in) : cost_name(cost_name_in) {}
     virtual ~CostBase() = default;
+    virtual void running_cost(RCost &, const State &x, const Contrl &u, const Output &y, T dt, float t) = 0;
+    virtual void running_cost_par(RCost &, const State &x, const Contrl &u, const Output &y, T dt, float t) = 0;
+    virtual void terminal_cost(TCost &, const State &x, float tend) = 0;
+    virtual void terminal_cost_par(TCost &, const State &x, float tend) = 0;
+
     std::string cost_name;
 };
-template <typename T, size_t xs, size_t us, size_t ys>
+
+// PathConstraintBase (ConstraintsBase.h:88-327): per-knot constraint data and ReB parameters, the
+// ReB cost / partials, the parameter schedule; compute_violation / compute_partial per knot.
+template <typename T, size_t xs_, size_t us_, size_t ys_>
 class PathConstraintBase {
 public:
+    typedef VecM<T, xs_> State;
+    typedef VecM<T, us_> Contrl;
+    typedef VecM<T, ys_> Output;
+    typedef std::vector<IneqConstrData<T, xs_, us_, ys_>> ConstrDataType;
+    typedef std::vector<REB_Param_Struct<T>> ReBDataType;
+
+    size_t size = 0, len = 0;
+    std::string name;
+    std::deque<ConstrDataType> data;
+    std::deque<ReBDataType> params;
+    REB_Param_Struct<T> param_init;
+    T max_violation = 0, ReB_cost = 0;
+    VecM<T, us_> ReB_grad_u;
+    VecM<T, xs_> ReB_grad_x;
+    VecM<T, ys_> ReB_grad_y;
+    MatMN<T, us_, us_> ReB_hess_u;
+    MatMN<T, xs_, xs_> ReB_hess_x;
+    MatMN<T, ys_, ys_> ReB_hess_y;
+
+    PathConstraintBase() = default;
+    PathConstraintBase(const std::string &name_) : name(name_) {}
+    PathConstraintBase(int size_, int len_, const std::string &name_) : size(size_), len(len_), name(name_) {}
     virtual ~PathConstraintBase() = default;
-    std::string constraint_name;
-};
-template <typename T, size_t xs>
-class TerminalConstraintBase {
-public:
-    virtual ~TerminalConstraintBase() = default;
-    std::string constraint_name;
+
+    void create_data()
+    {
+        clear_data();
+        for (size_t i = 0; i < len; ++i) data.push_back(ConstrDataType(size));
+    }
+    void clear_data() { data.clear(); }
+    void initialize_params(const REB_Param_Struct<T> &p)
+    {
+        param_init = p;
+        params.clear();
+        for (size_t k = 0; k < len; ++k) params.push_back(ReBDataType(size, p));
+    }
+    void initialize_params()
+    {
+        REB_Param_Struct<T> p;
+        p.delta = 0.01; p.delta_min = 0.001; p.eps = 1;
+        initialize_params(p);
+    }
+    void reset_params() {}
+    void update_params(T thresh, T beta_relax, T beta_weight)  // :160-176
+    {
+        for (size_t k = 0; k < len; ++k)
+            for (size_t i = 0; i < size; ++i) {
+                if (data[k][i].g > -thresh) continue;
+                params[k][i].update_weight(beta_weight);
+                params[k][i].update_relax(beta_relax);
+            }
+    }
+    void update_horizon_len(int len_) { len = len_; }
+    void update_constraint_size(int size_in) { size = size_in; }
+    void update_max_violation(int k)  // :187-200
+    {
+        if (k == 0) max_violation = 0;
+        T m = 0;
+        for (auto &c : data[k]) m = std::min(m, c.g);
+        max_violation = std::min(max_violation, m);
+    }
+    void compute_ReB_cost(size_t k)  // :201-221
+    {
+        ReB_cost = 0;
+        for (size_t i = 0; i < size; ++i) {
+            const T g = data[k][i].g, delta = params[k][i].delta, eps = params[k][i].eps;
+            T barr;
+            if (g > delta) barr = -std::log(g);
+            else barr = .5 * (((g - 2 * delta) / delta) * ((g - 2 * delta) / delta) - 1) - std::log(delta);
+            ReB_cost += eps * barr;
+        }
+    }
+    void compute_ReB_partials(size_t k)  // :222-263
+    {
+        ReB_grad_u.setZero(); ReB_grad_x.setZero(); ReB_grad_y.setZero();
+        ReB_hess_u.setZero(); ReB_hess_x.setZero(); ReB_hess_y.setZero();
+        for (size_t i = 0; i < size; ++i) {
+            const auto &c = data[k][i];
+            const T g = c.g, delta = params[k][i].delta, eps = params[k][i].eps;
+            const T bd = g > delta ? -1.0 / g : (g - 2 * delta) / delta / delta;
+            const T bdd = g > delta ? std::pow(g, -2) : std::pow(delta, -2);
+            auto acc = [&](auto &grad, auto &hess, const auto &gv, const auto &gvv, size_t n) {
+                for (size_t a = 0; a < n; ++a) {
+                    grad[a] += eps * bd * gv[a];
+                    for (size_t b = 0; b < n; ++b) hess(a, b) += eps * (bdd * gv[a] * gv[b] + bd * gvv(a, b));
+                }
+            };
+            acc(ReB_grad_u, ReB_hess_u, c.gu, c.guu, us_);
+            acc(ReB_grad_x, ReB_hess_x, c.gx, c.gxx, xs_);
+            acc(ReB_grad_y, ReB_hess_y, c.gy, c.gyy, ys_);
+        }
+    }
+    // call update_max_violation in compute_violation in the derived class
+    virtual void compute_partial(const State &, const Contrl &, const Output &, int k) = 0;
+    virtual void compute_violation(const State &, const Contrl &, const Output &, int k) = 0;
+
+    void pop_front() { data.pop_front(); params.pop_front(); len--; }
+    void push_back() { data.push_back(ConstrDataType(size)); params.push_back(params.back()); len++; }
+    void pop_front_n(int n) { for (int i = 0; i < n; ++i) pop_front(); }
+    void push_back_n(int n) { for (int i = 0; i < n; ++i) push_back(); }
 };
 
+// TerminalConstraintBase (ConstraintsBase.h:329-405): AL parameters and terms of the phase end.
+template <typename T, size_t xs_>
+class TerminalConstraintBase {
+public:
+    typedef VecM<T, xs_> State;
+    size_t size = 0;
+    std::string name;
+    std::vector<TConstrData<T, xs_>> data;
+    std::vector<AL_Param_Struct<T>> params;
+    AL_Param_Struct<T> param_init;
+    T max_violation = 0, AL_cost = 0;
+    VecM<T, xs_> AL_gradient;
+    MatMN<T, xs_, xs_> AL_hessian;
+
+    TerminalConstraintBase() = default;
+    TerminalConstraintBase(const std::string &name_) : name(name_) {}
+    TerminalConstraintBase(int size_, const std::string &name_) : size(size_), name(name_) {}
+    virtual ~TerminalConstraintBase() = default;
+
+    void create_data() { data = std::vector<TConstrData<T, xs_>>(size); }
+    void clear_data() { data.clear(); }
+    void resize_data() { data.resize(size); }
+    void update_constraint_size(size_t size_) { size = size_; }
+    void initialize_params()
+    {
+        AL_Param_Struct<T> p;
+        p.lambda = 0; p.sigma = 5;
+        initialize_params(p);
+    }
+    void initialize_params(const AL_Param_Struct<T> &p) { param_init = p; params.assign(size, p); }
+    void reset_params() {}
+    void update_params(T thresh, T beta)  // :354-372
+    {
+        for (size_t i = 0; i < size; ++i) {
+            if (std::fabs(data[i].h) < thresh) continue;
+            if (std::fabs(data[i].h) > 0.005) {
+                params[i].update_penalty(beta);
+                params[i].sigma = std::min(params[i].sigma, params[i].sigma_max);
+            } else {
+                params[i].update_Lagrange(data[i].h);
+            }
+        }
+    }
+    void update_max_violation()
+    {
+        max_violation = 0.0;
+        for (auto &c : data) max_violation = std::max(max_violation, (T)std::fabs(c.h));
+    }
+    void compute_AL_cost()
+    {
+        AL_cost = 0;
+        for (size_t i = 0; i < size; ++i) {
+            const T s = params[i].sigma, l = params[i].lambda, h = data[i].h;
+            AL_cost += 0.5 * s * h * h;
+            AL_cost += l * h;
+        }
+    }
+    void compute_AL_partials()  // quirk A4: (sigma (1 + h) + lambda) hx hx^T
+    {
+        AL_gradient.setZero();
+        AL_hessian.setZero();
+        for (size_t i = 0; i < size; ++i) {
+            const T s = params[i].sigma, l = params[i].lambda, h = data[i].h;
+            const auto &hx = data[i].hx;
+            for (size_t a = 0; a < xs_; ++a) {
+                AL_gradient[a] += (s * h + l) * hx[a];
+                for (size_t b = 0; b < xs_; ++b) AL_hessian(a, b) += (s * (1 + h) + l) * (hx[a] * hx[b]);
+            }
+        }
+    }
+    virtual void compute_violation(const State &) = 0;
+    virtual void compute_partial(const State &) = 0;
+};
+
+// SinglePhaseBase (SinglePhaseBase.h:10-88): the interface MultiPhaseDDP drives per phase.
+struct HSDDP_OPTION;
 template <typename T>
 class SinglePhaseBase {
+    friend class MultiPhaseDDP<T>;
+
 public:
+    SinglePhaseBase() = default;
     virtual ~SinglePhaseBase() = default;
+    virtual void warmstart() = 0;
+    virtual void initialization() = 0;
+    virtual void set_initial_condition(DVec<T> &x0_) = 0;
+    virtual void set_initial_condition(DVec<T> &x0_, DVec<T> &xsim_0_) { (void)x0_; (void)xsim_0_; }
+    virtual void set_initial_condition_dx(DVec<T> &dx0_) = 0;
+    virtual void set_nominal_initial_condition(DVec<T> &x0_) { (void)x0_; }
+    virtual void linear_rollout(T eps, HSDDP_OPTION &) = 0;
+    virtual bool hybrid_rollout(T eps, HSDDP_OPTION &, bool is_last_phase = false) = 0;
+    virtual void LQ_approximation(HSDDP_OPTION &) = 0;
+    virtual bool backward_sweep(T regularization, DVec<T> Gprime, DMat<T> Hprime) = 0;
+    virtual DVec<T> resetmap(DVec<T> &) = 0;
+    virtual void resetmap_partial(DMat<T> &Px, DVec<T> &x) = 0;
+    virtual void get_value_approx(DVec<T> &G, DMat<T> &H) = 0;
+    virtual void get_exp_cost_change(T &dV_1, T &dV_2) = 0;
+    virtual void get_terminal_state(DVec<T> &xend) = 0;
+    virtual void get_terminal_state(DVec<T> &xend, DVec<T> &xsim_end) = 0;
+    virtual void get_terminal_state_dx(DVec<T> &dx_end) = 0;
+    virtual T get_actual_cost() = 0;
+    virtual T get_max_tconstrs() { return (T)(0); }
+    virtual T get_max_pconstrs() { return (T)(0); }
+    virtual size_t get_state_dim() { return 0; }
+    virtual size_t get_control_dim() { return 0; }
+    virtual void update_AL_params(HSDDP_OPTION &) {}
+    virtual void update_REB_params(HSDDP_OPTION &) {}
+    virtual void update_nominal_trajectory() = 0;
+    virtual void empty_control() {}
+    virtual void push_back_default() {}
+    virtual void pop_front() {}
+    virtual void reset_params() {}
+    virtual T measure_dynamics_feasibility(int norm_id) { (void)norm_id; return 0; }
+    virtual void update_SS_config(int ss_sz) { (void)ss_sz; }
+    virtual void compute_cost(const HSDDP_OPTION &option) = 0;
+    virtual void get_trajectory(std::vector<std::vector<float>> &x_tau, std::vector<std::vector<float>> &u_tau)
+    {
+        (void)x_tau; (void)u_tau;
+    }
+    virtual void print() {}
 };
 
 template <typename> class MultiPhaseDDP;
 
-// ---- SinglePhase (SinglePhase.h:21-92): the setters the HKD problem builder calls -----------
+// ---- SinglePhase (SinglePhase.h:21-170) -------------------------------------------------------
+// The setters HKDProblem calls, and SinglePhaseBase's interface.  The per-phase numerical steps
+// (linear / hybrid rollout, LQ approximation, backward sweep, compute_cost) run for all phases at
+// once inside the device solve (MultiPhaseDDP::solve); called one phase at a time from the host
+// they throw std::logic_error — there is no CPU implementation of them.  The accessors read the
+// state the last device solve left in the phase's Trajectory.
 template <typename T, size_t xs, size_t us, size_t ys>
 class SinglePhase : public SinglePhaseBase<T> {
 public:
@@ -221,7 +603,7 @@ public:
     typedef MatMN<T, ys == 0 ? 1 : ys, us> DirectMap;
     friend class MultiPhaseDDP<T>;
 
-    void set_trajectory(std::shared_ptr<Trajectory<T, xs, us, ys>> traj_) { traj = traj_; }
+    void set_trajectory(std::shared_ptr<Trajectory<T, xs, us, ys>> traj_) { traj = traj_; phase_horizon = traj_->horizon; }
     void set_dynamics(std::function<void(State &, Output &, State &, Contrl &, T)> f) { dynamics = f; }
     void set_dynamics_partial(
         std::function<void(StateMap &, ContrlMap &, OutputMap &, DirectMap &, State &, Contrl &, T)> f)
@@ -236,7 +618,87 @@ public:
     void add_terminalConstraint(std::shared_ptr<TerminalConstraintBase<T, xs>> c) { tconstraints.push_back(c); }
     std::shared_ptr<Trajectory<T, xs, us, ys>> get_trajectory() { return traj; }
 
+    // SinglePhaseBase
+    void warmstart() override {}  // the device solve starts from Trajectory::Xbar / Ubar / K
+    void initialization() override { SS_set.clear(); }
+    void set_initial_condition(DVec<T> &x0_) override { x_init = x0_; }
+    void set_initial_condition(DVec<T> &x0_, DVec<T> &xsim_0_) override { x_init = x0_; xsim_init = xsim_0_; }
+    void set_initial_condition_dx(DVec<T> &dx0_) override { dx_init = dx0_; }
+    void linear_rollout(T, HSDDP_OPTION &) override { device_only("linear_rollout"); }
+    bool hybrid_rollout(T, HSDDP_OPTION &, bool = false) override { device_only("hybrid_rollout"); return false; }
+    void LQ_approximation(HSDDP_OPTION &) override { device_only("LQ_approximation"); }
+    bool backward_sweep(T, DVec<T>, DMat<T>) override { device_only("backward_sweep"); return false; }
+    void compute_cost(const HSDDP_OPTION &) override { device_only("compute_cost"); }
+    DVec<T> resetmap(DVec<T> &x) override  // SinglePhase.cpp:62-71
+    {
+        DVec<T> xn(xs);
+        if (resetmap_func_handle) resetmap_func_handle(xn, x);
+        else xn = x;
+        return xn;
+    }
+    void resetmap_partial(DMat<T> &Px, DVec<T> &x) override  // :73-80
+    {
+        if (resetmap_partial_func_handle) resetmap_partial_func_handle(Px, x);
+        else { Px.setZero(xs, xs); for (size_t i = 0; i < xs; ++i) Px(i, i) = 1; }
+    }
+    void get_value_approx(DVec<T> &G_out, DMat<T> &H_out) override  // :82-87 (G[0], H[0] of the last sweep)
+    {
+        G_out = DVec<T>(traj->G[0]);
+        H_out.setZero(xs, xs);
+        for (size_t a = 0; a < xs; ++a)
+            for (size_t b = 0; b < xs; ++b) H_out(a, b) = traj->H[0](a, b);
+    }
+    void get_exp_cost_change(T &dV_1_out, T &dV_2_out) override { dV_1_out = dV_1; dV_2_out = dV_2; }
+    void get_terminal_state(DVec<T> &xend) override { xend = DVec<T>(traj->X.back()); }
+    void get_terminal_state(DVec<T> &xend, DVec<T> &xsim_end) override
+    {
+        xend = DVec<T>(traj->X.back());
+        xsim_end = DVec<T>(traj->Xsim.back());
+    }
+    void get_terminal_state_dx(DVec<T> &dx_end) override { dx_end = DVec<T>(traj->dX.back()); }
+    T get_actual_cost() override { return actual_cost; }  // running + terminal cost of the last compute_cost
+    size_t get_state_dim() override { return xs; }
+    size_t get_control_dim() override { return us; }
+    void update_nominal_trajectory() override { traj->update_nominal_vals(); }
+    void empty_control() override { for (auto &u : traj->Ubar) u.setZero(); }
+    void push_back_default() override  // SinglePhase.cpp:485-491
+    {
+        traj->push_back_state(DVec<T>(traj->X.back()));
+        for (auto &c : pconstraints) c->push_back_n(1);
+        phase_horizon = traj->horizon;
+    }
+    void pop_front() override  // :496-501
+    {
+        traj->pop_front();
+        for (auto &c : pconstraints) c->pop_front_n(1);
+        phase_horizon = traj->horizon;
+    }
+    T measure_dynamics_feasibility(int norm_id) override { return traj->measure_dynamics_feasibility(norm_id); }
+    void update_SS_config(int ss_sz) override  // SinglePhase.h:161-164
+    {
+        SS_set.clear();
+        for (int i = 0; i < ss_sz; ++i) SS_set.push_back(i);
+    }
+    void get_trajectory(std::vector<std::vector<float>> &x_tau, std::vector<std::vector<float>> &u_tau) override
+    {
+        for (int k = 0; k < phase_horizon; ++k) {
+            std::vector<float> xk, uk;
+            for (size_t i = 0; i < xs; ++i) xk.push_back((float)traj->X[k][i]);
+            for (size_t i = 0; i < us; ++i) uk.push_back((float)traj->U[k][i]);
+            x_tau.push_back(xk);
+            u_tau.push_back(uk);
+        }
+    }
+
+    std::vector<int> SS_set;
+    int phase_horizon = 0;
+
 private:
+    [[noreturn]] static void device_only(const char *what)
+    {
+        throw std::logic_error(std::string("SinglePhase::") + what +
+                               " runs for all phases inside the device solve (MultiPhaseDDP::solve)");
+    }
     std::function<void(State &, Output &, State &, Contrl &, T)> dynamics;
     std::function<void(StateMap &, ContrlMap &, OutputMap &, DirectMap &, State &, Contrl &, T)> dynamics_partial;
     std::function<void(DVec<T> &, DVec<T> &)> resetmap_func_handle;
@@ -246,36 +708,68 @@ private:
     std::vector<std::shared_ptr<TerminalConstraintBase<T, xs>>> tconstraints;
     std::shared_ptr<Trajectory<T, xs, us, ys>> traj;
     float t_offset = 0;
+    DVec<T> x_init, xsim_init, dx_init;
+    T actual_cost = 0, dV_1 = 0, dV_2 = 0;
 };
 
 // ---- the HKD registrations the device path evaluates ------------------------------------------
 namespace hkd {
 typedef SinglePhase<double, 24, 24, 0> Phase;
+typedef Phase::State State;
+typedef Phase::Contrl Contrl;
+typedef VecM<double, 0> Output;  // ys = 0: CostBase<double, 24, 24, 0>::Output
 
 namespace detail {
-// one batched model primitive on a single point, through device buffers (host convenience only:
-// the solver never calls these — it evaluates the model inside its kernels)
+// Point evaluations of the model / plugin primitives from the host (convenience for callers that
+// use them one point at a time; the solver never does — it evaluates the model in its kernels).
+// Device buffers come from a per-thread arena that only grows, so a call costs its copies and the
+// kernel, not allocations.
+struct Arena {
+    std::vector<std::pair<void *, size_t>> bufs;
+    void *get(size_t i, size_t bytes)
+    {
+        if (bufs.size() <= i) bufs.resize(i + 1, {nullptr, 0});
+        if (bufs[i].second < bytes) {
+            if (bufs[i].first) hsddp_device_free(bufs[i].first);
+            bufs[i].first = hsddp_device_alloc(bytes, 0);
+            bufs[i].second = bufs[i].first ? bytes : 0;
+            if (!bufs[i].first) throw std::runtime_error(hsddp_last_error());
+        }
+        return bufs[i].first;
+    }
+    ~Arena()
+    {
+        for (auto &b : bufs)
+            if (b.first) hsddp_device_free(b.first);
+    }
+};
+inline Arena &arena()
+{
+    thread_local Arena a;
+    return a;
+}
 template <typename F>
 inline void on_device(const std::vector<std::pair<const void *, size_t>> &in, const std::vector<std::pair<void *, size_t>> &out,
                       F call)
 {
     std::vector<void *> din, dout;
+    size_t slot = 0;
     for (auto &b : in) {
-        void *p = hsddp_device_alloc(b.second, 0);
-        if (!p || hsddp_memcpy_h2d(p, b.first, b.second) != HSDDP_OK) throw std::runtime_error(hsddp_last_error());
+        void *p = arena().get(slot++, b.second);
+        if (hsddp_memcpy_h2d(p, b.first, b.second) != HSDDP_OK) throw std::runtime_error(hsddp_last_error());
         din.push_back(p);
     }
-    for (auto &b : out) {
-        void *p = hsddp_device_alloc(b.second, 0);
-        if (!p) throw std::runtime_error(hsddp_last_error());
-        dout.push_back(p);
-    }
+    for (auto &b : out) dout.push_back(arena().get(slot++, b.second));
     const int rc = call(din, dout);
     if (rc == HSDDP_OK) hsddp_device_synchronize(0);
     for (size_t i = 0; i < out.size() && rc == HSDDP_OK; ++i) hsddp_memcpy_d2h(out[i].first, dout[i], out[i].second);
-    for (void *p : din) hsddp_device_free(p);
-    for (void *p : dout) hsddp_device_free(p);
     if (rc != HSDDP_OK) throw std::runtime_error(hsddp_last_error());
+}
+// knot index of time t on a grid starting at t0 with step dt (the references are held per knot)
+inline size_t knot_at(float t, float t0, double dt, size_t n)
+{
+    const long k = std::lround(((double)t - (double)t0) / dt);
+    return (size_t)std::min<long>(std::max<long>(k, 0), (long)n - 1);
 }
 }  // namespace detail
 
@@ -334,27 +828,175 @@ struct ResetmapPartial {
     }
 };
 
-// HKDTrackingCost (HKDCost.h:8-38) with its per-knot reference (HKDReference.cpp:8-57) and
-// HKDFootPlaceReg (HKDCost.cpp:5-63): weights shared by every phase of a problem
-struct TrackingCost : CostBase<double, 24, 24, 0> {
+// The HKD costs as CostBase plugins (HKDCost.h:8-99).  The references are held per knot of the
+// phase (x_ref, u_ref, foot_ref: horizon + 1 rows), looked up at t = t_start + k knot_dt (the
+// reference's costs look them up by time through HKDSinglePhaseReference / QuadReference).
+// Weights are shared by every phase of a problem.  Their virtuals evaluate on the device
+// (hsddp_hkd_running_cost / hsddp_hkd_terminal_cost) with the solver's own term formulas.
+struct HKDCostRefs {
+    std::array<int, 4> contact{};
+    std::vector<std::array<double, 24>> x_ref;   // horizon + 1 states
+    std::vector<std::array<double, 24>> u_ref;   // horizon + 1 (the last is unused, as the reference's lookup)
+    std::vector<std::array<double, 12>> foot_ref;  // horizon + 1 (HKDFootPlaceReg)
+    float t_start = 0;
+    double knot_dt = 0.01;
+};
+template <int TERMS>
+struct HKDCostTerm : CostBase<double, 24, 24, 0>, HKDCostRefs {
     hsddp_hkd_weights weights;
-    std::vector<std::array<double, 24>> x_ref;  // horizon + 1 states
-    std::vector<std::array<double, 24>> u_ref;  // horizon + 1 (the last is unused, as the reference's lookup)
-    TrackingCost() { hsddp_default_weights(&weights); cost_name = "HKD Tracking Cost"; }
+    explicit HKDCostTerm(const std::string &name) : CostBase<double, 24, 24, 0>(name) { hsddp_default_weights(&weights); }
+
+    void running_cost(RCost &rc, const State &x, const Contrl &u, const Output &, double dt, float t) override
+    {
+        eval_running(rc, x, u, dt, t, false);
+    }
+    void running_cost_par(RCost &rc, const State &x, const Contrl &u, const Output &, double dt, float t) override
+    {
+        eval_running(rc, x, u, dt, t, true);
+    }
+    void terminal_cost(TCost &tc, const State &x, float tend) override { eval_terminal(tc, x, tend, false); }
+    void terminal_cost_par(TCost &tc, const State &x, float tend) override { eval_terminal(tc, x, tend, true); }
+
+private:
+    void refs_at(float t, std::array<double, 24> &xr, std::array<double, 24> &ur, std::array<double, 12> &pf) const
+    {
+        const size_t n = x_ref.size();
+        if (!n) throw std::runtime_error(cost_name + ": no references set");
+        const size_t k = detail::knot_at(t, t_start, knot_dt, n);
+        xr = x_ref[k];
+        ur = k < u_ref.size() ? u_ref[k] : std::array<double, 24>{};
+        pf = k < foot_ref.size() ? foot_ref[k] : std::array<double, 12>{};
+    }
+    // running_cost fills l, running_cost_par the derivatives (HKDCost.cpp:5-33, 40-48 pattern)
+    void eval_running(RCost &rc, const State &x, const Contrl &u, double dt, float t, bool par) const
+    {
+        std::array<double, 24> xr, ur;
+        std::array<double, 12> pf;
+        refs_at(t, xr, ur, pf);
+        double l = 0, lxx[576], luu[576];
+        detail::on_device({{x.data(), 192}, {u.data(), 192}, {contact.data(), 16}, {xr.data(), 192}, {ur.data(), 192},
+                           {pf.data(), 96}},
+                          {{&l, 8}, {rc.lx.data(), 192}, {rc.lu.data(), 192}, {lxx, 4608}, {luu, 4608}},
+                          [&](std::vector<void *> &i, std::vector<void *> &o) {
+                              return hsddp_hkd_running_cost((double *)i[0], (double *)i[1], (int *)i[2], (double *)i[3],
+                                                            (double *)i[4], (double *)i[5], &weights, dt, TERMS,
+                                                            (double *)o[0], (double *)o[1], (double *)o[2],
+                                                            (double *)o[3], (double *)o[4], 1, nullptr);
+                          });
+        if (!par) { rc.l = l; return; }
+        std::memcpy(rc.lxx.data(), lxx, sizeof lxx);
+        std::memcpy(rc.luu.data(), luu, sizeof luu);
+        rc.lux.setZero();
+    }
+    void eval_terminal(TCost &tc, const State &x, float tend, bool par) const
+    {
+        std::array<double, 24> xr, ur;
+        std::array<double, 12> pf;
+        refs_at(tend, xr, ur, pf);
+        double Phi = 0, Phixx[576];
+        std::array<double, 24> Phix{};
+        detail::on_device({{x.data(), 192}, {contact.data(), 16}, {xr.data(), 192}, {pf.data(), 96}},
+                          {{&Phi, 8}, {Phix.data(), 192}, {Phixx, 4608}},
+                          [&](std::vector<void *> &i, std::vector<void *> &o) {
+                              return hsddp_hkd_terminal_cost((double *)i[0], (int *)i[1], (double *)i[2], (double *)i[3],
+                                                             &weights, TERMS, (double *)o[0], (double *)o[1],
+                                                             (double *)o[2], 1, nullptr);
+                          });
+        if (!par) { tc.Phi = Phi; return; }
+        for (int j = 0; j < 24; ++j) tc.Phix[j] = Phix[j];
+        std::memcpy(tc.Phixx.data(), Phixx, sizeof Phixx);
+    }
 };
-struct FootPlaceReg : CostBase<double, 24, 24, 0> {
-    std::vector<std::array<double, 12>> foot_ref;  // horizon + 1
-    FootPlaceReg() { cost_name = "HKD Foot Placement Regularization"; }
+// HKDTrackingCost (HKDCost.h:8-38) and HKDFootPlaceReg (HKDCost.h:40-99, HKDCost.cpp:5-63)
+struct TrackingCost : HKDCostTerm<HSDDP_TERM_TRACKING> {
+    TrackingCost() : HKDCostTerm("HKD Tracking Cost") {}
 };
-// GRFConstraint + ReB (HKDConstraints.cpp:7-66; ConstraintsBase.h:204-263) and
-// TouchDownConstraint + AL (HKDConstraints.cpp:69-171; ConstraintsBase.h:374-399)
+struct FootPlaceReg : HKDCostTerm<HSDDP_TERM_FOOT> {
+    FootPlaceReg() : HKDCostTerm("HKD Foot Placement Regularization") {}
+};
+
+// GRFConstraint + ReB (HKDConstraints.h:8-27, HKDConstraints.cpp:7-66; ConstraintsBase.h:204-263):
+// 5 friction-pyramid rows per stance leg
 struct GRFConstraint : PathConstraintBase<double, 24, 24, 0> {
-    hsddp_constraint_params params;
-    GRFConstraint() { hsddp_default_constraint_params(&params); constraint_name = "GRF constraint"; }
+    hsddp_constraint_params cparams;
+    std::array<int, 4> ctact_status{{1, 1, 1, 1}};
+    GRFConstraint() : PathConstraintBase("GRF") { hsddp_default_constraint_params(&cparams); set_contact(ctact_status); }
+    explicit GRFConstraint(const std::array<int, 4> &ctact) : GRFConstraint() { set_contact(ctact); }
+    void set_contact(const std::array<int, 4> &ctact)
+    {
+        ctact_status = ctact;
+        int n = 0;
+        for (int l = 0; l < 4; ++l) n += ctact[l] > 0;
+        update_constraint_size(5 * n);
+    }
+    void set_friction_coefficient(double mu) { cparams.mu_fric = mu; }
+    void compute_violation(const State &, const Contrl &u, const Output &, int k) override
+    {
+        if (data.empty()) create_data();
+        double g[20], gu[480];
+        eval(u, g, gu);
+        for (size_t i = 0; i < data[k].size(); ++i) data[k][i].g = g[i];
+        update_max_violation(k);
+    }
+    void compute_partial(const State &, const Contrl &u, const Output &, int k) override
+    {
+        double g[20], gu[480];
+        eval(u, g, gu);
+        for (size_t i = 0; i < data[k].size(); ++i)
+            for (int j = 0; j < 24; ++j) data[k][i].gu[j] = gu[24 * i + j];
+    }
+
+private:
+    void eval(const Contrl &u, double *g, double *gu) const
+    {
+        detail::on_device({{u.data(), 192}, {ctact_status.data(), 16}}, {{g, 160}, {gu, 3840}},
+                          [&](std::vector<void *> &i, std::vector<void *> &o) {
+                              return hsddp_hkd_grf_constraint((double *)i[0], (int *)i[1], cparams.mu_fric,
+                                                              (double *)o[0], (double *)o[1], 1, nullptr);
+                          });
+    }
 };
+// TouchDownConstraint + AL (HKDConstraints.h:29-51, HKDConstraints.cpp:69-171;
+// ConstraintsBase.h:374-399).  next_contact: the contact after the phase (the legs touching down
+// are those with contact 0 now and 1 next); ctor(impact_status) as the reference's.
 struct TouchDownConstraint : TerminalConstraintBase<double, 24> {
-    std::array<int, 4> next_contact{};
-    TouchDownConstraint() { constraint_name = "touch down constraint"; }
+    std::array<int, 4> contact{}, next_contact{};
+    double ground_height = 0;
+    TouchDownConstraint() : TerminalConstraintBase("TouchDwon") {}
+    explicit TouchDownConstraint(const std::array<int, 4> &impact_status) : TouchDownConstraint()
+    {
+        for (int l = 0; l < 4; ++l) { contact[l] = impact_status[l] ? 0 : 1; next_contact[l] = 1; }
+        size_t n = 0;
+        for (int l = 0; l < 4; ++l) n += impact_status[l] != 0;
+        update_constraint_size(n);
+    }
+    void update_ground_height(double g) { ground_height = g; }
+    void compute_violation(const State &x) override
+    {
+        double h[4], hx[96];
+        eval(x, h, hx);
+        if (data.size() != size) create_data();
+        for (size_t i = 0; i < size; ++i) data[i].h = h[i];
+        update_max_violation();
+    }
+    void compute_partial(const State &x) override
+    {
+        double h[4], hx[96];
+        eval(x, h, hx);
+        if (data.size() != size) create_data();
+        for (size_t i = 0; i < size; ++i)
+            for (int j = 0; j < 24; ++j) data[i].hx[j] = hx[24 * i + j];
+    }
+
+private:
+    void eval(const State &x, double *h, double *hx) const
+    {
+        detail::on_device({{x.data(), 192}, {contact.data(), 16}, {next_contact.data(), 16}}, {{h, 32}, {hx, 768}},
+                          [&](std::vector<void *> &i, std::vector<void *> &o) {
+                              return hsddp_hkd_touchdown_constraint((double *)i[0], (int *)i[1], (int *)i[2], ground_height,
+                                                                    (double *)o[0], (double *)o[1], 1, nullptr);
+                          });
+    }
 };
 }  // namespace hkd
 
@@ -376,20 +1018,22 @@ public:
     }
     void set_initial_condition(DVec<T> x0_in) { x0 = x0_in; }
 
-    // MultiPhaseDDP::solve (MultiPhaseDDP.cpp:232-428) for this one trajectory on the GPU
+    // MultiPhaseDDP::solve (MultiPhaseDDP.cpp:232-428) for this one trajectory on the GPU; afterwards
+    // every phase's Trajectory holds the solution, the working trajectory, the LQ model and terminal
+    // data of the last LQ_approximation and the value function at the phase start
     void solve(HSDDP_OPTION option);
 
     T get_actual_cost() { return actual_cost; }
     T measure_dynamics_feasibility(int = 2) { return feas; }
-    // final values only: the device solve keeps no per-iteration history (the reference appends
-    // one entry per accepted inner iteration, MultiPhaseDDP.cpp:277-280, 368-371)
+    // the per-iteration buffers (MultiPhaseDDP.cpp:532-541): the initial entry and one per inner
+    // iteration that passed the later-termination test (:277-280, 368-371)
     void get_solver_info(std::vector<float> &cost_out, std::vector<float> &dyn_feas_out,
                          std::vector<float> &eqn_feas_out, std::vector<float> &ineq_feas_out)
     {
-        cost_out = {(float)actual_cost};
-        dyn_feas_out = {(float)feas};
-        eqn_feas_out = {(float)max_tconstr};
-        ineq_feas_out = {(float)max_pconstr};
+        cost_out = cost_buffer;
+        dyn_feas_out = dyn_feas_buffer;
+        eqn_feas_out = eqn_feas_buffer;
+        ineq_feas_out = ineq_feas_buffer;
     }
     // per-element outcome of the last solve (hsddp_element_info)
     const hsddp_element_info &element_info() const { return info; }
@@ -420,6 +1064,7 @@ private:
     int n_phases = 0;
     DVec<T> x0;
     T actual_cost = 0, feas = 0, max_pconstr = 0, max_tconstr = 0;
+    std::vector<float> cost_buffer, dyn_feas_buffer, eqn_feas_buffer, ineq_feas_buffer;
     hsddp_element_info info{};
     hsddp_handle handle = nullptr;
 };
@@ -431,6 +1076,9 @@ void MultiPhaseDDP<T>::solve(HSDDP_OPTION option)
     if (n_phases < 1 || n_phases > HSDDP_MAX_PHASES) throw std::runtime_error("hsddp: 1..16 phases supported");
     if (x0.size() != 24) throw std::runtime_error("hsddp: set_initial_condition needs a 24-state x0");
     std::vector<Phase *> ph(n_phases);
+    std::vector<std::shared_ptr<Trajectory<double, 24, 24, 0>>> trajs(n_phases);
+    std::vector<const hkd::TrackingCost *> track(n_phases, nullptr);
+    std::vector<const hkd::FootPlaceReg *> foot(n_phases, nullptr);
     hsddp_problem_desc desc;
     std::memset(&desc, 0, sizeof desc);
     desc.device = 0;
@@ -440,92 +1088,83 @@ void MultiPhaseDDP<T>::solve(HSDDP_OPTION option)
     hsddp_default_weights(&desc.weights);
     hsddp_default_constraint_params(&desc.cparams);
     std::vector<int> contacts(4 * (n_phases + 1));
-    int S = 0, Kc = 0;
     for (int i = 0; i < n_phases; ++i) {
         ph[i] = dynamic_cast<Phase *>(phases[i].get());
         if (!ph[i]) throw std::runtime_error("phase " + std::to_string(i) + " is not SinglePhase<double,24,24,0>");
-        if (!ph[i]->traj) throw std::runtime_error("phase " + std::to_string(i) + " has no trajectory");
+        trajs[i] = ph[i]->traj;
         const auto *dyn = plugin<hkd::Dynamics>(ph[i]->dynamics, "Dynamics", i);
         plugin<hkd::DynamicsPartial>(ph[i]->dynamics_partial, "DynamicsPartial", i);
-        desc.horizons[i] = ph[i]->traj->horizon;
-        if (i == 0) desc.dt = ph[i]->traj->timeStep;
         for (int l = 0; l < 4; ++l) contacts[4 * i + l] = dyn->contact[l];
-        S += desc.horizons[i] + 1;
-        Kc += desc.horizons[i];
-        bool tracking = false, foot = false;
         for (auto &c : ph[i]->costs) {
-            if (auto *tc = dynamic_cast<hkd::TrackingCost *>(c.get())) { desc.weights = tc->weights; tracking = true; }
-            else if (dynamic_cast<hkd::FootPlaceReg *>(c.get())) foot = true;
+            if (auto *tc = dynamic_cast<hkd::TrackingCost *>(c.get())) { desc.weights = tc->weights; track[i] = tc; }
+            else if (auto *fr = dynamic_cast<hkd::FootPlaceReg *>(c.get())) foot[i] = fr;
             else throw std::runtime_error("phase " + std::to_string(i) + ": cost '" + c->cost_name + "' cannot run on the device");
         }
-        if (!tracking || !foot) throw std::runtime_error("phase " + std::to_string(i) + ": needs hkd::TrackingCost and hkd::FootPlaceReg");
+        if (!track[i] || !foot[i]) throw std::runtime_error("phase " + std::to_string(i) + ": needs hkd::TrackingCost and hkd::FootPlaceReg");
         for (auto &c : ph[i]->pconstraints) {
-            if (auto *g = dynamic_cast<hkd::GRFConstraint *>(c.get())) desc.cparams = g->params;
-            else throw std::runtime_error("phase " + std::to_string(i) + ": path constraint '" + c->constraint_name + "' cannot run on the device");
+            if (auto *g = dynamic_cast<hkd::GRFConstraint *>(c.get())) desc.cparams = g->cparams;
+            else throw std::runtime_error("phase " + std::to_string(i) + ": path constraint '" + c->name + "' cannot run on the device");
         }
         for (auto &c : ph[i]->tconstraints) {
             auto *td = dynamic_cast<hkd::TouchDownConstraint *>(c.get());
-            if (!td) throw std::runtime_error("phase " + std::to_string(i) + ": terminal constraint '" + c->constraint_name + "' cannot run on the device");
+            if (!td) throw std::runtime_error("phase " + std::to_string(i) + ": terminal constraint '" + c->name + "' cannot run on the device");
             if (i == n_phases - 1)
                 for (int l = 0; l < 4; ++l) contacts[4 * n_phases + l] = td->next_contact[l];
         }
     }
     if (ph[n_phases - 1]->tconstraints.empty())  // no touchdown after the horizon: keep the contact
         for (int l = 0; l < 4; ++l) contacts[4 * n_phases + l] = contacts[4 * (n_phases - 1) + l];
-    // references per state slot (phase-major, S = sum(N_i + 1))
-    std::vector<double> rx(24 * S), ru(24 * S), rf(12 * S), Xb(24 * S), Ub(24 * Kc), K(576 * Kc);
-    int s = 0, kc = 0;
-    for (int i = 0; i < n_phases; ++i) {
-        const hkd::TrackingCost *tc = nullptr;
-        const hkd::FootPlaceReg *fr = nullptr;
-        for (auto &c : ph[i]->costs) {
-            if (!tc) tc = dynamic_cast<hkd::TrackingCost *>(c.get());
-            if (!fr) fr = dynamic_cast<hkd::FootPlaceReg *>(c.get());
-        }
+    int S = 0, Kc = 0;
+    hsddp_pack::layout(trajs, desc.horizons, desc.dt, S, Kc);
+    // references per state slot from the costs' per-knot tables
+    std::vector<double> rx, ru, rf;
+    hsddp_pack::pack_references(n_phases, desc.horizons, [&](int i, int k, double *xr, double *ur, double *pf) {
+        const auto *tc = track[i];
+        const auto *fr = foot[i];
         const int N = desc.horizons[i];
         if ((int)tc->x_ref.size() != N + 1 || (int)tc->u_ref.size() < N || (int)fr->foot_ref.size() != N + 1)
             throw std::runtime_error("phase " + std::to_string(i) + ": reference lengths must match the horizon");
-        auto &tr = *ph[i]->traj;
-        for (int k = 0; k <= N; ++k, ++s) {
-            for (int j = 0; j < 24; ++j) {
-                rx[24 * s + j] = tc->x_ref[k][j];
-                ru[24 * s + j] = k < (int)tc->u_ref.size() ? tc->u_ref[k][j] : 0.0;
-                Xb[24 * s + j] = tr.Xbar[k][j];
-            }
-            for (int j = 0; j < 12; ++j) rf[12 * s + j] = fr->foot_ref[k][j];
-        }
-        for (int k = 0; k < N; ++k, ++kc)
-            for (int a = 0; a < 24; ++a) {
-                Ub[24 * kc + a] = tr.Ubar[k][a];
-                for (int b = 0; b < 24; ++b) K[576 * kc + 24 * a + b] = tr.K[k](a, b);  // row-major on the ABI
-            }
-    }
+        for (int j = 0; j < 24; ++j) { xr[j] = tc->x_ref[k][j]; ur[j] = k < (int)tc->u_ref.size() ? tc->u_ref[k][j] : 0.0; }
+        for (int j = 0; j < 12; ++j) pf[j] = fr->foot_ref[k][j];
+    }, rx, ru, rf);
+    std::vector<double> Xb, Ub, K;
+    hsddp_pack::pack_trajectories(trajs, Xb, Ub, K);
     release();
     check(hsddp_create(&desc, &handle));
     const hsddp_options o = option.to_c();
     check(hsddp_set_options(handle, &o));
+    check(hsddp_set_value_export(handle, 1));  // G[0], H[0] per phase for get_value_approx
     check(hsddp_upload_problem(handle, contacts.data(), x0.data(), rx.data(), ru.data(), rf.data()));
     check(hsddp_upload_warm_start(handle, Xb.data(), Ub.data(), K.data()));
     hsddp_stats st;
     check(hsddp_solve(handle, &st));
-    std::vector<double> X(24 * S), U(24 * Kc), D(24 * S), dX(24 * S), dU(24 * Kc);
+    // solution, working trajectory, LQ model, terminal data, value function, solver info
     check(hsddp_download_trajectory(handle, Xb.data(), Ub.data(), K.data()));
+    hsddp_pack::unpack_trajectories(trajs, Xb.data(), Ub.data(), K.data());
+    std::vector<double> X(24 * S), U(24 * Kc), D(24 * S), dX(24 * S), dU(24 * Kc);
     check(hsddp_download_working(handle, X.data(), U.data(), D.data(), dX.data(), dU.data()));
+    hsddp_pack::unpack_working(trajs, X.data(), U.data(), D.data(), dX.data(), dU.data());
+    std::vector<double> A(576 * Kc), Bm(576 * Kc), l(Kc), lx(24 * Kc), lu(24 * Kc), lxx(576 * Kc), luu(576 * Kc);
+    check(hsddp_download_lq(handle, A.data(), Bm.data(), l.data(), lx.data(), lu.data(), lxx.data(), luu.data()));
+    hsddp_pack::unpack_lq(trajs, A.data(), Bm.data(), l.data(), lx.data(), lu.data(), lxx.data(), luu.data());
+    std::vector<double> Phi(n_phases), Phix(24 * n_phases), Phixx(576 * n_phases), G(24 * n_phases), H(576 * n_phases);
+    check(hsddp_download_terminal(handle, Phi.data(), Phix.data(), Phixx.data(), nullptr));
+    check(hsddp_download_value(handle, G.data(), H.data()));
+    hsddp_pack::unpack_terminal_value(trajs, Phi.data(), Phix.data(), Phixx.data(), G.data(), H.data());
     check(hsddp_download_element_info(handle, &info));
-    s = kc = 0;
-    for (int i = 0; i < n_phases; ++i) {
-        auto &tr = *ph[i]->traj;
-        const int N = desc.horizons[i];
-        for (int k = 0; k <= N; ++k, ++s)
-            for (int j = 0; j < 24; ++j) {
-                tr.Xbar[k][j] = Xb[24 * s + j]; tr.X[k][j] = X[24 * s + j];
-                tr.Defect[k][j] = D[24 * s + j]; tr.dX[k][j] = dX[24 * s + j];
-            }
-        for (int k = 0; k < N; ++k, ++kc)
-            for (int a = 0; a < 24; ++a) {
-                tr.Ubar[k][a] = Ub[24 * kc + a]; tr.U[k][a] = U[24 * kc + a]; tr.dU[k][a] = dU[24 * kc + a];
-                for (int b = 0; b < 24; ++b) tr.K[k](a, b) = K[576 * kc + 24 * a + b];
-            }
+    const int cap = 1 + std::max(0, option.max_AL_iter) * std::max(0, option.max_DDP_iter);
+    std::vector<float> c(cap), f(cap), e(cap), q(cap);
+    int count = 0;
+    check(hsddp_download_solver_info(handle, cap, c.data(), f.data(), e.data(), q.data(), &count));
+    cost_buffer.assign(c.begin(), c.begin() + count);
+    dyn_feas_buffer.assign(f.begin(), f.begin() + count);
+    eqn_feas_buffer.assign(e.begin(), e.begin() + count);
+    ineq_feas_buffer.assign(q.begin(), q.begin() + count);
+    size_t kc = 0;
+    for (int i = 0; i < n_phases; ++i) {  // SinglePhase::get_actual_cost: running + terminal cost
+        double pc = 0;
+        for (int k = 0; k < desc.horizons[i]; ++k, ++kc) pc += l[kc];
+        ph[i]->actual_cost = pc + Phi[i];
     }
     actual_cost = info.cost;
     feas = info.feas;

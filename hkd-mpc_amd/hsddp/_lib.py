@@ -103,7 +103,8 @@ EXPORTS = [
     "hsddp_memcpy_h2d", "hsddp_memcpy_d2h", "hsddp_device_synchronize", "hsddp_extract_commands",
     "hsddp_shift", "hsddp_get_layout", "hsddp_update_problem", "hsddp_load_quad_reference",
     "hsddp_plan_phases", "hsddp_set_reference_table", "hsddp_build_references", "hsddp_download_references", "hsddp_advance",
-    "hsddp_get_phase_info",
+    "hsddp_get_phase_info", "hsddp_hkd_running_cost", "hsddp_hkd_terminal_cost", "hsddp_hkd_grf_constraint",
+    "hsddp_hkd_touchdown_constraint",
 ]
 
 
@@ -150,6 +151,11 @@ def lib():
     L.hsddp_hkd_foot_jacobian.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
     L.hsddp_hkd_resetmap.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
     L.hsddp_hkd_resetmap_partial.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    V = C.c_void_p
+    L.hsddp_hkd_running_cost.argtypes = [V] * 6 + [C.POINTER(Weights), C.c_double, C.c_int] + [V] * 5 + [C.c_int, V]
+    L.hsddp_hkd_terminal_cost.argtypes = [V] * 4 + [C.POINTER(Weights), C.c_int] + [V] * 3 + [C.c_int, V]
+    L.hsddp_hkd_grf_constraint.argtypes = [V, V, C.c_double, V, V, C.c_int, V]
+    L.hsddp_hkd_touchdown_constraint.argtypes = [V, V, V, C.c_double, V, V, C.c_int, V]
     L.hsddp_device_alloc.restype = C.c_void_p
     L.hsddp_device_alloc.argtypes = [C.c_size_t, C.c_int]
     L.hsddp_device_free.argtypes = [C.c_void_p]

@@ -11,7 +11,9 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import HSDDPError, check, lib
+import ctypes as _C
+
+from ._lib import HSDDPError, Weights, check, lib
 
 
 class _Dev:
@@ -92,3 +94,58 @@ def resetmap_partial(x, c, cn):
     out = _Dev(n * 576 * 8)
     check(lib().hsddp_hkd_resetmap_partial(dx.ptr, dc.ptr, dn.ptr, out.ptr, n, None))
     return out.get((n, 24, 24)).transpose(0, 2, 1)
+
+
+# ---- cost / constraint plugins (HKDCost.h, HKDConstraints.cpp; the C++ facade's hkd:: plugins) ----
+TERM_TRACKING, TERM_FOOT = 1, 2
+
+
+def _weights(w):
+    if w is None:
+        w = Weights()
+        lib().hsddp_default_weights(_C.byref(w))
+    return w
+
+
+def _pts(a, n, width, dtype=np.float64):
+    return _dev(np.broadcast_to(np.asarray(a, dtype=dtype), (n, width)), dtype)
+
+
+def running_cost(x, u, c, xr, ur, pf, terms=TERM_TRACKING | TERM_FOOT, dt=0.01, weights=None):
+    """RCostData of HKDTrackingCost (terms 1) / HKDFootPlaceReg (terms 2) at n points:
+    dict l [n], lx, lu [n, 24], lxx, luu [n, 24, 24]."""
+    x = np.atleast_2d(x); n = x.shape[0]
+    w = _weights(weights)
+    ins = [_dev(x), _pts(u, n, 24), _pts(c, n, 4, np.int32), _pts(xr, n, 24), _pts(ur, n, 24), _pts(pf, n, 12)]
+    outs = [_Dev(n * 8), _Dev(n * 192), _Dev(n * 192), _Dev(n * 4608), _Dev(n * 4608)]
+    check(lib().hsddp_hkd_running_cost(*[a.ptr for a in ins], _C.byref(w), dt, terms, *[o.ptr for o in outs], n, None))
+    return {"l": outs[0].get((n,)), "lx": outs[1].get((n, 24)), "lu": outs[2].get((n, 24)),
+            "lxx": outs[3].get((n, 24, 24)), "luu": outs[4].get((n, 24, 24))}
+
+
+def terminal_cost(x, c, xr, pf, terms=TERM_TRACKING | TERM_FOOT, weights=None):
+    """TCostData (Phi [n], Phix [n, 24], Phixx [n, 24, 24]) of the HKD terminal cost terms."""
+    x = np.atleast_2d(x); n = x.shape[0]
+    w = _weights(weights)
+    ins = [_dev(x), _pts(c, n, 4, np.int32), _pts(xr, n, 24), _pts(pf, n, 12)]
+    outs = [_Dev(n * 8), _Dev(n * 192), _Dev(n * 4608)]
+    check(lib().hsddp_hkd_terminal_cost(*[a.ptr for a in ins], _C.byref(w), terms, *[o.ptr for o in outs], n, None))
+    return {"Phi": outs[0].get((n,)), "Phix": outs[1].get((n, 24)), "Phixx": outs[2].get((n, 24, 24))}
+
+
+def grf_constraint(u, c, mu=0.7):
+    """GRFConstraint rows (5 per stance leg, leg order): g [n, 20], gu [n, 20, 24]."""
+    u = np.atleast_2d(u); n = u.shape[0]
+    du, dc = _dev(u), _pts(c, n, 4, np.int32)
+    g, gu = _Dev(n * 160), _Dev(n * 3840)
+    check(lib().hsddp_hkd_grf_constraint(du.ptr, dc.ptr, mu, g.ptr, gu.ptr, n, None))
+    return g.get((n, 20)), gu.get((n, 20, 24))
+
+
+def touchdown_constraint(x, c, cn, ground=0.0):
+    """TouchDownConstraint rows (legs with c = 0, cn = 1, leg order): h [n, 4], hx [n, 4, 24]."""
+    x = np.atleast_2d(x); n = x.shape[0]
+    dx, dc, dn = _dev(x), _pts(c, n, 4, np.int32), _pts(cn, n, 4, np.int32)
+    h, hx = _Dev(n * 32), _Dev(n * 768)
+    check(lib().hsddp_hkd_touchdown_constraint(dx.ptr, dc.ptr, dn.ptr, ground, h.ptr, hx.ptr, n, None))
+    return h.get((n, 4)), hx.get((n, 4, 24))

@@ -32,6 +32,10 @@
  *   hsddp_hkd_resetmap(_partial)              HKDReset::resetmap(_partial)          HKDReset.h:41-136
  *   hsddp_hkd_foot_position / _jacobian       compute_foot_position / comp_foot_jacob_{1..4}
  *                                             (CasadiGen/header/comp_foot_*.h via casadi_interface.cpp:5-80)
+ *   hsddp_hkd_running_cost / _terminal_cost   HKDTrackingCost / HKDFootPlaceReg running_cost(_par),
+ *                                             terminal_cost(_par)   HKDCost.h:8-99; HKDCost.cpp:5-63
+ *   hsddp_hkd_grf_constraint                  GRFConstraint::compute_violation/_partial HKDConstraints.cpp:7-66
+ *   hsddp_hkd_touchdown_constraint            TouchDownConstraint::compute_violation/_partial HKDConstraints.cpp:69-171
  *
  * Conventions
  *   - Return 0 on success, < 0 on error (hsddp_last_error() gives a message).  The reference
@@ -336,6 +340,29 @@ int hsddp_hkd_resetmap(const double *x, const int *c, const int *cn, double *xn,
 /* Px[n][24*24] column-major */
 int hsddp_hkd_resetmap_partial(const double *x, const int *c, const int *cn, double *Px, int n,
                                void *stream);
+
+/* HKD cost and constraint plugins at n points (the bodies of the C++ facade's hkd:: plugins; the
+ * solver evaluates the same terms inside its own kernels).  c, cn int32 [n][4]; xr, ur [n][24] and
+ * pf [n][12] the knot's references (ref_x, ref_u, ref_foot of hsddp_upload_problem).
+ * terms: HSDDP_TERM_TRACKING (HKDTrackingCost) | HSDDP_TERM_FOOT (HKDFootPlaceReg).
+ * Running cost (RCostData, HSDDP_CompoundTypes.h:91-122): l [n], lx, lu [n][24], lxx, luu [n][24*24]
+ * (symmetric; lux = 0).  Terminal cost (TCostData :125-150): Phi [n], Phix [n][24], Phixx [n][24*24].
+ * Any output may be NULL. */
+#define HSDDP_TERM_TRACKING 1
+#define HSDDP_TERM_FOOT 2
+int hsddp_hkd_running_cost(const double *x, const double *u, const int *c, const double *xr, const double *ur,
+                           const double *pf, const hsddp_hkd_weights *w, double dt, int terms, double *l, double *lx,
+                           double *lu, double *lxx, double *luu, int n, void *stream);
+int hsddp_hkd_terminal_cost(const double *x, const int *c, const double *xr, const double *pf,
+                            const hsddp_hkd_weights *w, int terms, double *Phi, double *Phix, double *Phixx, int n,
+                            void *stream);
+/* GRFConstraint: 5 friction-pyramid rows (A_leg, HKDConstraints.cpp:13-18) per stance leg in leg order,
+ * g [n][20] = A u, gu [n][20][24] = A rows (IneqConstrData g, gu); rows past 5 x (stance legs) are 0 */
+int hsddp_hkd_grf_constraint(const double *u, const int *c, double mu, double *g, double *gu, int n, void *stream);
+/* TouchDownConstraint: one row per leg touching down (c = 0, cn = 1) in leg order, h [n][4] = foot
+ * height - ground, hx [n][4][24] its state gradient (TConstrData h, hx); unused rows 0 */
+int hsddp_hkd_touchdown_constraint(const double *x, const int *c, const int *cn, double ground, double *h, double *hx,
+                                   int n, void *stream);
 
 /* device memory helpers for the primitives (so callers without a HIP runtime binding can use them) */
 void *hsddp_device_alloc(size_t bytes, int device);

@@ -29,6 +29,26 @@ def test_facade_builds_and_checks():
     assert "facade_check ok" in r.stdout
 
 
+def test_reference_plugin_api_compiles_and_works_on_the_host():
+    """plugin_check: a cost / constraints written with the reference's HKD plugin declarations
+    (HKDCost.h:75-81, HKDConstraints.h:21-37) and a user SinglePhaseBase compile against the facade;
+    the bases' ReB / AL helpers give their closed forms; a user cost is refused by solve()."""
+    _make()
+    r = subprocess.run([os.path.join(PKG, "plugin_check")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "plugin_check ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_hkd_plugins_evaluate_on_the_device():
+    """The facade's hkd:: plugins' virtuals (running_cost(_par), terminal_cost(_par),
+    compute_violation / compute_partial) through the device primitives."""
+    _make()
+    r = subprocess.run([os.path.join(PKG, "plugin_check"), "gpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "plugin_check ok" in r.stdout
+
+
 def _write_problem(d, prob):
     P = len(prob["horizons"])
     with open(os.path.join(d, "problem.txt"), "w") as f:
@@ -59,9 +79,26 @@ def test_facade_solve_matches_ctypes_path(tmp_path, gait, P, N):
     cost, feas, iters, outer, status, nls = open(os.path.join(tmp_path, "info.txt")).read().split()
 
     s = hsddp.Solver(prob, hsddp.load_settings(max_AL_iter=2, max_DDP_iter=4))
+    s.set_value_export(True)   # as the facade (get_value_approx)
     s.solve()
-    tr, info = s.trajectory(), s.element_info()
+    tr, info, wk, lq, term, val, hist = s.trajectory(), s.element_info(), s.working(), s.lq(), s.terminal(), s.value(), s.solver_info()
     s.close()
+    # Trajectory exports (TrajectoryManagement.h:49-81) equal the C-ABI downloads
+    rd = lambda n, shape, dt=np.float64: np.fromfile(os.path.join(tmp_path, n), dtype=dt).reshape(shape)
+    assert np.array_equal(rd("Xsim.f64", (S, 24)), wk["X"][0] + wk["Defect"][0])
+    assert np.array_equal(rd("A.f64", (Kc, 24, 24)), lq["A"][0])
+    assert np.array_equal(rd("l.f64", (Kc,)), lq["l"][0])
+    assert np.array_equal(rd("lx.f64", (Kc, 24)), lq["lx"][0])
+    assert np.array_equal(rd("luu.f64", (Kc, 24, 24)), lq["luu"][0])
+    assert np.array_equal(rd("Phix.f64", (P, 24)), term["Phix"][0])
+    assert np.array_equal(rd("G0.f64", (P, 24)), val["G"][0])
+    assert np.array_equal(rd("H0.f64", (P, 24, 24)), val["H"][0])
+    hz = np.cumsum([0] + list(prob["horizons"]))
+    pc = [lq["l"][0][hz[i]:hz[i + 1]].sum() + term["Phi"][0][i] for i in range(P)]
+    assert np.allclose(rd("phase_cost.f64", (P,)), pc, rtol=1e-14, atol=0)
+    got = rd("solver_info.f32", (-1, 4), np.float32)
+    want = np.stack([hist[k][0] for k in ("cost", "dyn_feas", "eqn_feas", "ineq_feas")], 1)
+    assert np.array_equal(got, want) and got.shape[0] >= 2
     assert np.array_equal(Xb, tr["Xbar"][0])
     assert np.array_equal(Ub, tr["Ubar"][0])
     assert np.array_equal(K, tr["K"][0])
