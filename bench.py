@@ -138,7 +138,10 @@ def main():
             dist.barrier()
 
     B = args.batch
-    prob = synthetic.make_batch(B, args.phases, args.knots, args.gait, mixed=args.mixed, first_element=rank * B)
+    # --mixed (config C4): per-element gaits, jumps on twice the phases of half the knots (8 x 25 beside
+    # 4 x 50: per-element layouts in one handle)
+    prob = synthetic.make_batch(B, args.phases, args.knots, args.gait, mixed=args.mixed, first_element=rank * B,
+                                jump_layout=args.mixed)
     opt = hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=args.warmup + args.steps)
     solver = hsddp.Solver(prob, opt, device=local, riccati_fp32=args.riccati_fp32)
     solver.begin()
@@ -176,6 +179,9 @@ def main():
 
     if rank == 0:
         S, Kc, P = prob["S"], prob["Kc"], len(prob["horizons"])
+        if prob.get("layouts"):  # per-element layouts: the byte model at the batch's mean layout
+            P = float(np.mean([len(h) for h in prob["layouts"]]))
+            S = Kc + P
         ms_step = elapsed / args.steps * 1e3
         mean_ls = total_ls / max(1.0, total_iters)
         kb = traffic.kernel_bytes(B, S, Kc, P, fp32=args.riccati_fp32, ref_per_element=args.mixed)
@@ -189,7 +195,7 @@ def main():
         gait = "mixed" if args.mixed else args.gait
         metric_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 4096)
         label = ("config C5: fp32 Riccati" if args.riccati_fp32 else "BASELINE metric config" if metric_cfg
-                 else "config C3: jump with resets" if gait == "jump" else "config C4 shard: mixed gaits" if args.mixed
+                 else "config C3: jump with resets" if gait == "jump" else "config C4 shard: mixed gaits, 4x50 / 8x25 layouts" if args.mixed
                  else "custom")
         cfg_key = f"{gait}_{args.phases}x{args.knots}_b{B}" + ("_fp32" if args.riccati_fp32 else "")
         meas, meas_src = load_traffic(cfg_key)

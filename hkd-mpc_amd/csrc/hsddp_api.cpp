@@ -240,6 +240,8 @@ struct hsddp_handle_t {
     std::vector<double> durations;
     int retry_cap_alloc = 0, retry_m_alloc = 0;  // parallel regularisation retry scratch (k_riccati_retry)
     float *hist = nullptr;  // solver-info history [B][p.hcap][4] (grown by ensure_history)
+    // per-element layouts (hsddp_set_element_layouts): host copies of Bufs::lay; empty = the handle's
+    std::vector<Layout> lays;
     double *value0 = nullptr;  // G[0], H[0] per phase [B][16][600] (hsddp_set_value_export)
 };
 
@@ -258,12 +260,30 @@ static int scratch(hsddp_handle h, size_t bytes, char **out)
     return HSDDP_OK;
 }
 
+// the layout of element b: the handle's, or its own (hsddp_set_element_layouts)
+static Layout layout_of(hsddp_handle h, size_t b)
+{
+    if (!h->lays.empty()) return h->lays[b];
+    const Params &p = h->p;
+    Layout L{};
+    L.P = p.P; L.S = p.S; L.has_tail = p.has_tail;
+    for (int i = 0; i < p.P; ++i) { L.N[i] = p.N[i]; L.s0[i] = p.s0[i]; L.k0[i] = p.k0[i]; L.ss[i] = p.ss[i]; }
+    return L;
+}
+
+// phase of control slot kc in a layout
+static int phase_of_control(const Layout &L, int kc)
+{
+    int i = 0;
+    while (i + 1 < L.P && kc >= L.k0[i + 1]) ++i;
+    return i;
+}
+
 // control u of compact gain row q at control slot k of element b (KCW layout, hsddp_internal.h)
 static int coupled_control(hsddp_handle h, size_t b, size_t k, int q)
 {
     const Params &p = h->p;
-    int i = 0;
-    while (i + 1 < p.P && (int)k >= p.k0[i + 1]) ++i;
+    const int i = phase_of_control(layout_of(h, b), (int)k);
     const int c = h->contacts[(b * (p.P + 1) + i) * 4 + q / 3];
     return c ? q : 12 + q;
 }
@@ -399,7 +419,8 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         (rc = dalloc(h, d.reb_eps, B * Kc * 20)) || (rc = dalloc(h, d.al_sigma, B * P * 4)) ||
         (rc = dalloc(h, d.al_lambda, B * P * 4)) || (rc = dalloc(h, d.term_h, B * P * 4)) ||
         (rc = dalloc(h, d.slot_cost, B * S)) || (rc = dalloc(h, d.slot_feas, B * S)) || (rc = dalloc(h, d.slot_viol, B * S)) ||
-        (rc = dalloc(h, d.slot_div, B * S)) || (rc = dalloc(h, d.el, B)) || (rc = dalloc(h, d.counter, 4))) {
+        (rc = dalloc(h, d.slot_div, B * S)) || (rc = dalloc(h, d.el, B)) || (rc = dalloc(h, d.counter, 4)) ||
+        (rc = dalloc(h, (Layout *&)d.lay, B)) || (rc = dalloc(h, (int *&)d.pairs, 2 * B + 2))) {
         hsddp_destroy(h);
         return rc;
     }
@@ -494,6 +515,56 @@ extern "C" int hsddp_set_options(hsddp_handle h, const hsddp_options *o)
     h->opt = *o;
     fill_params(h);
     return ensure_history(h);
+}
+
+extern "C" int hsddp_set_element_layouts(hsddp_handle h, const int *n_phases, const int *horizons)
+{
+    if (!h || !n_phases || !horizons) return fail(HSDDP_ERR_ARG, "null argument");
+    Params &p = h->p;
+    const int B = p.B;
+    std::vector<Layout> lays(B);
+    int Pmax = 0, Smax = 0;
+    for (int b = 0; b < B; ++b) {
+        Layout &L = lays[b];
+        L = Layout{};
+        L.P = n_phases[b];
+        if (L.P < 1 || L.P > HSDDP_MAX_PHASES) return fail(HSDDP_ERR_ARG, "element n_phases must lie in 1..16");
+        int s = 0, k = 0;
+        for (int i = 0; i < L.P; ++i) {
+            const int N = horizons[(size_t)b * HSDDP_MAX_PHASES + i];
+            if (N < 1) return fail(HSDDP_ERR_ARG, "phase horizons must be >= 1");
+            L.N[i] = N; L.s0[i] = s; L.k0[i] = k; L.ss[i] = N + 1;
+            s += N + 1; k += N;
+        }
+        if (k != p.Kc) return fail(HSDDP_ERR_ARG, "every element's horizons must sum to the handle's Kc");
+        L.S = s;
+        Pmax = std::max(Pmax, L.P);
+        Smax = std::max(Smax, L.S);
+    }
+    // the sweep runs two elements per wave in lockstep: pair elements of equal layouts
+    std::map<std::vector<int>, std::vector<int>> groups;
+    for (int b = 0; b < B; ++b) groups[std::vector<int>(lays[b].N, lays[b].N + lays[b].P)].push_back(b);
+    std::vector<int> pairs;
+    for (auto &g : groups)
+        for (size_t j = 0; j < g.second.size(); j += 2) {
+            pairs.push_back(g.second[j]);
+            pairs.push_back(j + 1 < g.second.size() ? g.second[j + 1] : -1);
+        }
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipMemcpy((void *)h->d.lay, lays.data(), B * sizeof(Layout), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void *)h->d.pairs, pairs.data(), pairs.size() * sizeof(int), hipMemcpyHostToDevice));
+    h->lays = lays;
+    p.elem_layout = 1;
+    p.n_pairs = (int)pairs.size() / 2;
+    p.P = Pmax;  // strides of the per-phase and per-slot buffers
+    p.S = Smax;
+    p.has_tail = 0;
+    for (int i = 0; i < Pmax; ++i) { p.N[i] = 0; p.s0[i] = 0; p.k0[i] = 0; p.ss[i] = 0; }
+    h->reach_end.assign(Pmax, 0);
+    h->have_problem = false;  // inputs of the new layouts next (hsddp_upload_problem)
+    h->contacts_current = false;
+    h->refs_on_device = false;
+    return HSDDP_OK;
 }
 
 static int h2d(void *dst, const void *src, size_t bytes, hipStream_t st)
@@ -947,13 +1018,6 @@ extern "C" int hsddp_download_solver_info(hsddp_handle h, int capacity, float *c
 // The device keeps the LQ model of a knot in the compact record (hsddp_internal.h); these host
 // routines expand it to the reference's dense blocks for callers that read them.
 
-// phase of control slot kc and of state slot s
-static int phase_of_control(const Params &p, int kc)
-{
-    int i = 0;
-    while (i + 1 < p.P && kc >= p.k0[i + 1]) ++i;
-    return i;
-}
 
 extern "C" int hsddp_download_lq(hsddp_handle h, double *A, double *Bm, double *l, double *lx, double *lu,
                                  double *lxx, double *luu)
@@ -976,7 +1040,7 @@ extern "C" int hsddp_download_lq(hsddp_handle h, double *A, double *Bm, double *
     for (size_t b = 0; b < B; ++b)
         for (size_t kc = 0; kc < Kc; ++kc) {
             const double *r = rec.data() + (b * Kc + kc) * W;
-            const int i = phase_of_control(p, (int)kc);
+            const int i = phase_of_control(layout_of(h, b), (int)kc);
             const int *c = h->contacts.data() + (b * (p.P + 1) + i) * 4;
             const size_t o = (b * Kc + kc);
             if (A) {  // A = I + S (hkd_model.h: Se, Sw, dt at (3 + a, 9 + a))
@@ -1039,18 +1103,27 @@ extern "C" int hsddp_download_terminal(hsddp_handle h, double *Phi, double *Phix
     std::vector<double> term(B * P * TW), cost(B * p.S);
     HIPCHK(hipMemcpy(term.data(), h->d.term, term.size() * sizeof(double), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(cost.data(), h->d.slot_cost, cost.size() * sizeof(double), hipMemcpyDeviceToHost));
-    for (size_t b = 0; b < B; ++b)
+    for (size_t b = 0; b < B; ++b) {
+        const Layout L = layout_of(h, b);
         for (size_t i = 0; i < P; ++i) {
             const double *t = term.data() + (b * P + i) * TW;
             const size_t o = b * P + i;
-            if (Phi) Phi[o] = cost[b * p.S + p.s0[i] + p.N[i]];
+            if ((int)i >= L.P) {  // past this element's phases
+                if (Phi) Phi[o] = 0;
+                if (Phix) std::fill(Phix + o * NX, Phix + (o + 1) * NX, 0.0);
+                if (Phixx) std::fill(Phixx + o * NN, Phixx + (o + 1) * NN, 0.0);
+                if (Px) std::fill(Px + o * NN, Px + (o + 1) * NN, 0.0);
+                continue;
+            }
+            if (Phi) Phi[o] = cost[b * p.S + L.s0[i] + L.N[i]];
             if (Phix) std::copy(t + TM_PHIX, t + TM_PHIX + NX, Phix + o * NX);
             if (Phixx) std::copy(t + TM_PHIXX, t + TM_PHIXX + NN, Phixx + o * NN);
             if (Px) {
-                if (i + 1 < P) std::copy(t + TM_PX, t + TM_PX + NN, Px + o * NN);
+                if ((int)i + 1 < L.P) std::copy(t + TM_PX, t + TM_PX + NN, Px + o * NN);
                 else std::fill(Px + o * NN, Px + (o + 1) * NN, 0.0);  // no reset after the last phase
             }
         }
+    }
     return HSDDP_OK;
 }
 
@@ -1225,6 +1298,8 @@ extern "C" int hsddp_extract_commands(hsddp_handle h, int nsteps_between_mpc, do
                                       const float *foot_placements, int feet_per_element, float solve_time,
                                       hsddp_mpc_command *out)
 {
+    if (h && !h->lays.empty())
+        return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts (hsddp_set_element_layouts): the MPC-side steps need the handle's shared layout");
     if (!h || !out) return fail(HSDDP_ERR_ARG, "null argument");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     const Params &p = h->p;
@@ -1281,6 +1356,8 @@ struct ShiftPhase {
 
 extern "C" int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_change)
 {
+    if (h && !h->lays.empty())
+        return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts (hsddp_set_element_layouts): the MPC-side steps need the handle's shared layout");
     if (!h || (n_steps > 0 && !contact_change)) return fail(HSDDP_ERR_ARG, "null argument");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     if (n_steps < 0) return fail(HSDDP_ERR_ARG, "n_steps must be >= 0");
@@ -1441,6 +1518,8 @@ static int build_refs(hsddp_handle h, const int *window_start, int window_len, c
 extern "C" int hsddp_build_references(hsddp_handle h, const int *window_start, int window_len,
                                       const float *phase_start_times, float dt_sim)
 {
+    if (h && !h->lays.empty())
+        return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts (hsddp_set_element_layouts): the MPC-side steps need the handle's shared layout");
     return build_refs(h, window_start, window_len, phase_start_times, dt_sim, true);
 }
 
@@ -1518,6 +1597,8 @@ static int build_refs(hsddp_handle h, const int *window_start, int window_len, c
 extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, float dt_mpc, const double *x0,
                              int *contact_change)
 {
+    if (h && !h->lays.empty())
+        return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts (hsddp_set_element_layouts): the MPC-side steps need the handle's shared layout");
     if (!h) return fail(HSDDP_ERR_ARG, "null handle");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     if (h->need_inputs) return fail(HSDDP_ERR_ARG, "the previous shift awaits hsddp_update_problem");

@@ -41,12 +41,28 @@ template <typename PT>
 DEV double foot_weight(const PT &p, const int *c, int j) { return p.foot_gain * p.foot_w[j % 3] * c[j / 3]; }
 DEV bool touchdown(const int *c, const int *cn, int l) { return c[l] == 0 && cn[l] == 1; }
 
-DEV void slot_phase(const Params &p, int s, int &i, int &k)
+// ---- the phase layout of element b ----------------------------------------------------------
+// The handle's layout (Params), or element b's own with per-element layouts (Bufs::lay).  Runtime
+// phase indices read Params in place (kparams), never the by-value copy.
+struct Lay {
+    const Layout *l;  // null: the handle's layout
+    DEV int P() const { return l ? l->P : kparams()->P; }
+    DEV int S() const { return l ? l->S : kparams()->S; }
+    DEV int N(int i) const { return l ? l->N[i] : kparams()->N[i]; }
+    DEV int s0(int i) const { return l ? l->s0[i] : kparams()->s0[i]; }
+    DEV int k0(int i) const { return l ? l->k0[i] : kparams()->k0[i]; }
+    DEV int ss(int i) const { return l ? l->ss[i] : kparams()->ss[i]; }
+};
+DEV Lay layout_of(const Bufs &d, int b) { return Lay{kparams()->elem_layout ? d.lay + b : nullptr}; }
+
+// phase i and knot k of state slot s
+DEV void slot_phase(const Lay &L, int s, int &i, int &k)
 {
     i = 0;
-    for (int j = 1; j < p.P; ++j)
-        if (s >= p.s0[j]) i = j;
-    k = s - p.s0[i];
+    const int P = L.P();
+    for (int j = 1; j < P; ++j)
+        if (s >= L.s0(j)) i = j;
+    k = s - L.s0(i);
 }
 
 DEV void load_contacts(const Bufs &d, const Params &p, int b, int i, int *c, int *cn)

@@ -50,7 +50,17 @@ constexpr int TM_PHIXX = 24;
 constexpr int TM_PX = 24 + NN;
 constexpr int TW = 24 + 2 * NN;          // 1176
 
+// Phase layout of one element: P phases of N_i knots, state slots s0_i .. s0_i + N_i, control slots
+// k0_i .. k0_i + N_i - 1, shooting states ss_i; S = sum(N_i + 1).  Per-element layouts
+// (hsddp_set_element_layouts) all have the handle's Kc.
+struct Layout {
+    int P, S, has_tail, pad;
+    int N[MAXP], s0[MAXP], k0[MAXP], ss[MAXP];
+};
+
 struct Params {
+    // B elements; P, S: the handle's layout (with per-element layouts: the largest P and S, the
+    // strides of the per-phase and per-slot buffers); Kc control slots of every element
     int B, P, S, Kc;
     int N[MAXP], s0[MAXP], k0[MAXP];
     int ref_per_element;
@@ -73,6 +83,8 @@ struct Params {
     // of backward_sweep_regularized (MultiPhaseDDP.cpp:141-181) at once; 0 = sequential only
     int retry_cap, retry_m;
     int hcap;  // solver-info history entries per element (Bufs::hist)
+    int elem_layout;  // 1: element b's layout is Bufs::lay[b] (N, s0, k0, ss above unused)
+    int n_pairs;      // sweep waves: Bufs::pairs [n_pairs][2] (elem_layout), else ceil(B / 2)
     int store_value;  // the sweep writes G[0], H[0] of every phase (Bufs::value0)
 };
 
@@ -113,6 +125,8 @@ struct Bufs {
     // get_solver_info buffers (MultiPhaseDDP.cpp:532-541): per element hcap entries of
     // (actual_cost, dynamics feasibility, max terminal violation, max path violation)
     float *hist;                           // [B][hcap][4]
+    const Layout *lay;                     // [B] per-element layouts (Params::elem_layout)
+    const int *pairs;                      // [n_pairs][2] the sweep's element pairs (same layout; -1 = none)
     double *value0;                        // [B][P][24 + 576]: G[0], H[0] per phase (store_value)
 };
 

@@ -79,8 +79,10 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     const int b = (int)(gid / p.S), s = (int)(gid % p.S);
     const ElemState &E = d.el[b];
     if (E.done || E.inner_done) return;
+    const Lay L = layout_of(d, b);
+    if (s >= L.S()) return;
     int i, k;
-    slot_phase(p, s, i, k);
+    slot_phase(L, s, i, k);
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     double x[NX];
@@ -98,13 +100,13 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
         for (int j = 0; j < NX; ++j) d32[j] = (float)dg[j];
     }
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
-    if (k == p.N[i]) {
+    if (k == L.N(i)) {
         double tv, h[4];
         const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
         d.slot_cost[(size_t)b * p.S + s] = terminal_cost(p, c, cn, x, xr, pf, sg, lm, tv, h);
         return;
     }
-    const int kc = p.k0[i] + k;
+    const int kc = L.k0(i) + k;
     sridx[w][lane] = (long)b * p.Kc + kc;
     double u[NU];
     const double *ug = d.U + ((size_t)b * p.Kc + kc) * NU;
@@ -183,9 +185,12 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
     const int b = blockIdx.x / p.P, i = blockIdx.x % p.P, t = threadIdx.x;
     const ElemState &E = d.el[b];
     if (E.done || E.inner_done) return;
+    const Lay L = layout_of(d, b);
+    const int P = L.P();
+    if (i >= P) return;
     __shared__ double sx[NX], shx[4][NX], scoef[4][2];
     __shared__ int sc[4], scn[4];
-    const int s = p.s0[i] + p.N[i];
+    const int s = L.s0(i) + L.N(i);
     if (t < NX) sx[t] = d.X[((size_t)b * p.S + s) * NX + t];
     if (t < 4) {
         const int *cc = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
@@ -242,7 +247,7 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
         for (int l = 0; l < 4; ++l) v += scoef[l][1] * (shx[l][r] * shx[l][cidx]);
         rec[TM_PHIXX + e] = v;
     }
-    if (i < p.P - 1) { // Px at X_i[N] (HKDReset.h:78-136), staged in LDS, stored coalesced by the wave
+    if (i < P - 1) { // Px at X_i[N] (HKDReset.h:78-136), staged in LDS, stored coalesced by the wave
         __shared__ double spx[NX * (NX + 1)];
         for (int e = t; e < NX * (NX + 1); e += 64) spx[e] = (e / (NX + 1) == e % (NX + 1)) ? 1.0 : 0.0;
         __syncthreads();
@@ -280,8 +285,8 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
 // Per-slot outputs of one rollout trial from the slot's state x = X[k], simulated state xs =
 // Xsim[k] and control u = U[k] (k < N): Defect, |Defect|^2, divergence flag, running or terminal
 // cost with its constraint violation and touchdown residuals (SinglePhase.cpp:196-232).
-DEV void finish_slot(const Params &p, const Bufs &d, int b, int s, int i, int k, const int *c, const int *cn,
-                     const double *x, const double *xs, const double *u)
+DEV void finish_slot(const Params &p, const Bufs &d, const Lay &L, int b, int s, int i, int k, const int *c,
+                     const int *cn, const double *x, const double *xs, const double *u)
 {
     const size_t sb = (size_t)b * p.S;
     double nrm = 0.0, fs = 0.0;
@@ -296,7 +301,7 @@ DEV void finish_slot(const Params &p, const Bufs &d, int b, int s, int i, int k,
     d.slot_feas[sb + s] = fs;
     d.slot_div[sb + s] = (k > 0 && sqrt(nrm) > 1e6) ? 1 : 0;
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
-    if (k == p.N[i]) {
+    if (k == L.N(i)) {
         double tv, h[4];
         const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
         d.slot_cost[sb + s] = terminal_cost(p, c, cn, x, xr, pf, sg, lm, tv, h);
@@ -304,7 +309,7 @@ DEV void finish_slot(const Params &p, const Bufs &d, int b, int s, int i, int k,
 #pragma unroll
         for (int l = 0; l < 4; ++l) d.term_h[((size_t)b * p.P + i) * 4 + l] = h[l];
     } else {
-        const int kc = p.k0[i] + k;
+        const int kc = L.k0(i) + k;
         const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
         const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
         double viol;
@@ -388,8 +393,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     if (gid >= total) return;
     const int b = (int)(gid / p.S), s = (int)(gid % p.S);
     if (!active(b)) return;
+    const Lay L = layout_of(d, b);
+    if (s >= L.S()) return;
     int i, k;
-    slot_phase(p, s, i, k);
+    slot_phase(L, s, i, k);
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     const double *x = Xt + (gid - xr0) * RS;
@@ -411,14 +418,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
         hkd_step(x - RS, up, cd, p.dt, xs);
     }
     double u[NU];  // read by finish_slot only when k < N
-    if (k < p.N[i]) {
+    if (k < L.N(i)) {
         trial_row(d, kq, eps, u);
         typedef double d2 __attribute__((ext_vector_type(2)));
         d2 *ug = (d2 *)(d.U + kq * NU);
 #pragma unroll
         for (int j = 0; j < NU / 2; ++j) ug[j] = d2{u[2 * j], u[2 * j + 1]};
     }
-    finish_slot(p, d, b, s, i, k, c, cn, x, xs, u);
+    finish_slot(p, d, L, b, s, i, k, c, cn, x, xs, u);
 }
 
 // k_rollout_tail: the non-shooting states of a phase (k >= ss; HKDProblem::update leaves a new
@@ -433,8 +440,9 @@ __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double ep
     const ElemState &E = d.el[b];
     if (!(init ? !E.done : E.ls_active != 0)) return;
     const size_t sb = (size_t)b * p.S, kb = (size_t)b * p.Kc;
-    for (int i = 0; i < p.P; ++i) {
-        const int N = p.N[i], ss = p.ss[i], s0 = p.s0[i], k0 = p.k0[i];
+    const Lay L = layout_of(d, b);
+    for (int i = 0; i < L.P(); ++i) {
+        const int N = L.N(i), ss = L.ss(i), s0 = L.s0(i), k0 = L.k0(i);
         if (ss >= N + 1) continue;
         int c[4], cn[4];
         load_contacts(d, p, b, i, c, cn);
@@ -476,7 +484,7 @@ __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double ep
                 for (int j = 0; j < NU; ++j) { u[j] = ub[j] + eps * du[j] + u[j]; ug[j] = u[j]; }
                 up = u;
             }
-            finish_slot(p, d, b, s, i, k, c, cn, x, xs, up);
+            finish_slot(p, d, L, b, s, i, k, c, cn, x, xs, up);
             if (k < N) hkd_step(x, u, cd, p.dt, xs);
         }
     }
@@ -493,11 +501,13 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
     const bool valid = b < p.B;
     const ElemState *Ep = valid ? &d.el[b] : nullptr;
     const bool act = valid && (init ? !Ep->done : Ep->ls_active);
+    const Lay L = layout_of(d, valid ? b : 0);
+    const int P = L.P();
     double ci = 0.0, fi = 0.0, pv = 0.0, tv = 0.0;
     int div = 0;
-    if (act && g < p.P) {
-        const size_t sb = (size_t)b * p.S + p.s0[g];
-        const int N = p.N[g];
+    if (act && g < P) {
+        const size_t sb = (size_t)b * p.S + L.s0(g);
+        const int N = L.N(g);
         for (int k = 0; k < N; ++k) {
             ci += d.slot_cost[sb + k];
             pv = fmin(pv, d.slot_viol[sb + k]);
@@ -508,7 +518,7 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
     }
     double cost = 0.0, feas = 0.0, max_p = 0.0, max_t = 0.0;
     int dv = 0;
-    for (int i = 0; i < p.P; ++i) {
+    for (int i = 0; i < p.P; ++i) {  // uniform bound (lanes g >= P add exact zeros)
         cost += __shfl(ci, base + i);
         feas += __shfl(fi, base + i);
         max_p = fmin(max_p, __shfl(pv, base + i));
@@ -593,9 +603,10 @@ __global__ __launch_bounds__(256) void k_reb_update(Params p, Bufs d)
     if (gid >= (long)p.B * p.Kc) return;
     const int b = (int)(gid / p.Kc), kc = (int)(gid % p.Kc);
     if (d.el[b].done) return;
+    const Lay L = layout_of(d, b);
     int i = 0;
-    for (int j = 1; j < p.P; ++j)
-        if (kc >= p.k0[j]) i = j;
+    for (int j = 1; j < L.P(); ++j)
+        if (kc >= L.k0(j)) i = j;
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     const double *u = d.U + gid * NU;
@@ -620,7 +631,8 @@ __global__ void k_outer_end(Params p, Bufs d)
     ElemState &E = d.el[b];
     if (E.done) return;
     if (p.AL_active) {
-        for (int i = 0; i < p.P; ++i) {
+        const int P = layout_of(d, b).P();
+        for (int i = 0; i < P; ++i) {
             int c[4], cn[4];
             load_contacts(d, p, b, i, c, cn);
             for (int l = 0; l < 4; ++l) {

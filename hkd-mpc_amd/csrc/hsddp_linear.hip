@@ -276,10 +276,12 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
     const int rr = rowl ? r : 0;
     const real *defg = Prec<real>::def(d);
     real v1 = 0, v2 = 0, dx = 0;
-    for (int i = 0; i < p.P; ++i) {
+    const Lay EL = layout_of(d, (int)b);
+    const int P = EL.P();
+    for (int i = 0; i < P; ++i) {
         PhaseConst<real> pc;
         load_phase(p, d, b, i, pc);
-        const int N = p.N[i], s0 = p.s0[i], k0 = p.k0[i];
+        const int N = EL.N(i), s0 = EL.s0(i), k0 = EL.k0(i);
         lin_fetch(B0, p, d, b, s0, k0, lane);  // the phase's first knot (its wait is in lin_knot)
         if (i > 0) { // dx_init = Px dX_end
             const double *Px = d.term + (b * p.P + (i - 1)) * TW + TM_PX;

@@ -149,9 +149,6 @@ struct Phase {
 
 // Phase layout entries with a runtime phase index, read from the kernel-argument segment (scalar
 // loads): indexing the by-value Params directly makes the compiler copy it to scratch.
-DEV int phase_N(int i) { return kparams()->N[i]; }
-DEV int phase_s0(int i) { return kparams()->s0[i]; }
-DEV int phase_k0(int i) { return kparams()->k0[i]; }
 
 template <typename real>
 DEV void load_phase(const Params &p, const Bufs &d, typename Lds<real>::Item &I, int b, int i, int pp, Phase<real> &ph)
@@ -603,11 +600,14 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
     bool live = it.act;
     int fail = -1;
     real h[NX], g = 0;
-    for (int i = p.P - 1; i >= 0; --i) {
+    // both items share one layout (the handle's, or paired by layout: Bufs::pairs)
+    const Lay PL = layout_of(d, b0);
+    const int P = PL.P();
+    for (int i = P - 1; i >= 0; --i) {
         Phase<real> ph;
         load_phase<real>(p, d, S.it[L.e], b, i, pp, ph);
         const double *rec = d.term + ((size_t)b * p.P + i) * TW;
-        if (i == p.P - 1) {
+        if (i == P - 1) {
 #pragma unroll
             for (int c = 0; c < NX; ++c) h[c] = L.row ? (real)rec[TM_PHIXX + pp * NX + c] : (real)0;
             g = L.row ? (real)rec[TM_PHIX + pp] : (real)0;
@@ -663,7 +663,7 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
             g = L.row ? (real)rec[TM_PHIX + pp] + gp : (real)0;
             SSYNC();
         }
-        const int N = phase_N(i), s0 = phase_s0(i), k0 = phase_k0(i);
+        const int N = PL.N(i), s0 = PL.s0(i), k0 = PL.k0(i);
         auto recp = [&](int bb, int k) { return lqg + ((size_t)bb * p.Kc + k0 + k) * Prec<real>::LQS; };
         auto defp = [&](int bb, int k) { return defg + ((size_t)bb * p.S + s0 + k + 1) * NX; };
         fetch(S, recp(b0, N - 1), defp(b0, N - 1), recp(b1, N - 1), defp(b1, N - 1), L.lane);
@@ -702,9 +702,10 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
 DEV void element_cost(const Params &p, const Bufs &d, int b, double &cost, double &feas)
 {
     cost = 0.0; feas = 0.0;
-    for (int i = 0; i < p.P; ++i) {
+    const Lay L = layout_of(d, b);
+    for (int i = 0; i < L.P(); ++i) {
         double ci = 0.0, fi = 0.0;
-        const int N = phase_N(i), s0 = phase_s0(i);
+        const int N = L.N(i), s0 = L.s0(i);
         for (int k = 0; k < N; ++k) ci += d.slot_cost[(size_t)b * p.S + s0 + k];
         ci += d.slot_cost[(size_t)b * p.S + s0 + N];
         for (int k = 0; k <= N; ++k) fi += d.slot_feas[(size_t)b * p.S + s0 + k];
@@ -755,9 +756,20 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
 #if HSDDP_STAMPS
     if (L.lane < 12) S.st[L.lane] = 0;
 #endif
-    const int b = 2 * blockIdx.x + L.e;
-    const bool valid = b < p.B;
-    const int bv = valid ? b : p.B - 1;
+    // the wave's two elements: 2 blockIdx + e, or a pair of elements with one layout (Bufs::pairs);
+    // an empty half runs on the other half's element, inactive
+    int b, bv;
+    bool valid;
+    if (p.elem_layout) {
+        const int e0 = d.pairs[2 * blockIdx.x], e1 = d.pairs[2 * blockIdx.x + 1];
+        b = L.e ? e1 : e0;
+        valid = b >= 0;
+        bv = valid ? b : (L.e ? e0 : e1);
+    } else {
+        b = 2 * blockIdx.x + L.e;
+        valid = b < p.B;
+        bv = valid ? b : p.B - 1;
+    }
     ElemState &E = d.el[bv];
     bool act = valid && !E.done && !E.inner_done;
     if (!__builtin_amdgcn_ballot_w64(act)) return;
@@ -805,7 +817,7 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
     }
 #if HSDDP_STAMPS
     SSYNC();
-    if (L.lane < 12) d.dbg[(size_t)(2 * blockIdx.x) * 16 + L.lane] += S.st[L.lane];
+    if (L.lane < 12) d.dbg[(size_t)__builtin_amdgcn_readfirstlane(bv) * 16 + L.lane] += S.st[L.lane];
 #endif
     if (act && L.pp == 0) {
         double cost, feas;
@@ -829,20 +841,24 @@ __global__ __launch_bounds__(64, 2) void k_riccati_retry(Params p, Bufs d)
     const Lane L = make_lane();
     zero_init(S, L.lane);
     const int n = min(*d.retry_count, p.retry_cap);
-    const int item = 2 * blockIdx.x + L.e, f = item / p.retry_m, a = item % p.retry_m + 1;
-    bool act = f < n;
+    // attempts a = 1 .. retry_m of deferred element f, padded to an even count so that a wave's two
+    // items always belong to one element (one layout)
+    const int mpad = p.retry_m + (p.retry_m & 1);
+    const int item = 2 * blockIdx.x + L.e, f = item / mpad, a = item % mpad + 1;
+    bool act = f < n && a <= p.retry_m;
     if (!__builtin_amdgcn_ballot_w64(act)) return;
-    const int fv = act ? f : 0;
+    const int fv = f < n ? f : 0;
     const RetryEntry e = d.retry_list[fv];
     double reg = e.reg;
     for (int t = 0; t < a; ++t) reg = fmax(reg * p.update_regularization, 1e-03);
-    int *flag = d.retry_flag + fv * p.retry_m + (a - 1);
+    const int av = a <= p.retry_m ? a : p.retry_m;  // a padding item addresses the last attempt's rows, inactive
+    int *flag = d.retry_flag + fv * p.retry_m + (av - 1);
     if (act && reg > 1e2) {  // past the loop's exit: never tried (the schedule is non-decreasing)
         if (L.pp == 0) *flag = 2;
         act = false;
     }
     if (!__builtin_amdgcn_ballot_w64(act)) return;
-    const size_t slot = (size_t)fv * p.retry_m + (a - 1);
+    const size_t slot = (size_t)fv * p.retry_m + (av - 1);
     Item<real> it;
     it.b = e.b;
     it.act = act;
@@ -911,13 +927,13 @@ __global__ __launch_bounds__(64) void k_riccati_select(Params p, Bufs d)
 void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
 {
     if (p.retry_cap > 0) (void)hipMemsetAsync(d.retry_count, 0, sizeof(int), st);
-    const dim3 g1((unsigned)((p.B + 1) / 2));
+    const dim3 g1((unsigned)(p.elem_layout ? p.n_pairs : (p.B + 1) / 2));
     if (p.fp32)
         hipLaunchKernelGGL(k_riccati<float>, g1, dim3(64), 0, st, p, d);
     else
         hipLaunchKernelGGL(k_riccati<double>, g1, dim3(64), 0, st, p, d);
     if (p.retry_cap > 0) {
-        const dim3 gr((unsigned)((p.retry_cap * p.retry_m + 1) / 2)), gs((unsigned)p.retry_cap);
+        const dim3 gr((unsigned)(p.retry_cap * (p.retry_m + (p.retry_m & 1)) / 2)), gs((unsigned)p.retry_cap);
         if (p.fp32) {
             hipLaunchKernelGGL(k_riccati_retry<float>, gr, dim3(64), 0, st, p, d);
             hipLaunchKernelGGL(k_riccati_select<float>, gs, dim3(64), 0, st, p, d);

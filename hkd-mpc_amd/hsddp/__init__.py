@@ -134,6 +134,15 @@ class Solver:
         h = C.c_void_p()
         check(L.hsddp_create(C.byref(desc), C.byref(h)))
         self._h = h
+        if prob.get("layouts") is not None:  # per-element phase layouts (largest layout = strides)
+            lays = prob["layouts"]
+            npz = np.array([len(x) for x in lays], np.int32)
+            hz = np.zeros((self.B, 16), np.int32)
+            for b, x in enumerate(lays):
+                hz[b, :len(x)] = x
+            check(L.hsddp_set_element_layouts(h, ip(npz), ip(hz)))
+            self.P = int(npz.max())
+            self.S = int(prob["S"])
         self.options = options if options is not None else load_settings()
         check(L.hsddp_set_options(h, C.byref(self.options)))
         if from_table:

@@ -104,7 +104,7 @@ EXPORTS = [
     "hsddp_shift", "hsddp_get_layout", "hsddp_update_problem", "hsddp_load_quad_reference",
     "hsddp_plan_phases", "hsddp_set_reference_table", "hsddp_build_references", "hsddp_download_references", "hsddp_advance",
     "hsddp_get_phase_info", "hsddp_hkd_running_cost", "hsddp_hkd_terminal_cost", "hsddp_hkd_grf_constraint",
-    "hsddp_hkd_touchdown_constraint",
+    "hsddp_hkd_touchdown_constraint", "hsddp_set_element_layouts",
 ]
 
 
@@ -156,6 +156,7 @@ def lib():
     L.hsddp_hkd_terminal_cost.argtypes = [V] * 4 + [C.POINTER(Weights), C.c_int] + [V] * 3 + [C.c_int, V]
     L.hsddp_hkd_grf_constraint.argtypes = [V, V, C.c_double, V, V, C.c_int, V]
     L.hsddp_hkd_touchdown_constraint.argtypes = [V, V, V, C.c_double, V, V, C.c_int, V]
+    L.hsddp_set_element_layouts.argtypes = [V, IP, IP]
     L.hsddp_device_alloc.restype = C.c_void_p
     L.hsddp_device_alloc.argtypes = [C.c_size_t, C.c_int]
     L.hsddp_device_free.argtypes = [C.c_void_p]

@@ -145,11 +145,22 @@ def initial_state(b: int, contact0, seed: int = SEED) -> np.ndarray:
 
 
 def make_batch(batch: int, n_phases: int = 4, knots: int = 50, gait: str = "trot",
-               mixed: bool = False, seed: int = SEED, dt: float = DT, first_element: int = 0) -> dict:
+               mixed: bool = False, seed: int = SEED, dt: float = DT, first_element: int = 0,
+               jump_layout: bool = False) -> dict:
     """Build a synthetic batch.  mixed=True draws a per-element gait.
 
     Element b of this batch is global element first_element + b (seed SEED + global index), so
-    shards of one global batch built on different ranks are disjoint and reproducible."""
+    shards of one global batch built on different ranks are disjoint and reproducible.
+    With mixed=True and jump_layout, jump elements run C4's 8 x 25 layout (twice the phases, half
+    the knots: the same Kc) beside the others' n_phases x knots — per-element layouts
+    (hsddp_set_element_layouts); otherwise every element is on n_phases x knots (jump running the
+    first n_phases phases of its cycle)."""
+    if mixed and jump_layout and knots % 2 == 0 and 2 * n_phases <= 16:
+        names = ["trot", "pace", "bound", "pronk", "jump"]
+        pick = (uniform_stream(seed ^ 0x5A5A, first_element + batch)[first_element:] * len(names)).astype(int)
+        gaits = [names[i] for i in pick]
+        lays = [(g, 2 * n_phases, knots // 2) if g == "jump" else (g, n_phases, knots) for g in gaits]
+        return make_layout_batch(lays, seed=seed, dt=dt, first_element=first_element)
     horizons = [knots] * n_phases
     S = sum(n + 1 for n in horizons)
     Kc = sum(horizons)
@@ -185,3 +196,59 @@ def make_batch(batch: int, n_phases: int = 4, knots: int = 50, gait: str = "trot
         "Xbar": Xbar, "Ubar": np.zeros((batch, Kc, 24)),
         "K": None,  # feedback gains default to zero on the device (3.8 GB as a host array at B=4096)
     }
+
+
+def make_layout_batch(layouts, seed: int = SEED, dt: float = DT, first_element: int = 0) -> dict:
+    """A batch whose elements have their own phase layouts: layouts[b] = (gait, n_phases, knots).
+    Every element's n_phases * knots must be equal (the handle's Kc).  Arrays use the largest
+    layout as the stride (include/hsddp.h, hsddp_set_element_layouts): contacts [B][Pmax+1][4]
+    (element b: rows 0 .. P_b), state-slot arrays [B][Smax][..] (element b: its first S_b rows)."""
+    batch = len(layouts)
+    hz = [[n] * p for _, p, n in layouts]
+    Kc = sum(hz[0])
+    if any(sum(h) != Kc for h in hz):
+        raise ValueError("every element's horizons must sum to the same Kc")
+    Pmax = max(len(h) for h in hz)
+    Smax = max(sum(n + 1 for n in h) for h in hz)
+    contacts = np.zeros((batch, Pmax + 1, 4), dtype=np.int32)
+    x0 = np.zeros((batch, 24))
+    ref_x = np.zeros((batch, Smax, 24)); ref_u = np.zeros((batch, Smax, 24)); ref_f = np.zeros((batch, Smax, 12))
+    refs = {}
+    for b, (g, P, n) in enumerate(layouts):
+        sched = phase_schedule(g, P)
+        contacts[b, :P + 1] = np.array(sched, dtype=np.int32)
+        x0[b] = initial_state(first_element + b, sched[0], seed)
+        if (g, P, n) not in refs:
+            refs[(g, P, n)] = _reference_slots(sched, [n] * P, dt)
+        rx, ru, rf = refs[(g, P, n)]
+        S_b = rx.shape[0]
+        ref_x[b, :S_b], ref_u[b, :S_b], ref_f[b, :S_b] = rx, ru, rf
+    return {
+        "batch": batch, "horizons": hz[0], "layouts": hz, "dt": dt, "S": Smax, "P": Pmax, "Kc": Kc,
+        "gaits": [g for g, _, _ in layouts], "contacts": contacts, "x0": x0, "ref_x": ref_x, "ref_u": ref_u,
+        "ref_foot": ref_f, "Xbar": ref_x.copy(), "Ubar": np.zeros((batch, Kc, 24)), "K": None,
+    }
+
+
+def layout_groups(prob: dict) -> dict:
+    """Elements of a per-element-layout batch grouped by layout: {tuple(horizons): [b, ...]}."""
+    out = {}
+    for b, h in enumerate(prob.get("layouts") or [prob["horizons"]] * prob["batch"]):
+        out.setdefault(tuple(h), []).append(b)
+    return out
+
+
+def sub_batch(prob: dict, elements, horizons) -> dict:
+    """The elements (all of one layout `horizons`) of a per-element-layout batch as an ordinary
+    batch of that layout (rows past its S and P dropped)."""
+    idx = list(elements)
+    P = len(horizons)
+    S = sum(n + 1 for n in horizons)
+    out = {"batch": len(idx), "horizons": list(horizons), "dt": prob["dt"], "S": S, "Kc": prob["Kc"],
+           "contacts": np.ascontiguousarray(prob["contacts"][idx, :P + 1]),
+           "x0": np.ascontiguousarray(prob["x0"][idx])}
+    for k in ("ref_x", "ref_u", "ref_foot", "Xbar"):
+        out[k] = np.ascontiguousarray(prob[k][idx, :S])
+    out["Ubar"] = np.ascontiguousarray(prob["Ubar"][idx])
+    out["K"] = None
+    return out

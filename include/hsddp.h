@@ -9,6 +9,7 @@
  *   hsddp_default_options / hsddp_options     HSDDP_OPTION            HSDDPSolver/common/HSDDP_CompoundTypes.h:18-60
  *   hsddp_load_settings                       loadHSDDPSetting        HSDDPSolver/common/HSDDP_CompoundTypes.h:62-87
  *   hsddp_load_constraint_params              loadConstrintParameters HKDMPC/HKD-TrajOpt/HKDProblem.h:70-90
+ *   hsddp_set_element_layouts                 HKDProblem::initialization's per-problem phase segmentation HKDProblem.cpp:40-68
  *   hsddp_create (+ problem descriptor)       HKDProblem::initialization/create_problem_one_phase/
  *                                             add_tconstr_one_phase   HKDMPC/HKD-TrajOpt/HKDProblem.cpp:15-111,225-310
  *                                             MultiPhaseDDP::set_multiPhaseProblem  MultiPhaseDDP.h:374-382
@@ -162,6 +163,17 @@ int hsddp_set_options(hsddp_handle h, const hsddp_options *opt);
  * iteration budgets, update_regularization > 1 with at most HSDDP_MAX_REG_ATTEMPTS retries from
  * mu = 0 to mu > 1e2.  The reference accepts any factor and spins forever on a factor <= 1. */
 int hsddp_validate_options(const hsddp_options *opt);
+
+/* Per-element phase layouts (HKDProblem::initialization segments each problem's horizon by its own
+ * gait, HKDProblem.cpp:40-68): element b has n_phases[b] phases of horizons[b][0 .. n_phases[b]-1]
+ * knots (horizons is [B][HSDDP_MAX_PHASES]); every element's horizons must sum to the handle's Kc
+ * (sum of desc->horizons).  Afterwards the per-element arrays of the solver API use the largest
+ * layout as their stride: contacts [B][Pmax+1][4] (element b: rows 0 .. n_phases[b], row
+ * n_phases[b] = the contact after its horizon), state-slot arrays [B][Smax][..] (element b: its
+ * first S_b = Kc + n_phases[b] rows), per-phase arrays [B][Pmax][..]; the problem must be uploaded
+ * again.  The MPC-side steps (hsddp_shift, _advance, _build_references, _extract_commands) keep
+ * requiring the shared layout. */
+int hsddp_set_element_layouts(hsddp_handle h, const int *n_phases, const int *horizons);
 
 /* contacts int32 [B][P+1][4] (row P: contact after the horizon, for the last phase's touchdown
  * constraint); x0 [B][24]; ref_x, ref_u [Bref][S][24]; ref_foot [Bref][S][12]. */

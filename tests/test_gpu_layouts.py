@@ -1,0 +1,104 @@
+"""Per-element phase layouts (hsddp_set_element_layouts): one handle whose elements segment the same
+Kc knots into their own phases, as HKDProblem::initialization does per problem (HKDProblem.cpp:
+40-68) — here trot-like gaits on n x N beside jumps on 2n x N/2.
+
+Each element of a mixed handle must be solved exactly as in a handle of its own layout: the mixed
+solve is compared bit for bit with uniform-layout solves of the same elements (same kernels, same
+arithmetic — the layout only changes which slots and phases a kernel visits and how the sweep
+pairs elements), and a sample against the oracle."""
+import numpy as np
+import pytest
+
+import hsddp
+import oracle_lib as O
+from hsddp import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(1e-300, np.max(np.abs(b))))
+
+
+def _mixed(B, P=4, N=10, seed=syn.SEED):
+    names = ["trot", "jump", "pace", "jump", "bound", "pronk", "jump"]
+    lays = [(g, 2 * P, N // 2) if g == "jump" else (g, P, N) for g in (names[b % len(names)] for b in range(B))]
+    return syn.make_layout_batch(lays, seed=seed)
+
+
+def _run(prob, opt, weights=None, **kw):
+    s = hsddp.Solver(prob, opt, weights=weights, **kw)
+    s.solve()
+    out = {**s.trajectory(), **s.working(), **s.element_info()}
+    out["lq"], out["term"] = s.lq(), s.terminal()
+    s.close()
+    return out
+
+
+def _check_against_uniform(prob, opt, weights=None):
+    g = _run(prob, opt, weights)
+    for hz, idx in syn.layout_groups(prob).items():
+        sub = syn.sub_batch(prob, idx, hz)
+        u = _run(sub, opt, weights)
+        S, P = sub["S"], len(hz)
+        for f in ("Xbar", "X", "Defect", "dX"):
+            assert np.array_equal(g[f][idx, :S], u[f]), (hz, f)
+        for f in ("Ubar", "U", "dU", "K"):
+            assert np.array_equal(g[f][idx], u[f]), (hz, f)
+        for f in ("cost", "feas", "merit", "max_tconstr", "max_pconstr", "iters", "outer_iters", "status", "n_ls_trials"):
+            assert np.array_equal(g[f][idx], u[f]), (hz, f)
+        for f in ("A", "B", "lx", "lu", "lxx", "luu", "l"):
+            assert np.array_equal(g["lq"][f][idx], u["lq"][f]), (hz, f)
+        for f in ("Phi", "Phix", "Phixx", "Px"):
+            assert np.array_equal(g["term"][f][idx, :P], u["term"][f]), (hz, f)
+            assert np.all(g["term"][f][idx, P:] == 0), (hz, f)
+    return g
+
+
+@pytest.mark.parametrize("B", [7, 24])
+def test_mixed_layouts_equal_uniform_handles_fixed_iterations(B):
+    prob = _mixed(B)
+    opt = hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=3)
+    g = _check_against_uniform(prob, opt)
+    # and against the oracle, per layout
+    for hz, idx in syn.layout_groups(prob).items():
+        sub = syn.sub_batch(prob, idx, hz)
+        r = O.solve_batch(sub, O.default_options(no_early_exit=1, max_AL_iter=1, max_DDP_iter=3), n_threads=8)
+        S = sub["S"]
+        assert np.array_equal(g["n_ls_trials"][idx], r["n_ls_trials"])
+        for f in ("Xbar", "Ubar", "K"):
+            a = g[f][idx, :S] if f == "Xbar" else g[f][idx]
+            assert rel(a, r[f]) < 1e-9, (hz, f)
+
+
+def test_mixed_layouts_full_solve_equal_uniform_handles():
+    """The reference loop with its early exits (default settings): per-element exits differ
+    between layouts inside one handle."""
+    _check_against_uniform(_mixed(21), hsddp.load_settings())
+
+
+def test_mixed_layouts_regularisation_retries(monkeypatch):
+    """Every first sweep fails (r_qJd < 0, test_gpu_parity.py::test_retries_match_oracle): the
+    parallel retries of a mixed handle pair attempts of one element per wave; the result equals
+    the uniform handles' and the sequential loop's."""
+    w = hsddp.Weights()
+    hsddp.lib().hsddp_default_weights(__import__("ctypes").byref(w))
+    w.r_qJd = -0.5
+    prob = _mixed(9)
+    opt = hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=2)
+    g = _check_against_uniform(prob, opt, w)
+    monkeypatch.setenv("HSDDP_SEQUENTIAL_RETRY", "1")
+    q = _run(prob, opt, w)
+    for f in ("Xbar", "Ubar", "K", "dU", "cost", "status", "n_ls_trials"):
+        assert np.array_equal(g[f], q[f]), f
+
+
+def test_layouts_validation():
+    prob = _mixed(4)
+    bad = dict(prob, layouts=[[10, 10, 10, 10], [5] * 8, [10, 10, 10, 9], [10] * 4])
+    with pytest.raises(hsddp.HSDDPError, match="Kc"):
+        hsddp.Solver(bad, hsddp.load_settings())
+    s = hsddp.Solver(prob, hsddp.load_settings())
+    with pytest.raises(hsddp.HSDDPError, match="shared layout"):
+        s.shift([0])
+    s.close()
