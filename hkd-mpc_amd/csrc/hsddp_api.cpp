@@ -242,6 +242,7 @@ struct hsddp_handle_t {
     float *hist = nullptr;  // solver-info history [B][p.hcap][4] (grown by ensure_history)
     // per-element layouts (hsddp_set_element_layouts): host copies of Bufs::lay; empty = the handle's
     std::vector<Layout> lays;
+    std::vector<int> reach_el;  // [B][16] is_phase_reach_end per element (with per-element layouts)
     double *value0 = nullptr;  // G[0], H[0] per phase [B][16][600] (hsddp_set_value_export)
 };
 
@@ -517,33 +518,20 @@ extern "C" int hsddp_set_options(hsddp_handle h, const hsddp_options *o)
     return ensure_history(h);
 }
 
-extern "C" int hsddp_set_element_layouts(hsddp_handle h, const int *n_phases, const int *horizons)
+// install per-element layouts: device records, sweep pairs (equal layouts share a wave), strides
+static int set_layouts(hsddp_handle h, const std::vector<Layout> &lays)
 {
-    if (!h || !n_phases || !horizons) return fail(HSDDP_ERR_ARG, "null argument");
     Params &p = h->p;
     const int B = p.B;
-    std::vector<Layout> lays(B);
-    int Pmax = 0, Smax = 0;
-    for (int b = 0; b < B; ++b) {
-        Layout &L = lays[b];
-        L = Layout{};
-        L.P = n_phases[b];
-        if (L.P < 1 || L.P > HSDDP_MAX_PHASES) return fail(HSDDP_ERR_ARG, "element n_phases must lie in 1..16");
-        int s = 0, k = 0;
-        for (int i = 0; i < L.P; ++i) {
-            const int N = horizons[(size_t)b * HSDDP_MAX_PHASES + i];
-            if (N < 1) return fail(HSDDP_ERR_ARG, "phase horizons must be >= 1");
-            L.N[i] = N; L.s0[i] = s; L.k0[i] = k; L.ss[i] = N + 1;
-            s += N + 1; k += N;
-        }
-        if (k != p.Kc) return fail(HSDDP_ERR_ARG, "every element's horizons must sum to the handle's Kc");
-        L.S = s;
-        Pmax = std::max(Pmax, L.P);
-        Smax = std::max(Smax, L.S);
-    }
-    // the sweep runs two elements per wave in lockstep: pair elements of equal layouts
+    int Pmax = 0, Smax = 0, tail = 0;
+    for (auto &L : lays) { Pmax = std::max(Pmax, L.P); Smax = std::max(Smax, L.S); tail |= L.has_tail; }
     std::map<std::vector<int>, std::vector<int>> groups;
-    for (int b = 0; b < B; ++b) groups[std::vector<int>(lays[b].N, lays[b].N + lays[b].P)].push_back(b);
+    for (int b = 0; b < B; ++b) {
+        std::vector<int> key(lays[b].N, lays[b].N + lays[b].P);
+        key.push_back(-1);
+        key.insert(key.end(), lays[b].ss, lays[b].ss + lays[b].P);
+        groups[key].push_back(b);
+    }
     std::vector<int> pairs;
     for (auto &g : groups)
         for (size_t j = 0; j < g.second.size(); j += 2) {
@@ -558,12 +546,57 @@ extern "C" int hsddp_set_element_layouts(hsddp_handle h, const int *n_phases, co
     p.n_pairs = (int)pairs.size() / 2;
     p.P = Pmax;  // strides of the per-phase and per-slot buffers
     p.S = Smax;
-    p.has_tail = 0;
-    for (int i = 0; i < Pmax; ++i) { p.N[i] = 0; p.s0[i] = 0; p.k0[i] = 0; p.ss[i] = 0; }
-    h->reach_end.assign(Pmax, 0);
+    p.has_tail = tail;
+    for (int i = 0; i < HSDDP_MAX_PHASES; ++i) { p.N[i] = 0; p.s0[i] = 0; p.k0[i] = 0; p.ss[i] = 0; }
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_set_element_layouts(hsddp_handle h, const int *n_phases, const int *horizons)
+{
+    if (!h || !n_phases || !horizons) return fail(HSDDP_ERR_ARG, "null argument");
+    Params &p = h->p;
+    const int B = p.B;
+    std::vector<Layout> lays(B);
+    for (int b = 0; b < B; ++b) {
+        Layout &L = lays[b];
+        L = Layout{};
+        L.P = n_phases[b];
+        if (L.P < 1 || L.P > HSDDP_MAX_PHASES) return fail(HSDDP_ERR_ARG, "element n_phases must lie in 1..16");
+        int s = 0, k = 0;
+        for (int i = 0; i < L.P; ++i) {
+            const int N = horizons[(size_t)b * HSDDP_MAX_PHASES + i];
+            if (N < 1) return fail(HSDDP_ERR_ARG, "phase horizons must be >= 1");
+            L.N[i] = N; L.s0[i] = s; L.k0[i] = k; L.ss[i] = N + 1;
+            s += N + 1; k += N;
+        }
+        if (k != p.Kc) return fail(HSDDP_ERR_ARG, "every element's horizons must sum to the handle's Kc");
+        L.S = s;
+    }
+    int rc = set_layouts(h, lays);
+    if (rc) return rc;
+    h->reach_el.assign((size_t)B * HSDDP_MAX_PHASES, 0);  // HKDProblem.cpp:56-57 (quirk A15)
     h->have_problem = false;  // inputs of the new layouts next (hsddp_upload_problem)
     h->contacts_current = false;
     h->refs_on_device = false;
+    return HSDDP_OK;
+}
+
+// the layout of every element: n_phases [B], horizons / shooting / reach_end [B][16] (any NULL)
+extern "C" int hsddp_get_element_layouts(hsddp_handle h, int *n_phases, int *horizons, int *shooting, int *reach_end)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    for (size_t b = 0; b < (size_t)h->p.B; ++b) {
+        const Layout L = layout_of(h, b);
+        if (n_phases) n_phases[b] = L.P;
+        for (int i = 0; i < HSDDP_MAX_PHASES; ++i) {
+            const bool in = i < L.P;
+            if (horizons) horizons[b * HSDDP_MAX_PHASES + i] = in ? L.N[i] : 0;
+            if (shooting) shooting[b * HSDDP_MAX_PHASES + i] = in ? L.ss[i] : 0;
+            if (reach_end)
+                reach_end[b * HSDDP_MAX_PHASES + i] =
+                    in ? (h->lays.empty() ? h->reach_end[i] : h->reach_el[b * HSDDP_MAX_PHASES + i]) : 0;
+        }
+    }
     return HSDDP_OK;
 }
 
@@ -582,6 +615,8 @@ static int upload_inputs(hsddp_handle h, const int *contacts, const double *x0, 
     if (!keep_refs && (!ref_x || !ref_u || !ref_foot)) return fail(HSDDP_ERR_ARG, "references: all three or none");
     if (keep_refs && !h->refs_on_device)
         return fail(HSDDP_ERR_ARG, "no device references for this layout (hsddp_build_references)");
+    if (!h->lays.empty() && h->Bref == 1 && h->p.B > 1)  // a shared reference is laid out for one layout
+        return fail(HSDDP_ERR_ARG, "per-element layouts need per-element references (desc.ref_per_element = 1)");
     HIPCHK(hipSetDevice(h->desc.device));
     const Params &p = h->p;
     const size_t B = p.B, S = p.S, P = p.P, Br = h->Bref;
@@ -1354,21 +1389,20 @@ struct ShiftPhase {
 };
 }  // namespace
 
-extern "C" int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_change)
+// HKDProblem::update's phase bookkeeping (HKDProblem.cpp:117-222) of one layout for n_steps steps,
+// step j with contact-change flag cc[j * cstride]: the phases afterwards, each with the old slots
+// its new slots come from (labels: >= 0 old slot, -2 - s old X row s, -1 zero)
+static int shift_phases(const Layout &L, const int *reach, int n_steps, const int *cc, size_t cstride,
+                        std::vector<ShiftPhase> &ph)
 {
-    if (h && !h->lays.empty())
-        return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts (hsddp_set_element_layouts): the MPC-side steps need the handle's shared layout");
-    if (!h || (n_steps > 0 && !contact_change)) return fail(HSDDP_ERR_ARG, "null argument");
-    if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
-    if (n_steps < 0) return fail(HSDDP_ERR_ARG, "n_steps must be >= 0");
-    Params &p = h->p;
-    std::vector<ShiftPhase> ph(p.P);
-    for (int i = 0; i < p.P; ++i) {
-        ph[i].N = p.N[i]; ph[i].ss = p.ss[i]; ph[i].reach = h->reach_end[i];
-        for (int k = 0; k <= p.N[i]; ++k) ph[i].xs.push_back(p.s0[i] + k);
-        for (int k = 0; k < p.N[i]; ++k) ph[i].us.push_back(p.k0[i] + k);
+    ph.assign(L.P, ShiftPhase{});
+    for (int i = 0; i < L.P; ++i) {
+        ph[i].N = L.N[i]; ph[i].ss = L.ss[i]; ph[i].reach = reach[i];
+        for (int k = 0; k <= L.N[i]; ++k) ph[i].xs.push_back(L.s0[i] + k);
+        for (int k = 0; k < L.N[i]; ++k) ph[i].us.push_back(L.k0[i] + k);
     }
     for (int j = 0; j < n_steps; ++j) {
+        const int change = cc[(size_t)j * cstride];
         // front: a first phase of one knot shrinks to a point and is removed (pop_front_phase,
         // HKDProblem.h:56-66); otherwise its first knot is dropped (SinglePhase::pop_front,
         // SinglePhase.cpp:496-501)
@@ -1386,7 +1420,7 @@ extern "C" int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_chang
         // push_back_default: X.back() copied into X and Xbar, zero control and gain
         // (SinglePhase.cpp:485-490, TrajectoryManagement.cpp:163-190)
         ShiftPhase &l = ph.back();
-        if (contact_change[j] && l.reach) {
+        if (change && l.reach) {
             if ((int)ph.size() >= HSDDP_MAX_PHASES) return fail(HSDDP_ERR_ARG, "shift exceeds HSDDP_MAX_PHASES phases");
             ShiftPhase n;
             n.N = 1; n.ss = 0; n.reach = 0;
@@ -1398,7 +1432,7 @@ extern "C" int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_chang
             l.xs.push_back(last >= 0 ? -2 - last : last);
             l.us.push_back(-1);
             l.N++;
-            if (contact_change[j]) l.reach = 1;
+            if (change) l.reach = 1;
         }
     }
     // update_SS_config after the steps (HKDProblem.cpp:203-217): every phase but a last one of
@@ -1408,16 +1442,71 @@ extern "C" int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_chang
         if (i < P - 1 || ph[i].N > 2) ph[i].ss = ph[i].N + 1;
     for (int i = 0; i < P - 1; ++i)
         if (ph[i].ss < ph[i].N + 1) return fail(HSDDP_ERR_UNSUPPORTED, "non-shooting states outside the last phase");
-    std::vector<int> smap, cmap;
-    for (auto &f : ph) {
-        smap.insert(smap.end(), f.xs.begin(), f.xs.end());
-        cmap.insert(cmap.end(), f.us.begin(), f.us.end());
+    return HSDDP_OK;
+}
+
+// the receding-horizon shift of every element: cc[b * bstride + j * sstride] is element b's flag of
+// step j.  Elements with equal (layout, reach flags, step flags) share one slot map; when every
+// element ends on one layout the handle keeps (or returns to) the shared layout.
+static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride, size_t sstride)
+{
+    if (!h || (n_steps > 0 && !cc)) return fail(HSDDP_ERR_ARG, "null argument");
+    if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
+    if (n_steps < 0) return fail(HSDDP_ERR_ARG, "n_steps must be >= 0");
+    Params &p = h->p;
+    const size_t B = p.B;
+    const bool elem = !h->lays.empty();
+    // per unique key: the new phases and slot maps
+    std::map<std::vector<int>, int> keys;
+    std::vector<std::vector<ShiftPhase>> phs;
+    std::vector<int> map_id(B);
+    for (size_t b = 0; b < B; ++b) {
+        const Layout L = layout_of(h, b);
+        const int *reach = elem ? &h->reach_el[b * HSDDP_MAX_PHASES] : h->reach_end.data();
+        std::vector<int> key(L.N, L.N + L.P);
+        key.push_back(-1);
+        key.insert(key.end(), L.ss, L.ss + L.P);
+        key.insert(key.end(), reach, reach + L.P);
+        for (int j = 0; j < n_steps; ++j) key.push_back(cc[b * bstride + j * sstride]);
+        auto it = keys.find(key);
+        if (it == keys.end()) {
+            std::vector<ShiftPhase> ph;
+            int rc = shift_phases(L, reach, n_steps, cc + b * bstride, sstride, ph);
+            if (rc) return rc;
+            it = keys.emplace(key, (int)phs.size()).first;
+            phs.push_back(ph);
+        }
+        map_id[b] = it->second;
     }
-    if (smap.size() > h->S_cap || (int)cmap.size() != p.Kc)
-        return fail(HSDDP_ERR_ARG, "shifted layout exceeds the handle's capacity");
+    const int nk = (int)phs.size();
+    std::vector<Layout> nl(nk);
+    int Snew = 0, Pnew = 0;
+    for (int q = 0; q < nk; ++q) {
+        Layout &L = nl[q];
+        L = Layout{};
+        L.P = (int)phs[q].size();
+        int s = 0, k = 0;
+        for (int i = 0; i < L.P; ++i) {
+            L.N[i] = phs[q][i].N; L.s0[i] = s; L.k0[i] = k; L.ss[i] = phs[q][i].ss;
+            s += L.N[i] + 1; k += L.N[i];
+            if (L.ss[i] < L.N[i] + 1) L.has_tail = 1;
+        }
+        L.S = s;
+        if (k != p.Kc || (size_t)s > h->S_cap) return fail(HSDDP_ERR_ARG, "shifted layout exceeds the handle's capacity");
+        Snew = std::max(Snew, s);
+        Pnew = std::max(Pnew, L.P);
+    }
+    // slot maps [nk][Snew] (padding rows: zero) and [nk][Kc]
+    std::vector<int> smap((size_t)nk * Snew, -1), cmap((size_t)nk * p.Kc);
+    for (int q = 0; q < nk; ++q) {
+        size_t s = 0, k = 0;
+        for (auto &f : phs[q]) {
+            for (int v : f.xs) smap[(size_t)q * Snew + s++] = v;
+            for (int v : f.us) cmap[(size_t)q * p.Kc + k++] = v;
+        }
+    }
     HIPCHK(hipSetDevice(h->desc.device));
     Bufs &d = h->d;
-    const size_t B = p.B;
     int rc;
     if (!h->spare_Xbar) {
         double *sx, *su;
@@ -1428,14 +1517,16 @@ extern "C" int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_chang
         h->spare_Xbar = sx; h->spare_Ubar = su; h->spare_K = sk;
     }
     char *buf;
-    if ((rc = scratch(h, (smap.size() + cmap.size()) * sizeof(int), &buf))) return rc;
-    int *dsm = (int *)buf, *dcm = dsm + smap.size();
+    if ((rc = scratch(h, (smap.size() + cmap.size() + (nk > 1 ? B : 0)) * sizeof(int), &buf))) return rc;
+    int *dsm = (int *)buf, *dcm = dsm + smap.size(), *did = dcm + cmap.size();
     if ((rc = h2d(dsm, smap.data(), smap.size() * sizeof(int), h->stream)) ||
-        (rc = h2d(dcm, cmap.data(), cmap.size() * sizeof(int), h->stream)))
+        (rc = h2d(dcm, cmap.data(), cmap.size() * sizeof(int), h->stream)) ||
+        (nk > 1 && (rc = h2d(did, map_id.data(), B * sizeof(int), h->stream))))
         return rc;
     ShiftArgs a;
-    a.S_old = p.S; a.S_new = (int)smap.size(); a.Kc = p.Kc;
+    a.S_old = p.S; a.S_new = Snew; a.Kc = p.Kc;
     a.smap = dsm; a.cmap = dcm;
+    a.map_id = nk > 1 ? did : nullptr;
     a.fp32 = p.fp32;
     a.zero_u0 = 1;  // trajectory_ptrs.front()->Ubar[0].setZero() (HKDProblem.cpp:219)
     launch_shift_gather(p.B, a, d, h->spare_Xbar, h->spare_Ubar, h->spare_K, h->stream);
@@ -1445,29 +1536,52 @@ extern "C" int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_chang
     std::swap(d.Ubar, h->spare_Ubar);
     if (p.fp32) { float *t = d.K32; d.K32 = (float *)h->spare_K; h->spare_K = t; }
     else { double *t = d.K; d.K = (double *)h->spare_K; h->spare_K = t; }
-    // the new layout
-    p.P = P;
-    int s = 0, k = 0;
-    p.has_tail = 0;
-    h->reach_end.resize(P);
-    for (int i = 0; i < P; ++i) {
-        p.N[i] = ph[i].N; p.s0[i] = s; p.k0[i] = k; p.ss[i] = ph[i].ss;
-        s += p.N[i] + 1; k += p.N[i];
-        h->reach_end[i] = ph[i].reach;
-        if (p.ss[i] < p.N[i] + 1) p.has_tail = 1;
+    // the new layouts
+    if (nk == 1) {  // one layout for the batch: the handle's own
+        const Layout &L = nl[0];
+        p.P = L.P;
+        p.has_tail = L.has_tail;
+        h->reach_end.resize(L.P);
+        for (int i = 0; i < L.P; ++i) {
+            p.N[i] = L.N[i]; p.s0[i] = L.s0[i]; p.k0[i] = L.k0[i]; p.ss[i] = L.ss[i];
+            h->reach_end[i] = phs[0][i].reach;
+        }
+        p.S = L.S;
+        p.elem_layout = 0;
+        h->lays.clear();
+        h->reach_el.clear();
+        h->desc.n_phases = L.P;
+        for (int i = 0; i < L.P; ++i) h->desc.horizons[i] = L.N[i];
+    } else {
+        std::vector<Layout> lays(B);
+        std::vector<int> reach(B * HSDDP_MAX_PHASES, 0);
+        for (size_t b = 0; b < B; ++b) {
+            lays[b] = nl[map_id[b]];
+            for (int i = 0; i < lays[b].P; ++i) reach[b * HSDDP_MAX_PHASES + i] = phs[map_id[b]][i].reach;
+        }
+        if ((rc = set_layouts(h, lays))) return rc;
+        h->reach_el = reach;
     }
-    p.S = s;
-    h->desc.n_phases = P;
-    for (int i = 0; i < P; ++i) h->desc.horizons[i] = p.N[i];
     h->need_inputs = true;
     h->refs_on_device = false;  // built for the old layout
     h->contacts_current = false;
     return HSDDP_OK;
 }
 
+extern "C" int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_change)
+{
+    return shift_impl(h, n_steps, contact_change, 0, 1);
+}
+
+extern "C" int hsddp_shift_elements(hsddp_handle h, int n_steps, const int *contact_change)
+{
+    return shift_impl(h, n_steps, contact_change, h ? (size_t)n_steps : 0, 1);
+}
+
 extern "C" int hsddp_get_layout(hsddp_handle h, int *n_phases, int *horizons, int *shooting, int *reach_end)
 {
     if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    if (!h->lays.empty()) return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts: hsddp_get_element_layouts");
     const Params &p = h->p;
     if (n_phases) *n_phases = p.P;
     for (int i = 0; i < p.P; ++i) {

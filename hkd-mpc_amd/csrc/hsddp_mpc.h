@@ -22,7 +22,8 @@ struct CmdArgs {
 // receding-horizon gather: new slot <- old slot (labels as hsddp_api.cpp ShiftPhase)
 struct ShiftArgs {
     int S_old, S_new, Kc;
-    const int *smap, *cmap;   // [S_new], [Kc] device
+    const int *smap, *cmap;   // [n_maps][S_new], [n_maps][Kc] device
+    const int *map_id;        // [B] map of each element (null: one map for the batch)
     int fp32, zero_u0;
 };
 void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, double *Xbar_new, double *Ubar_new, void *K_new,

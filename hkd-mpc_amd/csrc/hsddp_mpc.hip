@@ -86,8 +86,10 @@ __global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, const 
     if (gid >= (long)B * per) return;
     const long b = gid / per;
     long e = gid % per;
+    const int m = a.map_id ? a.map_id[b] : 0;
+    const int *smap = a.smap + (size_t)m * a.S_new, *cmap = a.cmap + (size_t)m * a.Kc;
     if (e < nx) {
-        const int s = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = a.smap[s];
+        const int s = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = smap[s];
         double2 v = {0.0, 0.0};
         if (lab >= 0) v = *(const double2 *)&Xbar[(b * a.S_old + lab) * NX + j];
         else if (lab <= -2) v = *(const double2 *)&X[(b * a.S_old + (-2 - lab)) * NX + j];
@@ -96,14 +98,14 @@ __global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, const 
     }
     e -= nx;
     if (e < nu) {
-        const int k = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = a.cmap[k];
+        const int k = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = cmap[k];
         double2 v = {0.0, 0.0};
         if (lab >= 0 && !(a.zero_u0 && k == 0)) v = *(const double2 *)&Ubar[(b * a.Kc + lab) * NX + j];
         *(double2 *)&Un[(b * nu + e) * 2] = v;
         return;
     }
     e -= nu;
-    const int k = (int)(KV * e / KCW), j = (int)(KV * e % KCW), lab = a.cmap[k];
+    const int k = (int)(KV * e / KCW), j = (int)(KV * e % KCW), lab = cmap[k];
     float4 v = {0.f, 0.f, 0.f, 0.f};
     if (lab >= 0) v = *(const float4 *)&K[((long)b * a.Kc + lab) * KCW + j];
     *(float4 *)&Kn[(b * nk + e) * KV] = v;

@@ -284,6 +284,24 @@ class Solver:
         return {"ref_x": rx, "ref_u": ru, "ref_foot": rf}
 
     # -- receding horizon (HKDProblem::update, HKDProblem.cpp:117-222) ------------------------
+    def shift_elements(self, contact_change) -> dict:
+        """hsddp_shift_elements: contact_change [B][n_steps], each element's own flags; returns the
+        per-element layouts afterwards (element_layouts)."""
+        cc = np.ascontiguousarray(contact_change, dtype=np.int32).reshape(self.B, -1)
+        check(lib().hsddp_shift_elements(self._h, int(cc.shape[1]), ip(cc)))
+        lay = self.element_layouts()
+        self.P = int(lay["n_phases"].max())
+        self.S = int(max(self.Kc + P for P in lay["n_phases"]))
+        return lay
+
+    def element_layouts(self) -> dict:
+        n = np.zeros(self.B, np.int32)
+        hz, ss, re = (np.zeros((self.B, 16), np.int32) for _ in range(3))
+        check(lib().hsddp_get_element_layouts(self._h, ip(n), ip(hz), ip(ss), ip(re)))
+        return {"n_phases": n, "horizons": [list(hz[b, :n[b]]) for b in range(self.B)],
+                "shooting": [list(ss[b, :n[b]]) for b in range(self.B)],
+                "reach_end": [list(re[b, :n[b]]) for b in range(self.B)]}
+
     def layout(self) -> dict:
         n = C.c_int()
         hz, ss, re = (C.c_int * 16)(), (C.c_int * 16)(), (C.c_int * 16)()
@@ -296,6 +314,11 @@ class Solver:
         returns the new layout.  Call update_problem with inputs of that layout before solving."""
         cc = np.ascontiguousarray(np.asarray(contact_change, dtype=np.int32).reshape(-1))
         check(lib().hsddp_shift(self._h, int(cc.size), ip(cc)))
+        el = self.element_layouts()
+        if any(h != el["horizons"][0] for h in el["horizons"]):  # per-element layouts
+            self.P = int(el["n_phases"].max())
+            self.S = int(max(self.Kc + P for P in el["n_phases"]))
+            return el
         lay = self.layout()
         self.P = len(lay["horizons"])
         self.S = sum(n + 1 for n in lay["horizons"])

@@ -105,6 +105,7 @@ EXPORTS = [
     "hsddp_plan_phases", "hsddp_set_reference_table", "hsddp_build_references", "hsddp_download_references", "hsddp_advance",
     "hsddp_get_phase_info", "hsddp_hkd_running_cost", "hsddp_hkd_terminal_cost", "hsddp_hkd_grf_constraint",
     "hsddp_hkd_touchdown_constraint", "hsddp_set_element_layouts",
+    "hsddp_shift_elements", "hsddp_get_element_layouts",
 ]
 
 
@@ -157,6 +158,8 @@ def lib():
     L.hsddp_hkd_grf_constraint.argtypes = [V, V, C.c_double, V, V, C.c_int, V]
     L.hsddp_hkd_touchdown_constraint.argtypes = [V, V, V, C.c_double, V, V, C.c_int, V]
     L.hsddp_set_element_layouts.argtypes = [V, IP, IP]
+    L.hsddp_shift_elements.argtypes = [V, C.c_int, IP]
+    L.hsddp_get_element_layouts.argtypes = [V, IP, IP, IP, IP]
     L.hsddp_device_alloc.restype = C.c_void_p
     L.hsddp_device_alloc.argtypes = [C.c_size_t, C.c_int]
     L.hsddp_device_free.argtypes = [C.c_void_p]

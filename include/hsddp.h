@@ -283,11 +283,21 @@ int hsddp_download_references(hsddp_handle h, double *ref_x, double *ref_u, doub
  * phase with a zero trajectory is appended.  Afterwards Ubar of the first knot is zeroed and every
  * phase gets all its states as shooting states except a last phase of horizon <= 2, which keeps its
  * set (empty for a new phase; its states are then simulated, SinglePhase.cpp:185-222).  The total
- * number of control knots is unchanged.  The layout (phases, horizons) is shared by the batch.
+ * number of control knots is unchanged.  The flags are shared by the batch (hsddp_shift_elements:
+ * per element).
  * After a shift, hsddp_update_problem must upload contacts / x0 / references of the new layout
  * before the next solve. */
 int hsddp_shift(hsddp_handle h, int n_steps, const int *contact_change);
-/* current layout: n_phases, horizons[16], shooting states[16], is_phase_reach_end[16] (any NULL) */
+/* hsddp_shift with a contact-change flag per element and step: contact_change [B][n_steps].  Each
+ * element's phases evolve by its own flags (robots crossing contact boundaries at different
+ * knots), so the handle moves to per-element layouts (as hsddp_set_element_layouts) unless every
+ * element ends on the same one; hsddp_shift on such a handle shifts every element by the shared
+ * flags from its own layout. */
+int hsddp_shift_elements(hsddp_handle h, int n_steps, const int *contact_change);
+/* every element's layout: n_phases [B], horizons, shooting states, is_phase_reach_end [B][16] (any NULL) */
+int hsddp_get_element_layouts(hsddp_handle h, int *n_phases, int *horizons, int *shooting, int *reach_end);
+/* current layout: n_phases, horizons[16], shooting states[16], is_phase_reach_end[16] (any NULL);
+ * HSDDP_ERR_UNSUPPORTED with per-element layouts (hsddp_get_element_layouts) */
 int hsddp_get_layout(hsddp_handle h, int *n_phases, int *horizons, int *shooting, int *reach_end);
 /* as hsddp_upload_problem, but keeps the warm start Xbar / Ubar / K (the MPC update's reuse of the
  * previous solution); resets X = Xbar, U = Ubar and the ReB / AL parameters (reset_params) */

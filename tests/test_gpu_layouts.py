@@ -99,6 +99,71 @@ def test_layouts_validation():
     with pytest.raises(hsddp.HSDDPError, match="Kc"):
         hsddp.Solver(bad, hsddp.load_settings())
     s = hsddp.Solver(prob, hsddp.load_settings())
+    s.solve()
     with pytest.raises(hsddp.HSDDPError, match="shared layout"):
-        s.shift([0])
+        s.extract_commands()
     s.close()
+
+
+def _inputs(gaits, horizons_list, offset, Pmax, Smax, B):
+    """contacts / references of each element's (possibly new) layout: the gait's schedule from
+    phase `offset`, the closed-form references on that layout."""
+    contacts = np.zeros((B, Pmax + 1, 4), np.int32)
+    rx = np.zeros((B, Smax, 24)); ru = np.zeros((B, Smax, 24)); rf = np.zeros((B, Smax, 12))
+    for b, (g, hz) in enumerate(zip(gaits, horizons_list)):
+        sched = syn.phase_schedule(g, len(hz), offset)
+        contacts[b, :len(hz) + 1] = sched
+        x, u, f = syn._reference_slots(sched, hz, t0=offset)
+        S = x.shape[0]
+        rx[b, :S], ru[b, :S], rf[b, :S] = x, u, f
+    return contacts, rx, ru, rf
+
+
+def test_shift_elements_equals_uniform_shifts():
+    """hsddp_shift_elements: robots crossing contact boundaries at different knots.  Group A's flags
+    add a phase (the first change marks the last phase's end, the second starts a new phase), group
+    B's only grow the last phase; each group must end exactly as a uniform handle of its elements
+    shifted by hsddp_shift with its flags — warm start after the shift, then a re-solve."""
+    B, P, N = 7, 4, 10
+    prob = syn.make_batch(B, P, N, "trot")
+    for k in ("ref_x", "ref_u", "ref_foot"):  # per-element references (the layouts diverge)
+        prob[k] = np.ascontiguousarray(np.repeat(prob[k], B, axis=0))
+    opt = hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=2)
+    flagsA, flagsB = [1, 1, 0], [0, 0, 0]
+    ga, gb = [0, 2, 3, 6], [1, 4, 5]
+    cc = np.array([flagsA if b in ga else flagsB for b in range(B)], np.int32)
+
+    m = hsddp.Solver(prob, opt)
+    m.solve()
+    lay = m.shift_elements(cc)
+    hzs = lay["horizons"]
+    assert hzs[ga[0]] != hzs[gb[0]] and all(hzs[b] == hzs[ga[0]] for b in ga) and all(hzs[b] == hzs[gb[0]] for b in gb)
+    gaits = ["trot"] * B
+    Pm, Sm = m.P, m.S
+    c, rx, ru, rf = _inputs(gaits, hzs, 1, Pm, Sm, B)
+    # the warm start right after the shift (before new inputs: X = Xbar is reset by update_problem)
+    m.update_problem(c, prob["x0"], rx, ru, rf)
+    wm = m.trajectory()
+    m.solve()
+    gm = {**m.trajectory(), **m.element_info()}
+    m.close()
+    for idx, flags in ((ga, flagsA), (gb, flagsB)):
+        sub = {k: (v[idx] if isinstance(v, np.ndarray) and v.shape[:1] == (B,) else v) for k, v in prob.items()}
+        sub["batch"] = len(idx)
+        u = hsddp.Solver(sub, opt)
+        u.solve()
+        ul = u.shift(flags)
+        assert ul["horizons"] == hzs[idx[0]]
+        S = u.S
+        cu, rxu, ruu, rfu = _inputs(["trot"] * len(idx), [ul["horizons"]] * len(idx), 1, u.P, S, len(idx))
+        u.update_problem(cu, prob["x0"][idx], rxu, ruu, rfu)
+        wu = u.trajectory()
+        for f in ("Xbar", "Ubar", "K"):
+            a = wm[f][idx, :S] if f == "Xbar" else wm[f][idx]
+            assert np.array_equal(a, wu[f]), ("warm start", f)
+        u.solve()
+        gu = {**u.trajectory(), **u.element_info()}
+        u.close()
+        assert np.array_equal(gm["Xbar"][idx, :S], gu["Xbar"]) and np.array_equal(gm["K"][idx], gu["K"])
+        for f in ("Ubar", "cost", "n_ls_trials", "iters", "status"):
+            assert np.array_equal(gm[f][idx], gu[f]), f
