@@ -408,10 +408,10 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
     int *contacts; double *x0, *rx, *ru, *rf;
     int rc = 0;
     if ((rc = dalloc(h, contacts, B * (P + 1) * 4)) || (rc = dalloc(h, x0, B * NX)) || (rc = dalloc(h, rx, Br * S * NX)) ||
-        (rc = dalloc(h, ru, Br * S * NX)) || (rc = dalloc(h, rf, Br * S * 12)) || (rc = dalloc(h, d.X, B * S * NX)) ||
-        (rc = dalloc(h, d.Xbar, B * S * NX)) || (rc = dalloc(h, d.Defect, B * S * NX)) ||
-        (rc = dalloc(h, d.Defect_bar, B * S * NX)) || (rc = dalloc(h, d.dX, B * S * NX)) ||
-        (rc = dalloc(h, d.U, B * Kc * NX)) || (rc = dalloc(h, d.Ubar, B * Kc * NX)) || (rc = dalloc(h, d.dU, B * Kc * NX)) ||
+        (rc = dalloc(h, ru, Br * S * NX)) || (rc = dalloc(h, rf, Br * S * 12)) || (rc = dalloc(h, d.Xb[0], B * S * NX)) ||
+        (rc = dalloc(h, d.Xb[1], B * S * NX)) || (rc = dalloc(h, d.Defect, B * S * NX)) || (rc = dalloc(h, d.sel, B)) ||
+        (rc = dalloc(h, d.dX, B * S * NX)) ||
+        (rc = dalloc(h, d.Ub[0], B * Kc * NX)) || (rc = dalloc(h, d.Ub[1], B * Kc * NX)) || (rc = dalloc(h, d.dU, B * Kc * NX)) ||
         (rc = dalloc(h, d.du, B * Kc * NX)) || (rc = dalloc(h, d.dbg, B * 16)) ||
         (p.fp32 ? ((rc = dalloc(h, d.K32, B * Kc * KCW)) || (rc = dalloc(h, d.lq32, B * Kc * LQW32)) ||
                    (rc = dalloc(h, d.def32, B * S * NX)))
@@ -652,9 +652,10 @@ extern "C" int hsddp_upload_problem(hsddp_handle h, const int *contacts, const d
     const Params &p = h->p;
     const size_t B = p.B, S = p.S, Br = h->Bref;
     // default warm start: Xbar = X = reference (HKDProblem.cpp:84-90), Ubar = U = 0, K = 0
-    if (Br == 1) launch_broadcast(h->d.Xbar, h->d.ref_x, S * NX, B, h->stream);
-    else HIPCHK(hipMemcpyAsync(h->d.Xbar, h->d.ref_x, B * S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
-    HIPCHK(hipMemsetAsync(h->d.Ubar, 0, B * p.Kc * NX * sizeof(double), h->stream));
+    HIPCHK(hipMemsetAsync(h->d.sel, 0, B * sizeof(int), h->stream));  // nominal and working rows in buffer 0
+    if (Br == 1) launch_broadcast(h->d.Xb[0], h->d.ref_x, S * NX, B, h->stream);
+    else HIPCHK(hipMemcpyAsync(h->d.Xb[0], h->d.ref_x, B * S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipMemsetAsync(h->d.Ub[0], 0, B * p.Kc * NX * sizeof(double), h->stream));
     if (p.fp32) HIPCHK(hipMemsetAsync(h->d.K32, 0, B * p.Kc * KCW * sizeof(float), h->stream));
     else HIPCHK(hipMemsetAsync(h->d.K, 0, B * p.Kc * KCW * sizeof(double), h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -685,8 +686,9 @@ extern "C" int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const
     const size_t B = p.B, S = p.S, Kc = p.Kc;
     Bufs &d = h->d;
     int rc;
-    if (Xbar && (rc = h2d(d.Xbar, Xbar, B * S * NX * sizeof(double), h->stream))) return rc;
-    if (Ubar && (rc = h2d(d.Ubar, Ubar, B * Kc * NX * sizeof(double), h->stream))) return rc;
+    launch_normalize(p, d, h->stream);  // every element's nominal rows in buffer 0
+    if (Xbar && (rc = h2d(d.Xb[0], Xbar, B * S * NX * sizeof(double), h->stream))) return rc;
+    if (Ubar && (rc = h2d(d.Ub[0], Ubar, B * Kc * NX * sizeof(double), h->stream))) return rc;
     if (K) { // keep the 12 coupled rows of each knot's gain (KCW layout, hsddp_internal.h)
         std::vector<double> kc(B * Kc * KCW);
         for (size_t b = 0; b < B; ++b)
@@ -704,8 +706,7 @@ extern "C" int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const
         }
         HIPCHK(hipStreamSynchronize(h->stream));
     }
-    HIPCHK(hipMemcpyAsync(d.X, d.Xbar, B * S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
-    HIPCHK(hipMemcpyAsync(d.U, d.Ubar, B * Kc * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipMemsetAsync(d.sel, 0, B * sizeof(int), h->stream));  // X = Xbar, U = Ubar: one buffer
     HIPCHK(hipMemsetAsync(d.dX, 0, B * S * NX * sizeof(double), h->stream));
     HIPCHK(hipMemsetAsync(d.du, 0, B * Kc * NX * sizeof(double), h->stream));
     HIPCHK(hipMemsetAsync(d.dU, 0, B * Kc * NX * sizeof(double), h->stream));
@@ -793,7 +794,6 @@ static void begin_launches(hsddp_handle h)
     launch_reset_elements(h->p, h->d, h->stream);
     launch_rollout(h->p, h->d, 0.0, 1, h->stream);
     launch_decide(h->p, h->d, 0.0, 0, 1, h->stream);
-    launch_update_nominal(h->p, h->d, 1, h->stream);
 }
 
 static void iteration_launches(hsddp_handle h, const std::vector<double> &trials, Timer &tm)
@@ -816,7 +816,6 @@ static void iteration_launches(hsddp_handle h, const std::vector<double> &trials
         launch_rollout(p, d, trials[t], 0, st);
         launch_decide(p, d, trials[t], t + 1 == trials.size(), 0, st);
     }
-    launch_update_nominal(p, d, 0, st);
     tm.end(2, e0);
 }
 
@@ -947,7 +946,9 @@ extern "C" int hsddp_download_trajectory(hsddp_handle h, double *Xbar, double *U
     HIPCHK(hipStreamSynchronize(h->stream));
     const size_t B = h->p.B, S = h->p.S, Kc = h->p.Kc;
     int rc;
-    if ((rc = d2h(Xbar, h->d.Xbar, B * S * NX * 8)) || (rc = d2h(Ubar, h->d.Ubar, B * Kc * NX * 8)))
+    launch_normalize(h->p, h->d, h->stream);  // nominal rows in buffer 0
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if ((rc = d2h(Xbar, h->d.Xb[0], B * S * NX * 8)) || (rc = d2h(Ubar, h->d.Ub[0], B * Kc * NX * 8)))
         return rc;
     if (K && h->need_inputs)
         return fail(HSDDP_ERR_ARG, "the layout changed (hsddp_shift): call hsddp_update_problem before downloading K");
@@ -988,10 +989,24 @@ extern "C" int hsddp_download_working(hsddp_handle h, double *X, double *U, doub
     HIPCHK(hipStreamSynchronize(h->stream));
     const size_t B = h->p.B, S = h->p.S, Kc = h->p.Kc;
     int rc;
-    if ((rc = d2h(X, h->d.X, B * S * NX * 8)) || (rc = d2h(U, h->d.U, B * Kc * NX * 8)) ||
-        (rc = d2h(Defect, h->d.Defect, B * S * NX * 8)) || (rc = d2h(dX, h->d.dX, B * S * NX * 8)) ||
+    if ((rc = d2h(Defect, h->d.Defect, B * S * NX * 8)) || (rc = d2h(dX, h->d.dX, B * S * NX * 8)) ||
         (rc = d2h(dU, h->d.dU, B * Kc * NX * 8)))
         return rc;
+    if (X || U) {  // each element's working rows from the buffer sel names
+        std::vector<int> sel(B);
+        HIPCHK(hipMemcpy(sel.data(), h->d.sel, B * sizeof(int), hipMemcpyDeviceToHost));
+        for (int q = 0; q < 2; ++q) {
+            std::vector<double> xb(X ? B * S * NX : 0), ub(U ? B * Kc * NX : 0);
+            if ((rc = d2h(X ? xb.data() : nullptr, h->d.Xb[q], B * S * NX * 8)) ||
+                (rc = d2h(U ? ub.data() : nullptr, h->d.Ub[q], B * Kc * NX * 8)))
+                return rc;
+            for (size_t b = 0; b < B; ++b) {
+                if (((sel[b] >> 1) & 1) != q) continue;
+                if (X) std::copy(xb.begin() + b * S * NX, xb.begin() + (b + 1) * S * NX, X + b * S * NX);
+                if (U) std::copy(ub.begin() + b * Kc * NX, ub.begin() + (b + 1) * Kc * NX, U + b * Kc * NX);
+            }
+        }
+    }
     return HSDDP_OK;
 }
 
@@ -1532,8 +1547,9 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     launch_shift_gather(p.B, a, d, h->spare_Xbar, h->spare_Ubar, h->spare_K, h->stream);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(h->stream));
-    std::swap(d.Xbar, h->spare_Xbar);
-    std::swap(d.Ubar, h->spare_Ubar);
+    std::swap(d.Xb[0], h->spare_Xbar);
+    std::swap(d.Ub[0], h->spare_Ubar);
+    HIPCHK(hipMemset(d.sel, 0, B * sizeof(int)));  // the gathered warm start is buffer 0's
     if (p.fp32) { float *t = d.K32; d.K32 = (float *)h->spare_K; h->spare_K = t; }
     else { double *t = d.K; d.K = (double *)h->spare_K; h->spare_K = t; }
     // the new layouts

@@ -42,21 +42,26 @@ DEV double foot_weight(const PT &p, const int *c, int j) { return p.foot_gain * 
 DEV bool touchdown(const int *c, const int *cn, int l) { return c[l] == 0 && cn[l] == 1; }
 
 // ---- the phase layout of element b ----------------------------------------------------------
-// The handle's layout (Params), or element b's own with per-element layouts (Bufs::lay).  Runtime
-// phase indices read Params in place (kparams), never the by-value copy.
-struct Lay {
-    const Layout *l;  // null: the handle's layout
-    DEV int P() const { return l ? l->P : kparams()->P; }
-    DEV int S() const { return l ? l->S : kparams()->S; }
-    DEV int N(int i) const { return l ? l->N[i] : kparams()->N[i]; }
-    DEV int s0(int i) const { return l ? l->s0[i] : kparams()->s0[i]; }
-    DEV int k0(int i) const { return l ? l->k0[i] : kparams()->k0[i]; }
-    DEV int ss(int i) const { return l ? l->ss[i] : kparams()->ss[i]; }
+// The handle's layout (Params, read in place: runtime phase indices never index the by-value copy)
+// or, with per-element layouts (Params::elem_layout, hsddp_set_element_layouts), element b's own
+// (Bufs::lay).  The kernels are instantiated for both (EL), so the shared-layout path carries no
+// per-access selection.
+template <bool EL>
+struct LayT {
+    const Layout *l;
+    DEV int P() const { if constexpr (EL) return l->P; else return kparams()->P; }
+    DEV int S() const { if constexpr (EL) return l->S; else return kparams()->S; }
+    DEV int N(int i) const { if constexpr (EL) return l->N[i]; else return kparams()->N[i]; }
+    DEV int s0(int i) const { if constexpr (EL) return l->s0[i]; else return kparams()->s0[i]; }
+    DEV int k0(int i) const { if constexpr (EL) return l->k0[i]; else return kparams()->k0[i]; }
+    DEV int ss(int i) const { if constexpr (EL) return l->ss[i]; else return kparams()->ss[i]; }
 };
-DEV Lay layout_of(const Bufs &d, int b) { return Lay{kparams()->elem_layout ? d.lay + b : nullptr}; }
+template <bool EL>
+DEV LayT<EL> layout_of(const Bufs &d, int b) { return LayT<EL>{EL ? d.lay + b : nullptr}; }
 
 // phase i and knot k of state slot s
-DEV void slot_phase(const Lay &L, int s, int &i, int &k)
+template <typename L_>
+DEV void slot_phase(const L_ &L, int s, int &i, int &k)
 {
     i = 0;
     const int P = L.P();
@@ -64,6 +69,10 @@ DEV void slot_phase(const Lay &L, int s, int &i, int &k)
         if (s >= L.s0(j)) i = j;
     k = s - L.s0(i);
 }
+
+// element b's nominal (Xbar / Ubar), working (X / U) and trial-target buffers (Bufs::sel)
+DEV int nom_buf(const Bufs &d, int b) { return d.sel[b] & 1; }
+DEV int work_buf(const Bufs &d, int b) { return (d.sel[b] >> 1) & 1; }
 
 DEV void load_contacts(const Bufs &d, const Params &p, int b, int i, int *c, int *cn)
 {

@@ -1,8 +1,8 @@
 // hsddp_internal.h — device data layout and kernel interface of the batched HS-DDP solver.
 //
 // HBM layout (element-major, fp64; b = element, s = state slot, kc = control slot):
-//   X, Xbar, Defect, Defect_bar, dX   [B][S][24]
-//   U, Ubar, dU, du                   [B][Kc][24]     du = dU + K dX (linear-rollout control step)
+//   Xb[2], Defect, dX                 [B][S][24]     Xb: the nominal Xbar and the working / trial X (sel)
+//   Ub[2], dU, du                     [B][Kc][24]     du = dU + K dX (linear-rollout control step)
 //   K                                 [B][Kc][12][24] row-major, coupled controls only (below)
 //   lq                                [B][Kc][LQW]    compact LQ model of one knot (below)
 //   term                              [B][P][TW]      Phix | Phixx | Px (reset-map Jacobian at X_i[N])
@@ -105,8 +105,12 @@ struct Bufs {
     const int *contacts;                   // [B][P+1][4]
     const double *x0;                      // [B][24]
     const double *ref_x, *ref_u, *ref_foot; // [Bref][S][24|24|12]
-    double *X, *Xbar, *Defect, *Defect_bar, *dX;
-    double *U, *Ubar, *dU, *du;
+    // Trajectory::update_nominal_vals without copies: each element's nominal (Xbar, Ubar) and working
+    // (X, U) rows live in one of two buffers, sel[b] bit 0 = the nominal's, bit 1 = the working one's.
+    // A line-search trial writes the non-nominal buffer; accepting it flips both bits to it.
+    double *Xb[2], *Defect, *dX;
+    double *Ub[2], *dU, *du;
+    int *sel;                              // [B]
     double *K, *lq, *term;
     double *reb_delta, *reb_eps, *al_sigma, *al_lambda, *term_h;
     double *slot_cost, *slot_feas, *slot_viol;
@@ -133,7 +137,8 @@ struct Bufs {
 // kernel launchers (hsddp_kernels.hip)
 void launch_rollout(const Params &p, const Bufs &d, double eps, int init, hipStream_t st);
 void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, hipStream_t st);
-void launch_update_nominal(const Params &p, const Bufs &d, int init, hipStream_t st);
+// nominal rows of every element into buffer 0 (Bufs::sel bit 0 cleared), for host transfers
+void launch_normalize(const Params &p, const Bufs &d, hipStream_t st);
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st);
 void launch_riccati(const Params &p, const Bufs &d, hipStream_t st);
 void launch_lin_rollout(const Params &p, const Bufs &d, hipStream_t st);

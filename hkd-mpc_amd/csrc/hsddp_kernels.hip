@@ -66,7 +66,7 @@ DEV void lq_stage_store(T *wl, const long *ridx, const double *v, T *lq, int ldw
 // control slots (SinglePhase::compute_cost + LQ_approximation, SinglePhase.cpp:235-296).
 // F32: config C5's fp32 Riccati mode (records in fp32 plus an fp32 copy of Defect for the sweep)
 // The A - I / B pieces go out by direct stores (staging them would keep all 102 values live).
-template <bool F32>
+template <bool F32, bool EL>
 __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 {
     using T = std::conditional_t<F32, float, double>;
@@ -79,14 +79,15 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     const int b = (int)(gid / p.S), s = (int)(gid % p.S);
     const ElemState &E = d.el[b];
     if (E.done || E.inner_done) return;
-    const Lay L = layout_of(d, b);
+    const auto L = layout_of<EL>(d, b);
     if (s >= L.S()) return;
     int i, k;
     slot_phase(L, s, i, k);
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     double x[NX];
-    const double *xg = d.X + ((size_t)b * p.S + s) * NX;
+    const int wb = work_buf(d, b);
+    const double *xg = d.Xb[wb] + ((size_t)b * p.S + s) * NX;
 #pragma unroll
     for (int j = 0; j < NX; ++j) x[j] = xg[j];
     const double *dg = d.Defect + ((size_t)b * p.S + s) * NX;
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     const int kc = L.k0(i) + k;
     sridx[w][lane] = (long)b * p.Kc + kc;
     double u[NU];
-    const double *ug = d.U + ((size_t)b * p.Kc + kc) * NU;
+    const double *ug = d.Ub[wb] + ((size_t)b * p.Kc + kc) * NU;
 #pragma unroll
     for (int j = 0; j < NU; ++j) u[j] = ug[j];
     const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
@@ -180,18 +181,19 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 }
 
 // k_terminal: one wave per (element, phase): Phix, Phixx (+AL, quirk A4) and reset-map Jacobian Px.
+template <bool EL>
 __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
 {
     const int b = blockIdx.x / p.P, i = blockIdx.x % p.P, t = threadIdx.x;
     const ElemState &E = d.el[b];
     if (E.done || E.inner_done) return;
-    const Lay L = layout_of(d, b);
+    const auto L = layout_of<EL>(d, b);
     const int P = L.P();
     if (i >= P) return;
     __shared__ double sx[NX], shx[4][NX], scoef[4][2];
     __shared__ int sc[4], scn[4];
     const int s = L.s0(i) + L.N(i);
-    if (t < NX) sx[t] = d.X[((size_t)b * p.S + s) * NX + t];
+    if (t < NX) sx[t] = d.Xb[work_buf(d, b)][((size_t)b * p.S + s) * NX + t];
     if (t < 4) {
         const int *cc = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
         sc[t] = cc[t]; scn[t] = cc[4 + t];
@@ -285,7 +287,8 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
 // Per-slot outputs of one rollout trial from the slot's state x = X[k], simulated state xs =
 // Xsim[k] and control u = U[k] (k < N): Defect, |Defect|^2, divergence flag, running or terminal
 // cost with its constraint violation and touchdown residuals (SinglePhase.cpp:196-232).
-DEV void finish_slot(const Params &p, const Bufs &d, const Lay &L, int b, int s, int i, int k, const int *c,
+template <typename L_>
+DEV void finish_slot(const Params &p, const Bufs &d, const L_ &L, int b, int s, int i, int k, const int *c,
                      const int *cn, const double *x, const double *xs, const double *u)
 {
     const size_t sb = (size_t)b * p.S;
@@ -329,11 +332,12 @@ DEV void finish_slot(const Params &p, const Bufs &d, const Lay &L, int b, int s,
 constexpr int RS = NX + 1;  // LDS row stride (doubles): conflict-free row-per-lane reads
 constexpr int RW = 65;      // rows per wave: 64 slots and the one before
 
-// X_t = Xbar + eps dX (or U_t = Ubar + eps du) for rows r0 .. r0 + RW - 1 of an [rows][24] pair
-// into LDS; rows of inactive elements are skipped, own rows (own(r)) are stored to `out`
-template <typename Act, typename Own>
-DEV void stage_trial(double *L, const double *bar, const double *del, double *out, long r0, long nrows, int per,
-                     double eps, int lane, Act active, Own own)
+// X_t = Xbar + eps dX for rows r0 .. r0 + RW - 1 of the [rows][24] state buffers into LDS; rows
+// of inactive elements are skipped, own rows (own(r)) are stored to the element's trial buffer
+// (buf[nom ^ 1], the nominal being buf[nom], nom = nomof(element))
+template <typename Act, typename Own, typename Nom>
+DEV void stage_trial(double *L, double *const *buf, const double *del, long r0, long nrows, int per, double eps,
+                     int lane, Act active, Own own, Nom nomof)
 {
     constexpr int CH = NX / 2;  // 16-byte chunks per row
 #pragma unroll 1
@@ -341,6 +345,9 @@ DEV void stage_trial(double *L, const double *bar, const double *del, double *ou
         const int row = f / CH, cc = 2 * (f % CH);
         const long r = r0 + row;
         if (r < 0 || r >= nrows || !active((int)(r / per))) continue;
+        const int nb = nomof((int)(r / per));
+        const double *bar = buf[nb];
+        double *out = buf[nb ^ 1];
         typedef double d2 __attribute__((ext_vector_type(2)));
         const d2 xb = *(const d2 *)(bar + r * NX + cc), dx = *(const d2 *)(del + r * NX + cc);
         d2 v;
@@ -358,10 +365,10 @@ DEV void stage_trial(double *L, const double *bar, const double *del, double *ou
 
 // trial control row r: U = Ubar + eps du, straight from global memory (the wave's 64 rows are one
 // contiguous 12 KB range, so the row-per-lane loads are served by the vector L1 / L2)
-DEV void trial_row(const Bufs &d, long r, double eps, double *u)
+DEV void trial_row(const Bufs &d, const double *Ubar, long r, double eps, double *u)
 {
     typedef double d2 __attribute__((ext_vector_type(2)));
-    const d2 *ub = (const d2 *)(d.Ubar + r * NU), *du = (const d2 *)(d.du + r * NU);
+    const d2 *ub = (const d2 *)(Ubar + r * NU), *du = (const d2 *)(d.du + r * NU);
 #pragma unroll
     for (int j = 0; j < NU / 2; ++j) {
         const d2 a = ub[j], e = du[j];
@@ -373,6 +380,7 @@ DEV void trial_row(const Bufs &d, long r, double eps, double *u)
 // Only the state rows go through LDS (13 KB per wave); the control rows are read per lane
 // (trial_row), the slot's own control row stored from registers.  With both row sets in LDS
 // (26 KB per wave) only 6 waves fit a CU: 1.25 ms/step of line search vs 0.93 here.
+template <bool EL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOUT_WAVES))) void k_rollout(Params p, Bufs d, double eps, int init)
 {
     __shared__ double Xt[RW * RS];
@@ -386,14 +394,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     for (int b = bA + 1; b < bB && !any; ++b) any = act(b);
     if (!any) return;
     auto active = [&](int b) { return b == bA ? aA : b == bB ? aB : act(b); };
+    const int nA = nom_buf(d, bA), nB = nom_buf(d, bB);
+    auto nomof = [&](int b) { return b == bA ? nA : b == bB ? nB : nom_buf(d, b); };
     const long xr0 = g0 - 1;
-    stage_trial(Xt, d.Xbar, d.dX, d.X, xr0, total, p.S, eps, lane, active,
-                [&](long r) { return r >= g0; });
+    stage_trial(Xt, d.Xb, d.dX, xr0, total, p.S, eps, lane, active, [&](long r) { return r >= g0; }, nomof);
     __syncthreads();
     if (gid >= total) return;
     const int b = (int)(gid / p.S), s = (int)(gid % p.S);
     if (!active(b)) return;
-    const Lay L = layout_of(d, b);
+    const auto L = layout_of<EL>(d, b);
     if (s >= L.S()) return;
     int i, k;
     slot_phase(L, s, i, k);
@@ -401,6 +410,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     load_contacts(d, p, b, i, c, cn);
     const double *x = Xt + (gid - xr0) * RS;
     const long kq = (long)b * p.Kc + s - i;  // the slot's control row (k < N)
+    const int nb = nomof(b);
     double xs[NX];
     if (k == 0) {
         if (i == 0) {
@@ -413,15 +423,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
         }
     } else {
         double up[NU];
-        trial_row(d, kq - 1, eps, up);
+        trial_row(d, d.Ub[nb], kq - 1, eps, up);
         double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
         hkd_step(x - RS, up, cd, p.dt, xs);
     }
     double u[NU];  // read by finish_slot only when k < N
     if (k < L.N(i)) {
-        trial_row(d, kq, eps, u);
+        trial_row(d, d.Ub[nb], kq, eps, u);
         typedef double d2 __attribute__((ext_vector_type(2)));
-        d2 *ug = (d2 *)(d.U + kq * NU);
+        d2 *ug = (d2 *)(d.Ub[nb ^ 1] + kq * NU);
 #pragma unroll
         for (int j = 0; j < NU / 2; ++j) ug[j] = d2{u[2 * j], u[2 * j + 1]};
     }
@@ -433,6 +443,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
 // SinglePhase::hybrid_rollout's sequential branch (SinglePhase.cpp:185-222), X[k] = Xsim[k]
 // (X[0] = x_init when the set is empty) and U[k] = Ubar[k] + eps dU[k] + K[k] (X[k] - Xbar[k]),
 // then the slot outputs of those states.  One thread per element; rare (a few states per element).
+template <bool EL>
 __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double eps, int init)
 {
     const int b = blockIdx.x * 64 + threadIdx.x;
@@ -440,7 +451,10 @@ __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double ep
     const ElemState &E = d.el[b];
     if (!(init ? !E.done : E.ls_active != 0)) return;
     const size_t sb = (size_t)b * p.S, kb = (size_t)b * p.Kc;
-    const Lay L = layout_of(d, b);
+    const auto L = layout_of<EL>(d, b);
+    const int nb = nom_buf(d, b);
+    const double *Xbar = d.Xb[nb], *Ubar = d.Ub[nb];
+    double *X = d.Xb[nb ^ 1], *U = d.Ub[nb ^ 1];  // the trial's rows (k_rollout wrote the shooting ones)
     for (int i = 0; i < L.P(); ++i) {
         const int N = L.N(i), ss = L.ss(i), s0 = L.s0(i), k0 = L.k0(i);
         if (ss >= N + 1) continue;
@@ -454,22 +468,22 @@ __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double ep
             } else {
                 int cp_[4], cpn[4];
                 load_contacts(d, p, b, i - 1, cp_, cpn);
-                hkd_resetmap(d.X + (sb + s0 - 1) * NX, cp_, cpn, xs);
+                hkd_resetmap(X + (sb + s0 - 1) * NX, cp_, cpn, xs);
             }
         } else { // Xsim[ss] from the last shooting state and its control (written by k_rollout)
-            const double *xg = d.X + (sb + s0 + ss - 1) * NX, *ug = d.U + (kb + k0 + ss - 1) * NU;
+            const double *xg = X + (sb + s0 + ss - 1) * NX, *ug = U + (kb + k0 + ss - 1) * NU;
             for (int j = 0; j < NX; ++j) x[j] = xg[j];
             for (int j = 0; j < NU; ++j) u[j] = ug[j];
             hkd_step(x, u, cd, p.dt, xs);
         }
         for (int k = ss; k <= N; ++k) {
             const int s = s0 + k;
-            double *xg = d.X + (sb + s) * NX;
+            double *xg = X + (sb + s) * NX;
             for (int j = 0; j < NX; ++j) { x[j] = xs[j]; xg[j] = xs[j]; }
             const double *up = nullptr;
             if (k < N) {
                 const int kc = k0 + k;
-                const double *xb = d.Xbar + (sb + s) * NX, *ub = d.Ubar + (kb + kc) * NU, *du = d.dU + (kb + kc) * NU;
+                const double *xb = Xbar + (sb + s) * NX, *ub = Ubar + (kb + kc) * NU, *du = d.dU + (kb + kc) * NU;
                 double dx[NX];
                 for (int j = 0; j < NX; ++j) dx[j] = x[j] - xb[j];
                 for (int j = 0; j < NU; ++j) u[j] = 0.0;
@@ -480,7 +494,7 @@ __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double ep
                     for (int j = 0; j < NX; ++j) acc += (p.fp32 ? (double)d.K32[kr + j] : d.K[kr + j]) * dx[j];
                     u[c[q / 3] ? q : 12 + q] = acc;
                 }
-                double *ug = d.U + (kb + kc) * NU;
+                double *ug = U + (kb + kc) * NU;
                 for (int j = 0; j < NU; ++j) { u[j] = ub[j] + eps * du[j] + u[j]; ug[j] = u[j]; }
                 up = u;
             }
@@ -494,6 +508,7 @@ __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double ep
 // later-termination test (:358).  16 lanes per element, one per phase: each lane sums its phase's
 // slots in order, and the phase sums are added in phase order — the reference's summation order
 // (compute_cost, MultiPhaseDDP.cpp:431-440; SinglePhase.cpp:235-262).
+template <bool EL>
 __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int last, int init)
 {
     const int lane = threadIdx.x, g = lane & 15, base = lane & ~15;
@@ -501,7 +516,7 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
     const bool valid = b < p.B;
     const ElemState *Ep = valid ? &d.el[b] : nullptr;
     const bool act = valid && (init ? !Ep->done : Ep->ls_active);
-    const Lay L = layout_of(d, valid ? b : 0);
+    const auto L = layout_of<EL>(d, valid ? b : 0);
     const int P = L.P();
     double ci = 0.0, fi = 0.0, pv = 0.0, tv = 0.0;
     int div = 0;
@@ -539,7 +554,9 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
         }
         E.hist_n += 1;
     };
-    if (init) {
+    const int nb = d.sel[b] & 1;
+    if (init) {  // the initial rollout is taken (update_nominal_trajectory, MultiPhaseDDP.cpp:258)
+        d.sel[b] = (nb ^ 1) * 3;
         E.cost = cost; E.feas = feas; E.accepted = 1;
         push_info();  // the initial information (:277-280)
         return;
@@ -552,8 +569,10 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
     bool fin = false;
     if ((merit <= E.merit_prev + p.gamma * exp_merit) && !dv) {
         E.accepted = 1; E.ls_active = 0; fin = true;
+        d.sel[b] = (nb ^ 1) * 3;  // the trial becomes the nominal and the working trajectory
     } else if (last) {
         E.accepted = 0; E.ls_active = 0; E.cost = E.cost_prev; E.merit = E.merit_prev; fin = true;
+        d.sel[b] = nb | ((nb ^ 1) << 1);  // quirk A2: the last trial stays the working trajectory
     }
     if (fin) {
         // the later-termination test breaks before the iteration's entry is buffered (:358-371)
@@ -564,23 +583,36 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
     }
 }
 
-// Trajectory::update_nominal_vals for accepted elements (copy X->Xbar, U->Ubar, Defect->Defect_bar)
-__global__ __launch_bounds__(256) void k_update_nominal(Params p, Bufs d, int init)
+// Trajectory::update_nominal_vals (TrajectoryManagement.cpp:110-115) is k_decide's flip of
+// Bufs::sel: the accepted trial's buffer becomes the nominal one, no rows are copied.  (Defect_bar
+// is never read by the solver, MultiPhaseDDP.cpp / SinglePhase.cpp, and is not kept.)
+
+// one element's nominal rows into buffer 0 (a swap of the two buffers where sel says buffer 1):
+// host downloads and uploads see Xbar / Ubar in buffer 0; sel is fixed up by k_normalize_sel
+__global__ __launch_bounds__(256) void k_normalize(Params p, Bufs d)
 {
-    // one thread per 16-byte pair (rows of 24 doubles: X, Defect [B][S][24], U [B][Kc][24])
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long per = (long)p.S * (NX / 2);
     if (gid >= (long)p.B * per) return;
     const int b = (int)(gid / per);
-    const ElemState &E = d.el[b];
-    if (!E.accepted || (init && E.done)) return;
-    reinterpret_cast<double2 *>(d.Xbar)[gid] = reinterpret_cast<const double2 *>(d.X)[gid];
-    reinterpret_cast<double2 *>(d.Defect_bar)[gid] = reinterpret_cast<const double2 *>(d.Defect)[gid];
+    if (!(d.sel[b] & 1)) return;
+    double2 *x0 = reinterpret_cast<double2 *>(d.Xb[0]), *x1 = reinterpret_cast<double2 *>(d.Xb[1]);
+    const double2 t = x0[gid];
+    x0[gid] = x1[gid];
+    x1[gid] = t;
     const long r = gid % per;
     if (r < (long)p.Kc * (NU / 2)) {
         const long ug = (long)b * p.Kc * (NU / 2) + r;
-        reinterpret_cast<double2 *>(d.Ubar)[ug] = reinterpret_cast<const double2 *>(d.U)[ug];
+        double2 *u0 = reinterpret_cast<double2 *>(d.Ub[0]), *u1 = reinterpret_cast<double2 *>(d.Ub[1]);
+        const double2 v = u0[ug];
+        u0[ug] = u1[ug];
+        u1[ug] = v;
     }
+}
+__global__ void k_normalize_sel(Params p, Bufs d)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < p.B && (d.sel[b] & 1)) d.sel[b] ^= 3;  // nominal now in 0, the working one moved with it
 }
 
 __global__ void k_outer_begin(Params p, Bufs d)
@@ -597,19 +629,20 @@ __global__ void k_outer_begin(Params p, Bufs d)
 }
 
 // update_REB_params (ConstraintsBase.h:168-183) per (element, control slot)
+template <bool EL>
 __global__ __launch_bounds__(256) void k_reb_update(Params p, Bufs d)
 {
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long)p.B * p.Kc) return;
     const int b = (int)(gid / p.Kc), kc = (int)(gid % p.Kc);
     if (d.el[b].done) return;
-    const Lay L = layout_of(d, b);
+    const auto L = layout_of<EL>(d, b);
     int i = 0;
     for (int j = 1; j < L.P(); ++j)
         if (kc >= L.k0(j)) i = j;
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
-    const double *u = d.U + gid * NU;
+    const double *u = d.Ub[work_buf(d, b)] + gid * NU;
     double *dl = d.reb_delta + gid * 20, *ep = d.reb_eps + gid * 20;
     for (int l = 0; l < 4; ++l) {
         if (!c[l]) continue;
@@ -624,6 +657,7 @@ __global__ __launch_bounds__(256) void k_reb_update(Params p, Bufs d)
 }
 
 // update_AL_params (ConstraintsBase.h:349-365) + outer convergence tests (MultiPhaseDDP.cpp:397-408)
+template <bool EL>
 __global__ void k_outer_end(Params p, Bufs d)
 {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -631,7 +665,7 @@ __global__ void k_outer_end(Params p, Bufs d)
     ElemState &E = d.el[b];
     if (E.done) return;
     if (p.AL_active) {
-        const int P = layout_of(d, b).P();
+        const int P = layout_of<EL>(d, b).P();
         for (int i = 0; i < P; ++i) {
             int c[4], cn[4];
             load_contacts(d, p, b, i, c, cn);
@@ -903,26 +937,38 @@ __global__ void k_model_reset(const double *x, const int *c, const int *cn, doub
 // ---------------------------------------------------------------------------------------------
 static inline unsigned blocks_for(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
+// the kernel instantiation for the handle's layout mode (shared / per element)
+#define LAUNCH_EL(kern, grid, block, st, ...)                                                       \
+    do {                                                                                            \
+        if (p.elem_layout) hipLaunchKernelGGL(kern<true>, grid, block, 0, st, __VA_ARGS__);         \
+        else hipLaunchKernelGGL(kern<false>, grid, block, 0, st, __VA_ARGS__);                      \
+    } while (0)
+
 void launch_rollout(const Params &p, const Bufs &d, double eps, int init, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_rollout, dim3(blocks_for((long)p.B * p.S, 64)), dim3(64), 0, st, p, d, eps, init);
-    if (p.has_tail) hipLaunchKernelGGL(k_rollout_tail, dim3((p.B + 63) / 64), dim3(64), 0, st, p, d, eps, init);
+    LAUNCH_EL(k_rollout, dim3(blocks_for((long)p.B * p.S, 64)), dim3(64), st, p, d, eps, init);
+    if (p.has_tail) LAUNCH_EL(k_rollout_tail, dim3((p.B + 63) / 64), dim3(64), st, p, d, eps, init);
 }
 void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_decide, dim3((p.B + 3) / 4), dim3(64), 0, st, p, d, eps, last, init);
+    LAUNCH_EL(k_decide, dim3((p.B + 3) / 4), dim3(64), st, p, d, eps, last, init);
 }
-void launch_update_nominal(const Params &p, const Bufs &d, int init, hipStream_t st)
+void launch_normalize(const Params &p, const Bufs &d, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_update_nominal, dim3(blocks_for((long)p.B * p.S * (NX / 2), 256)), dim3(256), 0, st, p, d, init);
+    hipLaunchKernelGGL(k_normalize, dim3(blocks_for((long)p.B * p.S * (NX / 2), 256)), dim3(256), 0, st, p, d);
+    hipLaunchKernelGGL(k_normalize_sel, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);
 }
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
 {
-    if (p.fp32)
-        hipLaunchKernelGGL(k_lq<true>, dim3(blocks_for((long)p.B * p.S, 256)), dim3(256), 0, st, p, d);
-    else
-        hipLaunchKernelGGL(k_lq<false>, dim3(blocks_for((long)p.B * p.S, 256)), dim3(256), 0, st, p, d);
-    hipLaunchKernelGGL(k_terminal, dim3(p.B * p.P), dim3(64), 0, st, p, d);
+    const dim3 g(blocks_for((long)p.B * p.S, 256));
+    if (p.fp32) {
+        if (p.elem_layout) hipLaunchKernelGGL((k_lq<true, true>), g, dim3(256), 0, st, p, d);
+        else hipLaunchKernelGGL((k_lq<true, false>), g, dim3(256), 0, st, p, d);
+    } else {
+        if (p.elem_layout) hipLaunchKernelGGL((k_lq<false, true>), g, dim3(256), 0, st, p, d);
+        else hipLaunchKernelGGL((k_lq<false, false>), g, dim3(256), 0, st, p, d);
+    }
+    LAUNCH_EL(k_terminal, dim3(p.B * p.P), dim3(64), st, p, d);
 }
 
 __global__ __launch_bounds__(256) void k_broadcast(double *dst, const double *src, size_t n, size_t total)
@@ -942,11 +988,11 @@ void launch_outer_begin(const Params &p, const Bufs &d, hipStream_t st)
 }
 void launch_reb_update(const Params &p, const Bufs &d, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_reb_update, dim3(blocks_for((long)p.B * p.Kc, 256)), dim3(256), 0, st, p, d);
+    LAUNCH_EL(k_reb_update, dim3(blocks_for((long)p.B * p.Kc, 256)), dim3(256), st, p, d);
 }
 void launch_outer_end(const Params &p, const Bufs &d, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_outer_end, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);
+    LAUNCH_EL(k_outer_end, dim3(blocks_for(p.B, 256)), dim3(256), st, p, d);
 }
 void launch_reset_elements(const Params &p, const Bufs &d, hipStream_t st)
 {

@@ -183,10 +183,14 @@ DEV void lin_knot(const Params &p, const Bufs &d, LinElem<real> &S, LinBuf<real>
     const bool rowl = r < NX, st = rowl && hf == 0;
     const int rr = rowl ? r : 0;
     const real dt = p.dt;
+#ifndef HSDDP_LIN_NOWAIT
+#define HSDDP_LIN_NOWAIT 0  // diagnostic (wrong results): no wait for the knot's image
+#endif
     if (more) {
         lin_fetch(nxt, p, d, b, s + 1, kc + 1, lane);
         // all but the I::NI just issued
-        if constexpr (I::NI == 4)
+        if (HSDDP_LIN_NOWAIT) {
+        } else if constexpr (I::NI == 4)
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else
             asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
@@ -262,7 +266,7 @@ DEV void lin_knot(const Params &p, const Bufs &d, LinElem<real> &S, LinBuf<real>
     LSYNC();
 }
 
-template <typename real>
+template <typename real, bool EL>
 __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
 {
     __shared__ LinElem<real> S;
@@ -276,12 +280,12 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
     const int rr = rowl ? r : 0;
     const real *defg = Prec<real>::def(d);
     real v1 = 0, v2 = 0, dx = 0;
-    const Lay EL = layout_of(d, (int)b);
-    const int P = EL.P();
+    const auto LY = layout_of<EL>(d, (int)b);
+    const int P = LY.P();
     for (int i = 0; i < P; ++i) {
         PhaseConst<real> pc;
         load_phase(p, d, b, i, pc);
-        const int N = EL.N(i), s0 = EL.s0(i), k0 = EL.k0(i);
+        const int N = LY.N(i), s0 = LY.s0(i), k0 = LY.k0(i);
         lin_fetch(B0, p, d, b, s0, k0, lane);  // the phase's first knot (its wait is in lin_knot)
         if (i > 0) { // dx_init = Px dX_end
             const double *Px = d.term + (b * p.P + (i - 1)) * TW + TM_PX;
@@ -340,10 +344,13 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
 
 void launch_lin_rollout(const Params &p, const Bufs &d, hipStream_t st)
 {
-    if (p.fp32)
-        hipLaunchKernelGGL(k_lin_rollout<float>, dim3(p.B), dim3(64), 0, st, p, d);
-    else
-        hipLaunchKernelGGL(k_lin_rollout<double>, dim3(p.B), dim3(64), 0, st, p, d);
+    if (p.fp32) {
+        if (p.elem_layout) hipLaunchKernelGGL((k_lin_rollout<float, true>), dim3(p.B), dim3(64), 0, st, p, d);
+        else hipLaunchKernelGGL((k_lin_rollout<float, false>), dim3(p.B), dim3(64), 0, st, p, d);
+    } else {
+        if (p.elem_layout) hipLaunchKernelGGL((k_lin_rollout<double, true>), dim3(p.B), dim3(64), 0, st, p, d);
+        else hipLaunchKernelGGL((k_lin_rollout<double, false>), dim3(p.B), dim3(64), 0, st, p, d);
+    }
 }
 
 }  // namespace hsddp

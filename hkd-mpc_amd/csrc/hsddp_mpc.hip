@@ -12,6 +12,7 @@
 //                        front knots / phases, pushed-back copies of X.back(), zero new phases —
 //                        as one gather over (element, new slot, entry) from host-built slot maps.
 #include "../../include/hsddp.h"
+#include "hsddp_device.h"
 #include "hsddp_mpc.h"
 
 namespace hsddp {
@@ -24,14 +25,15 @@ __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdA
     const int b = blockIdx.x, t = threadIdx.x;
     hsddp_mpc_command &o = out[b];
     const int *cb = d.contacts + (size_t)b * (p.P + 1) * 4;
+    const double *Xbar = d.Xb[nom_buf(d, b)], *Ubar = d.Ub[nom_buf(d, b)];
     // controls, body states, feedback rows (zero past N_mpcsteps, as a fresh message)
     for (int e = t; e < HSDDP_CMD_STEPS * 24; e += blockDim.x) {
         const int k = e / 24, j = e % 24;
-        o.hkd_controls[k][j] = k < a.n ? (float)d.Ubar[((size_t)b * p.Kc + a.kc[k]) * NX + j] : 0.f;
+        o.hkd_controls[k][j] = k < a.n ? (float)Ubar[((size_t)b * p.Kc + a.kc[k]) * NX + j] : 0.f;
     }
     for (int e = t; e < HSDDP_CMD_STEPS * 12; e += blockDim.x) {
         const int k = e / 12, j = e % 12;
-        o.des_body_state[k][j] = k < a.n ? (float)d.Xbar[((size_t)b * p.S + a.xs[k]) * NX + j] : 0.f;
+        o.des_body_state[k][j] = k < a.n ? (float)Xbar[((size_t)b * p.S + a.xs[k]) * NX + j] : 0.f;
     }
     // K(m, n), m, n < 12: control m is leg m/3's GRF; its gain row is compact row m when the leg
     // is in stance and exactly zero when it swings (KCW layout, hsddp_internal.h)
@@ -61,7 +63,7 @@ __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdA
         float pf = a.feet ? a.feet[(size_t)(a.feet_per_elem ? b : 0) * 12 + t] : 0.f;
         for (int i = 0; i < p.P - 1 && i <= 4; ++i) {
             if (cb[i * 4 + l] == 0 && cb[(i + 1) * 4 + l] == 1) {
-                pf = (float)d.Xbar[((size_t)b * p.S + p.s0[i + 1]) * NX + 12 + 3 * l + ax];
+                pf = (float)Xbar[((size_t)b * p.S + p.s0[i + 1]) * NX + 12 + 3 * l + ax];
                 break;
             }
         }
@@ -77,8 +79,8 @@ __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdA
 // multiples of 4) of the new Xbar / Ubar rows and compact K rows of every element; gathered reads,
 // contiguous writes.
 template <typename KT>
-__global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, const double *Xbar, const double *X,
-                                                      const double *Ubar, const KT *K, double *Xn, double *Un, KT *Kn)
+__global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, Bufs d, const KT *K, double *Xn, double *Un,
+                                                      KT *Kn)
 {
     constexpr int KV = 16 / sizeof(KT);  // K values per thread
     const long nx = (long)a.S_new * NX / 2, nu = (long)a.Kc * NX / 2, nk = (long)a.Kc * KCW / KV, per = nx + nu + nk;
@@ -87,6 +89,7 @@ __global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, const 
     const long b = gid / per;
     long e = gid % per;
     const int m = a.map_id ? a.map_id[b] : 0;
+    const double *Xbar = d.Xb[nom_buf(d, (int)b)], *X = d.Xb[work_buf(d, (int)b)], *Ubar = d.Ub[nom_buf(d, (int)b)];
     const int *smap = a.smap + (size_t)m * a.S_new, *cmap = a.cmap + (size_t)m * a.Kc;
     if (e < nx) {
         const int s = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = smap[s];
@@ -119,11 +122,11 @@ void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, double *Xbar_
     const long n = (long)B * ((long)a.S_new * NX / 2 + (long)a.Kc * NX / 2 + (long)a.Kc * KCW / KV);
     const dim3 g((unsigned)((n + 255) / 256));
     if (a.fp32)
-        hipLaunchKernelGGL(k_shift_gather<float>, g, dim3(256), 0, st, B, a, d.Xbar, d.X, d.Ubar, d.K32, Xbar_new,
-                           Ubar_new, (float *)K_new);
+        hipLaunchKernelGGL(k_shift_gather<float>, g, dim3(256), 0, st, B, a, d, d.K32, Xbar_new, Ubar_new,
+                           (float *)K_new);
     else
-        hipLaunchKernelGGL(k_shift_gather<double>, g, dim3(256), 0, st, B, a, d.Xbar, d.X, d.Ubar, d.K, Xbar_new,
-                           Ubar_new, (double *)K_new);
+        hipLaunchKernelGGL(k_shift_gather<double>, g, dim3(256), 0, st, B, a, d, d.K, Xbar_new, Ubar_new,
+                           (double *)K_new);
 }
 
 // HKDSinglePhaseReference::get_reference_at_t (HKDReference.cpp:8-57) at state slot s of reference

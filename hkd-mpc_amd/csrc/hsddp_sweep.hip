@@ -589,7 +589,7 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
 // MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229) for the wave's two items with their
 // own regularisation.  Returns, per half, -1 (success) or the control slot of the first knot whose
 // Quu fails the PSD test (that knot and the ones below it are not written).
-template <typename real>
+template <typename real, bool EL>
 DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, const Item<real> &it)
 {
     const int pp = L.pp;
@@ -601,7 +601,7 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
     int fail = -1;
     real h[NX], g = 0;
     // both items share one layout (the handle's, or paired by layout: Bufs::pairs)
-    const Lay PL = layout_of(d, b0);
+    const auto PL = layout_of<EL>(d, b0);
     const int P = PL.P();
     for (int i = P - 1; i >= 0; --i) {
         Phase<real> ph;
@@ -699,10 +699,11 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
 
 // ElemState cost / feasibility of element b at the start of the inner iteration
 // (MultiPhaseDDP.cpp:306-307; the reference's summation order)
+template <bool EL>
 DEV void element_cost(const Params &p, const Bufs &d, int b, double &cost, double &feas)
 {
     cost = 0.0; feas = 0.0;
-    const Lay L = layout_of(d, b);
+    const auto L = layout_of<EL>(d, b);
     for (int i = 0; i < L.P(); ++i) {
         double ci = 0.0, fi = 0.0;
         const int N = L.N(i), s0 = L.s0(i);
@@ -747,7 +748,7 @@ using namespace sweep;
 // the sweep with each element's mu, then (for an element whose first sweep fails and that the
 // parallel retry cannot take) mu = max(mu * update_regularization, 1e-3) until a sweep succeeds or
 // mu > 1e2, then mu / 20 (0 below 1e-6) as the next regularisation.
-template <typename real>
+template <typename real, bool EL>
 __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
 {
     __shared__ Lds<real> S;
@@ -760,7 +761,7 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
     // an empty half runs on the other half's element, inactive
     int b, bv;
     bool valid;
-    if (p.elem_layout) {
+    if constexpr (EL) {
         const int e0 = d.pairs[2 * blockIdx.x], e1 = d.pairs[2 * blockIdx.x + 1];
         b = L.e ? e1 : e0;
         valid = b >= 0;
@@ -782,7 +783,7 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
     for (int attempt = 0; __builtin_amdgcn_ballot_w64(need); ++attempt) {
         it.act = need;
         it.reg = (real)reg;
-        const int fk = sweep_pair(p, d, S, L, it);
+        const int fk = sweep_pair<real, EL>(p, d, S, L, it);
         if (need) {
             if (fk < 0) {
                 ok = true;
@@ -804,7 +805,7 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
                     need = false;
                     if (L.pp == 0) {
                         double cost, feas;
-                        element_cost(p, d, bv, cost, feas);
+                        element_cost<EL>(p, d, bv, cost, feas);
                         E.iters += 1; E.cost = cost; E.feas = feas; E.accepted = 0;
                     }
                     act = false;  // finished by k_riccati_select
@@ -821,7 +822,7 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
 #endif
     if (act && L.pp == 0) {
         double cost, feas;
-        element_cost(p, d, bv, cost, feas);
+        element_cost<EL>(p, d, bv, cost, feas);
         double rn = reg / 20;
         if (rn < 1e-06) rn = 0;
         E.iters += 1; E.cost = cost; E.feas = feas; E.accepted = 0;
@@ -834,7 +835,7 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
 // item (f, a) sweeps deferred element f with the a-th next mu of the schedule into its own scratch
 // rows, two items per wave.  Every attempt is the sweep the sequential loop would run with that mu,
 // so taking the first success (k_riccati_select) gives the loop's result.
-template <typename real>
+template <typename real, bool EL>
 __global__ __launch_bounds__(64, 2) void k_riccati_retry(Params p, Bufs d)
 {
     __shared__ Lds<real> S;
@@ -865,7 +866,7 @@ __global__ __launch_bounds__(64, 2) void k_riccati_retry(Params p, Bufs d)
     it.reg = (real)reg;
     it.K = (real *)d.retry_K + slot * p.Kc * KCW;
     it.dU = d.retry_dU + slot * p.Kc * NX;
-    const int fk = sweep_pair(p, d, S, L, it);
+    const int fk = sweep_pair<real, EL>(p, d, S, L, it);
     if (act && L.pp == 0) *flag = fk < 0 ? 1 : -1 - fk;  // success, or -1 - (the failing control slot)
 }
 
@@ -928,17 +929,22 @@ void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
 {
     if (p.retry_cap > 0) (void)hipMemsetAsync(d.retry_count, 0, sizeof(int), st);
     const dim3 g1((unsigned)(p.elem_layout ? p.n_pairs : (p.B + 1) / 2));
-    if (p.fp32)
-        hipLaunchKernelGGL(k_riccati<float>, g1, dim3(64), 0, st, p, d);
-    else
-        hipLaunchKernelGGL(k_riccati<double>, g1, dim3(64), 0, st, p, d);
+    if (p.fp32) {
+        if (p.elem_layout) hipLaunchKernelGGL((k_riccati<float, true>), g1, dim3(64), 0, st, p, d);
+        else hipLaunchKernelGGL((k_riccati<float, false>), g1, dim3(64), 0, st, p, d);
+    } else {
+        if (p.elem_layout) hipLaunchKernelGGL((k_riccati<double, true>), g1, dim3(64), 0, st, p, d);
+        else hipLaunchKernelGGL((k_riccati<double, false>), g1, dim3(64), 0, st, p, d);
+    }
     if (p.retry_cap > 0) {
         const dim3 gr((unsigned)(p.retry_cap * (p.retry_m + (p.retry_m & 1)) / 2)), gs((unsigned)p.retry_cap);
         if (p.fp32) {
-            hipLaunchKernelGGL(k_riccati_retry<float>, gr, dim3(64), 0, st, p, d);
+            if (p.elem_layout) hipLaunchKernelGGL((k_riccati_retry<float, true>), gr, dim3(64), 0, st, p, d);
+            else hipLaunchKernelGGL((k_riccati_retry<float, false>), gr, dim3(64), 0, st, p, d);
             hipLaunchKernelGGL(k_riccati_select<float>, gs, dim3(64), 0, st, p, d);
         } else {
-            hipLaunchKernelGGL(k_riccati_retry<double>, gr, dim3(64), 0, st, p, d);
+            if (p.elem_layout) hipLaunchKernelGGL((k_riccati_retry<double, true>), gr, dim3(64), 0, st, p, d);
+            else hipLaunchKernelGGL((k_riccati_retry<double, false>), gr, dim3(64), 0, st, p, d);
             hipLaunchKernelGGL(k_riccati_select<double>, gs, dim3(64), 0, st, p, d);
         }
     }

@@ -44,8 +44,7 @@ def kernel_bytes(B: int, S: int, Kc: int, P: int, fp32: bool = False, ref_per_el
     # k_rollout (one line-search trial): per slot Xbar, dX read, X, Defect written, cost /
     # feasibility / violation / divergence written; per control knot Ubar, du read, U written
     out["k_rollout"] = B * (S * (4 * NX * d + 4 * d) + Kc * 3 * NX * d + ref)
-    # k_update_nominal: X -> Xbar, Defect -> Defect_bar per slot, U -> Ubar per control knot
-    out["k_update_nominal"] = B * (S * 2 * NX * d * 2 + Kc * NX * d * 2)
+    # (Trajectory::update_nominal_vals moves no bytes: k_decide flips the element's buffer selector)
     return out
 
 
