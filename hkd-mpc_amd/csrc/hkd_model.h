@@ -224,6 +224,99 @@ HKD_FN void hkd_partial_compact(const double *x, const double *u, const double *
     }
 }
 
+// hkd_partial_compact's values, each handed to emit(piece, index, value) as soon as it is computed
+// (piece 0: Se[index], 1: Sw[index], 2: Bw[index]) — the same expression per value, but a column
+// of the omega rows at a time, columns in increasing order (the record's column-major positions,
+// sw_at / bw_at), so a caller that stores each value right away never holds the 102 outputs (or
+// the 3 x 17 moment Jacobian) at once.
+template <typename Emit>
+HKD_FN void hkd_partial_emit(const double *x, const double *u, const double *c, double dt, Emit emit)
+{
+    const double *om = x + 6;
+    double cp = cos(x[1]), sp = sin(x[1]), cr = cos(x[2]), sr = sin(x[2]);
+    double a = sr * om[1] + cr * om[2], b = cr * om[1] - sr * om[2];
+    double icp = 1.0 / cp, tp = sp / cp;
+    emit(0, 0, dt * a * sp / (cp * cp)); emit(0, 1, dt * b / cp); emit(0, 2, 0.0); emit(0, 3, dt * sr / cp);
+    emit(0, 4, dt * cr / cp); emit(0, 5, 0.0); emit(0, 6, -dt * a); emit(0, 7, 0.0); emit(0, 8, dt * cr);
+    emit(0, 9, -dt * sr); emit(0, 10, dt * a * icp * icp); emit(0, 11, dt * tp * b); emit(0, 12, dt);
+    emit(0, 13, dt * sr * tp); emit(0, 14, dt * cr * tp);
+    Rot R, Dy, Dp, Dr;
+    rot_zyx(x, R);
+    rot_zyx_grad(x, Dy, Dp, Dr);
+    // omega rows: column q of M = d(tau - omega x I omega)/dx, then dt Iinv M[:, q]
+    auto col = [&](const double (&v)[3], int q) {
+        double o[3];
+        inertia_inv_apply(v, o);
+        emit(1, q, dt * o[0]); emit(1, 17 + q, dt * o[1]); emit(1, 34 + q, dt * o[2]);
+    };
+    {   // columns 0..2: the contact moment rotated by the Euler-angle derivatives of R
+        double w[3];
+        contact_moment(x, u, c, w);
+        double v[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) v[i] = Dy.r[0][i] * w[0] + Dy.r[1][i] * w[1] + Dy.r[2][i] * w[2];
+        col(v, 0);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) v[i] = Dp.r[0][i] * w[0] + Dp.r[1][i] * w[1] + Dp.r[2][i] * w[2];
+        col(v, 1);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) v[i] = Dr.r[0][i] * w[0] + Dr.r[1][i] * w[1] + Dr.r[2][i] * w[2];
+        col(v, 2);
+    }
+    // R^T skew(f_l) terms: columns 3 + k (summed over the legs in leg order) and 9 + 2 l + k (k < 2)
+    auto tl = [&](int l, int i, int k) {
+        const double *f = u + 3 * l;
+        const double Sf[3][3] = {{0.0, -f[2], f[1]}, {f[2], 0.0, -f[0]}, {-f[1], f[0], 0.0}};
+        return c[l] * (R.r[0][i] * Sf[0][k] + R.r[1][i] * Sf[1][k] + R.r[2][i] * Sf[2][k]);
+    };
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        double v[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) v[i] += tl(l, i, k);
+        col(v, 3 + k);
+    }
+    {   // columns 6..8, gyroscopic: skew(I w) - skew(w) I
+        double Iw[3];
+        inertia_apply(om, Iw);
+        const double Ssk[3][3] = {{0.0, -Iw[2], Iw[1]}, {Iw[2], 0.0, -Iw[0]}, {-Iw[1], Iw[0], 0.0}};
+        const double So[3][3] = {{0.0, -om[2], om[1]}, {om[2], 0.0, -om[0]}, {-om[1], om[0], 0.0}};
+        const double In[3][3] = {{kI00, kI01, kI02}, {kI01, kI11, 0.0}, {kI02, 0.0, kI22}};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            double v[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) v[i] = Ssk[i][k] - (So[i][0] * In[0][k] + So[i][1] * In[1][k] + So[i][2] * In[2][k]);
+            col(v, 6 + k);
+        }
+    }
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            double v[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) v[i] = -tl(l, i, k);
+            col(v, 9 + 2 * l + k);
+        }
+    // B omega rows: dt Iinv R^T c_l skew(r_l), GRF column 3 l + k
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        double r0 = x[12 + 3 * l] - x[3], r1 = x[13 + 3 * l] - x[4], r2 = -x[5];
+        double Sr[3][3] = {{0.0, -r2, r1}, {r2, 0.0, -r0}, {-r1, r0, 0.0}};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            double v[3], o[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) v[i] = c[l] * (R.r[0][i] * Sr[0][k] + R.r[1][i] * Sr[1][k] + R.r[2][i] * Sr[2][k]);
+            inertia_inv_apply(v, o);
+            emit(2, 3 * l + k, dt * o[0]); emit(2, 12 + 3 * l + k, dt * o[1]); emit(2, 24 + 3 * l + k, dt * o[2]);
+        }
+    }
+}
+
 // dense column-major expansion (Eigen layout of the reference's StateMap / ContrlMap)
 HKD_FN void hkd_expand_colmajor(const double *Se, const double *Sw, const double *Bw, const double *c, double dt,
                                 double *A, double *B)

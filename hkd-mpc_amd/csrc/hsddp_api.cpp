@@ -1101,13 +1101,13 @@ extern "C" int hsddp_download_lq(hsddp_handle h, double *A, double *Bm, double *
                     for (int q = 0; q < 5; ++q) a[rr * NX + hkd::se_col(q)] += r[LQ_SE + 5 * rr + q];
                 for (int q = 0; q < 3; ++q) a[(3 + q) * NX + 9 + q] += dt;
                 for (int rr = 0; rr < 3; ++rr)
-                    for (int q = 0; q < 17; ++q) a[(6 + rr) * NX + hkd::sw_col(q)] += r[LQ_SW + 17 * rr + q];
+                    for (int q = 0; q < 17; ++q) a[(6 + rr) * NX + hkd::sw_col(q)] += r[sw_at(rr, q)];
             }
             if (Bm) {
                 double *bb = Bm + o * NN;
                 std::fill(bb, bb + NN, 0.0);
                 for (int rr = 0; rr < 3; ++rr)
-                    for (int q = 0; q < 12; ++q) bb[(6 + rr) * NX + q] = r[LQ_BW + 12 * rr + q];
+                    for (int q = 0; q < 12; ++q) bb[(6 + rr) * NX + q] = r[bw_at(rr, q)];
                 for (int lg = 0; lg < 4; ++lg)
                     for (int a = 0; a < 3; ++a) {
                         bb[(9 + a) * NX + 3 * lg + a] = dt * c[lg] / hkd::kMass;

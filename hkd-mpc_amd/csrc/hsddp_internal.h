@@ -31,14 +31,19 @@ constexpr int KCW = 12 * 24;
 // compact LQ record per control slot.  Every piece starts at an even index (16-byte aligned in
 // fp64); the slot after SE and after SW is an exact zero (written by k_lq) that the sweep's
 // lane-indexed reads use for structurally absent entries.
-constexpr int LQ_SE = 0;                 // 15  A - I, eul rows (+1 zero)
-constexpr int LQ_SW = 16;                // 51  A - I, omega rows (+1 zero)
-constexpr int LQ_BW = 68;                // 36  B, omega rows x GRF cols
+constexpr int LQ_SE = 0;                 // 15  A - I, eul rows (+1 zero), row-major [3][5]
+constexpr int LQ_SW = 16;                // 51  A - I, omega rows (+1 zero), column-major [17][3]
+constexpr int LQ_BW = 68;                // 36  B, omega rows x GRF cols, column-major [12][3]
 constexpr int LQ_LX = 104;               // 24
 constexpr int LQ_LU = 128;               // 24
 constexpr int LQ_RB = 152;               // 24  dt * ReB Hessian, 4 legs x sym 3x3 (00,01,02,11,12,22)
 constexpr int LQW = 176;
 constexpr int LQW32 = 176;               // fp32 record stride (16-byte pieces)
+// record position of omega-row r (0..2) x sparse column q of A - I, and of B's omega row r x GRF
+// column k: column-major, so k_lq emits the pieces in position order (hkd_partial_emit) and
+// stores them through its LDS stage in contiguous chunks
+constexpr int sw_at(int r, int q) { return LQ_SW + 3 * q + r; }
+constexpr int bw_at(int r, int k) { return LQ_BW + 3 * k + r; }
 static_assert(LQ_SE + 15 < LQ_SW && LQ_SW + 51 < LQ_BW && LQ_BW + 36 == LQ_LX && LQ_LX + 24 == LQ_LU &&
               LQ_LU + 24 == LQ_RB && LQ_RB + 24 == LQW, "record layout");
 

@@ -35,11 +35,11 @@ using namespace hkd;
 // element, phase-end slot) left ridx = -1 and their records are skipped.
 constexpr int LQ_STG = 25; // LDS stride per lane (pieces of 24, +1)
 
-template <typename T, int OFF, int N>
-DEV void lq_stage_store(T *wl, const long *ridx, const double *v, T *lq, int ldw, int lane)
+// the wave's staged values (record positions OFF .. OFF + N - 1 at stage columns 0 .. N - 1) to the
+// records, pair by pair, by the still-active lanes
+template <typename T>
+DEV void lq_flush(T *wl, const long *ridx, T *lq, int ldw, int lane, int OFF, int N)
 {
-#pragma unroll
-    for (int j = 0; j < N; ++j) wl[lane * LQ_STG + j] = (T)v[j];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -59,6 +59,14 @@ DEV void lq_stage_store(T *wl, const long *ridx, const double *v, T *lq, int ldw
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename T, int OFF, int N>
+DEV void lq_stage_store(T *wl, const long *ridx, const double *v, T *lq, int ldw, int lane)
+{
+#pragma unroll
+    for (int j = 0; j < N; ++j) wl[lane * LQ_STG + j] = (T)v[j];
+    lq_flush(wl, ridx, lq, ldw, lane, OFF, N);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -119,22 +127,24 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     d.slot_cost[(size_t)b * p.S + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
 
     // the record in the solver's Riccati precision (fp64, or fp32 in config C5's mode)
-    struct Rec {
-        std::conditional_t<F32, float, double> *r;
-        DEV void set(int j, double v) const { r[j] = v; }
-    } const rec{F32 ? (decltype(Rec::r))(d.lq32 + ((size_t)b * p.Kc + kc) * LQW32)
-                    : (decltype(Rec::r))(d.lq + ((size_t)b * p.Kc + kc) * LQW)};
+    T *lqT = F32 ? (T *)d.lq32 : (T *)d.lq;
+    const int ldw = F32 ? LQW32 : LQW;
     double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
-    double Se[SE_N], Sw[SW_N], Bw[BW_N];
-    hkd_partial_compact(x, u, cd, p.dt, Se, Sw, Bw);
-#pragma unroll
-    for (int j = 0; j < SE_N; ++j) rec.set(LQ_SE + j, Se[j]);
-#pragma unroll
-    for (int j = 0; j < SW_N; ++j) rec.set(LQ_SW + j, Sw[j]);
-#pragma unroll
-    for (int j = 0; j < BW_N; ++j) rec.set(LQ_BW + j, Bw[j]);
-    rec.set(LQ_SE + SE_N, 0.0);  // the record's two zero slots (hsddp_internal.h)
-    rec.set(LQ_SW + SW_N, 0.0);
+    // A - I and B pieces (record positions 0 .. 103) in position order (hkd_partial_emit): each
+    // value goes to this wave's LDS stage as it is computed and the stage is stored coalesced, one
+    // contiguous chunk of the records at a time; positions 15 and 67 are the record's zero slots
+    T *wl = stage[w];
+    constexpr int CH_LO[6] = {0, 16, 40, 64, 68, 86}, CH_N[6] = {16, 24, 24, 4, 18, 18};
+    wl[lane * LQ_STG + 15] = 0;
+    hkd_partial_emit(x, u, cd, p.dt, [&](int piece, int j, double v) {
+        const int pos = piece == 0 ? LQ_SE + j : piece == 1 ? sw_at(j / 17, j % 17) : bw_at(j / 12, j % 12);
+        const int ch = pos < 16 ? 0 : pos < 40 ? 1 : pos < 64 ? 2 : pos < 68 ? 3 : pos < 86 ? 4 : 5;
+        wl[lane * LQ_STG + pos - CH_LO[ch]] = (T)v;
+        if (pos == CH_LO[ch] + CH_N[ch] - (ch == 0 || ch == 3 ? 2 : 1)) {  // the chunk's last value
+            lq_flush(wl, sridx[w], lqT, ldw, lane, CH_LO[ch], CH_N[ch]);
+            if (ch == 2) wl[lane * LQ_STG + 67 - 64] = 0;
+        }
+    });
     // lx: tracking + foot regularisation (HKDCost.cpp:22-37)
     double lx[NX];
 #pragma unroll
@@ -146,8 +156,6 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
         lx[3 + j % 3] += -v;
         lx[12 + j] += v;
     }
-    T *lqT = F32 ? (T *)d.lq32 : (T *)d.lq;
-    const int ldw = F32 ? LQW32 : LQW;
     lq_stage_store<T, LQ_LX, NX>(stage[w], sridx[w], lx, lqT, ldw, lane);
     // lu + ReB gradient / Hessian (SinglePhase.cpp:380-394)
     double lu[NU], rb[24];

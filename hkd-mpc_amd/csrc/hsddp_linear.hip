@@ -225,7 +225,7 @@ DEV void lin_knot(const Params &p, const Bufs &d, LinElem<real> &S, LinBuf<real>
             sdx = dt * S.dx[r + 6];
         } else if (r < 9) {
 #pragma unroll
-            for (int q = 0; q < 17; ++q) sdx += lq[LQ_SW + 17 * (r - 6) + q] * S.dx[sw_col(q)];
+            for (int q = 0; q < 17; ++q) sdx += lq[sw_at(r - 6, q)] * S.dx[sw_col(q)];
         }
         real bdu = 0, lxd = lx_.diag * dx, lud = ru * du;
         if (r < 6) {
@@ -235,7 +235,7 @@ DEV void lin_knot(const Params &p, const Bufs &d, LinElem<real> &S, LinBuf<real>
             }
         } else if (r < 9) {
 #pragma unroll
-            for (int c = 0; c < 12; ++c) bdu += lq[LQ_BW + 12 * (r - 6) + c] * S.du[c];
+            for (int c = 0; c < 12; ++c) bdu += lq[bw_at(r - 6, c)] * S.du[c];
         } else if (r < 12) {
 #pragma unroll
             for (int l = 0; l < 4; ++l) bdu += pc.bv[l] * S.du[3 * l + r - 9];

@@ -233,7 +233,7 @@ DEV void emit_SA(real (&acc)[NX], const real (&x)[NX], const real (&cf)[8], real
 {
     auto sw_row = [&](auto I) {
         constexpr int i = I;
-        static_for<17>([&](auto Q) { vfma<V_SW + 17 * i + Q>(acc[sw_col(Q)], cf, x[6 + i]); });
+        static_for<17>([&](auto Q) { vfma<sw_at(i, Q)>(acc[sw_col(Q)], cf, x[6 + i]); });
     };
     auto se_row = [&](auto I) {
         constexpr int i = I;
@@ -260,9 +260,9 @@ DEV void emit_Bc(real (&acc)[HC], real y6, real y7, real y8, const real *y9, con
     for (int q = 0; q < HC; ++q) acc[q] = __builtin_fma(y12[q], bq[q / 3], acc[q]);
 #pragma unroll
     for (int q = 0; q < HC; ++q) acc[q] = __builtin_fma(y9[q % 3], bv[q / 3], acc[q]);
-    static_for<HC>([&](auto Q) { vfma<V_BW + Q>(acc[Q], cf, y6); });
-    static_for<HC>([&](auto Q) { vfma<V_BW + 12 + Q>(acc[Q], cf, y7); });
-    static_for<HC>([&](auto Q) { vfma<V_BW + 24 + Q>(acc[Q], cf, y8); });
+    static_for<HC>([&](auto Q) { vfma<bw_at(0, Q)>(acc[Q], cf, y6); });
+    static_for<HC>([&](auto Q) { vfma<bw_at(1, Q)>(acc[Q], cf, y7); });
+    static_for<HC>([&](auto Q) { vfma<bw_at(2, Q)>(acc[Q], cf, y8); });
 }
 
 // Gaussian elimination without pivoting on the columns held in lanes, then back substitution:
