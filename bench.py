@@ -194,7 +194,9 @@ def main():
         step_b = traffic.step_bytes(B, S, Kc, P, mean_ls, fp32=args.riccati_fp32, ref_per_element=args.mixed)
         gait = "mixed" if args.mixed else args.gait
         metric_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 4096)
+        c1_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 1024)
         label = ("config C5: fp32 Riccati" if args.riccati_fp32 else "BASELINE metric config" if metric_cfg
+                 else "config C1: batch 1024" if c1_cfg
                  else "config C3: jump with resets" if gait == "jump" else "config C4 shard: mixed gaits, 4x50 / 8x25 layouts" if args.mixed
                  else "custom")
         cfg_key = f"{gait}_{args.phases}x{args.knots}_b{B}" + ("_fp32" if args.riccati_fp32 else "")
