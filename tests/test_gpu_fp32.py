@@ -63,3 +63,38 @@ def test_fp32_warm_start_and_gain_round_trip():
     s.close()
     assert np.array_equal(K2, K.astype(np.float32).astype(np.float64))
     assert np.any(K != 0)
+
+
+@pytest.mark.parametrize("B,cap", [(5, None), (200, None), (7, "2")])
+def test_fp32_retries_parallel_equals_sequential(monkeypatch, B, cap):
+    """The fp32 instantiations of the parallel retry (k_riccati_retry<float> / k_riccati_select<float>)
+    and of the in-kernel overflow loop give the sequential schedule's result bit for bit, on the
+    deterministic retry workload of test_gpu_parity.test_retries_match_oracle (r_qJd = -0.5: every
+    element's first sweep fails the PSD test, MultiPhaseDDP.cpp:141-181); against the fp64 path
+    within this module's one-iteration tolerance, with the same line-search decisions."""
+    if cap:
+        monkeypatch.setenv("HSDDP_RETRY_CAP", cap)
+    prob = syn.make_batch(B, 2, 10, "trot")
+    kw = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=3)
+    w = hsddp.Weights()
+    hsddp._lib.lib().hsddp_default_weights(__import__("ctypes").byref(w))
+    w.r_qJd = -0.5
+
+    def run(fp32):
+        s = hsddp.Solver(prob, hsddp.load_settings(**kw), weights=w, riccati_fp32=fp32)
+        s.solve()
+        out = {**s.trajectory(), **s.working(), **s.element_info()}
+        s.close()
+        return out
+
+    g = run(True)
+    monkeypatch.setenv("HSDDP_SEQUENTIAL_RETRY", "1")
+    q = run(True)
+    for f in ("Xbar", "Ubar", "K", "dU", "cost", "status", "n_ls_trials"):
+        assert np.array_equal(g[f], q[f]), f
+    monkeypatch.delenv("HSDDP_SEQUENTIAL_RETRY")
+    r = run(False)
+    assert np.array_equal(g["status"], r["status"]) and np.all(r["status"] == 0)
+    assert np.array_equal(g["n_ls_trials"], r["n_ls_trials"])
+    for f in ("K", "dU", "Xbar", "Ubar"):
+        assert rel(g[f], r[f]) < 5e-5, f
