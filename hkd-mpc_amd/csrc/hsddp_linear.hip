@@ -2,7 +2,7 @@
 //
 // MultiPhaseDDP::linear_rollout (HSDDPSolver/source/MultiPhaseDDP.cpp:20-50) over
 // SinglePhase::linear_rollout (SinglePhase.cpp:144-178), then the merit function
-// (MultiPhaseDDP.cpp:309-318), one wave per element: dX, du = dU + K dX, and the expected cost
+// (MultiPhaseDDP.cpp:309-318), two elements per wave: dX, du = dU + K dX, and the expected cost
 // change of quirk A3 (it replaces the sweep's dV).  Templates on `real` as the sweep
 // (hsddp_sweep.hip): double, or float in config C5's fp32 mode.
 #include "hsddp_wave.h"
@@ -37,17 +37,18 @@ struct PhaseConst {
     real bq[4];  // dt (1 - c_l)   (B rows 12..23)
 };
 
-// Wave-uniform: contacts through the scalar cache, and selects instead of arithmetic so the
-// constants stay in SGPRs (dt * c / m is dt / m or 0 exactly for c in {0, 1}).
+// Both elements' contacts through the scalar cache, then this half's by selects; dt * c / m is
+// dt / m or 0 exactly for c in {0, 1}.
 template <typename real>
-DEV void load_phase(const Params &p, const Bufs &d, size_t b, int i, PhaseConst<real> &pc)
+DEV void load_phase(const Params &p, const Bufs &d, const size_t (&b)[2], int hf, int i, PhaseConst<real> &pc)
 {
     typedef const __attribute__((address_space(4))) int cint;
-    cint *cs = (cint *)(d.contacts + (b * (p.P + 1) + i) * 4);
+    cint *c0 = (cint *)(d.contacts + (b[0] * (p.P + 1) + i) * 4), *c1 = (cint *)(d.contacts + (b[1] * (p.P + 1) + i) * 4);
     pc.cmask = 0;
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
-        pc.c[l] = cs[l];
+        const int a0 = c0[l], a1 = c1[l];
+        pc.c[l] = hf ? a1 : a0;
         pc.cmask |= (pc.c[l] != 0) << l;
         pc.bv[l] = pc.c[l] ? (real)p.dt_m : (real)0;
         pc.bq[l] = pc.c[l] ? (real)0 : (real)p.dt;
@@ -117,13 +118,16 @@ DEV void lxx_row(const Params &p, const PhaseConst<real> &pc, int r, LxxRow<real
 }
 
 // ---------------------------------------------------------------------------------------------
-// MultiPhaseDDP::linear_rollout(1.0): dX, du = dU + K dX, and the expected cost change (quirk
-// A3: it replaces the sweep's dV), then the merit function (MultiPhaseDDP.cpp:309-318).
-// Lanes r < 24 of each half compute row r of the same vectors; the first half stores them.
-// A knot's inputs (compact K, LQ record, Defect[k+1], dU) are one LDS image (4080 bytes in fp64,
-// 2144 in the fp32 mode) filled by 16-byte-per-lane LDS-DMA loads (global_load_lds_dwordx4, four
-// or three instructions); the next knot's image is loaded into the other buffer while this knot
-// computes.
+// MultiPhaseDDP::linear_rollout(1.0): dX, du = dU + K dX, and the expected cost change (quirk A3:
+// it replaces the sweep's dV), then the merit function (MultiPhaseDDP.cpp:309-318).
+// Two elements per wave, one per half-wave (the sweep's pairing, hsddp_sweep.hip): lane r < 24 of
+// half h computes row r of element h's vectors.  A knot's inputs (compact K, LQ record,
+// Defect[k+1], dU) are one LDS image per element (4080 bytes in fp64, 2144 in the fp32 mode) filled
+// by 16-byte-per-lane LDS-DMA loads (global_load_lds_dwordx4, four or three instructions per
+// element); the next knot's images are loaded into the other buffer while this knot computes.  The
+// per-lane DMA sources advance by a fixed per-segment stride from knot to knot, and a knot's dX /
+// du stores are issued after the next knot's DMA so that the wait for the current image never
+// waits for them.
 template <typename real>
 struct LinImg {
     static constexpr int K = 0;                                       // byte offsets
@@ -131,117 +135,180 @@ struct LinImg {
     static constexpr int D = LQ + Prec<real>::LQS * (int)sizeof(real);
     static constexpr int DU = D + NX * (int)sizeof(real);
     static constexpr int END = DU + NX * 8;                           // dU stays fp64
-    static constexpr int NI = (END / 16 + 63) / 64;                   // DMA instructions
-    static_assert(LQ % 16 == 0 && D % 16 == 0 && DU % 16 == 0 && END % 16 == 0 && NI <= 4, "16-byte pieces");
+    static constexpr int NI = (END / 16 + 63) / 64;                   // DMA instructions per element
+    static_assert(LQ % 16 == 0 && D % 16 == 0 && DU % 16 == 0 && END % 16 == 0 && (NI == 4 || NI == 3), "16-byte pieces");
 };
 template <typename real>
 struct LinBuf {
-    alignas(16) char v[LinImg<real>::NI * 64 * 16];
+    alignas(16) char v[2][LinImg<real>::NI * 1024];  // element h's image at v[h]
 };
 template <typename real>
-struct LinElem {
-    real dx[NX], du[NX];
+struct LinVec {
+    real dx[2][NX], du[2][NX];
+};
+
+// This lane's LDS-DMA sources: piece 64 j + lane of each element's image (spare pieces repeat the
+// last), and the per-knot stride of the segment the piece lies in.
+template <typename real>
+struct LinSrc {
+    using I = LinImg<real>;
+    const char *p[2][I::NI];
+    unsigned step[I::NI];
+
+    static DEV int piece(int j, int lane)
+    {
+        const int o = 16 * (64 * j + lane);
+        return o < I::END ? o : I::END - 16;
+    }
+    DEV void init(const Params &pr, const Bufs &d, const size_t (&b)[2], int s, int kc, int lane)
+    {
+#pragma unroll
+        for (int j = 0; j < I::NI; ++j) {
+            const int o = piece(j, lane);
+            step[j] = o < I::LQ ? KCW * sizeof(real) : o < I::D ? Prec<real>::LQS * sizeof(real) : o < I::DU ? NX * sizeof(real) : NX * 8;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const size_t kq = b[h] * pr.Kc + kc;
+                const char *base = o < I::LQ ? (const char *)(Prec<real>::K(d) + kq * KCW) - I::K
+                                 : o < I::D  ? (const char *)(Prec<real>::lq(d) + kq * Prec<real>::LQS) - I::LQ
+                                 : o < I::DU ? (const char *)(Prec<real>::def(d) + (b[h] * pr.S + s + 1) * NX) - I::D
+                                             : (const char *)(d.dU + kq * NX) - I::DU;
+                p[h][j] = base + o;
+            }
+        }
+    }
+    DEV void advance()
+    {
+#pragma unroll
+        for (int j = 0; j < I::NI; ++j) {
+            p[0][j] += step[j];
+            p[1][j] += step[j];
+        }
+    }
 };
 
 // Issued as inline asm so the waitcnt pass does not track the LDS writes (it would otherwise wait
 // for every DMA in flight before any LDS read); lin_knot waits explicitly.  LDS destination of
-// piece t: M0 + 16 * lane, contiguous.
+// element h's piece 64 j + lane: v[h] + 1024 j + 16 lane.
 template <typename real>
-DEV void lin_fetch(LinBuf<real> &buf, const Params &p, const Bufs &d, size_t b, int s, int kc, int lane)
+DEV void lin_fetch(LinBuf<real> &buf, const LinSrc<real> &src)
 {
-    using I = LinImg<real>;
-    const size_t kq = b * p.Kc + kc;
-    // one base per segment, biased so that base + o addresses image byte o
-    const size_t kB = (size_t)(Prec<real>::K(d) + kq * KCW) - I::K,
-                 lB = (size_t)(Prec<real>::lq(d) + kq * Prec<real>::LQS) - I::LQ,
-                 dB = (size_t)(Prec<real>::def(d) + (b * p.S + s + 1) * NX) - I::D,
-                 uB = (size_t)(d.dU + kq * NX) - I::DU;
 #pragma unroll
-    for (int t = 0; t < I::NI; ++t) {
-        int o = 16 * (64 * t + lane);    // first byte of this lane's 16-byte piece
-        o = o < I::END ? o : I::END - 16;  // spare pieces repeat the last
-        const size_t base = o < I::LQ ? kB : o < I::D ? lB : o < I::DU ? dB : uB;
-        const char *src = (const char *)(base + (size_t)o);
-        const unsigned m0 = (unsigned)(size_t)(buf.v + 1024 * t);
-        unsigned keep;  // M0 is compiler-reserved: saved, set (one wait state before the DMA), restored
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(src), "s"(m0)
-                     : "memory");
-    }
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < LinImg<real>::NI; ++j) lds_dma16(src.p[h][j], (unsigned)(size_t)(buf.v[h] + 1024 * j));
 }
 
-// one knot of SinglePhase::linear_rollout (SinglePhase.cpp:144-178) from the LDS image `cur`;
-// when `more`, the next knot's image is requested into `nxt` first
+template <int W>
+DEV void vm_wait()
+{
+    if constexpr (W == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (W == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (W == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (W == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (W == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else static_assert(W < 0, "wait count");
+}
+
+// per-lane constants of one phase
 template <typename real>
-DEV void lin_knot(const Params &p, const Bufs &d, LinElem<real> &S, LinBuf<real> &cur, LinBuf<real> &nxt, bool more,
-                  size_t b, int s, int kc, const PhaseConst<real> &pc, const LxxRow<real> &lx_, real ru, bool cpl,
-                  int krow0, real &dx, real &v1, real &v2)
+struct LinRow {
+    PhaseConst<real> pc;
+    LxxRow<real> lx;
+    real ru;
+    bool cpl;   // control r has a coupled gain row (KCW layout)
+    int krow0;  // its first entry in the K image
+};
+
+// a knot's results, stored one knot later
+template <typename real>
+struct LinOut {
+    double *du, *dx;  // this lane's entries of the pending knot
+    real vu, vx;
+};
+
+// one knot of SinglePhase::linear_rollout (SinglePhase.cpp:144-178) from the LDS images `cur`;
+// when `more`, the next knot's images are requested into `nxt` first; when `pend`, the previous
+// knot's stores follow them
+template <typename real>
+DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<real> &nxt, bool more, bool pend,
+                  LinSrc<real> &src, const LinRow<real> &R, bool st, LinOut<real> &out, real &dx, real &q1s, real &q2s)
 {
     using I = LinImg<real>;
-    const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5, cb = HC * hf;
-    const bool rowl = r < NX, st = rowl && hf == 0;
+    constexpr int NI2 = 2 * I::NI;
+    const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5;
+    const bool rowl = r < NX;
     const int rr = rowl ? r : 0;
     const real dt = p.dt;
-#ifndef HSDDP_LIN_NOWAIT
-#define HSDDP_LIN_NOWAIT 0  // diagnostic (wrong results): no wait for the knot's image
-#endif
     if (more) {
-        lin_fetch(nxt, p, d, b, s + 1, kc + 1, lane);
-        // all but the I::NI just issued
-        if (HSDDP_LIN_NOWAIT) {
-        } else if constexpr (I::NI == 4)
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        src.advance();
+        lin_fetch(nxt, src);
     }
-    static_assert(I::NI == 4 || I::NI == 3, "waitcnt above");
+    if (pend) {
+        if (st) {
+            *out.du = out.vu;
+            *out.dx = out.vx;
+        }
+        out.du += NX;
+        out.dx += NX;
+    }
+    // all but what was just issued: the 2 NI DMA of the next knot, the 2 stores of the previous
+    if (more) {
+        if (pend) vm_wait<NI2 + 2>();
+        else vm_wait<NI2>();
+    } else {
+        if (pend) vm_wait<2>();
+        else vm_wait<0>();
+    }
     LSYNC();
-    const real *kimg = (const real *)(cur.v + I::K), *lq = (const real *)(cur.v + I::LQ),
-               *dd = (const real *)(cur.v + I::D);
-    const double *dUi = (const double *)(cur.v + I::DU);
-    real krow[HC];
+    const char *img = cur.v[hf];
+    const real *kimg = (const real *)(img + I::K), *lq = (const real *)(img + I::LQ), *dd = (const real *)(img + I::D);
+    const double *dUi = (const double *)(img + I::DU);
+    real *sdxv = S.dx[hf], *sduv = S.du[hf];
+    real krow[NX];
 #pragma unroll
-    for (int c = 0; c < HC; ++c) krow[c] = cpl ? kimg[krow0 + c] : (real)0;
+    for (int c = 0; c < NX; ++c) krow[c] = R.cpl ? kimg[R.krow0 + c] : (real)0;
     const real dUr = (real)dUi[rr];
-    if (lane < NX) S.dx[lane] = dx;
+    if (rowl) sdxv[r] = dx;
     LSYNC();
-    real kd = 0;
+    // K dX as two 12-column sums (the order of the one-element-per-wave kernel's two halves)
+    real k0 = 0, k1 = 0;
 #pragma unroll
-    for (int c = 0; c < HC; ++c) kd += krow[c] * S.dx[cb + c];
-    kd += other_half(kd);
-    const real du = dUr + kd;
-    if (lane < NX) S.du[lane] = du;
+    for (int c = 0; c < HC; ++c) {
+        k0 += krow[c] * sdxv[c];
+        k1 += krow[HC + c] * sdxv[HC + c];
+    }
+    const real du = dUr + (k0 + k1);
+    if (rowl) sduv[r] = du;
     LSYNC();
-    real nx = 0, q1 = 0, q2 = 0;
+    real nx = 0;
     if (rowl) {
+        const PhaseConst<real> &pc = R.pc;
         real sdx = 0;
         if (r < 3) {
 #pragma unroll
-            for (int q = 0; q < 5; ++q) sdx += lq[LQ_SE + 5 * r + q] * S.dx[se_col(q)];
+            for (int q = 0; q < 5; ++q) sdx += lq[LQ_SE + 5 * r + q] * sdxv[se_col(q)];
         } else if (r < 6) {
-            sdx = dt * S.dx[r + 6];
+            sdx = dt * sdxv[r + 6];
         } else if (r < 9) {
 #pragma unroll
-            for (int q = 0; q < 17; ++q) sdx += lq[sw_at(r - 6, q)] * S.dx[sw_col(q)];
+            for (int q = 0; q < 17; ++q) sdx += lq[sw_at(r - 6, q)] * sdxv[sw_col(q)];
         }
-        real bdu = 0, lxd = lx_.diag * dx, lud = ru * du;
+        real bdu = 0, lxd = R.lx.diag * dx, lud = R.ru * du;
         if (r < 6) {
             if (r >= 3) {
 #pragma unroll
-                for (int l = 0; l < 4; ++l) lxd += lx_.xq[l] * S.dx[12 + 3 * l + r - 3];
+                for (int l = 0; l < 4; ++l) lxd += R.lx.xq[l] * sdxv[12 + 3 * l + r - 3];
             }
         } else if (r < 9) {
 #pragma unroll
-            for (int c = 0; c < 12; ++c) bdu += lq[bw_at(r - 6, c)] * S.du[c];
+            for (int c = 0; c < 12; ++c) bdu += lq[bw_at(r - 6, c)] * sduv[c];
         } else if (r < 12) {
 #pragma unroll
-            for (int l = 0; l < 4; ++l) bdu += pc.bv[l] * S.du[3 * l + r - 9];
+            for (int l = 0; l < 4; ++l) bdu += pc.bv[l] * sduv[3 * l + r - 9];
         } else {
-            bdu = pick4(pc.bq, (r - 12) / 3) * S.du[r];
-            lxd += lx_.xp * S.dx[3 + (r - 12) % 3];
+            bdu = pick4(pc.bq, (r - 12) / 3) * sduv[r];
+            lxd += R.lx.xp * sdxv[3 + (r - 12) % 3];
         }
         if (r < 12) {
             const real *rb = lq + LQ_RB + 6 * (r / 3);
@@ -249,51 +316,64 @@ DEV void lin_knot(const Params &p, const Bufs &d, LinElem<real> &S, LinBuf<real>
             const real b0 = a == 0 ? rb[0] : a == 1 ? rb[1] : rb[2];
             const real b1 = a == 0 ? rb[1] : a == 1 ? rb[3] : rb[4];
             const real b2 = a == 0 ? rb[2] : a == 1 ? rb[4] : rb[5];
-            lud += b0 * S.du[u0] + b1 * S.du[u0 + 1] + b2 * S.du[u0 + 2];
+            lud += b0 * sduv[u0] + b1 * sduv[u0 + 1] + b2 * sduv[u0 + 2];
         }
         nx = (dx + sdx) + bdu + dd[r];
-        q1 = lq[LQ_LX + r] * dx + lq[LQ_LU + r] * du;
-        q2 = dx * lxd + du * lud;
-        if (st) {
-            const size_t kq = b * p.Kc + kc;
-            d.du[kq * NX + r] = du;
-            d.dX[(b * p.S + s + 1) * NX + r] = nx;
-        }
+        q1s += lq[LQ_LX + r] * dx + lq[LQ_LU + r] * du;
+        q2s += dx * lxd + du * lud;
     }
-    v1 += half_sum(q1);
-    v2 += half_sum(q2);
+    out.vu = du;
+    out.vx = nx;
     dx = nx;
     LSYNC();
 }
 
 template <typename real, bool EL>
-__global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
+__global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
 {
-    __shared__ LinElem<real> S;
+    __shared__ LinVec<real> S;
     __shared__ LinBuf<real> B0;
     __shared__ LinBuf<real> B1;
-    const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5, cb = HC * hf;
-    const size_t b = blockIdx.x;
+    const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5;
+    // the wave's two elements (as k_riccati): 2 blockIdx + h, or a pair of elements with one
+    // layout (Bufs::pairs); an empty half runs on the other half's element, inactive
+    size_t eb[2];
+    bool valid;
+    if constexpr (EL) {
+        const int e0 = d.pairs[2 * blockIdx.x], e1 = d.pairs[2 * blockIdx.x + 1];
+        eb[0] = e0;
+        eb[1] = e1 >= 0 ? e1 : e0;
+        valid = hf == 0 || e1 >= 0;
+    } else {
+        const int e0 = 2 * blockIdx.x, e1 = e0 + 1;
+        eb[0] = e0;
+        eb[1] = e1 < p.B ? e1 : e0;
+        valid = hf == 0 || e1 < p.B;
+    }
+    const size_t b = hf ? eb[1] : eb[0];
     ElemState &E = d.el[b];
-    if (E.done || E.inner_done) return;
-    const bool rowl = r < NX, st = rowl && hf == 0;
+    const bool act = valid && !E.done && !E.inner_done;
+    if (!__builtin_amdgcn_ballot_w64(act)) return;
+    const bool rowl = r < NX, st = rowl && act;
     const int rr = rowl ? r : 0;
     const real *defg = Prec<real>::def(d);
     real v1 = 0, v2 = 0, dx = 0;
-    const auto LY = layout_of<EL>(d, (int)b);
+    const auto LY = layout_of<EL>(d, (int)eb[0]);
     const int P = LY.P();
     for (int i = 0; i < P; ++i) {
-        PhaseConst<real> pc;
-        load_phase(p, d, b, i, pc);
         const int N = LY.N(i), s0 = LY.s0(i), k0 = LY.k0(i);
-        lin_fetch(B0, p, d, b, s0, k0, lane);  // the phase's first knot (its wait is in lin_knot)
+        LinSrc<real> src;
+        src.init(p, d, eb, s0, k0, lane);
+        lin_fetch(B0, src);  // the phase's first knot (its wait is in lin_knot)
+        LinRow<real> R;
+        load_phase(p, d, eb, hf, i, R.pc);
         if (i > 0) { // dx_init = Px dX_end
             const double *Px = d.term + (b * p.P + (i - 1)) * TW + TM_PX;
-            if (lane < NX) S.dx[lane] = dx;
+            if (rowl) S.dx[hf][r] = dx;
             LSYNC();
             real a = 0;
             if (rowl)
-                for (int j = 0; j < NX; ++j) a += (real)Px[r * NX + j] * S.dx[j];
+                for (int j = 0; j < NX; ++j) a += (real)Px[r * NX + j] * S.dx[hf][j];
             dx = a;
             LSYNC();
         } else {
@@ -304,33 +384,36 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
             if (st) d.dX[(b * p.S + s0) * NX + r] = dx;
         }
         // lxx row r (HKDCost.cpp:32): diagonal + foot cross terms
-        LxxRow<real> lx_;
-        lxx_row(p, pc, r, lx_);
-        const real ru = rowl ? (real)(p.dt * r_diag(p, r)) : (real)0;
+        lxx_row(p, R.pc, r, R.lx);
+        R.ru = rowl ? (real)(p.dt * r_diag(p, r)) : (real)0;
         // control r has a gain row only when its B column is non-zero (KCW layout)
-        const bool stl = contact(pc, (rr % HC) / 3) != 0;
-        const bool cpl = rowl && (rr < HC ? stl : !stl);
-        const int krow0 = (rr % HC) * NX + cb;
+        const bool stl = contact(R.pc, (rr % HC) / 3) != 0;
+        R.cpl = rowl && (rr < HC ? stl : !stl);
+        R.krow0 = (rr % HC) * NX;
+        LinOut<real> out{d.du + (b * p.Kc + k0) * NX + rr, d.dX + (b * p.S + s0 + 1) * NX + rr, 0, 0};
+        real q1s = 0, q2s = 0;
         for (int k = 0; k < N; k += 2) {
-            lin_knot(p, d, S, B0, B1, k + 1 < N, b, s0 + k, k0 + k, pc, lx_, ru, cpl, krow0, dx, v1, v2);
-            if (k + 1 < N)
-                lin_knot(p, d, S, B1, B0, k + 2 < N, b, s0 + k + 1, k0 + k + 1, pc, lx_, ru, cpl, krow0, dx, v1, v2);
+            lin_knot(p, S, B0, B1, k + 1 < N, k > 0, src, R, st, out, dx, q1s, q2s);
+            if (k + 1 < N) lin_knot(p, S, B1, B0, k + 2 < N, true, src, R, st, out, dx, q1s, q2s);
+        }
+        if (st) {  // the phase's last knot
+            *out.du = out.vu;
+            *out.dx = out.vx;
         }
         const double *rec = d.term + (b * p.P + i) * TW;
-        if (lane < NX) S.dx[lane] = dx;
+        if (rowl) S.dx[hf][r] = dx;
         LSYNC();
-        real q1 = 0, q2 = 0;
         if (rowl) {
-            q1 = (real)rec[TM_PHIX + r] * dx;
+            q1s += (real)rec[TM_PHIX + r] * dx;
             real a = 0;
-            for (int c = 0; c < NX; ++c) a += (real)rec[TM_PHIXX + r * NX + c] * S.dx[c];
-            q2 = dx * a;
+            for (int c = 0; c < NX; ++c) a += (real)rec[TM_PHIXX + r * NX + c] * S.dx[hf][c];
+            q2s += dx * a;
         }
-        v1 += half_sum(q1);
-        v2 += half_sum(q2);
+        v1 += half_sum(q1s);
+        v2 += half_sum(q2s);
         LSYNC();
     }
-    if (lane == 0) {
+    if (r == 0 && act) {
         const double cost = E.cost, feas = E.feas, w1 = v1, w2 = v2;
         const double dV_abs = fabs(w1 + 0.5 * w2);
         const double rho = (feas > p.feas_thresh) ? dV_abs / ((1 - p.merit_scale) * feas) + p.merit_offset : 0;
@@ -344,12 +427,13 @@ __global__ __launch_bounds__(64) void k_lin_rollout(Params p, Bufs d)
 
 void launch_lin_rollout(const Params &p, const Bufs &d, hipStream_t st)
 {
+    const dim3 g((unsigned)(p.elem_layout ? p.n_pairs : (p.B + 1) / 2));
     if (p.fp32) {
-        if (p.elem_layout) hipLaunchKernelGGL((k_lin_rollout<float, true>), dim3(p.B), dim3(64), 0, st, p, d);
-        else hipLaunchKernelGGL((k_lin_rollout<float, false>), dim3(p.B), dim3(64), 0, st, p, d);
+        if (p.elem_layout) hipLaunchKernelGGL((k_lin_rollout<float, true>), g, dim3(64), 0, st, p, d);
+        else hipLaunchKernelGGL((k_lin_rollout<float, false>), g, dim3(64), 0, st, p, d);
     } else {
-        if (p.elem_layout) hipLaunchKernelGGL((k_lin_rollout<double, true>), dim3(p.B), dim3(64), 0, st, p, d);
-        else hipLaunchKernelGGL((k_lin_rollout<double, false>), dim3(p.B), dim3(64), 0, st, p, d);
+        if (p.elem_layout) hipLaunchKernelGGL((k_lin_rollout<double, true>), g, dim3(64), 0, st, p, d);
+        else hipLaunchKernelGGL((k_lin_rollout<double, false>), g, dim3(64), 0, st, p, d);
     }
 }
 
