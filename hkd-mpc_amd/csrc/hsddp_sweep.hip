@@ -350,8 +350,8 @@ DEV void eliminate(real (&w)[HC], real (&w2)[HC], unsigned long long &bad)
 // sweep (SinglePhase.cpp:357-358) is not formed: the MS linear rollout replaces it (quirk A3).
 template <typename real>
 DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &ph, const Item<real> &it, int kc,
-              real (&h)[NX], real &g, bool &live, bool more, const real *nrec0, const real *ndef0, const real *nrec1,
-              const real *ndef1)
+              real (&h)[NX], real &g, bool &live, bool first, bool more, const real *nrec0, const real *ndef0,
+              const real *nrec1, const real *ndef1)
 {
     typename Lds<real>::Item &I = S.it[L.e];
     const real *img = S.img[L.e];
@@ -359,7 +359,9 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     const real dt = (real)p.dt;
     real reg = it.reg;
     STAMP(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this knot's images (and the last knot's stores)
+    // this knot's images: a phase's first knot waits for them here, every other knot's landed before
+    // the previous knot's output stores (end of knot)
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // coefficient registers: V[16 k + pos] on register k of every DPP row
     real cf[8];
 #pragma unroll
@@ -480,11 +482,7 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     live = live && okh;
     const bool st = live;  // this half writes the knot's outputs
     STAMP(6);
-    // ---- outputs: K_c rows, dU (SinglePhase.cpp:354-356) ----------------------------------------
-    real *Kg = it.K + (size_t)kc * KCW;
-    if (st && L.row)
-#pragma unroll
-        for (int q = 0; q < HC; ++q) Kg[q * NX + pp] = w2[q];
+    // ---- outputs: dU through LDS (K_c rows and dU go out at the end of the knot) ---------------------
     if (pp == NX)  // coupled dU from position 24
 #pragma unroll
         for (int q = 0; q < HC; ++q) I.du[(((ph.cmask >> (q / 3)) & 1) ? 0 : 12) + q] = w2[q];
@@ -498,7 +496,6 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
 #pragma unroll
         for (int q = 0; q < HC; ++q) I.TI[pp * TS + q] = quxs[q];
     SSYNC();
-    if (st && L.row) it.dU[(size_t)kc * NX + pp] = I.du[pp];
     // G = Qx - Qux_c^T Quu_cc^-1 Qu_c = Qx + Qux_c^T dU_c (SinglePhase.cpp:359)
     real gq4[4] = {qx, 0, 0, 0};
 #pragma unroll
@@ -553,7 +550,6 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     for (int c = 0; c < NX; ++c) h[c] = qxx[c] + prow[c];
 #else
     SSYNC();
-    if (st && L.row) it.dU[(size_t)kc * NX + pp] = I.du[pp];
     // K_c columns of both DPP rows at every DPP position (column c of the item on position c & 15
     // of ka (c < 16) or kb (c >= 16)); the coupled dU_c is position 24's: kb at position 8
     real ka[HC], kb[HC];
@@ -582,6 +578,17 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     STAMP(8);
 #endif
     g = L.row ? gq : (real)0;
+    // K_c rows and dU (SinglePhase.cpp:354-356).  Issued after a wait for all vector memory
+    // operations — the next knot's image DMA (requested before the elimination) and the previous
+    // knot's stores, both long complete — so no later wait counts these stores: the next knot reads
+    // its images without waiting (vector memory operations complete in order).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (st && L.row) {
+        real *Kg = it.K + (size_t)kc * KCW;
+#pragma unroll
+        for (int q = 0; q < HC; ++q) Kg[q * NX + pp] = w2[q];
+        it.dU[(size_t)kc * NX + pp] = I.du[pp];
+    }
     SSYNC();
     STAMP(9);
 }
@@ -673,7 +680,8 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
             const bool more = k > 0;
             const int kn = more ? k - 1 : 0;
             const bool was = live;
-            knot(p, S, L, ph, it, k0 + k, h, g, live, more, recp(b0, kn), defp(b0, kn), recp(b1, kn), defp(b1, kn));
+            knot(p, S, L, ph, it, k0 + k, h, g, live, k == N - 1, more, recp(b0, kn), defp(b0, kn), recp(b1, kn),
+                 defp(b1, kn));
             if (was && !live) fail = k0 + k;
             if (!__builtin_amdgcn_ballot_w64(live)) break;
         }
