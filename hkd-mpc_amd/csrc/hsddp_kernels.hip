@@ -243,17 +243,24 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
         for (int l = 0; l < 4; ++l) v += scoef[l][0] * shx[l][j];
         rec[TM_PHIX + j] = v;
     }
+    // foot Hessian 20 D^T Qfoot D: weight of (leg l, axis j), entries (3 + j, 3 + j) (summed over
+    // the legs in leg order), (12 + 3 l + j, 12 + 3 l + j) and, negated, the two cross entries
+    auto fw = [&](int l, int j) { return p.foot_term_grad * sc[l] * sc[l] * foot_weight(kp, sc, 3 * l + j); };
     for (int e = t; e < NN; e += 64) { // Phixx
         const int r = e / NX, cidx = e % NX;
-        double v = (r == cidx) ? kp.qf_gain * kp.qf_scale[r] * q_diag(kp, sc, r) : 0.0;
-        // foot Hessian 20 D^T Qfoot D
-        for (int l = 0; l < 4; ++l)
-            for (int j = 0; j < 3; ++j) {
-                double w = p.foot_term_grad * sc[l] * sc[l] * foot_weight(kp, sc, 3 * l + j);
-                int a = 3 + j, bb = 12 + 3 * l + j;
-                if ((r == a && cidx == a) || (r == bb && cidx == bb)) v += w;
-                if ((r == a && cidx == bb) || (r == bb && cidx == a)) v -= w;
+        double v = 0.0;
+        if (r == cidx) {
+            v = kp.qf_gain * kp.qf_scale[r] * q_diag(kp, sc, r);
+            if (r >= 3 && r < 6) {
+                for (int l = 0; l < 4; ++l) v += fw(l, r - 3);
+            } else if (r >= 12) {
+                v += fw((r - 12) / 3, (r - 12) % 3);
             }
+        } else if (r >= 3 && r < 6 && cidx >= 12 && (cidx - 12) % 3 == r - 3) {
+            v -= fw((cidx - 12) / 3, r - 3);
+        } else if (cidx >= 3 && cidx < 6 && r >= 12 && (r - 12) % 3 == cidx - 3) {
+            v -= fw((r - 12) / 3, cidx - 3);
+        }
         for (int l = 0; l < 4; ++l) v += scoef[l][1] * (shx[l][r] * shx[l][cidx]);
         rec[TM_PHIXX + e] = v;
     }
