@@ -83,7 +83,7 @@ constexpr int TS = 14;        // T / Qux^T / Kp^T image row stride
 constexpr int WS = 25;        // W image row stride (phase boundary)
 // coefficient vector V of a knot image: record [0, 104) = SE | SW | BW, then Defect[k+1] (24), then
 // record [104, 176) = LX | LU | RB
-constexpr int V_SE = LQ_SE, V_SW = LQ_SW, V_BW = LQ_BW, V_D = 104, V_LX = 128, V_LU = 152, V_RB = 176, VW = 200;
+constexpr int V_SE = LQ_SE, V_D = 104, V_LX = 128, V_LU = 152, V_RB = 176, VW = 200;
 static_assert(LQ_BW + 36 == V_D && LQ_LX + 24 == V_LX && LQ_LU + 24 == V_LU && LQ_RB + 24 == V_RB, "image layout");
 
 template <typename real>
