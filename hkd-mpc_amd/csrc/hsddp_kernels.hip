@@ -538,12 +538,18 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
     if (act && g < P) {
         const size_t sb = (size_t)b * p.S + L.s0(g);
         const int N = L.N(g);
+        // one pass, unrolled so that the loads of several slots are in flight together (each sum
+        // keeps its slot order)
+#pragma unroll 10
         for (int k = 0; k < N; ++k) {
             ci += d.slot_cost[sb + k];
             pv = fmin(pv, d.slot_viol[sb + k]);
+            fi += d.slot_feas[sb + k];
+            div |= d.slot_div[sb + k];
         }
         ci += d.slot_cost[sb + N];
-        for (int k = 0; k <= N; ++k) { fi += d.slot_feas[sb + k]; div |= d.slot_div[sb + k]; }
+        fi += d.slot_feas[sb + N];
+        div |= d.slot_div[sb + N];
         tv = d.slot_viol[sb + N];
     }
     double cost = 0.0, feas = 0.0, max_p = 0.0, max_t = 0.0;
