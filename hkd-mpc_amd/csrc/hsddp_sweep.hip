@@ -708,18 +708,28 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
 // ElemState cost / feasibility of element b at the start of the inner iteration
 // (MultiPhaseDDP.cpp:306-307; the reference's summation order)
 template <bool EL>
-DEV void element_cost(const Params &p, const Bufs &d, int b, double &cost, double &feas)
+DEV void element_cost(const Params &p, const Bufs &d, int b, int lane, double &cost, double &feas)
 {
+    // lane g < P of the half sums phase g's slots in slot order (unrolled: ten loads in flight),
+    // then every lane adds the phase sums in phase order (compute_cost's order)
+    const auto LY = layout_of<EL>(d, b);
+    const int P = LY.P(), g = lane & 31;
+    double ci = 0.0, fi = 0.0;
+    if (g < P) {
+        const int N = LY.N(g);
+        const double *c = d.slot_cost + (size_t)b * p.S + LY.s0(g), *f = d.slot_feas + (size_t)b * p.S + LY.s0(g);
+#pragma unroll 10
+        for (int k = 0; k < N; ++k) {
+            ci += c[k];
+            fi += f[k];
+        }
+        ci += c[N];
+        fi += f[N];
+    }
     cost = 0.0; feas = 0.0;
-    const auto L = layout_of<EL>(d, b);
-    for (int i = 0; i < L.P(); ++i) {
-        double ci = 0.0, fi = 0.0;
-        const int N = L.N(i), s0 = L.s0(i);
-        for (int k = 0; k < N; ++k) ci += d.slot_cost[(size_t)b * p.S + s0 + k];
-        ci += d.slot_cost[(size_t)b * p.S + s0 + N];
-        for (int k = 0; k <= N; ++k) fi += d.slot_feas[(size_t)b * p.S + s0 + k];
-        cost += ci;
-        feas += fi;
+    for (int i = 0; i < P; ++i) {
+        cost += __shfl(ci, (lane & 32) + i);
+        feas += __shfl(fi, (lane & 32) + i);
     }
     feas = sqrt(feas);
 }
@@ -782,6 +792,9 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
     ElemState &E = d.el[bv];
     bool act = valid && !E.done && !E.inner_done;
     if (!__builtin_amdgcn_ballot_w64(act)) return;
+    // the slot sums come from k_lq's pass: taken here, all lanes active
+    double ecost, efeas;
+    element_cost<EL>(p, d, bv, L.lane, ecost, efeas);
     double reg = E.reg;
     Item<real> it;
     it.b = bv;
@@ -811,11 +824,7 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
                 }
                 if (deferred) {
                     need = false;
-                    if (L.pp == 0) {
-                        double cost, feas;
-                        element_cost<EL>(p, d, bv, cost, feas);
-                        E.iters += 1; E.cost = cost; E.feas = feas; E.accepted = 0;
-                    }
+                    if (L.pp == 0) { E.iters += 1; E.cost = ecost; E.feas = efeas; E.accepted = 0; }
                     act = false;  // finished by k_riccati_select
                 } else {
                     reg = fmax(reg * p.update_regularization, 1e-03);
@@ -829,11 +838,9 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
     if (L.lane < 12) d.dbg[(size_t)__builtin_amdgcn_readfirstlane(bv) * 16 + L.lane] += S.st[L.lane];
 #endif
     if (act && L.pp == 0) {
-        double cost, feas;
-        element_cost<EL>(p, d, bv, cost, feas);
         double rn = reg / 20;
         if (rn < 1e-06) rn = 0;
-        E.iters += 1; E.cost = cost; E.feas = feas; E.accepted = 0;
+        E.iters += 1; E.cost = ecost; E.feas = efeas; E.accepted = 0;
         if (ok) E.reg = rn;
         else { E.reg = rn; E.status = 1; E.done = 1; E.ls_active = 0; }
     }
