@@ -374,6 +374,51 @@ DEV void stage_trial(double *L, double *const *buf, const double *del, long r0, 
     }
 }
 
+// The same for per >= RW: the wave's 64 slots belong to its elements bA and bB, whose activity and
+// nominal buffers are known (no per-row lookups), and the loads of all chunks are issued before any
+// is used.  Row r0 may be the previous element's last slot: no slot of this wave reads it (slot 0
+// of an element starts from x0 or a reset map of its own rows), so it is skipped.  Rows of
+// inactive elements are read (in range, harmless) but neither staged nor stored.
+DEV void stage_trial2(double *L, const Bufs &d, long r0, long nrows, int per, double eps, int lane, long g0, int bA,
+                      bool aA, int nA, int bB, bool aB, int nB)
+{
+    constexpr int CH = NX / 2, NIT = (RW * CH + 63) / 64;
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    // the two buffers by constant index (a runtime index into the kernel argument is a memory read)
+    const double *barA = nA ? d.Xb[1] : d.Xb[0], *barB = nB ? d.Xb[1] : d.Xb[0], *del = d.dX;
+    double *outA = nA ? d.Xb[0] : d.Xb[1], *outB = nB ? d.Xb[0] : d.Xb[1];
+    d2 xb[NIT], dx[NIT];
+    long rr[NIT];
+    bool use[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int f = lane + 64 * it, row = f / CH, cc = 2 * (f % CH);
+        const long r = r0 + row;
+        const bool in = f < RW * CH && r >= 0 && r < nrows;
+        const long rc = in ? r : (r0 + 1 > 0 ? r0 + 1 : 0);  // a valid row for out-of-range chunks
+        const long eb = rc / per;
+        const bool first = eb == bA;
+        use[it] = in && (first ? aA : eb == bB && aB);
+        rr[it] = rc;
+        const double *bar = first ? barA : barB;
+        xb[it] = *(const d2 *)(bar + rc * NX + cc);
+        dx[it] = *(const d2 *)(del + rc * NX + cc);
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        if (!use[it]) continue;
+        const int f = lane + 64 * it, row = f / CH, cc = 2 * (f % CH);
+        const long r = rr[it];
+        d2 v;
+        v.x = xb[it].x + eps * dx[it].x;
+        v.y = xb[it].y + eps * dx[it].y;
+        L[row * RS + cc] = v.x;
+        L[row * RS + cc + 1] = v.y;
+        const bool first = r / per == bA;
+        if (r >= g0) *(d2 *)((first ? outA : outB) + r * NX + cc) = v;
+    }
+}
+
 #ifndef HSDDP_ROLLOUT_WAVES
 #define HSDDP_ROLLOUT_WAVES 2  // measured: 2 (256 VGPRs, no spills) 0.93 ms/step forward vs 3: 1.23, 4: 1.07
 #endif
@@ -412,7 +457,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     const int nA = nom_buf(d, bA), nB = nom_buf(d, bB);
     auto nomof = [&](int b) { return b == bA ? nA : b == bB ? nB : nom_buf(d, b); };
     const long xr0 = g0 - 1;
-    stage_trial(Xt, d.Xb, d.dX, xr0, total, p.S, eps, lane, active, [&](long r) { return r >= g0; }, nomof);
+    if (p.S >= RW)
+        stage_trial2(Xt, d, xr0, total, p.S, eps, lane, g0, bA, aA, nA, bB, aB, nB);
+    else
+        stage_trial(Xt, d.Xb, d.dX, xr0, total, p.S, eps, lane, active, [&](long r) { return r >= g0; }, nomof);
     __syncthreads();
     if (gid >= total) return;
     const int b = (int)(gid / p.S), s = (int)(gid % p.S);
