@@ -208,7 +208,8 @@ struct hsddp_handle_t {
     Params p;
     Bufs d;
     hipStream_t stream = nullptr;
-    int *host_counter = nullptr;
+    int *host_counter = nullptr;                // [8]: k_count's activity counts, stat sums
+    std::vector<hipEvent_t> events;             // the stats timer's pool (reused, destroyed with the handle)
     std::vector<void *> allocs;
     size_t bytes = 0;
     int Bref = 1;
@@ -420,7 +421,7 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         (rc = dalloc(h, d.reb_eps, B * Kc * 20)) || (rc = dalloc(h, d.al_sigma, B * P * 4)) ||
         (rc = dalloc(h, d.al_lambda, B * P * 4)) || (rc = dalloc(h, d.term_h, B * P * 4)) ||
         (rc = dalloc(h, d.slot_cost, B * S)) || (rc = dalloc(h, d.slot_feas, B * S)) || (rc = dalloc(h, d.slot_viol, B * S)) ||
-        (rc = dalloc(h, d.slot_div, B * S)) || (rc = dalloc(h, d.el, B)) || (rc = dalloc(h, d.counter, 4)) ||
+        (rc = dalloc(h, d.slot_div, B * S)) || (rc = dalloc(h, d.el, B)) || (rc = dalloc(h, d.counter, 8)) ||
         (rc = dalloc(h, (Layout *&)d.lay, B)) || (rc = dalloc(h, (int *&)d.pairs, 2 * B + 2))) {
         hsddp_destroy(h);
         return rc;
@@ -451,7 +452,7 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         }
     }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void **)&h->host_counter, 4 * sizeof(int), 0) != hipSuccess) {
+        hipHostMalloc((void **)&h->host_counter, 8 * sizeof(int), 0) != hipSuccess) {
         hsddp_destroy(h);
         return fail(HSDDP_ERR_DEVICE, "stream / pinned allocation failed");
     }
@@ -481,6 +482,7 @@ extern "C" int hsddp_destroy(hsddp_handle h)
     if (h->value0) hipFree(h->value0);
 
     if (h->host_counter) hipHostFree(h->host_counter);
+    for (hipEvent_t e : h->events) hipEventDestroy(e);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
     return HSDDP_OK;
@@ -722,19 +724,29 @@ namespace {
 struct Timer {
     hipStream_t st;
     bool on;
+    std::vector<hipEvent_t> *pool;  // the handle's events, handed out in order (no create / destroy per launch)
+    size_t used = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[5];  // lq, riccati, forward, other, linear
+    hipEvent_t next()
+    {
+        if (used == pool->size()) {
+            hipEvent_t e;
+            hipEventCreate(&e);
+            pool->push_back(e);
+        }
+        return (*pool)[used++];
+    }
     void begin(int cat, hipEvent_t &e0)
     {
         if (!on) return;
-        hipEventCreate(&e0);
+        e0 = next();
         hipEventRecord(e0, st);
         (void)cat;
     }
     void end(int cat, hipEvent_t e0)
     {
         if (!on) return;
-        hipEvent_t e1;
-        hipEventCreate(&e1);
+        hipEvent_t e1 = next();
         hipEventRecord(e1, st);
         ev[cat].push_back({e0, e1});
     }
@@ -745,8 +757,6 @@ struct Timer {
             float ms = 0;
             hipEventElapsedTime(&ms, pr.first, pr.second);
             t += ms;
-            hipEventDestroy(pr.first);
-            hipEventDestroy(pr.second);
         }
         ev[cat].clear();
         return t;
@@ -850,9 +860,13 @@ static int finish_stats(hsddp_handle h, Timer &tm, hipEvent_t e0, hsddp_stats *s
     stats->inner_iterations = iters;
     stats->outer_iterations = outers;
     stats->n_backward_launches = nbwd;
-    std::vector<ElemState> el(h->p.B);
-    HIPCHK(hipMemcpy(el.data(), h->d.el, h->p.B * sizeof(ElemState), hipMemcpyDeviceToHost));
-    for (auto &e : el) { stats->ls_trials += e.n_ls; stats->element_iterations += e.iters; }
+    // the two sums on the device (a copy of every element's state would be ~0.6 MB per call)
+    HIPCHK(hipMemsetAsync(h->d.counter + 4, 0, 2 * sizeof(int), h->stream));
+    launch_stat_sums(h->p, h->d, h->stream);
+    HIPCHK(hipMemcpyAsync(h->host_counter + 4, h->d.counter + 4, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    stats->ls_trials = h->host_counter[4];
+    stats->element_iterations = h->host_counter[5];
     return HSDDP_OK;
 }
 
@@ -870,7 +884,7 @@ extern "C" int hsddp_solve(hsddp_handle h, hsddp_stats *stats)
 {
     int rc = solve_check(h);
     if (rc) return rc;
-    Timer tm{h->stream, stats != nullptr, {}};
+    Timer tm{h->stream, stats != nullptr, &h->events};
     hipEvent_t e0 = start_stats(h, stats);
     const std::vector<double> trials = ls_steps(h->opt.alpha);
     begin_launches(h);
@@ -914,7 +928,7 @@ extern "C" int hsddp_iterate(hsddp_handle h, int n, hsddp_stats *stats)
     int rc = solve_check(h);
     if (rc) return rc;
     if (n < 0) return fail(HSDDP_ERR_ARG, "negative iteration count");
-    Timer tm{h->stream, stats != nullptr, {}};
+    Timer tm{h->stream, stats != nullptr, &h->events};
     hipEvent_t e0 = start_stats(h, stats);
     const std::vector<double> trials = ls_steps(h->opt.alpha);
     for (int i = 0; i < n; ++i) iteration_launches(h, trials, tm);
@@ -925,7 +939,7 @@ extern "C" int hsddp_solve_end(hsddp_handle h)
 {
     int rc = solve_check(h);
     if (rc) return rc;
-    Timer tm{h->stream, false, {}};
+    Timer tm{h->stream, false, &h->events};
     outer_end_launches(h, tm);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(h->stream));

@@ -123,7 +123,7 @@ struct Bufs {
     // fp32 Riccati mode only: LQ records [B][Kc][LQW32], gains [B][Kc][KCW], Defect copy [B][S][24]
     float *lq32, *K32, *def32;
     ElemState *el;
-    int *counter;                          // [4] host-visible activity counters
+    int *counter;                          // [8] host-visible activity counters [0..2], stat sums [4..5]
     // parallel regularisation retries: deferred elements [retry_cap], their count, per attempt a
     // success flag [retry_cap][retry_m] and the attempt's gains / dU rows [retry_cap][retry_m][Kc][..]
     RetryEntry *retry_list;
@@ -153,6 +153,7 @@ void launch_outer_end(const Params &p, const Bufs &d, hipStream_t st);
 void launch_reset_elements(const Params &p, const Bufs &d, hipStream_t st);
 void launch_init_params(const Params &p, const Bufs &d, hipStream_t st);
 void launch_count(const Params &p, const Bufs &d, int which, hipStream_t st);
+void launch_stat_sums(const Params &p, const Bufs &d, hipStream_t st);
 // dst[c][n] = src[n] for c < copies
 void launch_broadcast(double *dst, const double *src, size_t n, size_t copies, hipStream_t st);
 

@@ -787,6 +787,26 @@ __global__ void k_count(Params p, Bufs d, int which)
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(&d.counter[which], __popcll(m));
 }
 
+// sums of n_ls and iters over the elements into counter[4], counter[5] (hsddp_stats)
+__global__ void k_stat_sums(Params p, Bufs d)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    int a = 0, c = 0;
+    if (b < p.B) {
+        a = d.el[b].n_ls;
+        c = d.el[b].iters;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o);
+        c += __shfl_xor(c, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&d.counter[4], a);
+        atomicAdd(&d.counter[5], c);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // model primitives
 __global__ void k_model_dynamics(const double *x, const double *u, const double *c, double dt, double *xn, int n)
@@ -1073,6 +1093,11 @@ void launch_init_params(const Params &p, const Bufs &d, hipStream_t st)
     if ((long)p.B * p.P * 4 > n) n = (long)p.B * p.P * 4;
     hipLaunchKernelGGL(k_init_params, dim3(blocks_for(n, 256)), dim3(256), 0, st, p, d);
 }
+void launch_stat_sums(const Params &p, const Bufs &d, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_stat_sums, dim3((p.B + 255) / 256), dim3(256), 0, st, p, d);
+}
+
 void launch_count(const Params &p, const Bufs &d, int which, hipStream_t st)
 {
     hipLaunchKernelGGL(k_count, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d, which);
