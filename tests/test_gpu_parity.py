@@ -123,12 +123,20 @@ def test_full_solve_matches_oracle(gait, P, N, mixed):
     g = _run(prob)
     r, chaotic = _chaotic(prob, {}, list(range(16)))
     ok = [b for b in range(16) if b not in chaotic]
-    assert len(ok) >= 12
+    # measured on the oracle: no chaotic element on trot / mixed, one (element 2) on jump 8x25,
+    # whose final cost moves 17 % under a 1e-15 relative x0 perturbation
+    assert len(ok) >= 15
     for f in ("iters", "outer_iters", "status", "n_ls_trials"):
         assert np.array_equal(g[f][ok], r[f][ok]), f
     for f in ("Xbar", "Ubar"):
         assert rel(g[f][ok], r[f][ok]) < 1e-7, f
     assert rel(g["cost"][ok], r["cost"][ok]) < 1e-9
+    # a screened element still ends with the oracle's status and a finite trajectory; its cost is
+    # not comparable (measured: the GPU's rounding takes element 2 of jump 8x25 to a final cost of
+    # 9.4e3 against the oracle's 1.16e3)
+    for b in sorted(chaotic):
+        assert g["status"][b] == r["status"][b], b
+        assert np.all(np.isfinite(g["Xbar"][b])) and np.all(np.isfinite(g["Ubar"][b])), b
 
 
 def test_regularization_overflow_status():
