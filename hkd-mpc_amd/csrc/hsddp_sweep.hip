@@ -21,11 +21,17 @@
 //   Gn = G + H d;  T = H B_c;  M = H A                         (rows in registers)
 //   M, T rows -> LDS; lane c reads column c of M
 //   Z = M + (S^T M)^T (row c);  Qux_c column c = B_c^T M[:, c];  position 24: S^T Gn, Qu_c
-//   Qxx = lxx + reg I + (Z + Z^T) / 2  (lxx, reg added in LDS by ds_add_f64, transposed read)
+//   Qxx = lxx + reg I + (Z + Z^T) / 2  (each lane adds lxx, reg to its own Z row in LDS; transposed
+//                                       read)
 //   Quu_cc column q = luu + reg + B_c^T T[:, q]    (T columns from LDS)
-//   Gauss-Jordan on [Quu_cc | Qux_c | Qu_c]: 12 pivot steps, columns in lanes, pivots by DPP
-//   K = -Quu_cc^-1 Qux_c, dU, G = Qx - Qux_c^T Quu_cc^-1 Qu_c, dV
-//   H = Qxx - Qux_c^T Quu_cc^-1 Qux_c on the matrix cores (v_mfma_f64_16x16x4_f64, symmetric tiles)
+//   the next knot's images requested by LDS-DMA
+//   elimination on [Quu_cc | Qux_c | Qu_c] in LDL^T order (12 pivot steps, pivots by DPP
+//   broadcast, the next pivot's reciprocal threaded through the current step), back substitution
+//   K = -Quu_cc^-1 Qux_c, dU, G = Qx - Qux_c^T Quu_cc^-1 Qu_c  (the sweep's dV is not formed: the
+//   MS linear rollout replaces it, quirk A3)
+//   H = Qxx - Qux_c^T Quu_cc^-1 Qux_c by DPP broadcast of K from the lanes holding it
+//   (HSDDP_VALUE_MFMA = 1: on the matrix cores, v_mfma_f64_16x16x4_f64, symmetric tiles)
+//   K rows and dU stored after one wait for all vector memory operations (nothing waits on them)
 // Only the 12 coupled controls (those whose B column is non-zero, DESIGN.md §3.1 "Decoupled controls") enter
 // the elimination; the other 12 are decoupled: K row 0, dU = -lu / (dt R + reg), exactly as the
 // reference's dense 24-control solve gives them.  PSD test: every elimination pivot of Quu_cc and
