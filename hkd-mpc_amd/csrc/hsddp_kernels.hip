@@ -6,11 +6,12 @@
 //   k_terminal  (elem, phase)  Phix, Phixx (+AL), reset Jacobian   SinglePhase.cpp:286-295; HKDReset.h:78-136
 //   k_riccati   one wave/2 elems regularised Riccati sweep over all phases   (hsddp_sweep.hip)
 //                              MultiPhaseDDP.cpp:141-229; SinglePhase.cpp:298-367
-//   k_lin_rollout one wave/elem  MS linear rollout + merit                    (hsddp_linear.hip)
+//   k_lin_rollout one wave/2 elems  MS linear rollout + merit                (hsddp_linear.hip)
 //                              MultiPhaseDDP.cpp:20-50, 309-318; SinglePhase.cpp:144-178
 //   k_rollout   knot-parallel  one line-search trial (all knots are shooting states)  SinglePhase.cpp:181-233
-//   k_decide    per element    merit acceptance (MultiPhaseDDP.cpp:113-133) + inner-loop exit tests
-//   k_update_nominal           Trajectory::update_nominal_vals (TrajectoryManagement.cpp:110-115)
+//   k_decide    per element    merit acceptance (MultiPhaseDDP.cpp:113-133) + inner-loop exit tests;
+//                              Trajectory::update_nominal_vals (TrajectoryManagement.cpp:110-115)
+//                              is its flip of the element's nominal buffer (no copies)
 // plus the outer AL/ReB updates (ConstraintsBase.h:168-183, 349-365; MultiPhaseDDP.cpp:383-408).
 //
 // Every element carries its own control-flow state (ElemState): regularisation retries, line-search

@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-KERN='k_riccati|k_lin_rollout|k_lq|k_rollout|k_decide|k_update_nominal|k_terminal'
+KERN='k_riccati|k_lin_rollout|k_lq|k_rollout|k_decide|k_terminal'
 # PFX: output-directory prefix; BENCH_ARGS: extra bench.py arguments (e.g. --riccati-fp32)
 PFX=${PFX:-pmc}
 BENCH_ARGS=${BENCH_ARGS:-}
