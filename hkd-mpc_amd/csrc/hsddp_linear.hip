@@ -269,30 +269,51 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
 #pragma unroll
     for (int c = 0; c < NX; ++c) krow[c] = R.cpl ? kimg[R.krow0 + c] : (real)0;
     const real dUr = (real)dUi[rr];
-    if (rowl) sdxv[r] = dx;
-    LSYNC();
+    if (rowl) sdxv[r] = dx;  // for the products with lane-dependent columns below
+    // dX of this half's rows at every lane by DPP position (dxa: rows 0..15, dxb: rows 16..23):
+    // the products with compile-time columns take it by row broadcast, not from LDS
+    real dxa, dxb;
+    row_pair(dx, dxa, dxb);
+    asm volatile("" : "+v"(dxa), "+v"(dxb));
+    asm volatile("s_nop 1");  // DPP sources just written by the permlane swaps
     // K dX as two 12-column sums (the order of the one-element-per-wave kernel's two halves)
     real k0 = 0, k1 = 0;
-#pragma unroll
-    for (int c = 0; c < HC; ++c) {
-        k0 += krow[c] * sdxv[c];
-        k1 += krow[HC + c] * sdxv[HC + c];
-    }
+    static_for<HC>([&](auto C) {
+        constexpr int c = C, c1 = HC + C;
+        bfma<c>(k0, dxa, krow[c]);
+        if constexpr (c1 < 16) bfma<c1>(k1, dxa, krow[c1]);
+        else bfma<c1 - 16>(k1, dxb, krow[c1]);
+    });
     const real du = dUr + (k0 + k1);
+    // A - I rows 0..2 (SE) and 6..8 (SW) for every lane (rows clamped; the results are selected
+    // below): the broadcasts need every source lane active, so no branch around them
+    const int rse = r < 3 ? r : 0, rsw = (r >= 6 && r < 9) ? r - 6 : 0;
+    real se = 0, sw = 0;
+    static_for<5>([&](auto Q) { bfma<se_col(Q)>(se, dxa, lq[LQ_SE + 5 * rse + Q]); });
+    static_for<17>([&](auto Q) {
+        constexpr int col = sw_col(Q);
+        if constexpr (col < 16) bfma<col>(sw, dxa, lq[sw_at(0, Q) + rsw]);
+        else bfma<col - 16>(sw, dxb, lq[sw_at(0, Q) + rsw]);
+    });
     if (rowl) sduv[r] = du;
+    real dua, dub;
+    row_pair(du, dua, dub);
+    asm volatile("" : "+v"(dua), "+v"(dub));
+    asm volatile("s_nop 1");
+    real bw = 0;  // B rows 6..8 (BW) times du, columns 0..11
+    static_for<12>([&](auto C) { bfma<C>(bw, dua, lq[bw_at(0, C) + rsw]); });
+    (void)dub;
     LSYNC();
     real nx = 0;
     if (rowl) {
         const PhaseConst<real> &pc = R.pc;
         real sdx = 0;
         if (r < 3) {
-#pragma unroll
-            for (int q = 0; q < 5; ++q) sdx += lq[LQ_SE + 5 * r + q] * sdxv[se_col(q)];
+            sdx = se;
         } else if (r < 6) {
             sdx = dt * sdxv[r + 6];
         } else if (r < 9) {
-#pragma unroll
-            for (int q = 0; q < 17; ++q) sdx += lq[sw_at(r - 6, q)] * sdxv[sw_col(q)];
+            sdx = sw;
         }
         real bdu = 0, lxd = R.lx.diag * dx, lud = R.ru * du;
         if (r < 6) {
@@ -301,8 +322,7 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
                 for (int l = 0; l < 4; ++l) lxd += R.lx.xq[l] * sdxv[12 + 3 * l + r - 3];
             }
         } else if (r < 9) {
-#pragma unroll
-            for (int c = 0; c < 12; ++c) bdu += lq[bw_at(r - 6, c)] * sduv[c];
+            bdu = bw;
         } else if (r < 12) {
 #pragma unroll
             for (int l = 0; l < 4; ++l) bdu += pc.bv[l] * sduv[3 * l + r - 9];
