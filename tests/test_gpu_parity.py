@@ -330,3 +330,23 @@ def test_trajectory_exports_match_numpy_restatement(gait, P, N):
         if info["n_ls_trials"][b] < 4:  # accepted: the last trial's slot costs are the element's cost
             total = lq["l"][b].sum() + tm["Phi"][b].sum()
             assert abs(total - info["cost"][b]) <= 1e-12 * abs(total), b
+
+
+def test_failed_line_search_keeps_the_last_trial():
+    """Quirk A2 (MultiPhaseDDP.cpp:345-353) on the device: gamma = 1e6 rejects every trial, so the
+    nominal rows stay and the working rows are the last trial (eps = 0.001) — the buffer-flip
+    bookkeeping of k_decide.  The second iteration's LQ linearises about that
+    trial: its result equals the oracle's (test_oracle_pinning pins the oracle's A2)."""
+    prob = syn.make_batch(4, 2, 8, "trot")
+    g0 = _run(prob, no_early_exit=1, max_AL_iter=1, max_DDP_iter=0)
+    g1 = _run(prob, no_early_exit=1, max_AL_iter=1, max_DDP_iter=1, gamma=1e6)
+    assert np.all(g1["n_ls_trials"] == 4) and np.all(g1["status"] == 0)
+    assert np.array_equal(g1["Xbar"], g0["Xbar"]) and np.array_equal(g1["Ubar"], g0["Ubar"])
+    assert np.allclose(g1["X"], g1["Xbar"] + 1e-3 * g1["dX"], rtol=1e-14, atol=1e-14)
+    for n in (1, 2):
+        kw = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=n, gamma=1e6)
+        g = _run(prob, **kw)
+        r = O.solve_batch(prob, O.default_options(**kw), n_threads=8)
+        for f in ("X", "U", "Xbar", "Ubar", "K", "dU"):
+            assert rel(g[f], r[f]) < 1e-9, (n, f)
+        assert np.array_equal(g["n_ls_trials"], r["n_ls_trials"])
