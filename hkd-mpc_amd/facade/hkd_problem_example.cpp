@@ -1,0 +1,368 @@
+// hkd_problem_example — HKDProblem's own problem assembly, registration for registration, solved
+// through the facade on the GPU.  The phases are built exactly as HKD-TrajOpt builds them
+// (HKDProblem.cpp): a std::bind of HKD::Model<T>::dynamics / dynamics_partial with the phase
+// contact and dt, HKDTrackingCost<T>(contact) on an HKDSinglePhaseReference, HKDFootPlaceReg<T>
+// (contact) on the QuadReference, GRFConstraint<T>(contact) with the GRF ReB parameters, a
+// std::bind of HKDReset<T>::resetmap(_partial) with (contact, next contact) and
+// TouchDownConstraint<T>(touchdown legs) with the TD AL parameters; HKDMPC's initial state and
+// solve follow (HKDMPC.cpp:18-70), then `ticks` receding-horizon updates (HKDProblem::update,
+// HKDProblem.cpp:117-222) each re-solved with max_AL_iter = 2, max_DDP_iter = 1 (HKDMPC.cpp:102-103).
+//
+//   hkd_problem_example <quad_reference.csv> <ddp_setting.info> <constraint_params.info> <out_dir> [ticks]
+//
+// Writes per solve n = 0 .. ticks into out_dir: layout_<n>.txt (P, horizons, contacts), x0_<n>.f64,
+// Xbar_<n>.f64 [S][24], Ubar_<n>.f64 [Kc][24], K_<n>.f64 [Kc][24][24], A_<n>.f64, lx_<n>.f64,
+// G0_<n>.f64, H0_<n>.f64 (Trajectory exports) and info_<n>.txt (cost, feas, iters, status, n_ls).
+#include <cstdio>
+#include <fstream>
+#include <functional>
+#include <iostream>
+#include <memory>
+
+#include "hkd_trajopt.hpp"
+
+namespace pc = std::placeholders;
+using std::make_shared;
+using std::shared_ptr;
+
+// HKDProblem (HKDProblem.h:92-160) without its LCM publishing and pretty printing
+template <typename T>
+class HKDProblem {
+public:
+    void set_problem_data(HKDProblemData<T> *pdata_in, const HKDPlanConfig &config)
+    {
+        plan_duration = config.plan_duration;
+        dt_sim = config.timeStep;
+        nsteps_between_mpc = config.nsteps_between_mpc;
+        dt_mpc = dt_sim * nsteps_between_mpc;
+        pdata = pdata_in;
+        quad_ref_ptr = pdata_in->quad_ref_ptr;
+    }
+    void initialization(const std::string &constraint_params_fname);
+    void update();
+
+private:
+    void create_problem_one_phase(shared_ptr<SinglePhase<T, 24, 24, 0>> phase, int idx);
+    void add_tconstr_one_phase(shared_ptr<SinglePhase<T, 24, 24, 0>> phase, int idx);
+
+    HKDProblemData<T> *pdata = nullptr;
+    HKDSinglePhaseReference hkd_reference;
+    HKD::Model<T> hkdModel;
+    HKDReset<T> hkdReset;
+    QuadReference *quad_ref_ptr = nullptr;
+    REB_Param_Struct<T> grf_reb_param, swing_reb_param;
+    AL_Param_Struct<T> td_al_param;
+    float plan_duration = 0, dt_sim = 0, dt_mpc = 0;
+    int nsteps_between_mpc = 0;
+};
+
+// HKDProblem::initialization (HKDProblem.cpp:15-111): the window's phase segmentation (a phase ends
+// where the contact changes or the plan ends), then one SinglePhase per phase with its trajectory
+// initialised on the state reference
+template <typename T>
+void HKDProblem<T>::initialization(const std::string &constraint_params_fname)
+{
+    quad_ref_ptr->initialize(plan_duration);
+    hkd_reference.set_quadruped_reference(quad_ref_ptr);
+
+    VecM<int, 4> contact_prev, contact_cur;
+    VecM<double, 4> contact_duration;
+    float phase_start_time = 0, t = 0;
+    int n_phases = 0;
+    quad_ref_ptr->get_contact_at_t(contact_prev, t);
+    quad_ref_ptr->get_contact_duration_at_t(contact_duration, t);
+    for (; approx_leq_scalar(t, plan_duration); t += dt_sim) {
+        quad_ref_ptr->get_contact_at_t(contact_cur, t);
+        if (contact_cur.cwiseNotEqual(contact_prev).any() || approx_geq_scalar(t, plan_duration)) {
+            const float phase_end_time = t;
+            ++n_phases;
+            pdata->phase_start_times.push_back(phase_start_time);
+            pdata->phase_end_times.push_back(phase_end_time);
+            pdata->phase_contacts.push_back(contact_prev);
+            pdata->phase_horizons.push_back((int)round((phase_end_time - phase_start_time) / dt_sim));
+            pdata->contact_durations.push_back(contact_duration);
+            pdata->is_phase_reach_end.push_back(contact_prev.cwiseNotEqual(contact_prev).any());  // quirk A15: false
+            contact_prev = contact_cur;
+            quad_ref_ptr->get_contact_duration_at_t(contact_duration, t);
+            phase_start_time = phase_end_time;
+        }
+        pdata->n_phases = n_phases;
+    }
+    loadConstrintParameters(constraint_params_fname, grf_reb_param, swing_reb_param, td_al_param);
+
+    for (int i = 0; i < n_phases; i++) {
+        auto phase = make_shared<SinglePhase<T, 24, 24, 0>>();
+        auto traj = make_shared<Trajectory<T, 24, 24, 0>>(dt_sim, pdata->phase_horizons[i]);
+        VecM<double, 24> xr_k;
+        for (int k = 0; k <= pdata->phase_horizons[i]; k++) {
+            hkd_reference.get_reference_at_t(xr_k, pdata->phase_start_times[i] + k * dt_sim);
+            traj->X.at(k) = xr_k.cast<T>();
+            traj->Xbar.at(k) = xr_k.cast<T>();
+        }
+        phase->set_trajectory(traj);
+        create_problem_one_phase(phase, i);
+        add_tconstr_one_phase(phase, i);
+        phase->set_time_offset(pdata->phase_start_times[i] - pdata->phase_start_times[0]);
+        phase->initialization();
+        phase->update_SS_config(pdata->phase_horizons[i] + 1);
+        pdata->trajectory_ptrs.push_back(traj);
+        pdata->phase_ptrs.push_back(phase);
+    }
+}
+
+// HKDProblem::update (HKDProblem.cpp:117-222): per simulation step the window moves on; the front
+// phase loses its first knot (or is dropped when it has shrunk to a point); the back phase grows by
+// a knot, or a new phase starts when the contact at the new horizon end differs and the last phase
+// has already seen a change; then the time offsets and shooting sets are refreshed
+template <typename T>
+void HKDProblem<T>::update()
+{
+    for (int j = 0; j < nsteps_between_mpc; j++) {
+        quad_ref_ptr->step(dt_sim);
+        const float new_start_time = quad_ref_ptr->get_start_time(), new_end_time = quad_ref_ptr->get_end_time();
+        pdata->phase_start_times.front() += dt_sim;
+        if (approx_leq_scalar(pdata->phase_end_times.front(), new_start_time)) {
+            pdata->pop_front_phase();
+        } else {
+            pdata->phase_ptrs.front()->pop_front();
+            pdata->phase_horizons.front()--;
+            pdata->phase_start_times.front() = new_start_time;
+        }
+        VecM<int, 4> new_contact;
+        quad_ref_ptr->get_contact_at_t(new_contact, new_end_time - new_start_time);
+        const bool contact_change = new_contact.cwiseNotEqual(pdata->phase_contacts.back()).any();
+        if (contact_change && pdata->is_phase_reach_end.back()) {
+            const float new_phase_start_time = pdata->phase_end_times.back();
+            const int new_phase_horizon = (int)round((new_end_time - new_phase_start_time) / dt_sim);
+            VecM<double, 4> new_contact_duration;
+            quad_ref_ptr->get_contact_duration_at_t(new_contact_duration, new_end_time - new_start_time);
+            pdata->phase_start_times.push_back(new_phase_start_time);
+            pdata->phase_end_times.push_back(new_end_time);
+            pdata->phase_horizons.push_back(new_phase_horizon);
+            pdata->is_phase_reach_end.push_back(false);
+            pdata->phase_contacts.push_back(new_contact);
+            pdata->contact_durations.push_back(new_contact_duration);
+            pdata->n_phases++;
+            auto traj_to_add = make_shared<Trajectory<T, 24, 24, 0>>(dt_sim, new_phase_horizon);
+            auto phase_to_add = make_shared<SinglePhase<T, 24, 24, 0>>();
+            phase_to_add->set_trajectory(traj_to_add);
+            create_problem_one_phase(phase_to_add, pdata->n_phases - 1);
+            phase_to_add->initialization();
+            pdata->trajectory_ptrs.push_back(traj_to_add);
+            pdata->phase_ptrs.push_back(phase_to_add);
+        } else {
+            pdata->phase_end_times.back() = new_end_time;
+            pdata->phase_horizons.back()++;
+            if (contact_change) pdata->is_phase_reach_end.back() = true;
+            pdata->phase_ptrs.back()->push_back_default();
+        }
+        if (pdata->is_phase_reach_end.back()) add_tconstr_one_phase(pdata->phase_ptrs.back(), pdata->n_phases - 1);
+    }
+    for (int i = 0; i < pdata->n_phases; i++) {
+        pdata->phase_ptrs[i]->set_time_offset(pdata->phase_start_times[i] - pdata->phase_start_times[0]);
+        pdata->phase_ptrs[i]->reset_params();
+        if ((i == pdata->n_phases - 1 && pdata->phase_horizons[i] > 2) || i < pdata->n_phases - 1)
+            pdata->phase_ptrs[i]->update_SS_config(pdata->phase_horizons[i] + 1);
+        pdata->trajectory_ptrs.front()->Ubar[0].setZero();
+    }
+}
+
+// HKDProblem::create_problem_one_phase (HKDProblem.cpp:225-264), call for call
+template <typename T>
+void HKDProblem<T>::create_problem_one_phase(shared_ptr<SinglePhase<T, 24, 24, 0>> phase, int idx)
+{
+    const auto &phase_contact = pdata->phase_contacts[idx];
+    auto dynamics_callback = bind(&HKD::Model<T>::dynamics, &hkdModel, pc::_1, pc::_2, pc::_3, pc::_4, pc::_5,
+                                  phase_contact, (T)dt_sim);
+    auto dynamics_partial_callback = bind(&HKD::Model<T>::dynamics_partial, &hkdModel, pc::_1, pc::_2, pc::_3, pc::_4,
+                                          pc::_5, pc::_6, pc::_7, phase_contact, (T)dt_sim);
+    phase->set_dynamics(dynamics_callback);
+    phase->set_dynamics_partial(dynamics_partial_callback);
+
+    shared_ptr<HKDTrackingCost<T>> track_cost = make_shared<HKDTrackingCost<T>>(phase_contact);
+    track_cost->set_reference(&hkd_reference);
+    phase->add_cost(track_cost);
+
+    shared_ptr<HKDFootPlaceReg<T>> foot_reg = make_shared<HKDFootPlaceReg<T>>(phase_contact);
+    foot_reg->set_quad_reference(quad_ref_ptr);
+    phase->add_cost(foot_reg);
+
+    if (phase_contact.cwiseEqual(1).any()) {
+        shared_ptr<GRFConstraint<T>> grfConstraint = std::make_shared<GRFConstraint<T>>(phase_contact);
+        grfConstraint->update_horizon_len(pdata->phase_horizons[idx]);
+        grfConstraint->create_data();
+        grfConstraint->initialize_params(grf_reb_param);
+        phase->add_pathConstraint(grfConstraint);
+    }
+}
+
+// HKDProblem::add_tconstr_one_phase (HKDProblem.cpp:266-310), call for call
+template <typename T>
+void HKDProblem<T>::add_tconstr_one_phase(shared_ptr<SinglePhase<T, 24, 24, 0>> phase, int idx)
+{
+    const VecM<int, 4> &phase_contact_cur = pdata->phase_contacts[idx];
+    VecM<int, 4> touchdown_status, phase_contact_next;
+    touchdown_status.setZero();
+    if (idx < pdata->n_phases - 1)
+        phase_contact_next = pdata->phase_contacts[idx + 1];
+    else
+        quad_ref_ptr->get_contact_at_t(phase_contact_next, plan_duration + dt_mpc);
+    for (int leg = 0; leg < 4; leg++)
+        if (phase_contact_cur[leg] == 0 && phase_contact_next[leg] == 1) touchdown_status[leg] = 1;
+
+    auto resetmap_callback = bind(&HKDReset<T>::resetmap, &hkdReset, pc::_1, pc::_2, phase_contact_cur, phase_contact_next);
+    auto resetmap_partial_callback =
+        bind(&HKDReset<T>::resetmap_partial, &hkdReset, pc::_1, pc::_2, phase_contact_cur, phase_contact_next);
+    phase->set_resetmap(resetmap_callback);
+    phase->set_resetmap_partial(resetmap_partial_callback);
+
+    if (find_eigen(touchdown_status, 1).size() > 0) {
+        shared_ptr<TouchDownConstraint<T>> tdConstraint = std::make_shared<TouchDownConstraint<T>>(touchdown_status);
+        tdConstraint->create_data();
+        tdConstraint->initialize_params(td_al_param);
+        phase->add_terminalConstraint(tdConstraint);
+    }
+}
+
+template <typename V>
+static void write_bin(const std::string &path, const std::vector<V> &v)
+{
+    std::ofstream f(path, std::ios::binary);
+    f.write((const char *)v.data(), (std::streamsize)(v.size() * sizeof(V)));
+}
+
+static void dump(const std::string &dir, int n, HKDProblemData<double> &pdata, MultiPhaseDDP<double> &solver,
+                 const DVec<double> &x0)
+{
+    const std::string sfx = "_" + std::to_string(n);
+    std::ofstream lay(dir + "/layout" + sfx + ".txt");
+    lay << pdata.n_phases;
+    for (int i = 0; i < pdata.n_phases; ++i) lay << " " << pdata.phase_horizons[i];
+    lay << "\n";
+    std::vector<double> x(x0.data(), x0.data() + 24), Xb, Ub, K, A, lx, G0, H0;
+    for (int i = 0; i < pdata.n_phases; ++i) {
+        auto &tr = *pdata.trajectory_ptrs[i];
+        for (int k = 0; k <= tr.horizon; ++k)
+            for (int j = 0; j < 24; ++j) Xb.push_back(tr.Xbar[k][j]);
+        for (int k = 0; k < tr.horizon; ++k) {
+            for (int j = 0; j < 24; ++j) { Ub.push_back(tr.Ubar[k][j]); lx.push_back(tr.rcostData[k].lx[j]); }
+            for (int a = 0; a < 24; ++a)
+                for (int b = 0; b < 24; ++b) { K.push_back(tr.K[k](a, b)); A.push_back(tr.A[k](a, b)); }
+        }
+        for (int a = 0; a < 24; ++a) {
+            G0.push_back(tr.G[0][a]);
+            for (int b = 0; b < 24; ++b) H0.push_back(tr.H[0](a, b));
+        }
+    }
+    write_bin(dir + "/x0" + sfx + ".f64", x);
+    write_bin(dir + "/Xbar" + sfx + ".f64", Xb);
+    write_bin(dir + "/Ubar" + sfx + ".f64", Ub);
+    write_bin(dir + "/K" + sfx + ".f64", K);
+    write_bin(dir + "/A" + sfx + ".f64", A);
+    write_bin(dir + "/lx" + sfx + ".f64", lx);
+    write_bin(dir + "/G0" + sfx + ".f64", G0);
+    write_bin(dir + "/H0" + sfx + ".f64", H0);
+    const hsddp_element_info &info = solver.element_info();
+    std::ofstream out(dir + "/info" + sfx + ".txt");
+    out.precision(17);
+    out << solver.get_actual_cost() << " " << solver.measure_dynamics_feasibility() << " " << info.iters << " "
+        << info.outer_iters << " " << info.status << " " << info.n_ls_trials << "\n";
+}
+
+// the device problem MultiPhaseDDP::describe derives from the registrations (no device work)
+static void dump_problem(const std::string &dir, int n, const MultiPhaseDDP<double>::Problem &pr)
+{
+    const std::string sfx = "_" + std::to_string(n);
+    const hsddp_problem_desc &d = pr.desc;
+    std::ofstream f(dir + "/desc" + sfx + ".txt");
+    f.precision(17);
+    f << d.n_phases << " " << d.dt;
+    for (int i = 0; i < d.n_phases; ++i) f << " " << d.horizons[i];
+    f << "\n";
+    for (int v : pr.contacts) f << v << " ";
+    f << "\n";
+    const double *w = (const double *)&d.weights;
+    for (size_t j = 0; j < sizeof d.weights / sizeof(double); ++j) f << w[j] << " ";
+    f << "\n";
+    const double *c = (const double *)&d.cparams;
+    for (size_t j = 0; j < sizeof d.cparams / sizeof(double); ++j) f << c[j] << " ";
+    f << "\n";
+    write_bin(dir + "/ref_x" + sfx + ".f64", pr.ref_x);
+    write_bin(dir + "/ref_u" + sfx + ".f64", pr.ref_u);
+    write_bin(dir + "/ref_foot" + sfx + ".f64", pr.ref_foot);
+    write_bin(dir + "/Xbar" + sfx + ".f64", pr.Xbar);
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 5) {
+        std::cerr << "usage: hkd_problem_example <quad_reference.csv> <ddp_setting.info> <constraint_params.info> <out_dir> [ticks] [describe]\n";
+        return 2;
+    }
+    try {
+        const std::string dir = argv[4];
+        const int ticks = argc > 5 ? std::atoi(argv[5]) : 0;
+        if (argc > 6 && std::string(argv[6]) == "describe") {  // host only: what solve() would upload
+            QuadReference quad_reference;
+            quad_reference.load_top_level_data(argv[1]);
+            HKDProblemData<double> pdata;
+            pdata.quad_ref_ptr = &quad_reference;
+            HKDProblem<double> opt_problem;
+            opt_problem.set_problem_data(&pdata, HKDPlanConfig{.6f, 0.01f, 1});
+            opt_problem.initialization(argv[3]);
+            MultiPhaseDDP<double> solver;
+            for (int n = 0; n <= ticks; ++n) {
+                if (n > 0) opt_problem.update();
+                std::deque<shared_ptr<SinglePhaseBase<double>>> multiple_phases(pdata.phase_ptrs.begin(), pdata.phase_ptrs.end());
+                solver.set_multiPhaseProblem(multiple_phases);
+                solver.set_initial_condition(DVec<double>(24));
+                dump_problem(dir, n, solver.describe());
+            }
+            std::printf("hkd_problem_example describe ok\n");
+            return 0;
+        }
+        QuadReference quad_reference;
+        quad_reference.load_top_level_data(argv[1]);
+        HKDProblemData<double> pdata;
+        pdata.quad_ref_ptr = &quad_reference;
+        HKDPlanConfig mpc_config{.6f, 0.01f, 1};
+        HKDProblem<double> opt_problem;
+        opt_problem.set_problem_data(&pdata, mpc_config);
+        opt_problem.initialization(argv[3]);
+        HSDDP_OPTION ddp_options;
+        loadHSDDPSetting(argv[2], ddp_options);
+
+        // HKDMPCSolver::initialize's initial state (HKDMPC.cpp:42-55)
+        Vec3<double> eul, pos;
+        pos[2] = 0.2486;
+        VecM<double, 12> qJ, qdummy;
+        for (int l = 0; l < 4; ++l) { qJ[3 * l] = 0; qJ[3 * l + 1] = -0.8; qJ[3 * l + 2] = 1.6; }
+        compute_hkd_state(eul, pos, qJ, qdummy, pdata.phase_contacts.front());
+        DVec<double> xinit(24);
+        for (int a = 0; a < 3; ++a) xinit[3 + a] = pos[a];
+        for (int j = 0; j < 12; ++j) xinit[12 + j] = qdummy[j];
+
+        MultiPhaseDDP<double> solver;
+        for (int n = 0; n <= ticks; ++n) {
+            if (n > 0) {
+                // HKDMPCSolver::update (HKDMPC.cpp:96-143): the receding-horizon update, the state
+                // the previous plan reaches one step on as the new initial state, two AL x one DDP
+                xinit = DVec<double>(pdata.trajectory_ptrs.front()->Xbar[1]);
+                opt_problem.update();
+                ddp_options.max_AL_iter = 2;
+                ddp_options.max_DDP_iter = 1;
+            }
+            std::deque<shared_ptr<SinglePhaseBase<double>>> multiple_phases;
+            for (auto phase : pdata.phase_ptrs) multiple_phases.push_back(phase);
+            solver.set_multiPhaseProblem(multiple_phases);
+            solver.set_initial_condition(xinit);
+            solver.solve(ddp_options);
+            dump(dir, n, pdata, solver, xinit);
+        }
+        std::printf("hkd_problem_example ok: %d phases, cost %.17g\n", pdata.n_phases, solver.get_actual_cost());
+    } catch (const std::exception &ex) {
+        std::cerr << "error: " << ex.what() << "\n";
+        return 1;
+    }
+    return 0;
+}

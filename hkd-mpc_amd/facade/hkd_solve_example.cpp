@@ -78,8 +78,10 @@ int main(int argc, char **argv)
             hkd::Resetmap rm;
             hkd::ResetmapPartial rmp;
             hkd::TouchDownConstraint td_proto;
+            std::array<int, 4> phase_contact;
             for (int l = 0; l < 4; ++l) {
-                dyn.contact[l] = dpar.contact[l] = rm.contact[l] = rmp.contact[l] = contacts[4 * i + l];
+                phase_contact[l] = dyn.contact[l] = dpar.contact[l] = rm.contact[l] = rmp.contact[l] = td_proto.contact[l] =
+                    contacts[4 * i + l];
                 rm.next_contact[l] = rmp.next_contact[l] = td_proto.next_contact[l] = contacts[4 * (i + 1) + l];
             }
             dyn.dt = dpar.dt = dt;
@@ -90,7 +92,8 @@ int main(int argc, char **argv)
             phase->set_resetmap_partial(rmp);
             phase->add_cost(track);
             phase->add_cost(foot);
-            phase->add_pathConstraint(std::make_shared<hkd::GRFConstraint>());
+            if (phase_contact[0] + phase_contact[1] + phase_contact[2] + phase_contact[3] > 0)  // HKDProblem.cpp:255-263
+                phase->add_pathConstraint(std::make_shared<hkd::GRFConstraint>(phase_contact));
             phase->add_terminalConstraint(std::make_shared<hkd::TouchDownConstraint>(td_proto));
             phases.push_back(phase);
             trajs.push_back(traj);

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -78,14 +79,30 @@ private:
     std::vector<T> v_;
 };
 
+// element-wise comparison result (Eigen's cwiseEqual / cwiseNotEqual ... .any() / .all())
+template <size_t n>
+struct CwiseMask {
+    std::array<bool, n> m{};
+    bool any() const { for (bool b : m) if (b) return true; return false; }
+    bool all() const { for (bool b : m) if (!b) return false; return true; }
+};
+
 template <typename T, size_t n>
 class VecM {
 public:
+    typedef T Scalar;
     VecM() { a_.fill(T(0)); }
     VecM(const DVec<T> &v) { for (size_t i = 0; i < n; ++i) a_[i] = i < v.size() ? v[i] : T(0); }  // Eigen's DVec -> VecM
     static VecM Zero() { return VecM(); }
     static constexpr size_t size() { return n; }
     VecM &operator+=(const VecM &o) { for (size_t i = 0; i < n; ++i) a_[i] += o.a_[i]; return *this; }
+    template <typename U>
+    VecM<U, n> cast() const { VecM<U, n> r; for (size_t i = 0; i < n; ++i) r[i] = static_cast<U>(a_[i]); return r; }
+    CwiseMask<n> cwiseEqual(const T &v) const { CwiseMask<n> r; for (size_t i = 0; i < n; ++i) r.m[i] = a_[i] == v; return r; }
+    CwiseMask<n> cwiseEqual(const VecM &o) const { CwiseMask<n> r; for (size_t i = 0; i < n; ++i) r.m[i] = a_[i] == o.a_[i]; return r; }
+    CwiseMask<n> cwiseNotEqual(const VecM &o) const { CwiseMask<n> r; for (size_t i = 0; i < n; ++i) r.m[i] = a_[i] != o.a_[i]; return r; }
+    bool operator==(const VecM &o) const { return a_ == o.a_; }
+    bool operator!=(const VecM &o) const { return a_ != o.a_; }
     T &operator()(size_t i) { return a_[i]; }
     const T &operator()(size_t i) const { return a_[i]; }
     T &operator[](size_t i) { return a_[i]; }
@@ -331,10 +348,110 @@ public:
     TCostData<T, xs> tcostData;
 };
 
+// ---- what a phase's plugins tell the device solve ----------------------------------------------
+// The device evaluates the HKD model, costs and constraints in its own kernels, so
+// MultiPhaseDDP::solve never calls a plugin per knot.  Instead every plugin that can run there
+// describes itself once per solve through the interfaces below (the cost weights it applies, the
+// references it reads, its constraint parameters); solve() checks that the phases agree with each
+// other and with what one device handle can hold, and refuses anything else.
+namespace hsddp_facade {
+
+// Dynamics / reset callbacks are opaque std::functions (a std::bind of HKD::Model<T>::dynamics in
+// the reference, HKDProblem.cpp:229-239).  solve() reads the contact and dt they bind by calling
+// them once in probe mode: HKD::Model / HKDReset (hkd_trajopt.hpp) record their bound arguments
+// instead of evaluating.  A callback that never reaches them is not the HKD model.
+enum ProbeKind { PROBE_OFF = 0, PROBE_DYNAMICS, PROBE_DYNAMICS_PARTIAL, PROBE_RESET, PROBE_RESET_PARTIAL };
+struct Probe {
+    int kind = PROBE_OFF, hits = 0;
+    int c[4] = {0, 0, 0, 0}, cn[4] = {0, 0, 0, 0};
+    double dt = 0;
+};
+inline Probe &probe()
+{
+    thread_local Probe p;
+    return p;
+}
+// record the bound arguments when probing for `kind`; true = do not evaluate
+template <typename CV, typename DT>
+inline bool probe_record(int kind, const CV &c, const CV *cn, DT dt)
+{
+    Probe &p = probe();
+    if (p.kind != kind) return false;
+    ++p.hits;
+    for (int l = 0; l < 4; ++l) {
+        p.c[l] = (int)c[l];
+        p.cn[l] = cn ? (int)(*cn)[l] : 0;
+    }
+    p.dt = (double)dt;
+    return true;
+}
+
+// One cost term of one phase, as the device evaluates it: the effective weight diagonals under the
+// phase's contact (HKDTrackingCost Q, R, Qf: HKDCost.h:14-36; HKDFootPlaceReg Qfoot: HKDCost.h:56-69)
+// and the references at knot k / time t of the phase (t = t_offset + k dt, SinglePhase.cpp:243-287).
+struct CostSpec {
+    int terms = 0;  // HSDDP_TERM_TRACKING and / or HSDDP_TERM_FOOT
+    // tracking: Q, R, Qf diagonals (off-diagonal entries must be zero)
+    double q[24] = {}, r[24] = {}, qf[24] = {};
+    // foot regularisation: Qfoot diagonal, terminal cost / gradient factors (HKDCost.cpp:49,63)
+    double qfoot[12] = {}, foot_term_cost = 10, foot_term_grad = 20;
+    // the weights themselves when the plugin holds them as hsddp_hkd_weights (hkd:: types)
+    const hsddp_hkd_weights *exact = nullptr;
+    std::function<void(int k, float t, double *xr, double *ur)> track_ref;
+    // foot placements and the body position they are taken relative to (pcom NULL: x_ref's)
+    std::function<void(int k, float t, double *pf, double *pcom)> foot_ref;
+    bool foot_pcom = false;  // foot_ref writes pcom
+};
+struct DeviceCost {
+    virtual ~DeviceCost() = default;
+    virtual void device_spec(CostSpec &spec, const int *contact) const = 0;
+};
+// GRFConstraint + its ReB parameters (HKDConstraints.cpp:7-66, ConstraintsBase.h:204-263)
+struct GrfSpec {
+    int contact[4] = {0, 0, 0, 0};
+    double mu = 0.7, delta = 0.1, delta_min = 0.01, eps = 1;
+};
+struct DevicePathConstraint {
+    virtual ~DevicePathConstraint() = default;
+    virtual void device_spec(GrfSpec &spec) const = 0;
+};
+// TouchDownConstraint + its AL parameters (HKDConstraints.cpp:69-171, ConstraintsBase.h:374-399)
+struct TdSpec {
+    int impact[4] = {0, 0, 0, 0};
+    double sigma = 5, lambda = 0, sigma_max = 0, ground = 0;
+};
+struct DeviceTerminalConstraint {
+    virtual ~DeviceTerminalConstraint() = default;
+    virtual void device_spec(TdSpec &spec) const = 0;
+};
+
+// The weight diagonals the device applies under contact c (q_diag, r_diag, foot_weight and the
+// terminal Qf of csrc/hsddp_device.h), in the device's operation order
+inline void device_diagonals(const hsddp_hkd_weights &w, const int *c, double *q, double *r, double *qf, double *qfoot)
+{
+    for (int j = 0; j < 24; ++j) {
+        const double qb = j < 3 ? w.q_eul[j] : j < 6 ? w.q_pos[j - 3] : j < 9 ? w.q_omega[j - 6] : j < 12 ? w.q_v[j - 9] : 0.0;
+        q[j] = j < 12 ? qb : w.q_qJ * (1 - c[(j - 12) / 3]);
+        r[j] = j < 12 ? w.r_grf : w.r_qJd;
+        qf[j] = w.qf_gain * w.qf_scale[j] * q[j];
+        if (j < 12) qfoot[j] = w.foot_gain * w.foot_w[j % 3] * c[j / 3];
+    }
+}
+
+// device of the facade's point evaluations (the hkd:: plugin virtuals) on this thread
+inline int &device()
+{
+    thread_local int d = 0;
+    return d;
+}
+inline void set_device(int d) { device() = d; }
+
+}  // namespace hsddp_facade
+
 // ---- plugin bases with the reference's signatures ---------------------------------------------
 // CostBase (SinglePhaseInterface.h:35-57).  The solver evaluates costs on the device; a cost runs
-// there only when it is one of the hkd:: registrations below (their virtuals evaluate the same
-// terms on the device for callers that use them point by point).
+// there only when it describes itself to the solve (hsddp_facade::DeviceCost: the hkd:: types
+// below, HKDTrackingCost / HKDFootPlaceReg in hkd_trajopt.hpp).
 template <typename T, size_t xs_, size_t us_, size_t ys_>
 class CostBase {
 public:
@@ -352,6 +469,147 @@ public:
     virtual void terminal_cost_par(TCost &, const State &x, float tend) = 0;
 
     std::string cost_name;
+};
+
+// SinglePhaseReferenceAbstract (SinglePhaseInterface.h:12-34): the reference a tracking cost reads
+template <size_t xs, size_t us, size_t ys>
+class SinglePhaseReferenceAbstract {
+public:
+    virtual ~SinglePhaseReferenceAbstract() = default;
+    virtual void get_reference_at_t(VecM<double, xs> &xr, VecM<double, us> &ur, VecM<double, ys> &yr, float t)
+    {
+        (void)xr; (void)ur; (void)yr; (void)t;
+        std::printf("Need to wrap around the function get_reference_at_t for your problem \n");
+    }
+    virtual void get_reference_at_t(VecM<double, xs> &xr, float t)
+    {
+        (void)xr; (void)t;
+        std::printf("Need to wrap around the function get_reference_at_t for your problem \n");
+    }
+};
+
+// QuadraticCost / QuadraticTrackingCost (SinglePhaseInterface.h:59-134, .cpp:5-118): diagonal-free
+// generic weights Q, R, S, Qf.  Their point evaluations are plain host arithmetic (these are the
+// solver library's generic plugin bases, not the device path: a phase runs on the device only with
+// a cost that describes itself, e.g. HKDTrackingCost, whose Q / R / Qf the solve reads).
+template <typename T, size_t xs_, size_t us_, size_t ys_>
+class QuadraticCost : public CostBase<T, xs_, us_, ys_> {
+public:
+    typedef CostBase<T, xs_, us_, ys_> Base;
+    using typename Base::State;
+    using typename Base::Contrl;
+    using typename Base::Output;
+    using typename Base::RCost;
+    using typename Base::TCost;
+
+    explicit QuadraticCost(const std::string &name = "Quadratic Cost") : Base(name)
+    {
+        Q.setIdentity(); R.setIdentity(); S.setZero(); Qf.setIdentity();
+    }
+    void running_cost(RCost &rc, const State &x, const Contrl &u, const Output &y, T dt, float t = 0) override
+    {
+        (void)t;
+        rc.l = dt * (0.5 * quad(Q, x) + 0.5 * quad(R, u) + 0.5 * quad(S, y));
+    }
+    void running_cost_par(RCost &rc, const State &x, const Contrl &u, const Output &y, T dt, float t = 0) override
+    {
+        (void)t; (void)y;
+        mul(Q, x, dt, rc.lx); mul(R, u, dt, rc.lu);
+        scale(Q, dt, rc.lxx); scale(R, dt, rc.luu); rc.lux.setZero();
+    }
+    void terminal_cost(TCost &tc, const State &x, float tend = 0) override { (void)tend; tc.Phi = 0.5 * quad(Qf, x); }
+    void terminal_cost_par(TCost &tc, const State &x, float tend = 0) override
+    {
+        (void)tend;
+        mul(Qf, x, T(1), tc.Phix);
+        tc.Phixx = Qf;
+    }
+
+protected:
+    template <size_t n>
+    static T quad(const MatMN<T, n, n> &M, const VecM<T, n> &v)
+    {
+        T s = 0;
+        for (size_t a = 0; a < n; ++a)
+            for (size_t b = 0; b < n; ++b) s += v[a] * M(a, b) * v[b];
+        return s;
+    }
+    template <size_t n>
+    static void mul(const MatMN<T, n, n> &M, const VecM<T, n> &v, T f, VecM<T, n> &out)
+    {
+        for (size_t a = 0; a < n; ++a) {
+            T s = 0;
+            for (size_t b = 0; b < n; ++b) s += M(a, b) * v[b];
+            out[a] = f * s;
+        }
+    }
+    template <size_t n>
+    static void scale(const MatMN<T, n, n> &M, T f, MatMN<T, n, n> &out)
+    {
+        for (size_t a = 0; a < n; ++a)
+            for (size_t b = 0; b < n; ++b) out(a, b) = f * M(a, b);
+    }
+    MatMN<T, xs_, xs_> Q;
+    MatMN<T, us_, us_> R;
+    MatMN<T, ys_, ys_> S;
+    MatMN<T, xs_, xs_> Qf;
+};
+
+template <typename T, size_t xs_, size_t us_, size_t ys_>
+class QuadraticTrackingCost : public QuadraticCost<T, xs_, us_, ys_> {
+public:
+    typedef QuadraticCost<T, xs_, us_, ys_> Base;
+    using typename Base::State;
+    using typename Base::Contrl;
+    using typename Base::Output;
+    using typename Base::RCost;
+    using typename Base::TCost;
+
+    explicit QuadraticTrackingCost(const std::string &name = "Quadratic Cost") : Base(name) {}
+    void set_reference(SinglePhaseReferenceAbstract<xs_, us_, ys_> *reference_in) { reference = reference_in; }
+    SinglePhaseReferenceAbstract<xs_, us_, ys_> *get_reference() const { return reference; }
+
+    void running_cost(RCost &rc, const State &x, const Contrl &u, const Output &y, T dt, float t = 0) override
+    {
+        State dx;
+        Contrl du;
+        diff(x, u, t, dx, du);
+        Base::running_cost(rc, dx, du, y, dt, t);
+    }
+    void running_cost_par(RCost &rc, const State &x, const Contrl &u, const Output &y, T dt, float t = 0) override
+    {
+        State dx;
+        Contrl du;
+        diff(x, u, t, dx, du);
+        Base::running_cost_par(rc, dx, du, y, dt, t);
+    }
+    void terminal_cost(TCost &tc, const State &x, float tend = 0) override
+    {
+        State dx;
+        Contrl du;
+        diff(x, Contrl(), tend, dx, du);
+        Base::terminal_cost(tc, dx, tend);
+    }
+    void terminal_cost_par(TCost &tc, const State &x, float tend = 0) override
+    {
+        State dx;
+        Contrl du;
+        diff(x, Contrl(), tend, dx, du);
+        Base::terminal_cost_par(tc, dx, tend);
+    }
+
+private:
+    void diff(const State &x, const Contrl &u, float t, State &dx, Contrl &du) const
+    {
+        if (!reference) throw std::runtime_error(this->cost_name + ": set_reference was not called");
+        VecM<double, xs_> xr;
+        VecM<double, us_> ur;
+        VecM<double, ys_> yr;
+        reference->get_reference_at_t(xr, ur, yr, t);
+        for (size_t j = 0; j < xs_; ++j) dx[j] = x[j] - (T)xr[j];
+        for (size_t j = 0; j < us_; ++j) du[j] = u[j] - (T)ur[j];
+    }
+    SinglePhaseReferenceAbstract<xs_, us_, ys_> *reference = nullptr;
 };
 
 // PathConstraintBase (ConstraintsBase.h:88-327): per-knot constraint data and ReB parameters, the
@@ -596,11 +854,11 @@ class SinglePhase : public SinglePhaseBase<T> {
 public:
     typedef VecM<T, xs> State;
     typedef VecM<T, us> Contrl;
-    typedef VecM<T, ys == 0 ? 1 : ys> Output;
+    typedef VecM<T, ys> Output;  // zero-size for HKD (ys = 0), as HKD::Model's OutputType
     typedef MatMN<T, xs, xs> StateMap;
     typedef MatMN<T, xs, us> ContrlMap;
-    typedef MatMN<T, ys == 0 ? 1 : ys, xs> OutputMap;
-    typedef MatMN<T, ys == 0 ? 1 : ys, us> DirectMap;
+    typedef MatMN<T, ys, xs> OutputMap;
+    typedef MatMN<T, ys, us> DirectMap;
     friend class MultiPhaseDDP<T>;
 
     void set_trajectory(std::shared_ptr<Trajectory<T, xs, us, ys>> traj_) { traj = traj_; phase_horizon = traj_->horizon; }
@@ -731,7 +989,7 @@ struct Arena {
         if (bufs.size() <= i) bufs.resize(i + 1, {nullptr, 0});
         if (bufs[i].second < bytes) {
             if (bufs[i].first) hsddp_device_free(bufs[i].first);
-            bufs[i].first = hsddp_device_alloc(bytes, 0);
+            bufs[i].first = hsddp_device_alloc(bytes, hsddp_facade::device());
             bufs[i].second = bufs[i].first ? bytes : 0;
             if (!bufs[i].first) throw std::runtime_error(hsddp_last_error());
         }
@@ -761,7 +1019,7 @@ inline void on_device(const std::vector<std::pair<const void *, size_t>> &in, co
     }
     for (auto &b : out) dout.push_back(arena().get(slot++, b.second));
     const int rc = call(din, dout);
-    if (rc == HSDDP_OK) hsddp_device_synchronize(0);
+    if (rc == HSDDP_OK) hsddp_device_synchronize(hsddp_facade::device());
     for (size_t i = 0; i < out.size() && rc == HSDDP_OK; ++i) hsddp_memcpy_d2h(out[i].first, dout[i], out[i].second);
     if (rc != HSDDP_OK) throw std::runtime_error(hsddp_last_error());
 }
@@ -842,9 +1100,34 @@ struct HKDCostRefs {
     double knot_dt = 0.01;
 };
 template <int TERMS>
-struct HKDCostTerm : CostBase<double, 24, 24, 0>, HKDCostRefs {
-    hsddp_hkd_weights weights;
+struct HKDCostTerm : CostBase<double, 24, 24, 0>, HKDCostRefs, hsddp_facade::DeviceCost {
+    hsddp_hkd_weights weights;  // TrackingCost: its tracking fields apply; FootPlaceReg: its foot fields
     explicit HKDCostTerm(const std::string &name) : CostBase<double, 24, 24, 0>(name) { hsddp_default_weights(&weights); }
+
+    // the device solve reads this term's weights and its per-knot references (knot k of the phase)
+    void device_spec(hsddp_facade::CostSpec &spec, const int *c) const override
+    {
+        spec.terms = TERMS;
+        spec.exact = &weights;
+        double qfoot[12];
+        hsddp_facade::device_diagonals(weights, c, spec.q, spec.r, spec.qf, qfoot);
+        if (TERMS & HSDDP_TERM_FOOT) {
+            std::copy(qfoot, qfoot + 12, spec.qfoot);
+            spec.foot_term_cost = weights.foot_term_cost;
+            spec.foot_term_grad = weights.foot_term_grad;
+        }
+        const std::string nm = cost_name;
+        if (TERMS & HSDDP_TERM_TRACKING)
+            spec.track_ref = [this, nm](int k, float, double *xr, double *ur) {
+                if (k >= (int)x_ref.size()) throw std::runtime_error(nm + ": reference lengths must match the horizon");
+                for (int j = 0; j < 24; ++j) { xr[j] = x_ref[k][j]; ur[j] = k < (int)u_ref.size() ? u_ref[k][j] : 0.0; }
+            };
+        if (TERMS & HSDDP_TERM_FOOT)
+            spec.foot_ref = [this, nm](int k, float, double *pf, double *) {
+                if (k >= (int)foot_ref.size()) throw std::runtime_error(nm + ": reference lengths must match the horizon");
+                for (int j = 0; j < 12; ++j) pf[j] = foot_ref[k][j];
+            };
+    }
 
     void running_cost(RCost &rc, const State &x, const Contrl &u, const Output &, double dt, float t) override
     {
@@ -917,8 +1200,8 @@ struct FootPlaceReg : HKDCostTerm<HSDDP_TERM_FOOT> {
 
 // GRFConstraint + ReB (HKDConstraints.h:8-27, HKDConstraints.cpp:7-66; ConstraintsBase.h:204-263):
 // 5 friction-pyramid rows per stance leg
-struct GRFConstraint : PathConstraintBase<double, 24, 24, 0> {
-    hsddp_constraint_params cparams;
+struct GRFConstraint : PathConstraintBase<double, 24, 24, 0>, hsddp_facade::DevicePathConstraint {
+    hsddp_constraint_params cparams;  // mu_fric and the GRF_ReB parameters apply
     std::array<int, 4> ctact_status{{1, 1, 1, 1}};
     GRFConstraint() : PathConstraintBase("GRF") { hsddp_default_constraint_params(&cparams); set_contact(ctact_status); }
     explicit GRFConstraint(const std::array<int, 4> &ctact) : GRFConstraint() { set_contact(ctact); }
@@ -930,6 +1213,12 @@ struct GRFConstraint : PathConstraintBase<double, 24, 24, 0> {
         update_constraint_size(5 * n);
     }
     void set_friction_coefficient(double mu) { cparams.mu_fric = mu; }
+    void device_spec(hsddp_facade::GrfSpec &spec) const override
+    {
+        for (int l = 0; l < 4; ++l) spec.contact[l] = ctact_status[l];
+        spec.mu = cparams.mu_fric;
+        spec.delta = cparams.grf_delta; spec.delta_min = cparams.grf_delta_min; spec.eps = cparams.grf_eps;
+    }
     void compute_violation(const State &, const Contrl &u, const Output &, int k) override
     {
         if (data.empty()) create_data();
@@ -959,10 +1248,22 @@ private:
 // TouchDownConstraint + AL (HKDConstraints.h:29-51, HKDConstraints.cpp:69-171;
 // ConstraintsBase.h:374-399).  next_contact: the contact after the phase (the legs touching down
 // are those with contact 0 now and 1 next); ctor(impact_status) as the reference's.
-struct TouchDownConstraint : TerminalConstraintBase<double, 24> {
+struct TouchDownConstraint : TerminalConstraintBase<double, 24>, hsddp_facade::DeviceTerminalConstraint {
     std::array<int, 4> contact{}, next_contact{};
     double ground_height = 0;
     TouchDownConstraint() : TerminalConstraintBase("TouchDwon") {}
+    // AL parameters: initialize_params' (ConstraintsBase.h:349-353), else the constraint_params.info defaults
+    void device_spec(hsddp_facade::TdSpec &spec) const override
+    {
+        for (int l = 0; l < 4; ++l) spec.impact[l] = contact[l] == 0 && next_contact[l] == 1;
+        hsddp_constraint_params cp;
+        hsddp_default_constraint_params(&cp);
+        const bool set = !params.empty();
+        spec.sigma = set ? param_init.sigma : cp.td_sigma;
+        spec.lambda = set ? param_init.lambda : cp.td_lambda;
+        spec.sigma_max = set ? param_init.sigma_max : cp.td_sigma_max;
+        spec.ground = ground_height;
+    }
     explicit TouchDownConstraint(const std::array<int, 4> &impact_status) : TouchDownConstraint()
     {
         for (int l = 0; l < 4; ++l) { contact[l] = impact_status[l] ? 0 : 1; next_contact[l] = 1; }
@@ -1017,11 +1318,25 @@ public:
         max_pconstr = max_tconstr = 0;
     }
     void set_initial_condition(DVec<T> x0_in) { x0 = x0_in; }
+    // extension: the HIP device this solver runs on (default 0)
+    void set_device(int d) { device = d; }
 
     // MultiPhaseDDP::solve (MultiPhaseDDP.cpp:232-428) for this one trajectory on the GPU; afterwards
     // every phase's Trajectory holds the solution, the working trajectory, the LQ model and terminal
     // data of the last LQ_approximation and the value function at the phase start
     void solve(HSDDP_OPTION option);
+
+    // The device problem the phases describe (no device work): descriptor (layout, dt, weights,
+    // ReB / AL parameters), contacts [P+1][4], per-slot references and the warm start.  solve()
+    // uploads exactly this; it throws std::runtime_error for anything one device handle cannot
+    // hold or that is not the HKD problem.
+    struct Problem {
+        hsddp_problem_desc desc;
+        int S = 0, Kc = 0;
+        std::vector<int> contacts;
+        std::vector<double> ref_x, ref_u, ref_foot, Xbar, Ubar, K;
+    };
+    Problem describe();
 
     T get_actual_cost() { return actual_cost; }
     T measure_dynamics_feasibility(int = 2) { return feas; }
@@ -1040,6 +1355,10 @@ public:
 
 private:
     typedef hkd::Phase Phase;
+    struct Bound {  // the arguments a dynamics / reset registration binds
+        int c[4] = {0, 0, 0, 0}, cn[4] = {0, 0, 0, 0};
+        double dt = 0;
+    };
     void release()
     {
         if (handle) hsddp_destroy(handle);
@@ -1049,96 +1368,345 @@ private:
     {
         if (rc != HSDDP_OK) throw std::runtime_error(std::string("hsddp: ") + hsddp_last_error());
     }
-    template <typename P, typename F>
-    static const P *plugin(const F &f, const char *what, int i)
+    [[noreturn]] static void refuse(int i, const std::string &what)
     {
-        const P *p = f ? f.template target<P>() : nullptr;
-        if (!p)
-            throw std::runtime_error("phase " + std::to_string(i) + ": " + what +
-                                     " is not the HKD registration (hkd::" + what +
-                                     "); only HKD problems run on the device");
-        return p;
+        throw std::runtime_error("phase " + std::to_string(i) + ": " + what);
     }
+    // call a registered callback once in probe mode: true when it reached the HKD model / reset
+    template <typename F, typename... A>
+    static bool probe_call(int kind, const F &f, Bound &out, A &...args)
+    {
+        if (!f) return false;
+        struct Guard {
+            ~Guard() { hsddp_facade::probe().kind = hsddp_facade::PROBE_OFF; }
+        } guard;
+        hsddp_facade::Probe &p = hsddp_facade::probe();
+        p.kind = kind;
+        p.hits = 0;
+        try {
+            f(args...);
+        } catch (...) {
+            return false;
+        }
+        if (p.hits != 1) return false;
+        for (int l = 0; l < 4; ++l) { out.c[l] = p.c[l]; out.cn[l] = p.cn[l]; }
+        out.dt = p.dt;
+        return true;
+    }
+    static bool read_dynamics(const Phase &ph, Bound &b);
+    static bool read_dynamics_partial(const Phase &ph, Bound &b);
+    static int read_reset(const Phase &ph, Bound &b);  // 0: none registered, 1: read, -1: not HKDReset
+    static hsddp_hkd_weights derive_weights(const std::vector<hsddp_facade::CostSpec> &track,
+                                            const std::vector<hsddp_facade::CostSpec> &foot,
+                                            const std::vector<int> &contacts);
 
     std::deque<std::shared_ptr<SinglePhaseBase<T>>> phases;
-    int n_phases = 0;
+    int n_phases = 0, device = 0;
     DVec<T> x0;
     T actual_cost = 0, feas = 0, max_pconstr = 0, max_tconstr = 0;
     std::vector<float> cost_buffer, dyn_feas_buffer, eqn_feas_buffer, ineq_feas_buffer;
     hsddp_element_info info{};
     hsddp_handle handle = nullptr;
+    hsddp_problem_desc handle_desc{};
 };
 
 template <typename T>
-void MultiPhaseDDP<T>::solve(HSDDP_OPTION option)
+bool MultiPhaseDDP<T>::read_dynamics(const Phase &ph, Bound &b)
+{
+    if (const auto *d = ph.dynamics.template target<hkd::Dynamics>()) {
+        for (int l = 0; l < 4; ++l) b.c[l] = d->contact[l];
+        b.dt = d->dt;
+        return true;
+    }
+    typename Phase::State xn, x;
+    typename Phase::Output y;
+    typename Phase::Contrl u;
+    double t = 0;
+    return probe_call(hsddp_facade::PROBE_DYNAMICS, ph.dynamics, b, xn, y, x, u, t);
+}
+
+template <typename T>
+bool MultiPhaseDDP<T>::read_dynamics_partial(const Phase &ph, Bound &b)
+{
+    if (const auto *d = ph.dynamics_partial.template target<hkd::DynamicsPartial>()) {
+        for (int l = 0; l < 4; ++l) b.c[l] = d->contact[l];
+        b.dt = d->dt;
+        return true;
+    }
+    typename Phase::StateMap A;
+    typename Phase::ContrlMap B;
+    typename Phase::OutputMap C;
+    typename Phase::DirectMap D;
+    typename Phase::State x;
+    typename Phase::Contrl u;
+    double t = 0;
+    return probe_call(hsddp_facade::PROBE_DYNAMICS_PARTIAL, ph.dynamics_partial, b, A, B, C, D, x, u, t);
+}
+
+template <typename T>
+int MultiPhaseDDP<T>::read_reset(const Phase &ph, Bound &b)
+{
+    const auto &f = ph.resetmap_func_handle;
+    const auto &fp = ph.resetmap_partial_func_handle;
+    if (!f && !fp) return 0;
+    Bound bp;
+    if (const auto *r = f.template target<hkd::Resetmap>()) {
+        for (int l = 0; l < 4; ++l) { b.c[l] = r->contact[l]; b.cn[l] = r->next_contact[l]; }
+    } else {
+        DVec<double> xn(24), x(24);
+        if (!probe_call(hsddp_facade::PROBE_RESET, f, b, xn, x)) return -1;
+    }
+    if (const auto *r = fp.template target<hkd::ResetmapPartial>()) {
+        for (int l = 0; l < 4; ++l) { bp.c[l] = r->contact[l]; bp.cn[l] = r->next_contact[l]; }
+    } else {
+        DMat<double> Px(24, 24);
+        DVec<double> x(24);
+        if (!probe_call(hsddp_facade::PROBE_RESET_PARTIAL, fp, bp, Px, x)) return -1;
+    }
+    for (int l = 0; l < 4; ++l)
+        if (b.c[l] != bp.c[l] || b.cn[l] != bp.cn[l]) return -1;
+    return 1;
+}
+
+// One hsddp_hkd_weights that reproduces every phase's effective diagonals bit for bit (the device
+// holds one weight set per handle and masks it by each phase's contact).  Terms holding their weights
+// as hsddp_hkd_weights (hkd::) give them directly; for the reference's classes (Q, R, Qf, Qfoot
+// matrices) the gains keep their default and each scale is the quotient that reproduces the product
+// the device forms.
+template <typename T>
+hsddp_hkd_weights MultiPhaseDDP<T>::derive_weights(const std::vector<hsddp_facade::CostSpec> &track,
+                                                   const std::vector<hsddp_facade::CostSpec> &foot,
+                                                   const std::vector<int> &contacts)
+{
+    hsddp_hkd_weights w;
+    hsddp_default_weights(&w);
+    const int P = (int)track.size();
+    // the factor f with g * f == target (g * f rounded): the default when it does, else near target / g
+    auto factor = [](double g, double target, double dflt) {
+        if (target == 0 || g * dflt == target) return dflt;
+        const double f0 = target / g;
+        for (double f : {f0, std::nextafter(f0, 1e300), std::nextafter(f0, -1e300)})
+            if (g * f == target) return f;
+        return f0;
+    };
+    if (track[0].exact) {
+        const hsddp_hkd_weights &e = *track[0].exact;
+        std::memcpy(w.q_eul, e.q_eul, sizeof w.q_eul); std::memcpy(w.q_pos, e.q_pos, sizeof w.q_pos);
+        std::memcpy(w.q_omega, e.q_omega, sizeof w.q_omega); std::memcpy(w.q_v, e.q_v, sizeof w.q_v);
+        w.q_qJ = e.q_qJ; std::memcpy(w.qf_scale, e.qf_scale, sizeof w.qf_scale); w.qf_gain = e.qf_gain;
+        w.r_grf = e.r_grf; w.r_qJd = e.r_qJd;
+    } else {
+        const double *q = track[0].q;
+        for (int a = 0; a < 3; ++a) { w.q_eul[a] = q[a]; w.q_pos[a] = q[3 + a]; w.q_omega[a] = q[6 + a]; w.q_v[a] = q[9 + a]; }
+        w.r_grf = track[0].r[0];
+        w.r_qJd = track[0].r[12];
+        bool qj = false;
+        for (int i = 0; i < P && !qj; ++i)
+            for (int l = 0; l < 4 && !qj; ++l)
+                if (!contacts[4 * i + l]) { w.q_qJ = track[i].q[12 + 3 * l]; qj = true; }
+        // the device forms (qf_gain * qf_scale) * q: the scale whose product rounds to Qf
+        for (int j = 0; j < 24; ++j)
+            for (int i = 0; i < P; ++i)
+                if (track[i].q[j] != 0) {
+                    const double tq = track[i].qf[j], qq = track[i].q[j], s0 = tq / qq / w.qf_gain;
+                    for (double s : {w.qf_scale[j], s0, std::nextafter(s0, 1e300), std::nextafter(s0, -1e300)})
+                        if (w.qf_gain * s * qq == tq) { w.qf_scale[j] = s; break; }
+                    break;
+                }
+    }
+    if (foot[0].exact) {
+        const hsddp_hkd_weights &e = *foot[0].exact;
+        std::memcpy(w.foot_w, e.foot_w, sizeof w.foot_w);
+        w.foot_gain = e.foot_gain;
+    } else {
+        for (int a = 0; a < 3; ++a)
+            for (int i = 0; i < P; ++i) {
+                int l = 0;
+                while (l < 4 && !contacts[4 * i + l]) ++l;
+                if (l < 4) { w.foot_w[a] = factor(w.foot_gain, foot[i].qfoot[3 * l + a], w.foot_w[a]); break; }
+            }
+    }
+    w.foot_term_cost = foot[0].foot_term_cost;
+    w.foot_term_grad = foot[0].foot_term_grad;
+    // every phase's diagonals as the device forms them from w
+    for (int i = 0; i < P; ++i) {
+        double q[24], r[24], qf[24], qfoot[12];
+        hsddp_facade::device_diagonals(w, &contacts[4 * i], q, r, qf, qfoot);
+        for (int j = 0; j < 24; ++j)
+            if (q[j] != track[i].q[j] || r[j] != track[i].r[j] || qf[j] != track[i].qf[j])
+                refuse(i, "tracking weights (Q, R, Qf) differ from the other phases' or are not the HKD pattern "
+                          "(diagonal, qJ weighted on swing legs only): one device handle holds one weight set");
+        for (int j = 0; j < 12; ++j)
+            if (qfoot[j] != foot[i].qfoot[j])
+                refuse(i, "foot-placement weights (Qfoot) differ from the other phases' or are not the HKD pattern");
+        if (foot[i].foot_term_cost != w.foot_term_cost || foot[i].foot_term_grad != w.foot_term_grad)
+            refuse(i, "foot-placement terminal factors differ from the other phases'");
+    }
+    return w;
+}
+
+template <typename T>
+typename MultiPhaseDDP<T>::Problem MultiPhaseDDP<T>::describe()
 {
     static_assert(std::is_same<T, double>::value, "the device path computes in fp64");
     if (n_phases < 1 || n_phases > HSDDP_MAX_PHASES) throw std::runtime_error("hsddp: 1..16 phases supported");
     if (x0.size() != 24) throw std::runtime_error("hsddp: set_initial_condition needs a 24-state x0");
-    std::vector<Phase *> ph(n_phases);
-    std::vector<std::shared_ptr<Trajectory<double, 24, 24, 0>>> trajs(n_phases);
-    std::vector<const hkd::TrackingCost *> track(n_phases, nullptr);
-    std::vector<const hkd::FootPlaceReg *> foot(n_phases, nullptr);
-    hsddp_problem_desc desc;
-    std::memset(&desc, 0, sizeof desc);
-    desc.device = 0;
+    const int P = n_phases;
+    Problem pr;
+    std::memset(&pr.desc, 0, sizeof pr.desc);
+    hsddp_problem_desc &desc = pr.desc;
+    desc.device = device;
     desc.batch = 1;
-    desc.n_phases = n_phases;
+    desc.n_phases = P;
     desc.ref_per_element = 0;
-    hsddp_default_weights(&desc.weights);
     hsddp_default_constraint_params(&desc.cparams);
-    std::vector<int> contacts(4 * (n_phases + 1));
-    for (int i = 0; i < n_phases; ++i) {
+    std::vector<Phase *> ph(P);
+    std::vector<std::shared_ptr<Trajectory<double, 24, 24, 0>>> trajs(P);
+    std::vector<Bound> dyn(P), rst(P);
+    std::vector<int> has_reset(P);
+    pr.contacts.assign(4 * (P + 1), 0);
+    for (int i = 0; i < P; ++i) {
         ph[i] = dynamic_cast<Phase *>(phases[i].get());
-        if (!ph[i]) throw std::runtime_error("phase " + std::to_string(i) + " is not SinglePhase<double,24,24,0>");
+        if (!ph[i]) refuse(i, "is not SinglePhase<double,24,24,0>");
         trajs[i] = ph[i]->traj;
-        const auto *dyn = plugin<hkd::Dynamics>(ph[i]->dynamics, "Dynamics", i);
-        plugin<hkd::DynamicsPartial>(ph[i]->dynamics_partial, "DynamicsPartial", i);
-        for (int l = 0; l < 4; ++l) contacts[4 * i + l] = dyn->contact[l];
-        for (auto &c : ph[i]->costs) {
-            if (auto *tc = dynamic_cast<hkd::TrackingCost *>(c.get())) { desc.weights = tc->weights; track[i] = tc; }
-            else if (auto *fr = dynamic_cast<hkd::FootPlaceReg *>(c.get())) foot[i] = fr;
-            else throw std::runtime_error("phase " + std::to_string(i) + ": cost '" + c->cost_name + "' cannot run on the device");
-        }
-        if (!track[i] || !foot[i]) throw std::runtime_error("phase " + std::to_string(i) + ": needs hkd::TrackingCost and hkd::FootPlaceReg");
-        for (auto &c : ph[i]->pconstraints) {
-            if (auto *g = dynamic_cast<hkd::GRFConstraint *>(c.get())) desc.cparams = g->cparams;
-            else throw std::runtime_error("phase " + std::to_string(i) + ": path constraint '" + c->name + "' cannot run on the device");
-        }
-        for (auto &c : ph[i]->tconstraints) {
-            auto *td = dynamic_cast<hkd::TouchDownConstraint *>(c.get());
-            if (!td) throw std::runtime_error("phase " + std::to_string(i) + ": terminal constraint '" + c->name + "' cannot run on the device");
-            if (i == n_phases - 1)
-                for (int l = 0; l < 4; ++l) contacts[4 * n_phases + l] = td->next_contact[l];
-        }
+        if (!trajs[i]) refuse(i, "has no trajectory (set_trajectory)");
+        Bound dp;
+        if (!read_dynamics(*ph[i], dyn[i]))
+            refuse(i, "Dynamics is not the HKD registration (hkd::Dynamics, or HKD::Model<T>::dynamics bound to the "
+                      "phase contact and dt); only HKD problems run on the device");
+        if (!read_dynamics_partial(*ph[i], dp))
+            refuse(i, "DynamicsPartial is not the HKD registration (hkd::DynamicsPartial, or "
+                      "HKD::Model<T>::dynamics_partial); only HKD problems run on the device");
+        for (int l = 0; l < 4; ++l)
+            if (dp.c[l] != dyn[i].c[l] || (dyn[i].c[l] != 0 && dyn[i].c[l] != 1))
+                refuse(i, "dynamics and dynamics_partial bind different contacts (or a contact other than 0 / 1)");
+        if (dp.dt != dyn[i].dt || dyn[i].dt != (double)trajs[i]->timeStep || dyn[i].dt != dyn[0].dt)
+            refuse(i, "the dynamics' dt must equal the trajectory time step of every phase");
+        for (int l = 0; l < 4; ++l) pr.contacts[4 * i + l] = dyn[i].c[l];
+        has_reset[i] = read_reset(*ph[i], rst[i]);
+        if (has_reset[i] < 0) refuse(i, "resetmap / resetmap_partial is not the HKD registration (hkd::Resetmap, or "
+                                        "HKDReset<T>::resetmap(_partial) bound to the phase's contacts)");
+        if (has_reset[i])
+            for (int l = 0; l < 4; ++l)
+                if (rst[i].c[l] != dyn[i].c[l]) refuse(i, "the resetmap's current contact differs from the dynamics'");
     }
-    if (ph[n_phases - 1]->tconstraints.empty())  // no touchdown after the horizon: keep the contact
-        for (int l = 0; l < 4; ++l) contacts[4 * n_phases + l] = contacts[4 * (n_phases - 1) + l];
-    int S = 0, Kc = 0;
-    hsddp_pack::layout(trajs, desc.horizons, desc.dt, S, Kc);
-    // references per state slot from the costs' per-knot tables
-    std::vector<double> rx, ru, rf;
-    hsddp_pack::pack_references(n_phases, desc.horizons, [&](int i, int k, double *xr, double *ur, double *pf) {
-        const auto *tc = track[i];
-        const auto *fr = foot[i];
-        const int N = desc.horizons[i];
-        if ((int)tc->x_ref.size() != N + 1 || (int)tc->u_ref.size() < N || (int)fr->foot_ref.size() != N + 1)
-            throw std::runtime_error("phase " + std::to_string(i) + ": reference lengths must match the horizon");
-        for (int j = 0; j < 24; ++j) { xr[j] = tc->x_ref[k][j]; ur[j] = k < (int)tc->u_ref.size() ? tc->u_ref[k][j] : 0.0; }
-        for (int j = 0; j < 12; ++j) pf[j] = fr->foot_ref[k][j];
-    }, rx, ru, rf);
-    std::vector<double> Xb, Ub, K;
-    hsddp_pack::pack_trajectories(trajs, Xb, Ub, K);
-    release();
-    check(hsddp_create(&desc, &handle));
+    // terminal constraints: touchdown legs and AL parameters per phase
+    std::vector<int> td_impact(4 * P, 0), has_td(P, 0);
+    hsddp_facade::TdSpec td0;
+    bool td_seen = false;
+    for (int i = 0; i < P; ++i)
+        for (auto &c : ph[i]->tconstraints) {
+            const auto *dc = dynamic_cast<const hsddp_facade::DeviceTerminalConstraint *>(c.get());
+            if (!dc) refuse(i, "terminal constraint '" + c->name + "' cannot run on the device");
+            hsddp_facade::TdSpec s;
+            dc->device_spec(s);
+            bool any = false;
+            for (int l = 0; l < 4; ++l) { td_impact[4 * i + l] |= s.impact[l]; any |= s.impact[l] != 0; }
+            if (has_td[i] && any) refuse(i, "more than one touchdown constraint");
+            has_td[i] |= any;
+            if (!any) continue;
+            if (td_seen && (s.sigma != td0.sigma || s.lambda != td0.lambda || s.sigma_max != td0.sigma_max ||
+                            s.ground != td0.ground))
+                refuse(i, "touchdown AL parameters / ground height differ from another phase's (one set per handle)");
+            td0 = s;
+            td_seen = true;
+        }
+    if (td_seen) {
+        desc.cparams.td_sigma = td0.sigma; desc.cparams.td_lambda = td0.lambda;
+        desc.cparams.td_sigma_max = td0.sigma_max; desc.cparams.ground_height = td0.ground;
+    }
+    // the contact after the horizon: the last phase's reset target, else the touchdown legs' stance
+    for (int l = 0; l < 4; ++l)
+        pr.contacts[4 * P + l] = has_reset[P - 1] ? rst[P - 1].cn[l]
+                                                  : (td_impact[4 * (P - 1) + l] ? 1 : pr.contacts[4 * (P - 1) + l]);
+    for (int i = 0; i < P; ++i)
+        for (int l = 0; l < 4; ++l) {
+            const int c = pr.contacts[4 * i + l], cn = pr.contacts[4 * (i + 1) + l];
+            if (has_reset[i] && rst[i].cn[l] != cn) refuse(i, "the resetmap's next contact differs from the next phase's");
+            if (!has_reset[i] && c != cn && i < P - 1)
+                refuse(i, "the contact changes at the phase end but no resetmap (HKDReset) is registered");
+            if ((c == 0 && cn == 1) != (td_impact[4 * i + l] != 0))
+                refuse(i, "touchdown constraint legs differ from the legs touching down at the phase end");
+        }
+    // path constraints: GRF friction pyramids with their ReB parameters
+    hsddp_facade::GrfSpec g0;
+    bool grf_seen = false;
+    for (int i = 0; i < P; ++i) {
+        int stance = 0, n_grf = 0;
+        for (int l = 0; l < 4; ++l) stance += pr.contacts[4 * i + l];
+        for (auto &c : ph[i]->pconstraints) {
+            const auto *dc = dynamic_cast<const hsddp_facade::DevicePathConstraint *>(c.get());
+            if (!dc) refuse(i, "path constraint '" + c->name + "' cannot run on the device");
+            hsddp_facade::GrfSpec s;
+            dc->device_spec(s);
+            for (int l = 0; l < 4; ++l)
+                if (s.contact[l] != pr.contacts[4 * i + l]) refuse(i, "GRF constraint contact differs from the phase's");
+            ++n_grf;
+            if (grf_seen && (s.mu != g0.mu || s.delta != g0.delta || s.delta_min != g0.delta_min || s.eps != g0.eps))
+                refuse(i, "GRF friction / ReB parameters differ from another phase's (one set per handle)");
+            g0 = s;
+            grf_seen = true;
+        }
+        if (stance > 0 && n_grf != 1) refuse(i, "a phase with stance legs needs exactly one GRF constraint");
+    }
+    if (grf_seen) {
+        desc.cparams.mu_fric = g0.mu;
+        desc.cparams.grf_delta = g0.delta; desc.cparams.grf_delta_min = g0.delta_min; desc.cparams.grf_eps = g0.eps;
+    }
+    // costs: one tracking and one foot-placement term per phase
+    std::vector<hsddp_facade::CostSpec> track(P), foot(P);
+    for (int i = 0; i < P; ++i) {
+        int nt = 0, nf = 0;
+        for (auto &c : ph[i]->costs) {
+            const auto *dc = dynamic_cast<const hsddp_facade::DeviceCost *>(c.get());
+            if (!dc) refuse(i, "cost '" + c->cost_name + "' cannot run on the device");
+            hsddp_facade::CostSpec s;
+            dc->device_spec(s, &pr.contacts[4 * i]);
+            if (s.terms & HSDDP_TERM_TRACKING) { track[i] = s; ++nt; }
+            if (s.terms & HSDDP_TERM_FOOT) { foot[i] = s; ++nf; }
+        }
+        if (nt != 1 || nf != 1)
+            refuse(i, "needs one HKD tracking cost and one foot-placement regularisation (HKDTrackingCost / "
+                      "HKDFootPlaceReg, or hkd::TrackingCost / hkd::FootPlaceReg)");
+    }
+    desc.weights = derive_weights(track, foot, pr.contacts);
+    hsddp_pack::layout(trajs, desc.horizons, desc.dt, pr.S, pr.Kc);
+    // references at every knot's time t = t_offset + k dt (SinglePhase.cpp:243-287)
+    hsddp_pack::pack_references(P, desc.horizons, [&](int i, int k, double *xr, double *ur, double *pf) {
+        const float t = (float)(ph[i]->t_offset + k * trajs[i]->timeStep);
+        double pcom[3] = {0, 0, 0};
+        track[i].track_ref(k, t, xr, ur);
+        foot[i].foot_ref(k, t, pf, pcom);
+        if (foot[i].foot_pcom && (pcom[0] != xr[3] || pcom[1] != xr[4] || pcom[2] != xr[5]))
+            refuse(i, "the foot-placement reference's body position differs from the tracking reference's at knot " +
+                          std::to_string(k) + " (the device takes both from one reference)");
+    }, pr.ref_x, pr.ref_u, pr.ref_foot);
+    hsddp_pack::pack_trajectories(trajs, pr.Xbar, pr.Ubar, pr.K);
+    return pr;
+}
+
+template <typename T>
+void MultiPhaseDDP<T>::solve(HSDDP_OPTION option)
+{
+    Problem pr = describe();
+    const int P = n_phases, S = pr.S, Kc = pr.Kc;
+    std::vector<std::shared_ptr<Trajectory<double, 24, 24, 0>>> trajs(P);
+    for (int i = 0; i < P; ++i) trajs[i] = dynamic_cast<Phase *>(phases[i].get())->traj;
+    // one handle while the problem's shape, weights and parameters stay the same (an MPC loop)
+    if (!handle || std::memcmp(&pr.desc, &handle_desc, sizeof handle_desc) != 0) {
+        release();
+        check(hsddp_create(&pr.desc, &handle));
+        handle_desc = pr.desc;
+        check(hsddp_set_value_export(handle, 1));  // G[0], H[0] per phase for get_value_approx
+    }
     const hsddp_options o = option.to_c();
     check(hsddp_set_options(handle, &o));
-    check(hsddp_set_value_export(handle, 1));  // G[0], H[0] per phase for get_value_approx
-    check(hsddp_upload_problem(handle, contacts.data(), x0.data(), rx.data(), ru.data(), rf.data()));
-    check(hsddp_upload_warm_start(handle, Xb.data(), Ub.data(), K.data()));
+    check(hsddp_upload_problem(handle, pr.contacts.data(), x0.data(), pr.ref_x.data(), pr.ref_u.data(), pr.ref_foot.data()));
+    check(hsddp_upload_warm_start(handle, pr.Xbar.data(), pr.Ubar.data(), pr.K.data()));
     hsddp_stats st;
     check(hsddp_solve(handle, &st));
     // solution, working trajectory, LQ model, terminal data, value function, solver info
+    std::vector<double> &Xb = pr.Xbar, &Ub = pr.Ubar, &K = pr.K;
     check(hsddp_download_trajectory(handle, Xb.data(), Ub.data(), K.data()));
     hsddp_pack::unpack_trajectories(trajs, Xb.data(), Ub.data(), K.data());
     std::vector<double> X(24 * S), U(24 * Kc), D(24 * S), dX(24 * S), dU(24 * Kc);
@@ -1147,7 +1715,7 @@ void MultiPhaseDDP<T>::solve(HSDDP_OPTION option)
     std::vector<double> A(576 * Kc), Bm(576 * Kc), l(Kc), lx(24 * Kc), lu(24 * Kc), lxx(576 * Kc), luu(576 * Kc);
     check(hsddp_download_lq(handle, A.data(), Bm.data(), l.data(), lx.data(), lu.data(), lxx.data(), luu.data()));
     hsddp_pack::unpack_lq(trajs, A.data(), Bm.data(), l.data(), lx.data(), lu.data(), lxx.data(), luu.data());
-    std::vector<double> Phi(n_phases), Phix(24 * n_phases), Phixx(576 * n_phases), G(24 * n_phases), H(576 * n_phases);
+    std::vector<double> Phi(P), Phix(24 * P), Phixx(576 * P), G(24 * P), H(576 * P);
     check(hsddp_download_terminal(handle, Phi.data(), Phix.data(), Phixx.data(), nullptr));
     check(hsddp_download_value(handle, G.data(), H.data()));
     hsddp_pack::unpack_terminal_value(trajs, Phi.data(), Phix.data(), Phixx.data(), G.data(), H.data());
@@ -1161,10 +1729,10 @@ void MultiPhaseDDP<T>::solve(HSDDP_OPTION option)
     eqn_feas_buffer.assign(e.begin(), e.begin() + count);
     ineq_feas_buffer.assign(q.begin(), q.begin() + count);
     size_t kc = 0;
-    for (int i = 0; i < n_phases; ++i) {  // SinglePhase::get_actual_cost: running + terminal cost
+    for (int i = 0; i < P; ++i) {  // SinglePhase::get_actual_cost: running + terminal cost
         double pc = 0;
-        for (int k = 0; k < desc.horizons[i]; ++k, ++kc) pc += l[kc];
-        ph[i]->actual_cost = pc + Phi[i];
+        for (int k = 0; k < pr.desc.horizons[i]; ++k, ++kc) pc += l[kc];
+        dynamic_cast<Phase *>(phases[i].get())->actual_cost = pc + Phi[i];
     }
     actual_cost = info.cost;
     feas = info.feas;

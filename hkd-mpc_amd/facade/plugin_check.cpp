@@ -213,6 +213,76 @@ static int host_checks()
     CHECK(traj->horizon == 5 && traj->Ubar.size() == 5 && traj->rcostData.size() == 5);
     UserPhase up;  // a user phase type is a SinglePhaseBase
     CHECK(up.get_state_dim() == 0);
+
+    // the weights the device solve applies come from the registered costs: FootPlaceReg's own foot
+    // weights, TrackingCost's tracking weights; phases that disagree are refused (one set per handle)
+    auto hkd_phase = [](int N, const std::array<int, 4> &c, const std::array<int, 4> &cn,
+                        std::shared_ptr<hkd::TrackingCost> &tc, std::shared_ptr<hkd::FootPlaceReg> &fr) {
+        auto ph = std::make_shared<Phase>();
+        ph->set_trajectory(std::make_shared<Trajectory<double, 24, 24, 0>>(0.01, N));
+        hkd::Dynamics d;
+        hkd::DynamicsPartial dp;
+        hkd::Resetmap rm;
+        hkd::ResetmapPartial rmp;
+        d.contact = dp.contact = rm.contact = rmp.contact = c;
+        rm.next_contact = rmp.next_contact = cn;
+        ph->set_dynamics(d);
+        ph->set_dynamics_partial(dp);
+        ph->set_resetmap(rm);
+        ph->set_resetmap_partial(rmp);
+        tc = std::make_shared<hkd::TrackingCost>();
+        fr = std::make_shared<hkd::FootPlaceReg>();
+        tc->x_ref.assign(N + 1, {});
+        tc->u_ref.assign(N + 1, {});
+        fr->foot_ref.assign(N + 1, {});
+        ph->add_cost(tc);
+        ph->add_cost(fr);
+        ph->add_pathConstraint(std::make_shared<hkd::GRFConstraint>(c));
+        return ph;
+    };
+    std::shared_ptr<hkd::TrackingCost> tc0, tc1;
+    std::shared_ptr<hkd::FootPlaceReg> fr0, fr1;
+    const std::array<int, 4> trot_a{{1, 0, 0, 1}}, trot_b{{0, 1, 1, 0}};
+    auto p0 = hkd_phase(4, trot_a, trot_a, tc0, fr0), p1 = hkd_phase(4, trot_a, trot_a, tc1, fr1);
+    for (auto &f : {fr0, fr1}) {  // non-default foot weights on the foot term only
+        f->weights.foot_w[0] = 2; f->weights.foot_w[1] = 0.5; f->weights.foot_gain = 10; f->weights.foot_term_cost = 7;
+    }
+    tc0->weights.q_pos[2] = tc1->weights.q_pos[2] = 42;
+    MultiPhaseDDP<double> ws;
+    ws.set_multiPhaseProblem({p0, p1});
+    ws.set_initial_condition(DVec<double>(24));
+    const hsddp_problem_desc d0 = ws.describe().desc;
+    CHECK(d0.weights.foot_w[0] == 2 && d0.weights.foot_w[1] == 0.5 && d0.weights.foot_gain == 10 &&
+          d0.weights.foot_term_cost == 7 && d0.weights.q_pos[2] == 42);
+    tc1->weights.q_pos[2] = 41;  // the phases disagree: refused
+    bool mixed = false;
+    try {
+        ws.describe();
+    } catch (const std::runtime_error &e) {
+        mixed = std::string(e.what()).find("phase 1: tracking weights") != std::string::npos;
+    }
+    CHECK(mixed);
+    tc1->weights.q_pos[2] = 42;
+    fr1->weights.foot_w[0] = 3;
+    mixed = false;
+    try {
+        ws.describe();
+    } catch (const std::runtime_error &e) {
+        mixed = std::string(e.what()).find("phase 1: foot-placement weights") != std::string::npos;
+    }
+    CHECK(mixed);
+    // a contact change at the phase end needs the reset registered; a GRF constraint's contact must be the phase's
+    auto q0 = hkd_phase(4, trot_a, trot_b, tc0, fr0), q1 = hkd_phase(4, trot_b, trot_b, tc1, fr1);
+    q0->set_resetmap(nullptr);
+    q0->set_resetmap_partial(nullptr);
+    ws.set_multiPhaseProblem({q0, q1});
+    mixed = false;
+    try {
+        ws.describe();
+    } catch (const std::runtime_error &e) {
+        mixed = std::string(e.what()).find("no resetmap") != std::string::npos;
+    }
+    CHECK(mixed);
     return 0;
 }
 
