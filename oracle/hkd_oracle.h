@@ -104,6 +104,10 @@ int orc_solve(const orc_problem *p, const orc_options *o, orc_element *e);
 int orc_solve_batch(const orc_problem *p, const orc_options *o, orc_element *elems, int n, int n_threads);
 
 /* Component entry points (for per-pass tests). */
+/* SinglePhase::backward_sweep on caller-supplied time-invariant LQ data (the outside Riccati pin) */
+int orc_riccati_lq(int N, const double *A, const double *B, const double *lxx, const double *luu, const double *lx,
+                   const double *lu, const double *Phix, const double *Phixx, double reg, double *K0, double *dU0,
+                   double *G0, double *H0);
 void orc_init_element(const orc_problem *p, orc_element *e); /* default ReB/AL params */
 
 #ifdef __cplusplus

@@ -566,6 +566,48 @@ static int phase_backward(ctx_t *C, int i, double reg, const double *Gp, const d
     return success;
 }
 
+/* SinglePhase::backward_sweep (SinglePhase.cpp:298-367) alone, on caller-supplied time-invariant LQ
+ * data over one phase of N knots: A, B, lxx, luu (24 x 24, row-major), lx, lu, terminal Phix, Phixx,
+ * regularisation reg, zero defects.  The known-answer entry for the outside Riccati pin (SURVEY.md
+ * §4.3 item 1): as N grows, K[0] and H[0] converge to the discrete algebraic Riccati solution.
+ * Outputs K0, H0 (24 x 24), dU0, G0 (24); returns the sweep's success flag (PSD test). */
+int orc_riccati_lq(int N, const double *A, const double *B, const double *lxx, const double *luu, const double *lx,
+                   const double *lu, const double *Phix, const double *Phixx, double reg, double *K0, double *dU0,
+                   double *G0, double *H0)
+{
+    if (N < 1 || N > 100000) return 0;
+    const int S = N + 1;
+    ctx_t C;
+    memset(&C, 0, sizeof C);
+    orc_element e;
+    memset(&e, 0, sizeof e);
+    C.e = &e;
+    C.P = 1; C.S = S; C.Kc = N;
+    C.N[0] = N; C.s0[0] = 0; C.k0[0] = 0;
+    double *buf = calloc((size_t)N * (2 * NN + 3 * NN + 2 * NX) + (size_t)S * (NN + NX + NX) + NX + NN + (size_t)N * (NN + NX), sizeof(double));
+    if (!buf) return 0;
+    double *q = buf;
+    C.A = q; q += (size_t)N * NN; C.B = q; q += (size_t)N * NN;
+    C.lxx = q; q += (size_t)N * NN; C.luu = q; q += (size_t)N * NN; C.lux = q; q += (size_t)N * NN;
+    C.lx = q; q += (size_t)N * NX; C.lu = q; q += (size_t)N * NX;
+    C.H = q; q += (size_t)S * NN; C.G = q; q += (size_t)S * NX; e.Defect = q; q += (size_t)S * NX;
+    C.Phix = q; q += NX; C.Phixx = q; q += NN;
+    e.K = q; q += (size_t)N * NN; e.dU = q;
+    for (int k = 0; k < N; ++k) {
+        memcpy(C.A + (size_t)k * NN, A, sizeof(double) * NN); memcpy(C.B + (size_t)k * NN, B, sizeof(double) * NN);
+        memcpy(C.lxx + (size_t)k * NN, lxx, sizeof(double) * NN); memcpy(C.luu + (size_t)k * NN, luu, sizeof(double) * NN);
+        memcpy(C.lx + (size_t)k * NX, lx, sizeof(double) * NX); memcpy(C.lu + (size_t)k * NX, lu, sizeof(double) * NX);
+    }
+    memcpy(C.Phix, Phix, sizeof(double) * NX);
+    memcpy(C.Phixx, Phixx, sizeof(double) * NN);
+    double Gp[NX] = {0}, Hp[NN] = {0};
+    const int ok = phase_backward(&C, 0, reg, Gp, Hp);
+    memcpy(K0, e.K, sizeof(double) * NN); memcpy(dU0, e.dU, sizeof(double) * NX);
+    memcpy(G0, C.G, sizeof(double) * NX); memcpy(H0, C.H, sizeof(double) * NN);
+    free(buf);
+    return ok;
+}
+
 /* SinglePhase::linear_rollout (SinglePhase.cpp:144-178) */
 static void phase_linear_rollout(ctx_t *C, int i, double eps, const double *dx_init)
 {

@@ -86,6 +86,7 @@ def lib():
         _lib.orc_resetmap.argtypes = [DP, IP, IP, DP]
         _lib.orc_resetmap_partial.argtypes = [DP, IP, IP, DP]
         _lib.orc_knot_eval.argtypes = [C.POINTER(OrcProblem), C.POINTER(OrcOptions), IP, IP] + [DP] * 13
+        _lib.orc_riccati_lq.argtypes = [C.c_int] + [DP] * 8 + [C.c_double] + [DP] * 4
     return _lib
 
 
@@ -187,6 +188,17 @@ def knot_eval(c, cn, x, u, xr, ur, pf, x_end=None, xr_end=None, pf_end=None, reb
     for k in ("Phixx", "A", "B"):
         r[k] = out[q:q + N].reshape(24, 24); q += N
     return r
+
+
+def riccati_lq(N, A, B, lxx, luu, lx=None, lu=None, Phix=None, Phixx=None, reg=0.0):
+    """orc_riccati_lq: SinglePhase::backward_sweep on time-invariant LQ data over N knots (zero
+    defects); returns (ok, K0, dU0, G0, H0)."""
+    f = lambda a, shape: np.ascontiguousarray(np.zeros(shape) if a is None else a, dtype=np.float64)  # noqa: E731
+    args = [f(A, (24, 24)), f(B, (24, 24)), f(lxx, (24, 24)), f(luu, (24, 24)), f(lx, 24), f(lu, 24), f(Phix, 24),
+            f(Phixx, (24, 24))]
+    K0, H0, dU0, G0 = np.zeros((24, 24)), np.zeros((24, 24)), np.zeros(24), np.zeros(24)
+    ok = lib().orc_riccati_lq(int(N), *[dp(a) for a in args], float(reg), dp(K0), dp(dU0), dp(G0), dp(H0))
+    return bool(ok), K0, dU0, G0, H0
 
 
 # ---- solver -----------------------------------------------------------------------------------

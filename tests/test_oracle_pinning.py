@@ -203,3 +203,32 @@ def test_failed_line_search_keeps_the_last_trial():
             assert np.allclose(r1["U"][:, kc], u, rtol=1e-14, atol=1e-14)
             kc += 1
     assert S == dx.shape[1]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_riccati_recursion_converges_to_the_dare_solution(seed):
+    """Outside pin of the Riccati recursion (SinglePhase.cpp:298-367): on
+    time-invariant LQ data the oracle's backward sweep, run long enough, reaches the discrete
+    algebraic Riccati solution scipy computes independently — H[0] -> P and K[0] -> -(R + B^T P B)^-1
+    B^T P A, with dU[0], G[0] -> 0 for zero gradients.  The system has 24 states and 24 controls,
+    open-loop unstable (spectral radius 1.05), dense."""
+    la = pytest.importorskip("scipy.linalg")
+    rng = np.random.default_rng(seed)
+    A = rng.standard_normal((24, 24))
+    A *= 1.05 / np.max(np.abs(np.linalg.eigvals(A)))
+    B = rng.standard_normal((24, 24)) / 5
+    M = rng.standard_normal((24, 24))
+    Q = M @ M.T / 24 + np.eye(24)
+    N2 = rng.standard_normal((24, 24))
+    R = N2 @ N2.T / 24 + 0.5 * np.eye(24)
+    P = la.solve_discrete_are(A, B, Q, R)
+    Kd = -np.linalg.solve(R + B.T @ P @ B, B.T @ P @ A)
+    ok, K0, dU0, G0, H0 = O.riccati_lq(400, A, B, Q, R)
+    assert ok
+    assert np.max(np.abs(H0 - P)) / np.max(np.abs(P)) <= 1e-10
+    assert np.max(np.abs(K0 - Kd)) / np.max(np.abs(Kd)) <= 1e-10
+    assert np.all(dU0 == 0) and np.all(G0 == 0)
+    # one knot from the DARE solution is its fixed point (P, Kd as terminal data)
+    ok1, K1, _, _, H1 = O.riccati_lq(1, A, B, Q, R, Phixx=P)
+    assert ok1 and np.max(np.abs(H1 - P)) / np.max(np.abs(P)) <= 1e-10
+    assert np.max(np.abs(K1 - Kd)) / np.max(np.abs(Kd)) <= 1e-10
