@@ -93,6 +93,60 @@ def cpu_baseline(args):
                       f"{threads} threads, {dt:.1f} s wall"}
 
 
+def latency_c1(args) -> None:
+    """BASELINE config 1 (Mini Cheetah trot, 1 phase x 50 knots, batch = 1): the reference's own use
+    of the solver — one robot, one full MultiPhaseDDP::solve with the shipped ddp_setting.info
+    (early exits on) through the C-ABI — as solve latency, with the oracle's single-problem CPU solve
+    of the same problem beside it (one thread).  Not the driver's metric line (that is the default
+    run); written for the record by `bench.py --config c1`."""
+    prob = synthetic.make_batch(1, 1, 50, "trot")
+    opt = hsddp.load_settings()
+    solver = hsddp.Solver(prob, opt, device=0)
+    times, iters = [], []
+    for rep in range(args.warmup + args.steps):
+        solver.warm_start()  # Xbar = reference, Ubar = K = 0 (HKDProblem.cpp:84-90)
+        solver.synchronize()
+        t0 = time.perf_counter()
+        solver.solve()
+        t1 = time.perf_counter()
+        if rep >= args.warmup:
+            times.append((t1 - t0) * 1e3)
+            iters.append(int(solver.element_info()["iters"][0]))
+    info = solver.element_info()
+    solver.close()
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    reps = max(5, args.steps)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = O.solve_batch(prob, O.default_options(), n_threads=1)
+    cpu_ms = (time.perf_counter() - t0) / reps * 1e3
+    model, nproc, affinity = host_cpu()
+    ms = float(np.median(times))
+    out = {"metric": "full solve latency, 1-phase 50-knot HKD trot, batch=1 (BASELINE config 1)", "value": ms,
+           "unit": "ms/solve", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+           "higher_is_better": False, "scaling": "none", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic: seeded random initial state (splitmix64), closed-form trot reference (SURVEY.md §8d)",
+           "config": {"workload": "HKD trot, 1 phase x 50 knots, batch=1 (BASELINE config 1), ddp_setting.info "
+                                  "(max_AL_iter 5, max_DDP_iter 10, early exits)", "global_batch": 1},
+           "extra": {"ms_min": float(np.min(times)), "ms_max": float(np.max(times)), "inner_iterations": iters[0],
+                     "iterations_equal_oracle": bool(iters[0] == int(r["iters"][0])),
+                     "cost_rel_diff_vs_oracle": float(abs(info["cost"][0] - r["cost"][0]) / abs(r["cost"][0])),
+                     "us_per_inner_iteration": ms * 1e3 / max(1, iters[0])},
+           "cpu_baseline": {"value": cpu_ms, "unit": "ms/solve", "cores": 1, "kind": "port",
+                            "host": {"cpu_model": model, "nproc": nproc, "affinity_cpus": affinity},
+                            "sample": f"oracle/hsddp_oracle.c (-O2, fp64), the same problem and options, "
+                                      f"{reps} solves on one thread"}}
+    print(json.dumps(out), flush=True)
+
+
+# BASELINE.json's configs (SURVEY.md §8): C1 = 1x50 trot at batch 1 (latency), C2 = 4x50 trot at
+# batch 1024, C3 = 8x25 jump at 4096, C4 = the mixed-gait shard of the 8-GPU run (4096 per GPU),
+# C5 = fp32 Riccati at 4096; the metric line is 4x50 trot at 4096.
+CONFIGS = {"metric": {}, "c2": {"batch": 1024}, "c3": {"gait": "jump", "phases": 8, "knots": 25},
+           "c4": {"mixed": True}, "c5": {"riccati_fp32": True}}
+
+
 def spawn_ranks(args) -> int:
     """Run this script as N torch.distributed ranks (one per GPU) in a child launcher."""
     with socket.socket() as s:
@@ -120,7 +174,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--riccati-fp32", action="store_true",
                     help="config C5: fp32 LQ records / Riccati sweep / linear rollout (fp64 rollout, costs, outer loop)")
+    ap.add_argument("--config", default="metric", choices=["metric", "c1", "c2", "c3", "c4", "c5"],
+                    help="BASELINE.json config (c1: batch-1 solve latency; default: the metric config)")
     args = ap.parse_args()
+    for k, v in CONFIGS.get(args.config, {}).items():
+        setattr(args, k, v)
+    if args.config == "c1":
+        torch.cuda.set_device(0)
+        latency_c1(args)
+        return
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))  # nothing above touched the GPU
@@ -194,9 +256,9 @@ def main():
         step_b = traffic.step_bytes(B, S, Kc, P, mean_ls, fp32=args.riccati_fp32, ref_per_element=args.mixed)
         gait = "mixed" if args.mixed else args.gait
         metric_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 4096)
-        c1_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 1024)
+        c2_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 1024)
         label = ("config C5: fp32 Riccati" if args.riccati_fp32 else "BASELINE metric config" if metric_cfg
-                 else "config C1: batch 1024" if c1_cfg
+                 else "config C2: batch 1024" if c2_cfg
                  else "config C3: jump with resets" if gait == "jump" else "config C4 shard: mixed gaits, 4x50 / 8x25 layouts" if args.mixed
                  else "custom")
         cfg_key = f"{gait}_{args.phases}x{args.knots}_b{B}" + ("_fp32" if args.riccati_fp32 else "")

@@ -515,9 +515,17 @@ extern "C" int hsddp_set_options(hsddp_handle h, const hsddp_options *o)
     if (!h || !o) return fail(HSDDP_ERR_ARG, "null argument");
     int rc = hsddp_validate_options(o);
     if (rc) return rc;
+    // the solver-info history must hold every entry of the new budget (1 + outer x inner)
+    if (1 + (long)std::max(0, o->max_AL_iter) * std::max(0, o->max_DDP_iter) > (1L << 20))
+        return fail(HSDDP_ERR_ARG, "max_AL_iter * max_DDP_iter exceeds the solver-info history (2^20 entries)");
+    const hsddp_options old = h->opt;
     h->opt = *o;
+    if ((rc = ensure_history(h))) {  // allocation failed: the handle keeps its previous options
+        h->opt = old;
+        return rc;
+    }
     fill_params(h);
-    return ensure_history(h);
+    return HSDDP_OK;
 }
 
 // install per-element layouts: device records, sweep pairs (equal layouts share a wave), strides
@@ -558,6 +566,8 @@ extern "C" int hsddp_set_element_layouts(hsddp_handle h, const int *n_phases, co
     if (!h || !n_phases || !horizons) return fail(HSDDP_ERR_ARG, "null argument");
     Params &p = h->p;
     const int B = p.B;
+    if (B > 1 && h->Bref == 1)  // a shared reference is laid out for one layout
+        return fail(HSDDP_ERR_ARG, "per-element layouts need per-element references (ref_per_element = 1)");
     std::vector<Layout> lays(B);
     for (int b = 0; b < B; ++b) {
         Layout &L = lays[b];
@@ -1210,16 +1220,18 @@ extern "C" int hsddp_set_value_export(hsddp_handle h, int on)
 extern "C" int hsddp_download_value(hsddp_handle h, double *G, double *H)
 {
     if (!h) return fail(HSDDP_ERR_ARG, "null handle");
-    if (!h->value0) return fail(HSDDP_ERR_ARG, "value export is off (hsddp_set_value_export)");
+    if (!h->value0 || !h->p.store_value) return fail(HSDDP_ERR_ARG, "value export is off (hsddp_set_value_export)");
     HIPCHK(hipSetDevice(h->desc.device));
     HIPCHK(hipStreamSynchronize(h->stream));
     const size_t B = h->p.B, P = h->p.P;
     std::vector<double> v(B * P * (NX + NN));
     HIPCHK(hipMemcpy(v.data(), h->value0, v.size() * sizeof(double), hipMemcpyDeviceToHost));
     for (size_t o = 0; o < B * P; ++o) {
+        // phases past the element's own layout (per-element layouts, or left from before a shift) are zero
+        const bool live = (int)(o % P) < layout_of(h, o / P).P;
         const double *s = v.data() + o * (NX + NN);
-        if (G) std::copy(s, s + NX, G + o * NX);
-        if (H) std::copy(s + NX, s + NX + NN, H + o * NN);
+        if (G) { if (live) std::copy(s, s + NX, G + o * NX); else std::fill(G + o * NX, G + (o + 1) * NX, 0.0); }
+        if (H) { if (live) std::copy(s + NX, s + NX + NN, H + o * NN); else std::fill(H + o * NN, H + (o + 1) * NN, 0.0); }
     }
     return HSDDP_OK;
 }
@@ -1508,6 +1520,9 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
         map_id[b] = it->second;
     }
     const int nk = (int)phs.size();
+    if (nk > 1 && h->Bref == 1 && B > 1)  // checked before any device work: the handle stays usable
+        return fail(HSDDP_ERR_ARG, "the elements' shifts diverge into per-element layouts, which need per-element "
+                                   "references (ref_per_element = 1)");
     std::vector<Layout> nl(nk);
     int Snew = 0, Pnew = 0;
     for (int q = 0; q < nk; ++q) {

@@ -167,3 +167,32 @@ def test_shift_elements_equals_uniform_shifts():
         assert np.array_equal(gm["Xbar"][idx, :S], gu["Xbar"]) and np.array_equal(gm["K"][idx], gu["K"])
         for f in ("Ubar", "cost", "n_ls_trials", "iters", "status"):
             assert np.array_equal(gm[f][idx], gu[f]), f
+
+
+def test_diverging_shift_with_shared_references_fails_and_keeps_the_handle():
+    """A handle with one reference for the batch cannot hold per-element layouts: a per-element shift
+    whose elements diverge is refused before any device work, and the handle still solves as
+    before (the shared layout untouched); hsddp_set_element_layouts refuses likewise."""
+    prob = syn.make_batch(4, 2, 10, "trot")
+    opt = hsddp.load_settings(max_AL_iter=1, max_DDP_iter=1, no_early_exit=1)
+    s = hsddp.Solver(prob, opt)
+    s.solve()
+    before = s.trajectory()
+    with pytest.raises(hsddp.HSDDPError, match="per-element references"):
+        s.shift_elements(np.array([[1], [0], [0], [0]]))  # element 0 alone crosses a contact change
+    lay = s.layout()
+    assert list(lay["horizons"]) == list(prob["horizons"])
+    with pytest.raises(hsddp.HSDDPError, match="per-element references"):
+        hz = np.zeros((4, 16), np.int32); hz[:, 0] = 20
+        hsddp.check(hsddp.lib().hsddp_set_element_layouts(s._h, hsddp.ip(np.ones(4, np.int32)), hsddp.ip(hz)))
+    s.warm_start(before["Xbar"], before["Ubar"], before["K"])
+    s.solve()
+    assert np.all(np.isfinite(s.trajectory()["Xbar"]))
+    # value export off: the download is refused instead of returning a stale buffer
+    s.set_value_export(True)
+    s.solve()
+    assert np.all(np.isfinite(s.value()["H"]))
+    s.set_value_export(False)
+    with pytest.raises(hsddp.HSDDPError, match="value export is off"):
+        s.value()
+    s.close()
