@@ -35,7 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hkd-mpc_amd"))
 
 import hsddp  # noqa: E402
-from hsddp import synthetic, traffic  # noqa: E402
+from hsddp import shard, synthetic, traffic  # noqa: E402
 
 METRIC = "batched DDP iters/sec (fwd+bwd), 4-phase 200-knot HKD fp64, batch=4096"
 UNIT = "trajectory-iterations/s"
@@ -220,6 +220,13 @@ def main():
 
     red = torch.tensor([t1 - t0, elem_iters, float(st.ls_trials)], dtype=torch.float64, device=dev)
     rank_ms = [(t1 - t0) / args.steps * 1e3]
+    # after the timed region: every element's command block (hkd_command_lcmt, HKDMPC.cpp:232-298)
+    # extracted on the device into the tensor the final gather sends (not for per-element layouts)
+    cmd = None
+    if not args.mixed:
+        cmd = torch.empty(B * hsddp.MPC_COMMAND.itemsize, dtype=torch.uint8, device=dev)
+        solver.extract_commands_device(cmd.data_ptr())
+    gather = {"summary_bytes_per_element": 48, "command_bytes_per_element": hsddp.MPC_COMMAND.itemsize if cmd is not None else 0}
     if world > 1:
         allr = [torch.zeros_like(red) for _ in range(world)]
         dist.all_gather(allr, red)
@@ -227,17 +234,24 @@ def main():
         elapsed = max(float(r[0]) for r in allr)
         total_iters = sum(float(r[1]) for r in allr)
         total_ls = sum(float(r[2]) for r in allr)
-        # final gather of per-element summaries to rank 0 (outside the timed region; RCCL)
-        summ = torch.from_numpy(np.stack([info["cost"], info["feas"], info["max_tconstr"], info["max_pconstr"],
-                                          info["iters"].astype(np.float64), info["status"].astype(np.float64)], 1)).to(dev)
-        gathered = [torch.empty_like(summ) for _ in range(world)] if rank == 0 else None
-        dist.gather(summ, gathered, dst=0)
-        finite = bool(torch.isfinite(torch.cat(gathered)).all()) if rank == 0 else True
-        gathered_rows = int(sum(g.shape[0] for g in gathered)) if rank == 0 else 0
+        # the one collective of the path (RCCL): per-element summaries and command blocks to rank 0
+        summ = torch.from_numpy(shard.summary_rows(info)).to(dev)
+        torch.cuda.synchronize(); barrier()
+        g0 = time.perf_counter()
+        rows, cmds = shard.final_gather(dist, summ, cmd)
+        torch.cuda.synchronize()
+        gather["ms"] = (time.perf_counter() - g0) * 1e3
+        finite = bool(np.isfinite(rows).all()) if rank == 0 else True
+        gathered_rows = int(rows.shape[0]) if rank == 0 else 0
+        if rank == 0 and cmds is not None:
+            gather["commands_ok"] = bool(np.all(cmds["N_mpcsteps"] == 8) and np.isfinite(cmds["hkd_controls"]).all())
     else:
         elapsed, total_iters, total_ls = t1 - t0, elem_iters, float(st.ls_trials)
         finite = bool(np.isfinite(info["cost"]).all())
         gathered_rows = B
+        if cmd is not None:
+            cmds = np.frombuffer(cmd.cpu().numpy().tobytes(), dtype=hsddp.MPC_COMMAND)
+            gather["commands_ok"] = bool(np.all(cmds["N_mpcsteps"] == 8) and np.isfinite(cmds["hkd_controls"]).all())
 
     if rank == 0:
         S, Kc, P = prob["S"], prob["Kc"], len(prob["horizons"])
@@ -295,6 +309,7 @@ def main():
             "extra": {"batch_iterations_per_s": total_iters / elapsed / (B * world),
                       "mean_ls_trials": mean_ls, "device_ms_per_step": dms,
                       "rank_ms_per_step": rank_ms, "rccl_world_size": world, "gathered_elements": gathered_rows,
+                      "final_gather": gather,
                       "all_costs_finite": finite, "device_bytes": solver.device_bytes()},
         }
         if world == 1 and not args.no_cpu_baseline and not args.riccati_fp32 and not args.mixed:

@@ -1369,10 +1369,31 @@ extern "C" int hsddp_device_synchronize(int device)
 }
 
 // ---- MPC command extraction (HKDMPCSolver::update_foot_placement + publish_mpc_cmd) ----------
+static int extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
+                            const double *status_durations, int durations_per_element, const float *foot_placements,
+                            int feet_per_element, float solve_time, hsddp_mpc_command *out, bool out_on_device);
+
 extern "C" int hsddp_extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
                                       const double *status_durations, int durations_per_element,
                                       const float *foot_placements, int feet_per_element, float solve_time,
                                       hsddp_mpc_command *out)
+{
+    return extract_commands(h, nsteps_between_mpc, mpc_time, dt_mpc, status_durations, durations_per_element,
+                            foot_placements, feet_per_element, solve_time, out, false);
+}
+
+extern "C" int hsddp_extract_commands_device(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
+                                             const double *status_durations, int durations_per_element,
+                                             const float *foot_placements, int feet_per_element, float solve_time,
+                                             void *out_device)
+{
+    return extract_commands(h, nsteps_between_mpc, mpc_time, dt_mpc, status_durations, durations_per_element,
+                            foot_placements, feet_per_element, solve_time, (hsddp_mpc_command *)out_device, true);
+}
+
+static int extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
+                            const double *status_durations, int durations_per_element, const float *foot_placements,
+                            int feet_per_element, float solve_time, hsddp_mpc_command *out, bool out_on_device)
 {
     if (h && !h->lays.empty())
         return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts (hsddp_set_element_layouts): the MPC-side steps need the handle's shared layout");
@@ -1403,7 +1424,7 @@ extern "C" int hsddp_extract_commands(hsddp_handle h, int nsteps_between_mpc, do
     char *buf;
     int rc;
     if ((rc = scratch(h, cmd_bytes + dur_bytes + feet_bytes, &buf))) return rc;
-    hsddp_mpc_command *dcmd = (hsddp_mpc_command *)buf;
+    hsddp_mpc_command *dcmd = out_on_device ? out : (hsddp_mpc_command *)buf;
     if (status_durations) {
         a.durations = (const double *)(buf + cmd_bytes);
         if ((rc = h2d((void *)a.durations, status_durations, (a.dur_per_elem ? B : 1) * p.P * 4 * sizeof(double), h->stream))) return rc;
@@ -1414,7 +1435,7 @@ extern "C" int hsddp_extract_commands(hsddp_handle h, int nsteps_between_mpc, do
     }
     launch_extract_commands(p, h->d, a, dcmd, h->stream);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out, dcmd, B * sizeof(hsddp_mpc_command), hipMemcpyDeviceToHost, h->stream));
+    if (!out_on_device) HIPCHK(hipMemcpyAsync(out, dcmd, B * sizeof(hsddp_mpc_command), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return HSDDP_OK;
 }

@@ -264,6 +264,13 @@ class Solver:
             float(solve_time), out.ctypes.data))
         return out
 
+    def extract_commands_device(self, out_ptr: int, nsteps_between_mpc: int = 1, mpc_time: float = 0.0,
+                                dt_mpc: float = 0.01, solve_time: float = 0.0) -> None:
+        """extract_commands into device memory at out_ptr ([B] hsddp_mpc_command on the handle's
+        device, e.g. a torch uint8 tensor's data_ptr()): the command block of the final gather."""
+        check(lib().hsddp_extract_commands_device(self._h, int(nsteps_between_mpc), float(mpc_time), float(dt_mpc),
+                                                  None, 0, None, 0, float(solve_time), C.c_void_p(out_ptr)))
+
     def set_reference_table(self, table: np.ndarray, dt_ref: float) -> None:
         t = np.ascontiguousarray(table, dtype=QUAD_STATE)
         check(lib().hsddp_set_reference_table(self._h, t.ctypes.data, int(t.size), float(dt_ref)))

@@ -105,7 +105,7 @@ EXPORTS = [
     "hsddp_plan_phases", "hsddp_set_reference_table", "hsddp_build_references", "hsddp_download_references", "hsddp_advance",
     "hsddp_get_phase_info", "hsddp_hkd_running_cost", "hsddp_hkd_terminal_cost", "hsddp_hkd_grf_constraint",
     "hsddp_hkd_touchdown_constraint", "hsddp_set_element_layouts",
-    "hsddp_shift_elements", "hsddp_get_element_layouts",
+    "hsddp_shift_elements", "hsddp_get_element_layouts", "hsddp_extract_commands_device",
 ]
 
 
@@ -178,6 +178,7 @@ def lib():
     L.hsddp_update_problem.argtypes = [C.c_void_p, IP, DP, DP, DP, DP]
     L.hsddp_extract_commands.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_void_p, C.c_int,
                                          C.c_void_p, C.c_int, C.c_float, C.c_void_p]
+    L.hsddp_extract_commands_device.argtypes = L.hsddp_extract_commands.argtypes
     _lib = L
     return L
 

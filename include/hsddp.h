@@ -345,6 +345,13 @@ int hsddp_extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_ti
                            const double *status_durations, int durations_per_element,
                            const float *foot_placements, int feet_per_element, float solve_time,
                            hsddp_mpc_command *out);
+/* The same into device memory: out_device [B] hsddp_mpc_command on the handle's device (no host
+ * copy) — the optional first-knots command block of the final multi-GPU gather (SURVEY.md §8(e),
+ * HKDMPC.cpp:254-286), gathered by the caller's collective straight from HBM. */
+int hsddp_extract_commands_device(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
+                                  const double *status_durations, int durations_per_element,
+                                  const float *foot_placements, int feet_per_element, float solve_time,
+                                  void *out_device);
 
 /* ---- batched model primitives (device pointers, n points, async on `stream` (NULL = default)) */
 /* xn[n][24] = hkinodyn(x[n][24], u[n][24], dt, c[n][4]) */

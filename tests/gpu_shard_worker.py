@@ -15,7 +15,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "hkd-mpc_amd"))
 import hsddp  # noqa: E402
-from hsddp import synthetic as syn  # noqa: E402
+from hsddp import shard, synthetic as syn  # noqa: E402
 
 OPTS = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=3)
 
@@ -25,19 +25,21 @@ def main():
     out = sys.argv[5]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    shard = syn.make_batch(B, 4, 20, "trot", mixed=True, first_element=rank * B)
-    s = hsddp.Solver(shard, hsddp.load_settings(**OPTS), device=0)
+    part = syn.make_batch(B, 4, 20, "trot", mixed=True, first_element=rank * B)
+    s = hsddp.Solver(part, hsddp.load_settings(**OPTS), device=0)
     s.solve()
     info, tr = s.element_info(), s.trajectory()
+    # the command block extracted on the device into a torch tensor (as bench.py), sent from the host
+    cmd = torch.empty(B * hsddp.MPC_COMMAND.itemsize, dtype=torch.uint8, device="cuda:0")
+    s.extract_commands_device(cmd.data_ptr())
     s.close()
-    summ = torch.from_numpy(np.stack([info["cost"], info["feas"], info["max_tconstr"], info["max_pconstr"]], 1))
+    rows, cmds = shard.final_gather(dist, torch.from_numpy(shard.summary_rows(info)), cmd.cpu())
     xbar = torch.from_numpy(np.ascontiguousarray(tr["Xbar"]))
-    gs = [torch.empty_like(summ) for _ in range(world)] if rank == 0 else None
     gx = [torch.empty_like(xbar) for _ in range(world)] if rank == 0 else None
-    dist.gather(summ, gs, dst=0)
     dist.gather(xbar, gx, dst=0)
     if rank == 0:
-        np.save(os.path.join(out, "summ.npy"), torch.cat(gs).numpy())
+        np.save(os.path.join(out, "summ.npy"), rows)
+        np.save(os.path.join(out, "cmds.npy"), shard.command_bytes(cmds))
         np.save(os.path.join(out, "xbar.npy"), torch.cat(gx).numpy())
     dist.barrier()
     dist.destroy_process_group()

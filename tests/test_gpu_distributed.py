@@ -51,7 +51,9 @@ def test_two_rank_gpu_shards_equal_single_process(tmp_path):
     s = hsddp.Solver(full, hsddp.load_settings(**OPTS))
     s.solve()
     info, tr = s.element_info(), s.trajectory()
+    cmds = s.extract_commands()
     s.close()
-    ref = np.stack([info["cost"], info["feas"], info["max_tconstr"], info["max_pconstr"]], 1)
-    assert np.array_equal(np.load(tmp_path / "summ.npy"), ref)
+    from hsddp import shard
+    assert np.array_equal(np.load(tmp_path / "summ.npy"), shard.summary_rows(info))
+    assert np.array_equal(np.load(tmp_path / "cmds.npy"), shard.command_bytes(cmds))  # device extraction, gathered
     assert np.array_equal(np.load(tmp_path / "xbar.npy"), tr["Xbar"])
