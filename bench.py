@@ -104,7 +104,8 @@ def latency_c1(args) -> None:
     solver = hsddp.Solver(prob, opt, device=0)
     times, iters = [], []
     for rep in range(args.warmup + args.steps):
-        solver.warm_start()  # Xbar = reference, Ubar = K = 0 (HKDProblem.cpp:84-90)
+        # a fresh problem each time: Xbar = reference, Ubar = K = 0 (HKDProblem.cpp:84-90)
+        solver.upload_problem(prob["contacts"], prob["x0"], prob["ref_x"], prob["ref_u"], prob["ref_foot"])
         solver.synchronize()
         t0 = time.perf_counter()
         solver.solve()
