@@ -62,20 +62,32 @@ struct Rot {
     double r[3][3];
 };
 
-HKD_FN void rot_zyx(const double *eul, Rot &R)
+// sin / cos of the three Euler angles, each pair from one sincos (one argument reduction): the
+// model's rotation, its derivatives and the Euler-rate terms share them
+struct EulTrig {
+    double cy, sy, cp, sp, cr, sr;
+};
+HKD_FN EulTrig eul_trig(const double *eul)
 {
-    double cy = cos(eul[0]), sy = sin(eul[0]), cp = cos(eul[1]), sp = sin(eul[1]);
-    double cr = cos(eul[2]), sr = sin(eul[2]);
+    EulTrig t;
+    sincos(eul[0], &t.sy, &t.cy);
+    sincos(eul[1], &t.sp, &t.cp);
+    sincos(eul[2], &t.sr, &t.cr);
+    return t;
+}
+
+HKD_FN void rot_zyx(const EulTrig &t, Rot &R)
+{
+    const double cy = t.cy, sy = t.sy, cp = t.cp, sp = t.sp, cr = t.cr, sr = t.sr;
     R.r[0][0] = cy * cp; R.r[0][1] = cy * sp * sr - sy * cr; R.r[0][2] = sy * sr + cy * sp * cr;
     R.r[1][0] = sy * cp; R.r[1][1] = cy * cr + sy * sp * sr; R.r[1][2] = sy * sp * cr - cy * sr;
     R.r[2][0] = -sp;     R.r[2][1] = cp * sr;                R.r[2][2] = cp * cr;
 }
 
 // dR/d(yaw), dR/d(pitch), dR/d(roll)
-HKD_FN void rot_zyx_grad(const double *eul, Rot &Dy, Rot &Dp, Rot &Dr)
+HKD_FN void rot_zyx_grad(const EulTrig &t, Rot &Dy, Rot &Dp, Rot &Dr)
 {
-    double cy = cos(eul[0]), sy = sin(eul[0]), cp = cos(eul[1]), sp = sin(eul[1]);
-    double cr = cos(eul[2]), sr = sin(eul[2]);
+    const double cy = t.cy, sy = t.sy, cp = t.cp, sp = t.sp, cr = t.cr, sr = t.sr;
     Dy.r[0][0] = -sy * cp; Dy.r[0][1] = -sy * sp * sr - cy * cr; Dy.r[0][2] = cy * sr - sy * sp * cr;
     Dy.r[1][0] = cy * cp;  Dy.r[1][1] = cy * sp * sr - sy * cr;  Dy.r[1][2] = sy * sr + cy * sp * cr;
     Dy.r[2][0] = 0.0;      Dy.r[2][1] = 0.0;                     Dy.r[2][2] = 0.0;
@@ -86,6 +98,9 @@ HKD_FN void rot_zyx_grad(const double *eul, Rot &Dy, Rot &Dp, Rot &Dr)
     Dr.r[1][0] = 0.0; Dr.r[1][1] = sy * sp * cr - cy * sr; Dr.r[1][2] = -cy * cr - sy * sp * sr;
     Dr.r[2][0] = 0.0; Dr.r[2][1] = cp * cr;                Dr.r[2][2] = -cp * sr;
 }
+
+HKD_FN void rot_zyx(const double *eul, Rot &R) { rot_zyx(eul_trig(eul), R); }
+HKD_FN void rot_zyx_grad(const double *eul, Rot &Dy, Rot &Dp, Rot &Dr) { rot_zyx_grad(eul_trig(eul), Dy, Dp, Dr); }
 
 // sum_l c_l (r_l x f_l), lever r_l = (q_lx - px, q_ly - py, -pz): the generated model places
 // the stance foot on the ground plane (hkinodyn_casadi.cpp:272-289 never reads qdummy z).
@@ -119,7 +134,8 @@ HKD_FN void inertia_inv_apply(const double *v, double *o)
 HKD_FN void hkd_step(const double *x, const double *u, const double *c, double dt, double *xn)
 {
     const double *om = x + 6;
-    double cp = cos(x[1]), sp = sin(x[1]), cr = cos(x[2]), sr = sin(x[2]);
+    const EulTrig tr = eul_trig(x);
+    const double cp = tr.cp, sp = tr.sp, cr = tr.cr, sr = tr.sr;
     double ydot = (sr * om[1] + cr * om[2]) / cp;
     xn[0] = x[0] + dt * ydot;
     xn[1] = x[1] + dt * (cr * om[1] - sr * om[2]);
@@ -127,7 +143,7 @@ HKD_FN void hkd_step(const double *x, const double *u, const double *c, double d
 #pragma unroll
     for (int i = 0; i < 3; ++i) xn[3 + i] = x[3 + i] + dt * x[9 + i];
     Rot R;
-    rot_zyx(x, R);
+    rot_zyx(tr, R);
     double w[3], tau[3], Iw[3], rhs[3], acc[3];
     contact_moment(x, u, c, w);
 #pragma unroll
@@ -155,7 +171,8 @@ HKD_FN void hkd_partial_compact(const double *x, const double *u, const double *
                                 double *Sw, double *Bw)
 {
     const double *om = x + 6;
-    double cp = cos(x[1]), sp = sin(x[1]), cr = cos(x[2]), sr = sin(x[2]);
+    const EulTrig tr = eul_trig(x);
+    const double cp = tr.cp, sp = tr.sp, cr = tr.cr, sr = tr.sr;
     double a = sr * om[1] + cr * om[2], b = cr * om[1] - sr * om[2];
     double icp = 1.0 / cp, tp = sp / cp;
     // eul rows, cols {1, 2, 6, 7, 8}
@@ -164,8 +181,8 @@ HKD_FN void hkd_partial_compact(const double *x, const double *u, const double *
     Se[10] = dt * a * icp * icp;     Se[11] = dt * tp * b; Se[12] = dt;    Se[13] = dt * sr * tp; Se[14] = dt * cr * tp;
     // omega rows: dt * Iinv * d(tau - omega x I omega)/dx
     Rot R, Dy, Dp, Dr;
-    rot_zyx(x, R);
-    rot_zyx_grad(x, Dy, Dp, Dr);
+    rot_zyx(tr, R);
+    rot_zyx_grad(tr, Dy, Dp, Dr);
     double w[3];
     contact_moment(x, u, c, w);
     double M[3][17];
@@ -233,7 +250,8 @@ template <typename Emit>
 HKD_FN void hkd_partial_emit(const double *x, const double *u, const double *c, double dt, Emit emit)
 {
     const double *om = x + 6;
-    double cp = cos(x[1]), sp = sin(x[1]), cr = cos(x[2]), sr = sin(x[2]);
+    const EulTrig tr = eul_trig(x);
+    const double cp = tr.cp, sp = tr.sp, cr = tr.cr, sr = tr.sr;
     double a = sr * om[1] + cr * om[2], b = cr * om[1] - sr * om[2];
     double icp = 1.0 / cp, tp = sp / cp;
     emit(0, 0, dt * a * sp / (cp * cp)); emit(0, 1, dt * b / cp); emit(0, 2, 0.0); emit(0, 3, dt * sr / cp);
@@ -241,8 +259,8 @@ HKD_FN void hkd_partial_emit(const double *x, const double *u, const double *c, 
     emit(0, 9, -dt * sr); emit(0, 10, dt * a * icp * icp); emit(0, 11, dt * tp * b); emit(0, 12, dt);
     emit(0, 13, dt * sr * tp); emit(0, 14, dt * cr * tp);
     Rot R, Dy, Dp, Dr;
-    rot_zyx(x, R);
-    rot_zyx_grad(x, Dy, Dp, Dr);
+    rot_zyx(tr, R);
+    rot_zyx_grad(tr, Dy, Dp, Dr);
     // omega rows: column q of M = d(tau - omega x I omega)/dx, then dt Iinv M[:, q]
     auto col = [&](const double (&v)[3], int q) {
         double o[3];
@@ -341,8 +359,10 @@ HKD_FN void hkd_expand_colmajor(const double *Se, const double *Sw, const double
 HKD_FN void foot_body(int l, const double *q, double *pb, double (*dpb)[3])
 {
     double s = leg_side(l), f = leg_front(l);
-    double c0 = cos(q[0]), s0 = sin(q[0]), c1 = cos(q[1]), s1 = sin(q[1]);
-    double c12 = cos(q[1] + q[2]), s12 = sin(q[1] + q[2]);
+    double c0, s0, c1, s1, c12, s12;
+    sincos(q[0], &s0, &c0);
+    sincos(q[1], &s1, &c1);
+    sincos(q[1] + q[2], &s12, &c12);
     pb[0] = kHipX * f - kLower * s12 - kUpper * s1;
     pb[1] = kSideY * s + kAbad * s * c0 - kLower * s0 * c12 - kUpper * s0 * c1;
     pb[2] = kLower * c0 * c12 + kUpper * c0 * c1 + kAbad * s * s0;
@@ -369,8 +389,9 @@ HKD_FN void hkd_foot_position(int l, const double *pos, const double *eul, const
 HKD_FN void hkd_foot_jacobian(int l, const double *eul, const double *q, double *J)
 {
     Rot R, Dy, Dp, Dr;
-    rot_zyx(eul, R);
-    rot_zyx_grad(eul, Dy, Dp, Dr);
+    const EulTrig tr = eul_trig(eul);
+    rot_zyx(tr, R);
+    rot_zyx_grad(tr, Dy, Dp, Dr);
     double pb[3], dpb[3][3];
     foot_body(l, q, pb, dpb);
     for (int i = 0; i < 54; ++i) J[i] = 0.0;
@@ -388,8 +409,9 @@ HKD_FN void hkd_foot_jacobian(int l, const double *eul, const double *q, double 
 HKD_FN double hkd_foot_height_grad(int l, const double *x, double *hx)
 {
     Rot R, Dy, Dp, Dr;
-    rot_zyx(x, R);
-    rot_zyx_grad(x, Dy, Dp, Dr);
+    const EulTrig tr = eul_trig(x);
+    rot_zyx(tr, R);
+    rot_zyx_grad(tr, Dy, Dp, Dr);
     double pb[3], dpb[3][3];
     foot_body(l, x + 12 + 3 * l, pb, dpb);
     if (hx) {
@@ -409,8 +431,9 @@ HKD_FN double hkd_foot_height_grad(int l, const double *x, double *hx)
 HKD_FN double hkd_foot_height_grad_sparse(int l, const double *x, double *ge, double *gq)
 {
     Rot R, Dy, Dp, Dr;
-    rot_zyx(x, R);
-    rot_zyx_grad(x, Dy, Dp, Dr);
+    const EulTrig tr = eul_trig(x);
+    rot_zyx(tr, R);
+    rot_zyx_grad(tr, Dy, Dp, Dr);
     double pb[3], dpb[3][3];
     foot_body(l, x + 12 + 3 * l, pb, dpb);
     ge[0] = Dy.r[2][0] * pb[0] + Dy.r[2][1] * pb[1] + Dy.r[2][2] * pb[2];

@@ -275,8 +275,9 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
                 for (int k = 0; k < 3; ++k) spx[(12 + 3 * l + k) * (NX + 2)] = 0.0;
             } else if (!sc[l] && scn[l]) {  // rows k < 2: the foot Jacobian's rows (hkd_foot_jacobian)
                 Rot R, Dy, Dp, Dr;
-                rot_zyx(sx, R);
-                rot_zyx_grad(sx, Dy, Dp, Dr);
+                const EulTrig tr = eul_trig(sx);
+                rot_zyx(tr, R);
+                rot_zyx_grad(tr, Dy, Dp, Dr);
                 double pb[3], dpb[3][3];
                 foot_body(l, sx + 12 + 3 * l, pb, dpb);
 #pragma unroll
