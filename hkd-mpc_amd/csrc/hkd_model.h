@@ -174,9 +174,9 @@ HKD_FN void hkd_partial_compact(const double *x, const double *u, const double *
     const EulTrig tr = eul_trig(x);
     const double cp = tr.cp, sp = tr.sp, cr = tr.cr, sr = tr.sr;
     double a = sr * om[1] + cr * om[2], b = cr * om[1] - sr * om[2];
-    double icp = 1.0 / cp, tp = sp / cp;
+    const double icp = 1.0 / cp, tp = sp * icp;  // one reciprocal for the Euler-rate rows
     // eul rows, cols {1, 2, 6, 7, 8}
-    Se[0] = dt * a * sp / (cp * cp); Se[1] = dt * b / cp; Se[2] = 0.0;     Se[3] = dt * sr / cp; Se[4] = dt * cr / cp;
+    Se[0] = dt * a * sp * (icp * icp); Se[1] = dt * b * icp; Se[2] = 0.0; Se[3] = dt * sr * icp; Se[4] = dt * cr * icp;
     Se[5] = 0.0;                     Se[6] = -dt * a;     Se[7] = 0.0;     Se[8] = dt * cr;      Se[9] = -dt * sr;
     Se[10] = dt * a * icp * icp;     Se[11] = dt * tp * b; Se[12] = dt;    Se[13] = dt * sr * tp; Se[14] = dt * cr * tp;
     // omega rows: dt * Iinv * d(tau - omega x I omega)/dx
@@ -253,9 +253,9 @@ HKD_FN void hkd_partial_emit(const double *x, const double *u, const double *c, 
     const EulTrig tr = eul_trig(x);
     const double cp = tr.cp, sp = tr.sp, cr = tr.cr, sr = tr.sr;
     double a = sr * om[1] + cr * om[2], b = cr * om[1] - sr * om[2];
-    double icp = 1.0 / cp, tp = sp / cp;
-    emit(0, 0, dt * a * sp / (cp * cp)); emit(0, 1, dt * b / cp); emit(0, 2, 0.0); emit(0, 3, dt * sr / cp);
-    emit(0, 4, dt * cr / cp); emit(0, 5, 0.0); emit(0, 6, -dt * a); emit(0, 7, 0.0); emit(0, 8, dt * cr);
+    const double icp = 1.0 / cp, tp = sp * icp;  // one reciprocal for the Euler-rate rows
+    emit(0, 0, dt * a * sp * (icp * icp)); emit(0, 1, dt * b * icp); emit(0, 2, 0.0); emit(0, 3, dt * sr * icp);
+    emit(0, 4, dt * cr * icp); emit(0, 5, 0.0); emit(0, 6, -dt * a); emit(0, 7, 0.0); emit(0, 8, dt * cr);
     emit(0, 9, -dt * sr); emit(0, 10, dt * a * icp * icp); emit(0, 11, dt * tp * b); emit(0, 12, dt);
     emit(0, 13, dt * sr * tp); emit(0, 14, dt * cr * tp);
     Rot R, Dy, Dp, Dr;

@@ -93,10 +93,13 @@ DEV double reb_cost(double g, double delta, double log_delta)
     double t = (g - 2 * delta) / delta;
     return .5 * (t * t - 1) - log_delta;
 }
-DEV void reb_derivs(double g, double delta, double &d1, double &d2)
+// first and second derivative of reb_cost in g; inv_delta = 1 / delta.  One reciprocal per row
+// (the branches are selects across lanes, so both sides always execute)
+DEV void reb_derivs(double g, double delta, double inv_delta, double &d1, double &d2)
 {
-    if (g > delta) { d1 = -1.0 / g; d2 = 1.0 / (g * g); }
-    else { d1 = (g - 2 * delta) / delta / delta; d2 = 1.0 / (delta * delta); }
+    const double r = 1.0 / g, q = inv_delta * inv_delta;
+    d1 = g > delta ? -r : (g - 2 * delta) * q;
+    d2 = g > delta ? r * r : q;
 }
 
 // GRF friction pyramid (HKDConstraints.cpp:7-66): rows of A_leg applied to one leg's force
@@ -137,17 +140,34 @@ DEV double running_cost(const Params &p, const int *c, const double *x, const do
     // unrolled: a runtime leg index into u would put the control vector in scratch.  Uniform ReB
     // parameters (the default schedule): one log(delta) for the 20 rows, the value each would compute
     auto reb_sum = [&](auto uniform) {
-        const double log_du = uniform ? log(p.grf_delta) : 0.0;
+        if constexpr (decltype(uniform)::value) {
+            // uniform parameters (the default schedule): the rows with g > delta of one leg share one
+            // log of their product (sum of -log g = -log of the product), the others the quadratic branch
+            const double dl = p.grf_delta, e = p.grf_eps, log_du = log(dl), inv_dl = 1.0 / dl;
 #pragma unroll
-        for (int lg = 0; lg < 4; ++lg) {
-            if (!c[lg]) continue;
+            for (int lg = 0; lg < 4; ++lg) {
+                if (!c[lg]) continue;
+                double prod = 1.0, quad = 0.0;
 #pragma unroll
-            for (int r = 0; r < 5; ++r) {
-                double g = grf_value(p.mu, r, u + 3 * lg);
-                mk = fmin(mk, g);
-                const double e = uniform ? p.grf_eps : eps[5 * lg + r];
-                const double dl = uniform ? p.grf_delta : delta[5 * lg + r];
-                rc += e * reb_cost(g, dl, uniform ? log_du : log(dl));
+                for (int r = 0; r < 5; ++r) {
+                    const double g = grf_value(p.mu, r, u + 3 * lg);
+                    mk = fmin(mk, g);
+                    const double t = (g - 2 * dl) * inv_dl;
+                    prod *= g > dl ? g : 1.0;
+                    quad += g > dl ? 0.0 : .5 * (t * t - 1) - log_du;
+                }
+                rc += e * (quad - log(prod));
+            }
+        } else {
+#pragma unroll
+            for (int lg = 0; lg < 4; ++lg) {
+                if (!c[lg]) continue;
+#pragma unroll
+                for (int r = 0; r < 5; ++r) {
+                    double g = grf_value(p.mu, r, u + 3 * lg);
+                    mk = fmin(mk, g);
+                    rc += eps[5 * lg + r] * reb_cost(g, delta[5 * lg + r], log(delta[5 * lg + r]));
+                }
             }
         }
     };

@@ -165,6 +165,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 #pragma unroll
     for (int j = 0; j < 24; ++j) rb[j] = 0.0;
     if (p.ReB_active) {
+        const double inv_du = 1.0 / p.grf_delta;
 #pragma unroll
         for (int lg = 0; lg < 4; ++lg) {
             if (!c[lg]) continue;
@@ -174,7 +175,8 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
                 double row[3], d1, d2;
                 grf_row(p.mu, r, row);
                 double g = row[0] * u[3 * lg] + row[1] * u[3 * lg + 1] + row[2] * u[3 * lg + 2];
-                reb_derivs(g, p.reb_uniform ? p.grf_delta : dl[5 * lg + r], d1, d2);
+                const double dlr = p.reb_uniform ? p.grf_delta : dl[5 * lg + r];
+                reb_derivs(g, dlr, p.reb_uniform ? inv_du : 1.0 / dlr, d1, d2);
                 double e = p.reb_uniform ? p.grf_eps : ep[5 * lg + r];
                 for (int a = 0; a < 3; ++a) gu[a] += e * d1 * row[a];
                 hu[0] += e * (d2 * row[0] * row[0]); hu[1] += e * (d2 * row[0] * row[1]);
