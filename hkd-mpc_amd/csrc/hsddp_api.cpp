@@ -427,14 +427,18 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         return rc;
     }
     d.contacts = contacts; d.x0 = x0; d.ref_x = rx; d.ref_u = ru; d.ref_foot = rf;
-    {   // parallel regularisation retries: up to 128 deferred elements per launch, p.retry_m attempts each
-        // (HSDDP_SEQUENTIAL_RETRY=1 keeps every retry inside k_riccati: a diagnostic for tests)
-        // Scratch: cap x M attempts x (Kc gain rows + Kc dU rows), e.g. 128 x 17 x 200 x 312 x 8 B = 1.1 GB
-        // at the metric's horizon in fp64 (device_bytes counts it).  HSDDP_RETRY_CAP=n lowers the cap
-        // (a diagnostic: tests use it to send deferrals past the cap into the in-kernel loop).
+    {   // parallel regularisation retries: p.retry_m attempts for each of up to `cap` deferred elements
+        // per launch (HSDDP_SEQUENTIAL_RETRY=1 keeps every retry inside k_riccati: a diagnostic for
+        // tests).  Scratch per deferred element: M attempts x (Kc gain rows + Kc dU rows), 8.5 MB at the
+        // metric's horizon in fp64 (17 x 200 x 312 x 8 B).  The cap is 128 elements within a 256 MiB
+        // budget (30 at the metric's horizon; device_bytes counts it): the oracle's jump solves defer a
+        // few elements of 4096 per iteration, and deferrals past the cap run the same retries inside
+        // k_riccati.  HSDDP_RETRY_CAP=n lowers the cap (a diagnostic: tests use it to send deferrals
+        // past the cap into the in-kernel loop).
         const char *seq = std::getenv("HSDDP_SEQUENTIAL_RETRY");
         const char *capenv = std::getenv("HSDDP_RETRY_CAP");
-        size_t cap = std::min<size_t>(128, B);
+        const size_t per_elem = (size_t)std::max(1, p.retry_m) * Kc * (KCW * (p.fp32 ? 4 : 8) + NX * 8 + 4);
+        size_t cap = std::min<size_t>(std::min<size_t>(128, B), std::max<size_t>(2, ((size_t)256 << 20) / per_elem));
         if (capenv && std::atoi(capenv) > 0) cap = std::min<size_t>(cap, (size_t)std::atoi(capenv));
         const size_t M = (seq && seq[0] == '1') ? 0 : p.retry_m, n = cap * M;
         if (M > 0) {

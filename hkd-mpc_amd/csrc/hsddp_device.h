@@ -178,9 +178,10 @@ DEV double running_cost(const Params &p, const int *c, const double *x, const do
     return l;
 }
 
-// terminal cost Phi (tracking Qf + 10 * foot + AL), max |h| and h per touchdown leg
-DEV double terminal_cost(const Params &p, const int *c, const int *cn, const double *x, const double *xr,
-                         const double *pf, const double *sig, const double *lam, double &tviol, double *h_out)
+// terminal cost Phi (tracking Qf + 10 * foot + AL) from the touchdown legs' foot heights h[l]
+// (hkd_foot_height_grad - ground; any value for other legs), and max |h|
+DEV double terminal_cost_h(const Params &p, const int *c, const int *cn, const double *x, const double *xr,
+                           const double *pf, const double *sig, const double *lam, const double *hl, double &tviol)
 {
     double phi = 0.0, fc = 0.0;
 #pragma unroll
@@ -198,10 +199,8 @@ DEV double terminal_cost(const Params &p, const int *c, const int *cn, const dou
     double al = 0.0, tv = 0.0;
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
-        h_out[l] = 0.0;
         if (!touchdown(c, cn, l)) continue;
-        double h = hkd_foot_height_grad(l, x, nullptr) - p.ground;
-        h_out[l] = h;
+        const double h = hl[l];
         tv = fmax(tv, fabs(h));
         al += 0.5 * sig[l] * h * h;
         al += lam[l] * h;
@@ -210,6 +209,16 @@ DEV double terminal_cost(const Params &p, const int *c, const int *cn, const dou
     tviol = tv;
     return phi;
 }
+
+// terminal cost Phi (tracking Qf + 10 * foot + AL), max |h| and h per touchdown leg
+DEV double terminal_cost(const Params &p, const int *c, const int *cn, const double *x, const double *xr,
+                         const double *pf, const double *sig, const double *lam, double &tviol, double *h_out)
+{
+#pragma unroll
+    for (int l = 0; l < 4; ++l) h_out[l] = touchdown(c, cn, l) ? hkd_foot_height_grad(l, x, nullptr) - p.ground : 0.0;
+    return terminal_cost_h(p, c, cn, x, xr, pf, sig, lam, h_out, tviol);
+}
+
 
 
 }  // namespace hsddp

@@ -110,12 +110,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
         for (int j = 0; j < NX; ++j) d32[j] = (float)dg[j];
     }
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
-    if (k == L.N(i)) {
-        double tv, h[4];
-        const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
-        d.slot_cost[(size_t)b * p.S + s] = terminal_cost(p, c, cn, x, xr, pf, sg, lm, tv, h);
-        return;
-    }
+    if (k == L.N(i)) return;  // the terminal cost: k_terminal (the same function, from its foot heights)
     const int kc = L.k0(i) + k;
     sridx[w][lane] = (long)b * p.Kc + kc;
     double u[NU];
@@ -201,7 +196,7 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
     const auto L = layout_of<EL>(d, b);
     const int P = L.P();
     if (i >= P) return;
-    __shared__ double sx[NX], shx[4][NX], scoef[4][2];
+    __shared__ double sx[NX], shx[4][NX], scoef[4][2], sh[4];
     __shared__ int sc[4], scn[4];
     const int s = L.s0(i) + L.N(i);
     if (t < NX) sx[t] = d.Xb[work_buf(d, b)][((size_t)b * p.S + s) * NX + t];
@@ -224,11 +219,17 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
         double sg = d.al_sigma[((size_t)b * p.P + i) * 4 + l], lm = d.al_lambda[((size_t)b * p.P + i) * 4 + l];
         scoef[l][0] = (td && p.AL_active) ? sg * h + lm : 0.0;
         scoef[l][1] = (td && p.AL_active) ? sg * (1 + h) + lm : 0.0;
+        sh[l] = h;
     }
     __syncthreads();
     KParams &kp = *kparams();  // runtime-indexed weights
     double *rec = d.term + ((size_t)b * p.P + i) * TW;
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
+    if (t == 0) {  // the phase's terminal cost at X[N] (SinglePhase::compute_cost's last term) for k_lq's slot sums
+        double tv;
+        const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
+        d.slot_cost[(size_t)b * p.S + s] = terminal_cost_h(p, sc, scn, sx, xr, pf, sg, lm, sh, tv);
+    }
     if (t < NX) { // Phix
         const int j = t;
         double v = kp.qf_gain * kp.qf_scale[j] * q_diag(kp, sc, j) * (sx[j] - xr[j]);
@@ -306,9 +307,8 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
 // Per-slot outputs of one rollout trial from the slot's state x = X[k], simulated state xs =
 // Xsim[k] and control u = U[k] (k < N): Defect, |Defect|^2, divergence flag, running or terminal
 // cost with its constraint violation and touchdown residuals (SinglePhase.cpp:196-232).
-template <typename L_>
-DEV void finish_slot(const Params &p, const Bufs &d, const L_ &L, int b, int s, int i, int k, const int *c,
-                     const int *cn, const double *x, const double *xs, const double *u)
+// Defect = Xsim - X, its squared norm and the divergence flag of slot s
+DEV void finish_defect(const Params &p, const Bufs &d, int b, int s, int k, const double *x, const double *xs)
 {
     const size_t sb = (size_t)b * p.S;
     double nrm = 0.0, fs = 0.0;
@@ -322,22 +322,42 @@ DEV void finish_slot(const Params &p, const Bufs &d, const L_ &L, int b, int s, 
     }
     d.slot_feas[sb + s] = fs;
     d.slot_div[sb + s] = (k > 0 && sqrt(nrm) > 1e6) ? 1 : 0;
+}
+
+// the terminal cost of phase i at its last slot s (x = X[N]) with its violation and touchdown residuals
+DEV void finish_terminal(const Params &p, const Bufs &d, int b, int s, int i, const int *c, const int *cn, const double *x)
+{
+    const size_t sb = (size_t)b * p.S;
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
-    if (k == L.N(i)) {
-        double tv, h[4];
-        const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
-        d.slot_cost[sb + s] = terminal_cost(p, c, cn, x, xr, pf, sg, lm, tv, h);
-        d.slot_viol[sb + s] = tv;
+    double tv, h[4];
+    const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
+    d.slot_cost[sb + s] = terminal_cost(p, c, cn, x, xr, pf, sg, lm, tv, h);
+    d.slot_viol[sb + s] = tv;
 #pragma unroll
-        for (int l = 0; l < 4; ++l) d.term_h[((size_t)b * p.P + i) * 4 + l] = h[l];
-    } else {
-        const int kc = L.k0(i) + k;
-        const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
-        const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
-        double viol;
-        d.slot_cost[sb + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
-        d.slot_viol[sb + s] = viol;
-    }
+    for (int l = 0; l < 4; ++l) d.term_h[((size_t)b * p.P + i) * 4 + l] = h[l];
+}
+
+// the running cost of control slot kc = k0(i) + k at state slot s
+DEV void finish_running(const Params &p, const Bufs &d, int b, int s, int kc, const int *c, const double *x, const double *u)
+{
+    const size_t sb = (size_t)b * p.S;
+    const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
+    const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
+    const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
+    double viol;
+    d.slot_cost[sb + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
+    d.slot_viol[sb + s] = viol;
+}
+
+template <typename L_>
+DEV void finish_slot(const Params &p, const Bufs &d, const L_ &L, int b, int s, int i, int k, const int *c,
+                     const int *cn, const double *x, const double *xs, const double *u)
+{
+    finish_defect(p, d, b, s, k, x, xs);
+    if (k == L.N(i))
+        finish_terminal(p, d, b, s, i, c, cn, x);
+    else
+        finish_running(p, d, b, s, L.k0(i) + k, c, x, u);
 }
 
 // k_rollout: one line-search trial (eps) per (element, state slot).  All knots are shooting states
@@ -370,8 +390,8 @@ DEV void stage_trial(double *L, double *const *buf, const double *del, long r0, 
         typedef double d2 __attribute__((ext_vector_type(2)));
         const d2 xb = *(const d2 *)(bar + r * NX + cc), dx = *(const d2 *)(del + r * NX + cc);
         d2 v;
-        v.x = xb.x + eps * dx.x;
-        v.y = xb.y + eps * dx.y;
+        v.x = __builtin_fma(eps, dx.x, xb.x);
+        v.y = __builtin_fma(eps, dx.y, xb.y);
         L[row * RS + cc] = v.x;
         L[row * RS + cc + 1] = v.y;
         if (own(r)) *(d2 *)(out + r * NX + cc) = v;
@@ -413,9 +433,9 @@ DEV void stage_trial2(double *L, const Bufs &d, long r0, long nrows, int per, do
         if (!use[it]) continue;
         const int f = lane + 64 * it, row = f / CH, cc = 2 * (f % CH);
         const long r = rr[it];
-        d2 v;
-        v.x = xb[it].x + eps * dx[it].x;
-        v.y = xb[it].y + eps * dx[it].y;
+        d2 v;  // Xbar + eps dX as one rounding (rollout_boundary forms the same rows)
+        v.x = __builtin_fma(eps, dx[it].x, xb[it].x);
+        v.y = __builtin_fma(eps, dx[it].y, xb[it].y);
         L[row * RS + cc] = v.x;
         L[row * RS + cc + 1] = v.y;
         const bool first = r / per == bA;
@@ -444,12 +464,57 @@ DEV void trial_row(const Bufs &d, const double *Ubar, long r, double eps, double
 // Only the state rows go through LDS (13 KB per wave); the control rows are read per lane
 // (trial_row), the slot's own control row stored from registers.  With both row sets in LDS
 // (26 KB per wave) only 6 waves fit a CU: 1.25 ms/step of line search vs 0.93 here.
+// The phase-boundary work of one trial, one thread per (phase i, element b), i-major so that a
+// wave's threads share a phase (and, in a shared-gait batch, its contacts: no divergence): the
+// reset map into the phase's first slot (MultiPhaseDDP.cpp:73-81) with that slot's Defect, and the
+// terminal cost at its last slot.  These run in waves of their own: inside the slot waves, a
+// lane's reset map or terminal cost (foot kinematics) stalled its 63 neighbours.
+template <bool EL>
+DEV void rollout_boundary(const Params &p, const Bufs &d, double eps, int init, long t)
+{
+    if (t >= (long)p.B * p.P) return;
+    const int i = (int)(t / p.B), b = (int)(t % p.B);
+    const ElemState &E = d.el[b];
+    if (!(init ? !E.done : E.ls_active != 0)) return;
+    const auto L = layout_of<EL>(d, b);
+    if (i >= L.P()) return;
+    const int nb = nom_buf(d, b), s0 = L.s0(i), sN = s0 + L.N(i);
+    const double *Xbar = d.Xb[nb];
+    const size_t sb = (size_t)b * p.S;
+    // trial rows X = Xbar + eps dX (the slot waves' expression: the same values)
+    auto trial = [&](int s, double *x) {
+        const double *xb = Xbar + (sb + s) * NX, *dx = d.dX + (sb + s) * NX;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) x[j] = __builtin_fma(eps, dx[j], xb[j]);
+    };
+    int c[4], cn[4];
+    load_contacts(d, p, b, i, c, cn);
+    double x[NX];
+    if (i > 0) {
+        double xp[NX], xs[NX];
+        int cp_[4], cpn[4];
+        load_contacts(d, p, b, i - 1, cp_, cpn);
+        trial(s0 - 1, xp);
+        trial(s0, x);
+        hkd_resetmap(xp, cp_, cpn, xs);
+        finish_defect(p, d, b, s0, 0, x, xs);
+    }
+    trial(sN, x);
+    finish_terminal(p, d, b, sN, i, c, cn, x);
+}
+
 template <bool EL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOUT_WAVES))) void k_rollout(Params p, Bufs d, double eps, int init)
 {
     __shared__ double Xt[RW * RS];
     const int lane = threadIdx.x;
-    const long total = (long)p.B * p.S, g0 = (long)blockIdx.x * 64, gid = g0 + lane;
+    const long total = (long)p.B * p.S;
+    const long nslot = (total + 63) / 64;
+    if ((long)blockIdx.x >= nslot) {  // the phase-boundary waves (after the slot waves)
+        rollout_boundary<EL>(p, d, eps, init, ((long)blockIdx.x - nslot) * 64 + lane);
+        return;
+    }
+    const long g0 = (long)blockIdx.x * 64, gid = g0 + lane;
     const long gl = min(g0 + 63, total - 1);
     const int bA = (int)(g0 / p.S), bB = (int)(gl / p.S);
     auto act = [&](int b) { const ElemState &E = d.el[b]; return init ? !E.done : E.ls_active != 0; };
@@ -478,31 +543,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     const double *x = Xt + (gid - xr0) * RS;
     const long kq = (long)b * p.Kc + s - i;  // the slot's control row (k < N)
     const int nb = nomof(b);
-    double xs[NX];
-    if (k == 0) {
-        if (i == 0) {
+    // a phase's first slot: x_init = x0, or the reset map of X_{i-1}[N] (MultiPhaseDDP.cpp:73-81),
+    // whose Defect the boundary waves write
+    if (k > 0 || i == 0) {
+        double xs[NX];
+        if (k == 0) {
 #pragma unroll
             for (int j = 0; j < NX; ++j) xs[j] = d.x0[(size_t)b * NX + j];
-        } else { // x_init = resetmap(X_{i-1}[N]) (MultiPhaseDDP.cpp:73-81)
-            int cp_[4], cpn[4];
-            load_contacts(d, p, b, i - 1, cp_, cpn);
-            hkd_resetmap(x - RS, cp_, cpn, xs);
+        } else {
+            double up[NU];
+            trial_row(d, d.Ub[nb], kq - 1, eps, up);
+            double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
+            hkd_step(x - RS, up, cd, p.dt, xs);
         }
-    } else {
-        double up[NU];
-        trial_row(d, d.Ub[nb], kq - 1, eps, up);
-        double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
-        hkd_step(x - RS, up, cd, p.dt, xs);
+        finish_defect(p, d, b, s, k, x, xs);
     }
-    double u[NU];  // read by finish_slot only when k < N
+    // the running cost of a control slot (the terminal cost at k = N: the boundary waves)
     if (k < L.N(i)) {
+        double u[NU];
         trial_row(d, d.Ub[nb], kq, eps, u);
         typedef double d2 __attribute__((ext_vector_type(2)));
         d2 *ug = (d2 *)(d.Ub[nb ^ 1] + kq * NU);
 #pragma unroll
         for (int j = 0; j < NU / 2; ++j) ug[j] = d2{u[2 * j], u[2 * j + 1]};
+        finish_running(p, d, b, s, L.k0(i) + k, c, x, u);
     }
-    finish_slot(p, d, L, b, s, i, k, c, cn, x, xs, u);
 }
 
 // k_rollout_tail: the non-shooting states of a phase (k >= ss; HKDProblem::update leaves a new
@@ -1039,7 +1104,9 @@ static inline unsigned blocks_for(long n, int bs) { return (unsigned)((n + bs - 
 
 void launch_rollout(const Params &p, const Bufs &d, double eps, int init, hipStream_t st)
 {
-    LAUNCH_EL(k_rollout, dim3(blocks_for((long)p.B * p.S, 64)), dim3(64), st, p, d, eps, init);
+    // slot waves, then the phase-boundary waves (k_rollout, rollout_boundary)
+    LAUNCH_EL(k_rollout, dim3(blocks_for((long)p.B * p.S, 64) + blocks_for((long)p.B * p.P, 64)), dim3(64), st, p, d,
+              eps, init);
     if (p.has_tail) LAUNCH_EL(k_rollout_tail, dim3((p.B + 63) / 64), dim3(64), st, p, d, eps, init);
 }
 void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, hipStream_t st)

@@ -13,6 +13,37 @@ using namespace hkd;
 
 constexpr int HC = 12;  // coupled controls per knot
 
+#ifndef HSDDP_STAMPS
+#define HSDDP_STAMPS 0
+#endif
+// Diagnostic build (make stamps): s_memtime at the stage boundaries of a knot, differences summed
+// per stage into LDS and written to Bufs::dbg of the wave's second element (tools/stamps.py)
+#if HSDDP_STAMPS
+struct LinStamps {
+    unsigned long long st[8], tprev;
+};
+DEV LinStamps &lin_stamps()
+{
+    __shared__ LinStamps s;
+    return s;
+}
+#define LSTAMP(n)                                                                             \
+    do {                                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        unsigned long long t_;                                                                \
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        if (threadIdx.x == 0) {                                                               \
+            if ((n) > 0) lin_stamps().st[n] += t_ - lin_stamps().tprev;                       \
+            lin_stamps().tprev = t_;                                                          \
+        }                                                                                     \
+    } while (0)
+#else
+#define LSTAMP(n) \
+    do {          \
+    } while (0)
+#endif
+
 // Per-precision buffers: LQ record (stride LQS), compact gains and the Defect copy the sweep reads.
 template <typename real> struct Prec;
 template <> struct Prec<double> {
@@ -142,9 +173,13 @@ template <typename real>
 struct LinBuf {
     alignas(16) char v[2][LinImg<real>::NI * 1024];  // element h's image at v[h]
 };
+// dX / du rows of the current knot (slots 24..31 stay zero: the index of an absent term) and a
+// zero region standing for the coefficients of structurally absent terms
+constexpr int LZ = 31;  // a zero slot of dx / du
 template <typename real>
 struct LinVec {
-    real dx[2][NX], du[2][NX];
+    real dx[2][32], du[2][32];
+    real zero[64];
 };
 
 // This lane's LDS-DMA sources: piece 64 j + lane of each element's image (spare pieces repeat the
@@ -210,7 +245,8 @@ DEV void vm_wait()
     else static_assert(W < 0, "wait count");
 }
 
-// per-lane constants of one phase
+// per-lane constants of one phase: every row's terms as one branch-free formula, a structurally
+// absent term reading a zero coefficient (LinVec::zero) or the zero slot LZ of dx / du
 template <typename real>
 struct LinRow {
     PhaseConst<real> pc;
@@ -218,7 +254,45 @@ struct LinRow {
     real ru;
     bool cpl;   // control r has a coupled gain row (KCW layout)
     int krow0;  // its first entry in the K image
+    bool use_se, use_sw, use_rb;  // rows 0..2: A - I eul row; rows 6..8: A - I omega row, BW row; rows < 12: ReB block
+    int se0, sw0, rb0, rbi[3];    // record offsets of those rows (rb: the leg's block, entry (r % 3, b))
+    real c3;                      // rows 3..5: dt (dX[r + 6]); else 0
+    int i3;                       // r + 6, or LZ
+    real cx[4];                   // lxx cross terms: rows 3..5 xq[l] (dX[12 + 3 l + r - 3]), rows >= 12 xp (dX[3 + (r - 12) % 3])
+    int ix[4];
+    real cu[4];                   // rows 9..11: bv[l] (du[3 l + r - 9])
+    int iu[4];
+    real cq;                      // rows >= 12: dt (1 - c) on the lane's own du
+    int iru;                      // rows < 12: first du of the leg's block (3 (r / 3)), else LZ
 };
+
+template <typename real>
+DEV void lin_row(const Params &p, LinRow<real> &R, int r)
+{
+    const int rr = r < NX ? r : 0;
+    R.use_se = r < 3;
+    R.use_sw = r >= 6 && r < 9;
+    R.use_rb = r < 12;
+    R.se0 = LQ_SE + 5 * (r < 3 ? r : 0);
+    R.sw0 = r >= 6 && r < 9 ? r - 6 : 0;
+    R.rb0 = LQ_RB + 6 * ((r < 12 ? r : 0) / 3);
+    const int a = (r < 12 ? r : 0) % 3;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) R.rbi[b] = a == 0 ? b : a == 1 ? (b == 0 ? 1 : b == 1 ? 3 : 4) : (b == 0 ? 2 : b == 1 ? 4 : 5);
+    R.iru = r < 12 ? 3 * (r / 3) : LZ;
+    R.c3 = (r >= 3 && r < 6) ? (real)p.dt : (real)0;
+    R.i3 = (r >= 3 && r < 6) ? r + 6 : LZ;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        const bool pos = r >= 3 && r < 6, q = r >= 12 && r < NX;
+        R.cx[l] = pos ? R.lx.xq[l] : (q && l == 0) ? R.lx.xp : (real)0;
+        R.ix[l] = pos ? 12 + 3 * l + r - 3 : (q && l == 0) ? 3 + (r - 12) % 3 : LZ;
+        const bool v = r >= 9 && r < 12;
+        R.cu[l] = v ? R.pc.bv[l] : (real)0;
+        R.iu[l] = v ? 3 * l + r - 9 : LZ;
+    }
+    R.cq = (r >= 12 && r < NX) ? pick4(R.pc.bq, (rr - 12) / 3) : (real)0;
+}
 
 // a knot's results, stored one knot later
 template <typename real>
@@ -240,6 +314,7 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
     const bool rowl = r < NX;
     const int rr = rowl ? r : 0;
     const real dt = p.dt;
+    LSTAMP(0);
     if (more) {
         src.advance();
         lin_fetch(nxt, src);
@@ -261,21 +336,34 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
         else vm_wait<0>();
     }
     LSYNC();
+    LSTAMP(1);
     const char *img = cur.v[hf];
     const real *kimg = (const real *)(img + I::K), *lq = (const real *)(img + I::LQ), *dd = (const real *)(img + I::D);
     const double *dUi = (const double *)(img + I::DU);
     real *sdxv = S.dx[hf], *sduv = S.du[hf];
-    real krow[NX];
+    // every coefficient of the knot read at once (one LDS wait, not one per multiply-add); an absent
+    // term's coefficient comes from the zero region
+    const real *kp = R.cpl ? kimg + R.krow0 : S.zero;
+    const real *sep = R.use_se ? lq + R.se0 : S.zero, *swp = R.use_sw ? lq + LQ_SW + R.sw0 : S.zero;
+    const real *bwp = R.use_sw ? lq + LQ_BW + R.sw0 : S.zero, *rbp = R.use_rb ? lq + R.rb0 : S.zero;
+    const real *lxp = rowl ? lq + LQ_LX : S.zero, *lup = rowl ? lq + LQ_LU : S.zero;
+    real krow[NX], cse[5], csw[17], cbw[12], crb[3];
 #pragma unroll
-    for (int c = 0; c < NX; ++c) krow[c] = R.cpl ? kimg[R.krow0 + c] : (real)0;
+    for (int c = 0; c < NX; ++c) krow[c] = kp[c];
     const real dUr = (real)dUi[rr];
-    if (rowl) sdxv[r] = dx;  // for the products with lane-dependent columns below
+#pragma unroll
+    for (int q = 0; q < 5; ++q) cse[q] = sep[5 * 0 + q];
+#pragma unroll
+    for (int q = 0; q < 17; ++q) csw[q] = swp[3 * q];
+    const real ddr = (rowl ? dd : S.zero)[rr], lxr = lxp[rr], lur = lup[rr];
+    if (rowl) sdxv[r] = dx;  // for the terms with lane-dependent columns below
     // dX of this half's rows at every lane by DPP position (dxa: rows 0..15, dxb: rows 16..23):
     // the products with compile-time columns take it by row broadcast, not from LDS
     real dxa, dxb;
     row_pair(dx, dxa, dxb);
     asm volatile("" : "+v"(dxa), "+v"(dxb));
     asm volatile("s_nop 1");  // DPP sources just written by the permlane swaps
+    pin(krow);
     // K dX as two 12-column sums (the order of the one-element-per-wave kernel's two halves)
     real k0 = 0, k1 = 0;
     static_for<HC>([&](auto C) {
@@ -285,67 +373,62 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
         else bfma<c1 - 16>(k1, dxb, krow[c1]);
     });
     const real du = dUr + (k0 + k1);
-    // A - I rows 0..2 (SE) and 6..8 (SW) for every lane (rows clamped; the results are selected
-    // below): the broadcasts need every source lane active, so no branch around them
-    const int rse = r < 3 ? r : 0, rsw = (r >= 6 && r < 9) ? r - 6 : 0;
+    LSTAMP(2);
+    SFENCE();  // the second batch of coefficient reads after K dX (not hoisted: registers)
+#pragma unroll
+    for (int q = 0; q < 12; ++q) cbw[q] = bwp[3 * q];
+#pragma unroll
+    for (int b = 0; b < 3; ++b) crb[b] = rbp[R.rbi[b]];
+    if (rowl) sduv[r] = du;
+    // dX terms with lane-dependent columns (rows 3..5: dt dX[r + 6]; lxx cross terms)
+    const real x3 = sdxv[R.i3];
+    real xc[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) xc[l] = sdxv[R.ix[l]];
+    // A - I rows 0..2 (SE) and 6..8 (SW), zero coefficients on the other rows
+    pin(cse);
+    pin(csw);
     real se = 0, sw = 0;
-    static_for<5>([&](auto Q) { bfma<se_col(Q)>(se, dxa, lq[LQ_SE + 5 * rse + Q]); });
+    static_for<5>([&](auto Q) { bfma<se_col(Q)>(se, dxa, cse[Q]); });
     static_for<17>([&](auto Q) {
         constexpr int col = sw_col(Q);
-        if constexpr (col < 16) bfma<col>(sw, dxa, lq[sw_at(0, Q) + rsw]);
-        else bfma<col - 16>(sw, dxb, lq[sw_at(0, Q) + rsw]);
+        if constexpr (col < 16) bfma<col>(sw, dxa, csw[Q]);
+        else bfma<col - 16>(sw, dxb, csw[Q]);
     });
-    if (rowl) sduv[r] = du;
     real dua, dub;
     row_pair(du, dua, dub);
     asm volatile("" : "+v"(dua), "+v"(dub));
     asm volatile("s_nop 1");
+    pin(cbw);
     real bw = 0;  // B rows 6..8 (BW) times du, columns 0..11
-    static_for<12>([&](auto C) { bfma<C>(bw, dua, lq[bw_at(0, C) + rsw]); });
+    static_for<12>([&](auto C) { bfma<C>(bw, dua, cbw[C]); });
     (void)dub;
     LSYNC();
-    real nx = 0;
-    if (rowl) {
-        const PhaseConst<real> &pc = R.pc;
-        real sdx = 0;
-        if (r < 3) {
-            sdx = se;
-        } else if (r < 6) {
-            sdx = dt * sdxv[r + 6];
-        } else if (r < 9) {
-            sdx = sw;
-        }
-        real bdu = 0, lxd = R.lx.diag * dx, lud = R.ru * du;
-        if (r < 6) {
-            if (r >= 3) {
+    LSTAMP(3);
+    // du terms with lane-dependent columns (rows 9..11: bv du of the legs' GRF; rows < 12: ReB block)
+    real uc[4], ur[3];
 #pragma unroll
-                for (int l = 0; l < 4; ++l) lxd += R.lx.xq[l] * sdxv[12 + 3 * l + r - 3];
-            }
-        } else if (r < 9) {
-            bdu = bw;
-        } else if (r < 12) {
+    for (int l = 0; l < 4; ++l) uc[l] = sduv[R.iu[l]];
 #pragma unroll
-            for (int l = 0; l < 4; ++l) bdu += pc.bv[l] * sduv[3 * l + r - 9];
-        } else {
-            bdu = pick4(pc.bq, (r - 12) / 3) * sduv[r];
-            lxd += R.lx.xp * sdxv[3 + (r - 12) % 3];
-        }
-        if (r < 12) {
-            const real *rb = lq + LQ_RB + 6 * (r / 3);
-            const int a = r % 3, u0 = 3 * (r / 3);
-            const real b0 = a == 0 ? rb[0] : a == 1 ? rb[1] : rb[2];
-            const real b1 = a == 0 ? rb[1] : a == 1 ? rb[3] : rb[4];
-            const real b2 = a == 0 ? rb[2] : a == 1 ? rb[4] : rb[5];
-            lud += b0 * sduv[u0] + b1 * sduv[u0 + 1] + b2 * sduv[u0 + 2];
-        }
-        nx = (dx + sdx) + bdu + dd[r];
-        q1s += lq[LQ_LX + r] * dx + lq[LQ_LU + r] * du;
-        q2s += dx * lxd + du * lud;
-    }
+    for (int b = 0; b < 3; ++b) ur[b] = sduv[R.iru < LZ ? R.iru + b : LZ];
+    // one formula for every row: absent terms add exact zeros
+    const real sdx = (se + sw) + R.c3 * x3;
+    real lxd = R.lx.diag * dx;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) lxd += R.cx[l] * xc[l];
+    real bdu = bw;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) bdu += R.cu[l] * uc[l];
+    bdu += R.cq * du;
+    const real lud = R.ru * du + (crb[0] * ur[0] + crb[1] * ur[1] + crb[2] * ur[2]);
+    const real nx = rowl ? ((dx + sdx) + bdu) + ddr : (real)0;
+    q1s += lxr * dx + lur * du;
+    q2s += dx * lxd + du * lud;
     out.vu = du;
     out.vx = nx;
     dx = nx;
     LSYNC();
+    LSTAMP(4);
 }
 
 template <typename real, bool EL>
@@ -377,6 +460,13 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
     const bool rowl = r < NX, st = rowl && act;
     const int rr = rowl ? r : 0;
     const real *defg = Prec<real>::def(d);
+    S.zero[lane] = 0;
+    S.dx[hf][r] = 0;
+    S.du[hf][r] = 0;
+#if HSDDP_STAMPS
+    if (lane < 8) lin_stamps().st[lane] = 0;
+#endif
+    __syncthreads();
     real v1 = 0, v2 = 0, dx = 0;
     const auto LY = layout_of<EL>(d, (int)eb[0]);
     const int P = LY.P();
@@ -410,6 +500,7 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         const bool stl = contact(R.pc, (rr % HC) / 3) != 0;
         R.cpl = rowl && (rr < HC ? stl : !stl);
         R.krow0 = (rr % HC) * NX;
+        lin_row(p, R, r);
         LinOut<real> out{d.du + (b * p.Kc + k0) * NX + rr, d.dX + (b * p.S + s0 + 1) * NX + rr, 0, 0};
         real q1s = 0, q2s = 0;
         for (int k = 0; k < N; k += 2) {
@@ -433,6 +524,10 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         v2 += half_sum(q2s);
         LSYNC();
     }
+#if HSDDP_STAMPS
+    __syncthreads();
+    if (lane < 8) d.dbg[(size_t)__builtin_amdgcn_readfirstlane((int)eb[1]) * 16 + 8 + lane] += lin_stamps().st[lane];
+#endif
     if (r == 0 && act) {
         const double cost = E.cost, feas = E.feas, w1 = v1, w2 = v2;
         const double dV_abs = fabs(w1 + 0.5 * w2);

@@ -444,11 +444,20 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     }
     SSYNC();
     const real *zrow = L.row ? I.MI + pp * MS : S.zero;
-    real qxx[NX];
+    real qxx[NX], zc[NX];
 #pragma unroll
     for (int c = 0; c < NX; ++c) qxx[c] = zrow[c];
 #pragma unroll
-    for (int c = 0; c < NX; ++c) qxx[c] = (qxx[c] + I.MI[c * MS + pc]) * (real)0.5;
+    for (int c = 0; c < NX; ++c) zc[c] = I.MI[c * MS + pc];
+    // every row and column read in flight before the first use (one wait, not one per register reuse)
+    pin(qxx);
+    pin(zc);
+#pragma unroll
+    for (int c = 0; c < NX; ++c) qxx[c] *= (real)0.5;
+    // (r + c) / 2 as r / 2 + c / 2: halving is exact, so the same value, without an add -> multiply
+    // dependence per entry
+#pragma unroll
+    for (int c = 0; c < NX; ++c) qxx[c] = __builtin_fma(zc[c], (real)0.5, qxx[c]);
     pin(qxx);  // materialised here, not sunk to the value update (twice the registers across the elimination)
     // Qx = lx + A^T Gn = lx + Gn + S^T Gn
     const real qx = img[V_LX + (L.row ? pp : 0)] + (gn + I.MI[NX * MS + pc]);

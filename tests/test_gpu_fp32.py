@@ -18,6 +18,16 @@ from hsddp import synthetic as syn
 
 pytestmark = pytest.mark.gpu
 
+# jump 8 x 25 in the fp32 mode (test_fp32_jump_flip_rate_and_tolerance): bound on the fraction of
+# elements whose branch flips, and the tolerance of the others, per number of fixed iterations
+# (one iteration: every element that did not flip; three iterations: jump elements amplify rounding
+# chaotically — the fp64 oracle moves ~1e-9 under a 1e-15 change of x0 — so the bounds are on the
+# distribution: median and 90th percentile of the per-element difference)
+FLIP_BOUND = {1: 0.05, 3: 0.2}
+TOL_NONFLIP = {1: 5e-5, 3: None}               # largest per-element difference
+TOL_NONFLIP_MEDIAN = {1: 1e-5, 3: 1e-3}        # median over the elements
+TOL_NONFLIP_P90 = {1: 5e-5, 3: 5e-2}           # 90th percentile
+
 
 def rel(a, b):
     return float(np.max(np.abs(np.asarray(a) - np.asarray(b))) / max(1e-300, np.max(np.abs(b))))
@@ -98,3 +108,28 @@ def test_fp32_retries_parallel_equals_sequential(monkeypatch, B, cap):
     assert np.array_equal(g["n_ls_trials"], r["n_ls_trials"])
     for f in ("K", "dU", "Xbar", "Ubar"):
         assert rel(g[f], r[f]) < 5e-5, f
+
+
+def test_fp32_jump_flip_rate_and_tolerance():
+    """Impact-heavy jump 8 x 25 (7 reset boundaries) in the fp32 mode against the fp64 GPU path:
+    an fp32 rounding may move a Quu pivot across the PSD threshold (SinglePhase.cpp:342-352) or a
+    merit comparison across acceptance, changing that element's branch ("flip": its line-search trial
+    count or status differs).  The flip rate is bounded, and every element that did not flip is held
+    to this module's one-iteration tolerance (per element, relative to its largest entry).
+    Measured at B = 4096 (tools/fp32_tolerance.py -> profiles/round3_fp32_tolerance.json)."""
+    prob = syn.make_batch(256, 8, 25, "jump")
+    for iters in (1, 3):
+        kw = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=iters)
+        a, b = _run(prob, False, **kw), _run(prob, True, **kw)
+        flip = (a["n_ls_trials"] != b["n_ls_trials"]) | (a["status"] != b["status"])
+        assert np.mean(flip) <= FLIP_BOUND[iters], (iters, np.mean(flip))
+        keep = ~flip
+        for f in ("K", "dU", "dX", "Xbar", "Ubar"):
+            x = np.asarray(b[f])[keep].reshape(keep.sum(), -1)
+            y = np.asarray(a[f])[keep].reshape(keep.sum(), -1)
+            e = np.max(np.abs(x - y), axis=1) / np.maximum(1e-300, np.max(np.abs(y), axis=1))
+            if TOL_NONFLIP[iters] is not None:
+                assert e.max() < TOL_NONFLIP[iters], (iters, f, e.max())
+            assert np.median(e) < TOL_NONFLIP_MEDIAN[iters], (iters, f, np.median(e))
+            assert np.quantile(e, 0.9) < TOL_NONFLIP_P90[iters], (iters, f, np.quantile(e, 0.9))
+        assert np.all(np.isfinite(b["Xbar"]))

@@ -6,7 +6,12 @@ Writes gpurun_out/fp32_tolerance.json:
   * 10 fixed inner iterations, B = 4096 (C5 batch): cost / feasibility of fp32 vs fp64 GPU runs,
     line-search decisions that differ, time per inner iteration of each;
   * full solves with the shipped settings (AL + ReB outer loop, early exits), B = 4096, trot 4x50
-    and jump 8x25: final cost relative difference (median / p99 / max), statuses, iterations.
+    and jump 8x25: final cost relative difference (median / p99 / max), statuses, iterations;
+  * impact-heavy jump 8x25 (7 reset boundaries), B = 4096, 1 and 3 fixed inner iterations: the
+    "flip" rate — elements whose line-search trial count or status differs from the fp64 path (an
+    fp32 rounding that moves a Quu pivot across the PSD threshold or a merit comparison across
+    acceptance changes the element's branch) — and, on the elements that did not flip, the
+    per-element relative difference of K, dU, dX, Xbar, Ubar and cost against the fp64 path.
 """
 import json
 import os
@@ -38,8 +43,33 @@ def run(prob, fp32, **kw):
     return out
 
 
+def per_element_rel(a, b):
+    """max |a - b| / max |b| per element (leading axis)"""
+    a = np.asarray(a).reshape(len(a), -1); b = np.asarray(b).reshape(len(b), -1)
+    return np.max(np.abs(a - b), axis=1) / np.maximum(1e-300, np.max(np.abs(b), axis=1))
+
+
+def flips(prob, iters):
+    kw = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=iters)
+    a, b = run(prob, False, **kw), run(prob, True, **kw)
+    flip = (a["n_ls_trials"] != b["n_ls_trials"]) | (a["status"] != b["status"])
+    keep = ~flip
+    out = {"elements": int(len(flip)), "flip_rate": float(np.mean(flip)), "flipped": int(flip.sum()),
+           "status_fp32_nonzero": int(np.sum(b["status"] != 0)), "status_fp64_nonzero": int(np.sum(a["status"] != 0))}
+    for f in ("K", "dU", "dX", "Xbar", "Ubar", "cost"):
+        e = per_element_rel(b[f], a[f])[keep]
+        out[f"nonflip_{f}_rel_max"] = float(e.max()) if e.size else None
+        out[f"nonflip_{f}_rel_p99"] = float(np.quantile(e, .99)) if e.size else None
+    return out
+
+
 def main():
     res = {}
+    for iters in (1, 3):
+        res[f"jump_flips_{iters}it"] = flips(syn.make_batch(4096, 8, 25, "jump"), iters)
+        print("jump flips", iters, res[f"jump_flips_{iters}it"], flush=True)
+    res["trot_flips_3it"] = flips(syn.make_batch(4096, 4, 50, "trot"), 3)
+    print("trot flips", res["trot_flips_3it"], flush=True)
     prob = syn.make_batch(64, 4, 50, "trot")
     kw = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=1)
     g = run(prob, True, **kw)

@@ -18,8 +18,9 @@ import hsddp  # noqa: E402
 from hsddp import synthetic  # noqa: E402
 
 STAGES = ["wait DMA, coefficients", "Gn, T, M rows", "M columns, Z, Qux_c, Qu_c", "Qxx (symmetrise)",
-          "Quu_cc columns", "Gauss-Jordan (12 steps)", "K, dU, dV, G, images", "value update (MFMA)",
-          "H rows"]
+          "Quu_cc columns, DMA", "elimination (12 steps)", "dU, K broadcast, G", "value update (DPP)",
+          "K / dU stores"]
+LIN_STAGES = ["DMA issue, stores, image wait", "K dX, du", "A - I, B rows (DPP)", "row tail, dV"]
 
 
 def main():
@@ -39,6 +40,13 @@ def main():
     for name, c in zip(STAGES, cyc):
         print(f"{name:28s} {c / (3 * 200):10.0f} cycles/knot  {100 * c / tot:5.1f} %")
     print(f"{'total':28s} {tot / (3 * 200):10.0f} cycles/knot")
+    # k_lin_rollout (hsddp_linear.hip LSTAMP): written to the wave's second element, slots 8 + stage
+    lc = out[1::2, 9:13].astype(np.float64).mean(0)
+    lt = lc.sum()
+    print("k_lin_rollout")
+    for name, c in zip(LIN_STAGES, lc):
+        print(f"{name:28s} {c / (3 * 200):10.0f} cycles/knot  {100 * c / max(lt, 1):5.1f} %")
+    print(f"{'total':28s} {lt / (3 * 200):10.0f} cycles/knot")
 
 
 if __name__ == "__main__":
