@@ -203,6 +203,9 @@ extern "C" int hsddp_load_constraint_params(const char *path, hsddp_constraint_p
 
 // ---- handle ----------------------------------------------------------------------------------
 struct hsddp_handle_t {
+    // the slot costs / |Defect|^2 of the last rollout (k_rollout's per-slot outputs) belong to the
+    // working trajectory under the current cost parameters: k_lq need not recompute them
+    bool slots_fresh = false;
     hsddp_problem_desc desc;
     hsddp_options opt;
     Params p;
@@ -307,6 +310,7 @@ static int dalloc(hsddp_handle h, T *&ptr, size_t n)
 
 static void fill_params(hsddp_handle h)
 {
+    h->slots_fresh = false;
     Params &p = h->p;
     const hsddp_problem_desc &ds = h->desc;
     const hsddp_options &o = h->opt;
@@ -535,6 +539,7 @@ extern "C" int hsddp_set_options(hsddp_handle h, const hsddp_options *o)
 // install per-element layouts: device records, sweep pairs (equal layouts share a wave), strides
 static int set_layouts(hsddp_handle h, const std::vector<Layout> &lays)
 {
+    h->slots_fresh = false;
     Params &p = h->p;
     const int B = p.B;
     int Pmax = 0, Smax = 0, tail = 0;
@@ -696,6 +701,7 @@ extern "C" int hsddp_update_problem(hsddp_handle h, const int *contacts, const d
 extern "C" int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const double *Ubar, const double *K)
 {
     if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    h->slots_fresh = false;
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     HIPCHK(hipSetDevice(h->desc.device));
     const Params &p = h->p;
@@ -818,6 +824,7 @@ static void begin_launches(hsddp_handle h)
     launch_reset_elements(h->p, h->d, h->stream);
     launch_rollout(h->p, h->d, 0.0, 1, h->stream);
     launch_decide(h->p, h->d, 0.0, 0, 1, h->stream);
+    h->slots_fresh = true;
 }
 
 static void iteration_launches(hsddp_handle h, const std::vector<double> &trials, Timer &tm)
@@ -827,7 +834,12 @@ static void iteration_launches(hsddp_handle h, const std::vector<double> &trials
     hipStream_t st = h->stream;
     hipEvent_t e0;
     tm.begin(0, e0);
-    launch_lq(p, d, st);
+    {   // every path to here ran a rollout on the working trajectory (the initial one or the last
+        // line-search trial, quirk A2) unless the cost parameters changed since (slots_fresh)
+        Params pl = p;
+        pl.lq_slots = h->slots_fresh ? 0 : 1;
+        launch_lq(pl, d, st);
+    }
     tm.end(0, e0);
     tm.begin(1, e0);
     launch_riccati(p, d, st);
@@ -841,12 +853,15 @@ static void iteration_launches(hsddp_handle h, const std::vector<double> &trials
         launch_decide(p, d, trials[t], t + 1 == trials.size(), 0, st);
     }
     tm.end(2, e0);
+    h->slots_fresh = true;
 }
 
 static void outer_end_launches(hsddp_handle h, Timer &tm)
 {
     hipEvent_t e0;
     tm.begin(3, e0);
+    // update_REB_params moves per-knot (delta, eps) unless they stay uniform: the running costs change
+    if (h->opt.ReB_active && !h->p.reb_uniform) h->slots_fresh = false;
     if (h->opt.ReB_active) launch_reb_update(h->p, h->d, h->stream);
     launch_outer_end(h->p, h->d, h->stream);
     tm.end(3, e0);
@@ -1516,6 +1531,7 @@ static int shift_phases(const Layout &L, const int *reach, int n_steps, const in
 // element ends on one layout the handle keeps (or returns to) the shared layout.
 static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride, size_t sstride)
 {
+    h->slots_fresh = false;
     if (!h || (n_steps > 0 && !cc)) return fail(HSDDP_ERR_ARG, "null argument");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     if (n_steps < 0) return fail(HSDDP_ERR_ARG, "n_steps must be >= 0");
@@ -1702,6 +1718,7 @@ static int build_refs(hsddp_handle h, const int *window_start, int window_len, c
 extern "C" int hsddp_build_references(hsddp_handle h, const int *window_start, int window_len,
                                       const float *phase_start_times, float dt_sim)
 {
+    if (h) h->slots_fresh = false;  // new reference rows: the running costs change
     if (h && !h->lays.empty())
         return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts (hsddp_set_element_layouts): the MPC-side steps need the handle's shared layout");
     return build_refs(h, window_start, window_len, phase_start_times, dt_sim, true);

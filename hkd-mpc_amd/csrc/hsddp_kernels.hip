@@ -100,10 +100,12 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 #pragma unroll
     for (int j = 0; j < NX; ++j) x[j] = xg[j];
     const double *dg = d.Defect + ((size_t)b * p.S + s) * NX;
-    double fs = 0.0;
+    if (p.lq_slots) {  // |Defect|^2 (else the last rollout's, of this working trajectory)
+        double fs = 0.0;
 #pragma unroll
-    for (int j = 0; j < NX; ++j) fs += dg[j] * dg[j];
-    d.slot_feas[(size_t)b * p.S + s] = fs;
+        for (int j = 0; j < NX; ++j) fs += dg[j] * dg[j];
+        d.slot_feas[(size_t)b * p.S + s] = fs;
+    }
     if constexpr (F32) { // the sweep's and linear rollout's fp32 copy of Defect
         float *d32 = d.def32 + ((size_t)b * p.S + s) * NX;
 #pragma unroll
@@ -119,8 +121,10 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     for (int j = 0; j < NU; ++j) u[j] = ug[j];
     const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
     const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
-    double viol;
-    d.slot_cost[(size_t)b * p.S + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
+    if (p.lq_slots) {  // the running cost (else the last rollout's: same trajectory, same parameters)
+        double viol;
+        d.slot_cost[(size_t)b * p.S + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
+    }
 
     // the record in the solver's Riccati precision (fp64, or fp32 in config C5's mode)
     T *lqT = F32 ? (T *)d.lq32 : (T *)d.lq;
@@ -196,10 +200,15 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
     const auto L = layout_of<EL>(d, b);
     const int P = L.P();
     if (i >= P) return;
-    __shared__ double sx[NX], shx[4][NX], scoef[4][2], sh[4];
+    __shared__ double sx[NX], shx[4][NX], scoef[4][2], sh[4], sxr[NX], spf[12], ssl[8];
     __shared__ int sc[4], scn[4];
     const int s = L.s0(i) + L.N(i);
+    const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
     if (t < NX) sx[t] = d.Xb[work_buf(d, b)][((size_t)b * p.S + s) * NX + t];
+    // the terminal cost's other inputs, staged with X[N] (no memory round trip at the end)
+    if (t >= 32 && t < 32 + NX) sxr[t - 32] = xr[t - 32];
+    if (t >= 56 && t < 64) ssl[t - 56] = (t < 60 ? d.al_sigma : d.al_lambda)[((size_t)b * p.P + i) * 4 + (t & 3)];
+    if (t >= 4 && t < 16) spf[t - 4] = pf[t - 4];
     if (t < 4) {
         const int *cc = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
         sc[t] = cc[t]; scn[t] = cc[4 + t];
@@ -224,11 +233,9 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
     __syncthreads();
     KParams &kp = *kparams();  // runtime-indexed weights
     double *rec = d.term + ((size_t)b * p.P + i) * TW;
-    const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
     if (t == 0) {  // the phase's terminal cost at X[N] (SinglePhase::compute_cost's last term) for k_lq's slot sums
         double tv;
-        const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
-        d.slot_cost[(size_t)b * p.S + s] = terminal_cost_h(p, sc, scn, sx, xr, pf, sg, lm, sh, tv);
+        d.slot_cost[(size_t)b * p.S + s] = terminal_cost_h(p, sc, scn, sx, sxr, spf, ssl, ssl + 4, sh, tv);
     }
     if (t < NX) { // Phix
         const int j = t;
