@@ -214,18 +214,54 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
         sc[t] = cc[t]; scn[t] = cc[4 + t];
     }
     __syncthreads();
+    // Px at X_i[N] (HKDReset.h:78-136) is built in LDS from the identity (phase boundaries only)
+    __shared__ double spx[NX * (NX + 1)];
+    const bool bnd = i < P - 1;
     for (int e = t; e < 4 * NX; e += 64) (&shx[0][0])[e] = 0.0;
+    if (bnd)
+        for (int e = t; e < NX * (NX + 1); e += 64) spx[e] = (e / (NX + 1) == e % (NX + 1)) ? 1.0 : 0.0;
     __syncthreads();
-    if (t < 4) {  // touchdown legs: h and its gradient (non-zeros at 0..2, 5, 12 + 3 l + k)
+    if (t < 4) {
+        // touchdown legs: foot height h, its gradient (non-zeros at 0..2, 5, 12 + 3 l + k) and, at a
+        // phase boundary, the reset map's foot-Jacobian rows — from one evaluation of the leg's
+        // kinematics (hkd_foot_height_grad_sparse's and hkd_foot_jacobian's expressions)
         const int l = t;
         const bool td = touchdown(sc, scn, l);
-        double h = 0.0, ge[3], gq[3];
+        double h = 0.0;
         if (td) {
-            h = hkd_foot_height_grad_sparse(l, sx, ge, gq) - p.ground;
-            for (int k = 0; k < 3; ++k) { shx[l][k] = ge[k]; shx[l][12 + 3 * l + k] = gq[k]; }
+            Rot R, Dy, Dp, Dr;
+            const EulTrig tr = eul_trig(sx);
+            rot_zyx(tr, R);
+            rot_zyx_grad(tr, Dy, Dp, Dr);
+            double pb[3], dpb[3][3];
+            foot_body(l, sx + 12 + 3 * l, pb, dpb);
+            shx[l][0] = Dy.r[2][0] * pb[0] + Dy.r[2][1] * pb[1] + Dy.r[2][2] * pb[2];
+            shx[l][1] = Dp.r[2][0] * pb[0] + Dp.r[2][1] * pb[1] + Dp.r[2][2] * pb[2];
+            shx[l][2] = Dr.r[2][0] * pb[0] + Dr.r[2][1] * pb[1] + Dr.r[2][2] * pb[2];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) shx[l][12 + 3 * l + k] = R.r[2][0] * dpb[0][k] + R.r[2][1] * dpb[1][k] + R.r[2][2] * dpb[2][k];
             shx[l][5] = 1.0;
+            h = (sx[5] + R.r[2][0] * pb[0] + R.r[2][1] * pb[1] + R.r[2][2] * pb[2]) - p.ground;
+            if (bnd) {  // rows 12 + 3 l + k, k < 2: the foot Jacobian's rows; the k = 2 row is zero
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    double *row = spx + (12 + 3 * l + k) * (NX + 1);
+                    row[12 + 3 * l + k] = 0.0;
+                    if (k == 2) continue;
+                    row[0] = Dy.r[k][0] * pb[0] + Dy.r[k][1] * pb[1] + Dy.r[k][2] * pb[2];
+                    row[1] = Dp.r[k][0] * pb[0] + Dp.r[k][1] * pb[1] + Dp.r[k][2] * pb[2];
+                    row[2] = Dr.r[k][0] * pb[0] + Dr.r[k][1] * pb[1] + Dr.r[k][2] * pb[2];
+                    row[3 + k] = 1.0;
+#pragma unroll
+                    for (int m = 0; m < 3; ++m)
+                        row[12 + 3 * l + m] = R.r[k][0] * dpb[0][m] + R.r[k][1] * dpb[1][m] + R.r[k][2] * dpb[2][m];
+                }
+            }
+        } else if (bnd && sc[l] && !scn[l]) {  // lift-off: rows 12 + 3 l + k zero
+#pragma unroll
+            for (int k = 0; k < 3; ++k) spx[(12 + 3 * l + k) * (NX + 2)] = 0.0;
         }
-        double sg = d.al_sigma[((size_t)b * p.P + i) * 4 + l], lm = d.al_lambda[((size_t)b * p.P + i) * 4 + l];
+        const double sg = ssl[l], lm = ssl[4 + l];
         scoef[l][0] = (td && p.AL_active) ? sg * h + lm : 0.0;
         scoef[l][1] = (td && p.AL_active) ? sg * (1 + h) + lm : 0.0;
         sh[l] = h;
@@ -275,39 +311,8 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
         for (int l = 0; l < 4; ++l) v += scoef[l][1] * (shx[l][r] * shx[l][cidx]);
         rec[TM_PHIXX + e] = v;
     }
-    if (i < P - 1) { // Px at X_i[N] (HKDReset.h:78-136), staged in LDS, stored coalesced by the wave
-        __shared__ double spx[NX * (NX + 1)];
-        for (int e = t; e < NX * (NX + 1); e += 64) spx[e] = (e / (NX + 1) == e % (NX + 1)) ? 1.0 : 0.0;
-        __syncthreads();
-        if (t < 4) {  // rows 12 + 3 l + k of leg l: zero at lift-off, foot Jacobian rows at touchdown
-            const int l = t;
-            if (sc[l] && !scn[l]) {
-                for (int k = 0; k < 3; ++k) spx[(12 + 3 * l + k) * (NX + 2)] = 0.0;
-            } else if (!sc[l] && scn[l]) {  // rows k < 2: the foot Jacobian's rows (hkd_foot_jacobian)
-                Rot R, Dy, Dp, Dr;
-                const EulTrig tr = eul_trig(sx);
-                rot_zyx(tr, R);
-                rot_zyx_grad(tr, Dy, Dp, Dr);
-                double pb[3], dpb[3][3];
-                foot_body(l, sx + 12 + 3 * l, pb, dpb);
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    double *row = spx + (12 + 3 * l + k) * (NX + 1);
-                    row[12 + 3 * l + k] = 0.0;
-                    if (k == 2) continue;
-                    row[0] = Dy.r[k][0] * pb[0] + Dy.r[k][1] * pb[1] + Dy.r[k][2] * pb[2];
-                    row[1] = Dp.r[k][0] * pb[0] + Dp.r[k][1] * pb[1] + Dp.r[k][2] * pb[2];
-                    row[2] = Dr.r[k][0] * pb[0] + Dr.r[k][1] * pb[1] + Dr.r[k][2] * pb[2];
-                    row[3 + k] = 1.0;
-#pragma unroll
-                    for (int m = 0; m < 3; ++m)
-                        row[12 + 3 * l + m] = R.r[k][0] * dpb[0][m] + R.r[k][1] * dpb[1][m] + R.r[k][2] * dpb[2][m];
-                }
-            }
-        }
-        __syncthreads();
+    if (bnd)  // Px rows from LDS, stored coalesced by the wave
         for (int e = t; e < NN; e += 64) rec[TM_PX + e] = spx[(e / NX) * (NX + 1) + e % NX];
-    }
 }
 
 // ---------------------------------------------------------------------------------------------

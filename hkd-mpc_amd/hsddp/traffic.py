@@ -30,11 +30,12 @@ def kernel_bytes(B: int, S: int, Kc: int, P: int, fp32: bool = False, ref_per_el
     ref = (S * (24 + 12) + Kc * 24) * d if ref_per_element else 0   # ref_x, ref_foot per slot, ref_u per knot
     term = (P * TW_PHI + (P - 1) * TW_PX) * d                      # Phix, Phixx (every phase end), Px (boundaries)
     out = {}
-    # k_lq: per slot X, Defect read, slot cost / feasibility written (+ fp32 Defect copy); per control
-    # knot U read and the record written
-    out["k_lq"] = B * (S * (2 * NX * d + 2 * d + (NX * 4 if fp32 else 0)) + Kc * (NX * d + rec) + ref)
-    # k_terminal: per phase end X read (+ AL sigma, lambda), Phix, Phixx, Px written
-    out["k_terminal"] = B * (P * (NX + 8) * d + term)
+    # k_lq inside the inner loop: per slot X read (the slot costs and |Defect|^2 are the last
+    # rollout's: Params::lq_slots = 0), in the fp32 mode Defect read and its fp32 copy written; per
+    # control knot U read and the record written
+    out["k_lq"] = B * (S * (NX * d + (NX * d + NX * 4 if fp32 else 0)) + Kc * (NX * d + rec) + ref)
+    # k_terminal: per phase end X read (+ AL sigma, lambda), Phix, Phixx, Px and the terminal cost written
+    out["k_terminal"] = B * (P * (NX + 8 + 1) * d + term)
     # k_riccati: per control knot the record and Defect[k+1] read, gain rows and dU written; per
     # element the terminal records and the slot cost / feasibility partial sums read
     out["k_riccati"] = B * (Kc * (rec + NX * f + KCW * f + NX * d) + term + 2 * S * d)
