@@ -261,14 +261,18 @@ def main():
             S = Kc + P
         ms_step = elapsed / args.steps * 1e3
         mean_ls = total_ls / max(1.0, total_iters)
-        kb = traffic.kernel_bytes(B, S, Kc, P, fp32=args.riccati_fp32, ref_per_element=args.mixed)
+        # per-knot ReB parameters are read unless the schedule keeps them uniform (default
+        # constraint parameters: delta = delta_min = 0.1, hsddp_default_constraint_params)
+        reb_rows = traffic.reb_rows_per_knot(prob, opt, 0.1, 0.1)
+        kb = traffic.kernel_bytes(B, S, Kc, P, fp32=args.riccati_fp32, ref_per_element=args.mixed, reb_rows=reb_rows)
         # k_riccati time from HIP events recorded around its launches on the solver's stream
         avg_bwd_ms = st.ms_backward / max(1, st.n_backward_launches)
         bytes_launch = kb["k_riccati"]
         achieved = bytes_launch / (avg_bwd_ms * 1e-3) / 1e9
         flop_launch = traffic.RICCATI_FLOP_PER_KNOT * Kc * B
         tflops = flop_launch / (avg_bwd_ms * 1e-3) / 1e12
-        step_b = traffic.step_bytes(B, S, Kc, P, mean_ls, fp32=args.riccati_fp32, ref_per_element=args.mixed)
+        step_b = traffic.step_bytes(B, S, Kc, P, mean_ls, fp32=args.riccati_fp32, ref_per_element=args.mixed,
+                                    reb_rows=reb_rows)
         gait = "mixed" if args.mixed else args.gait
         metric_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 4096)
         c2_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 1024)

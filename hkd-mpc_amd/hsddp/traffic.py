@@ -22,8 +22,11 @@ TW_PHI = 24 + 576       # Phix + Phixx per phase end
 TW_PX = 576             # reset-map Jacobian per phase boundary
 
 
-def kernel_bytes(B: int, S: int, Kc: int, P: int, fp32: bool = False, ref_per_element: bool = False) -> dict:
-    """Algorithmic bytes per launch of each kernel of one inner iteration."""
+def kernel_bytes(B: int, S: int, Kc: int, P: int, fp32: bool = False, ref_per_element: bool = False,
+                 reb_rows: float = 0.0) -> dict:
+    """Algorithmic bytes per launch of each kernel of one inner iteration.  reb_rows: GRF rows per
+    control knot whose per-knot ReB parameters (delta, eps) the cost kernels read — 5 per stance leg
+    unless the schedule keeps them uniform (Params::reb_uniform: then 0, two scalars instead)."""
     d = 8                              # fp64
     f = 4 if fp32 else 8               # Riccati precision: LQ record, gains, Defect copy (C5)
     rec = (LQW32 * 4) if fp32 else (LQW * 8)
@@ -33,7 +36,8 @@ def kernel_bytes(B: int, S: int, Kc: int, P: int, fp32: bool = False, ref_per_el
     # k_lq inside the inner loop: per slot X read (the slot costs and |Defect|^2 are the last
     # rollout's: Params::lq_slots = 0), in the fp32 mode Defect read and its fp32 copy written; per
     # control knot U read and the record written
-    out["k_lq"] = B * (S * (NX * d + (NX * d + NX * 4 if fp32 else 0)) + Kc * (NX * d + rec) + ref)
+    reb = 2 * reb_rows * d  # delta and eps of the knot's stance-leg GRF rows
+    out["k_lq"] = B * (S * (NX * d + (NX * d + NX * 4 if fp32 else 0)) + Kc * (NX * d + rec + reb) + ref)
     # k_terminal: per phase end X read (+ AL sigma, lambda), Phix, Phixx, Px and the terminal cost written
     out["k_terminal"] = B * (P * (NX + 8 + 1) * d + term)
     # k_riccati: per control knot the record and Defect[k+1] read, gain rows and dU written; per
@@ -44,17 +48,34 @@ def kernel_bytes(B: int, S: int, Kc: int, P: int, fp32: bool = False, ref_per_el
     out["k_lin_rollout"] = B * (Kc * (KCW * f + rec + NX * f + NX * d + 2 * NX * d) + term)
     # k_rollout (one line-search trial): per slot Xbar, dX read, X, Defect written, cost /
     # feasibility / violation / divergence written; per control knot Ubar, du read, U written
-    out["k_rollout"] = B * (S * (4 * NX * d + 4 * d) + Kc * 3 * NX * d + ref)
+    out["k_rollout"] = B * (S * (4 * NX * d + 4 * d) + Kc * (3 * NX * d + reb) + ref)
     # (Trajectory::update_nominal_vals moves no bytes: k_decide flips the element's buffer selector)
     return out
 
 
 def step_bytes(B: int, S: int, Kc: int, P: int, n_trials: float, fp32: bool = False,
-               ref_per_element: bool = False) -> float:
+               ref_per_element: bool = False, reb_rows: float = 0.0) -> float:
     """Algorithmic bytes of one inner iteration: every kernel once, k_rollout n_trials times
     (the measured mean number of line-search trials)."""
-    kb = kernel_bytes(B, S, Kc, P, fp32, ref_per_element)
+    kb = kernel_bytes(B, S, Kc, P, fp32, ref_per_element, reb_rows)
     return sum(v for k, v in kb.items() if k != "k_rollout") + n_trials * kb["k_rollout"]
+
+
+def reb_rows_per_knot(prob: dict, options, constraint_delta: float = 1.0, constraint_delta_min: float = 0.0) -> float:
+    """reb_rows for kernel_bytes: 0 when the ReB schedule keeps (delta, eps) uniform (update_ReB =
+    update_relax = 1, hsddp_api.cpp fill_params), else 5 GRF rows per stance leg, averaged over the
+    batch's control knots."""
+    import numpy as np
+    if options.update_ReB == 1.0 and options.update_relax == 1.0 and constraint_delta >= constraint_delta_min:
+        return 0.0
+    c = np.asarray(prob["contacts"])
+    lays = prob.get("layouts")
+    if lays:
+        per = [sum(n * float(np.sum(c[b, i] != 0)) for i, n in enumerate(h)) / sum(h) for b, h in enumerate(lays)]
+        return 5.0 * float(np.mean(per))
+    h = prob["horizons"]
+    stance = np.array([[float(np.sum(c[b, i] != 0)) for i in range(len(h))] for b in range(c.shape[0])])
+    return 5.0 * float(np.mean(stance @ np.asarray(h, float)) / sum(h))
 
 
 # fp64 FMAs of one knot of the backward sweep as k_riccati evaluates it (structure exploited:

@@ -371,3 +371,24 @@ def test_failed_line_search_keeps_the_last_trial():
         for f in ("X", "U", "Xbar", "Ubar", "K", "dU"):
             assert rel(g[f], r[f]) < 1e-9, (n, f)
         assert np.array_equal(g["n_ls_trials"], r["n_ls_trials"])
+
+
+@pytest.mark.parametrize("gait,P,N", [("trot", 4, 50), ("jump", 8, 25)])
+def test_nonuniform_reb_schedule_matches_oracle(gait, P, N):
+    """update_ReB = 7, update_relax = 0.1 (HSDDP_OPTION's defaults, not the shipped INFO file's 1 / 1):
+    update_REB_params (ConstraintsBase.h:168-183) moves each GRF row's (delta, eps) after every
+    outer iteration, so the per-knot parameter arrays are read and, after each outer update, k_lq
+    recomputes the slot costs the last line search left (Params::lq_slots).  Three outer x three
+    inner iterations against the oracle."""
+    prob = syn.make_batch(8, P, N, gait)
+    kw = dict(no_early_exit=1, max_AL_iter=3, max_DDP_iter=3, update_ReB=7.0, update_relax=0.1)
+    g = _run(prob, **kw)
+    r = O.solve_batch(prob, O.default_options(**kw), n_threads=8)
+    p2 = dict(prob); p2["x0"] = prob["x0"] * (1 + 1e-15)
+    r2 = O.solve_batch(p2, O.default_options(**kw), n_threads=8)
+    for f in ("Xbar", "Ubar", "K", "dU"):
+        assert rel(g[f], r[f]) < max(1e-9, 10 * rel(r2[f], r[f])), f
+    for f in ("cost", "feas", "max_pconstr"):
+        assert rel(g[f], r[f]) < max(1e-9, 10 * rel(r2[f], r[f])), f
+    for f in ("iters", "outer_iters", "status", "n_ls_trials"):
+        assert np.array_equal(g[f], r[f]), f
