@@ -132,15 +132,18 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
     // A - I and B pieces (record positions 0 .. 103) in position order (hkd_partial_emit): each
     // value goes to this wave's LDS stage as it is computed and the stage is stored coalesced, one
-    // contiguous chunk of the records at a time; positions 15 and 67 are the record's zero slots
+    // contiguous chunk of the records at a time; positions 15 and 67 are the record's zero slots.
+    // Chunk bounds are multiples of 8 values (64-byte lines of the 1408-byte, line-aligned records):
+    // a line written in two partial pieces at different times cost a second line write (PMC: 11 %
+    // more WRITE_SIZE than the records).
     T *wl = stage[w];
-    constexpr int CH_LO[6] = {0, 16, 40, 64, 68, 86}, CH_N[6] = {16, 24, 24, 4, 18, 18};
+    constexpr int CH_LO[6] = {0, 16, 40, 64, 72, 88}, CH_N[6] = {16, 24, 24, 8, 16, 16};
     wl[lane * LQ_STG + 15] = 0;
     hkd_partial_emit(x, u, cd, p.dt, [&](int piece, int j, double v) {
         const int pos = piece == 0 ? LQ_SE + j : piece == 1 ? sw_at(j / 17, j % 17) : bw_at(j / 12, j % 12);
-        const int ch = pos < 16 ? 0 : pos < 40 ? 1 : pos < 64 ? 2 : pos < 68 ? 3 : pos < 86 ? 4 : 5;
+        const int ch = pos < 16 ? 0 : pos < 40 ? 1 : pos < 64 ? 2 : pos < 72 ? 3 : pos < 88 ? 4 : 5;
         wl[lane * LQ_STG + pos - CH_LO[ch]] = (T)v;
-        if (pos == CH_LO[ch] + CH_N[ch] - (ch == 0 || ch == 3 ? 2 : 1)) {  // the chunk's last value
+        if (pos == CH_LO[ch] + CH_N[ch] - (ch == 0 ? 2 : 1)) {  // the chunk's last value
             lq_flush(wl, sridx[w], lqT, ldw, lane, CH_LO[ch], CH_N[ch]);
             if (ch == 2) wl[lane * LQ_STG + 67 - 64] = 0;
         }
