@@ -294,23 +294,35 @@ __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
         rec[TM_PHIX + j] = v;
     }
     // foot Hessian 20 D^T Qfoot D: weight of (leg l, axis j), entries (3 + j, 3 + j) (summed over
-    // the legs in leg order), (12 + 3 l + j, 12 + 3 l + j) and, negated, the two cross entries
+    // the legs in leg order), (12 + 3 l + j, 12 + 3 l + j) and, negated, the two cross entries.
+    // Lane r < 24 forms diagonal entry r, lane 24 + m the weight of joint column 12 + m (runtime-
+    // indexed weights read once per phase, not once per entry); the 576 entries then combine them.
     auto fw = [&](int l, int j) { return p.foot_term_grad * sc[l] * sc[l] * foot_weight(kp, sc, 3 * l + j); };
+    __shared__ double sdd[NX], scw[12];
+    if (t < NX) {
+        const int r = t;
+        double v = kp.qf_gain * kp.qf_scale[r] * q_diag(kp, sc, r);
+        if (r >= 3 && r < 6) {
+            for (int l = 0; l < 4; ++l) v += fw(l, r - 3);
+        } else if (r >= 12) {
+            v += fw((r - 12) / 3, (r - 12) % 3);
+        }
+        sdd[r] = v;
+    } else if (t < NX + 12) {
+        const int m = t - NX;
+        scw[m] = fw(m / 3, m % 3);
+    }
+    __syncthreads();
     for (int e = t; e < NN; e += 64) { // Phixx
         const int r = e / NX, cidx = e % NX;
         double v = 0.0;
-        if (r == cidx) {
-            v = kp.qf_gain * kp.qf_scale[r] * q_diag(kp, sc, r);
-            if (r >= 3 && r < 6) {
-                for (int l = 0; l < 4; ++l) v += fw(l, r - 3);
-            } else if (r >= 12) {
-                v += fw((r - 12) / 3, (r - 12) % 3);
-            }
-        } else if (r >= 3 && r < 6 && cidx >= 12 && (cidx - 12) % 3 == r - 3) {
-            v -= fw((cidx - 12) / 3, r - 3);
-        } else if (cidx >= 3 && cidx < 6 && r >= 12 && (r - 12) % 3 == cidx - 3) {
-            v -= fw((r - 12) / 3, cidx - 3);
-        }
+        if (r == cidx)
+            v = sdd[r];
+        else if (r >= 3 && r < 6 && cidx >= 12 && (cidx - 12) % 3 == r - 3)
+            v = -scw[cidx - 12];
+        else if (cidx >= 3 && cidx < 6 && r >= 12 && (r - 12) % 3 == cidx - 3)
+            v = -scw[r - 12];
+#pragma unroll
         for (int l = 0; l < 4; ++l) v += scoef[l][1] * (shx[l][r] * shx[l][cidx]);
         rec[TM_PHIXX + e] = v;
     }
