@@ -75,7 +75,9 @@ DEV void lq_stage_store(T *wl, const long *ridx, const double *v, T *lq, int ldw
 // control slots (SinglePhase::compute_cost + LQ_approximation, SinglePhase.cpp:235-296).
 // F32: config C5's fp32 Riccati mode (records in fp32 plus an fp32 copy of Defect for the sweep)
 // The A - I / B pieces go out by direct stores (staging them would keep all 102 values live).
-template <bool F32, bool EL>
+// SLOTS: the slot costs and |Defect|^2 are recomputed (Params::lq_slots; instantiated apart so the
+// common path keeps the registers the cost code would take)
+template <bool F32, bool EL, bool SLOTS>
 __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 {
     using T = std::conditional_t<F32, float, double>;
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 #pragma unroll
     for (int j = 0; j < NX; ++j) x[j] = xg[j];
     const double *dg = d.Defect + ((size_t)b * p.S + s) * NX;
-    if (p.lq_slots) {  // |Defect|^2 (else the last rollout's, of this working trajectory)
+    if (SLOTS) {  // |Defect|^2 (else the last rollout's, of this working trajectory)
         double fs = 0.0;
 #pragma unroll
         for (int j = 0; j < NX; ++j) fs += dg[j] * dg[j];
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     for (int j = 0; j < NU; ++j) u[j] = ug[j];
     const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
     const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
-    if (p.lq_slots) {  // the running cost (else the last rollout's: same trajectory, same parameters)
+    if (SLOTS) {  // the running cost (else the last rollout's: same trajectory, same parameters)
         double viol;
         d.slot_cost[(size_t)b * p.S + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
     }
@@ -1149,11 +1151,17 @@ void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
 {
     const dim3 g(blocks_for((long)p.B * p.S, 256));
     if (p.fp32) {
-        if (p.elem_layout) hipLaunchKernelGGL((k_lq<true, true>), g, dim3(256), 0, st, p, d);
-        else hipLaunchKernelGGL((k_lq<true, false>), g, dim3(256), 0, st, p, d);
+#define HSDDP_LQ(f, e)                                                          \
+    do {                                                                        \
+        if (p.lq_slots) hipLaunchKernelGGL((k_lq<f, e, true>), g, dim3(256), 0, st, p, d); \
+        else hipLaunchKernelGGL((k_lq<f, e, false>), g, dim3(256), 0, st, p, d);           \
+    } while (0)
+        if (p.elem_layout) HSDDP_LQ(true, true);
+        else HSDDP_LQ(true, false);
     } else {
-        if (p.elem_layout) hipLaunchKernelGGL((k_lq<false, true>), g, dim3(256), 0, st, p, d);
-        else hipLaunchKernelGGL((k_lq<false, false>), g, dim3(256), 0, st, p, d);
+        if (p.elem_layout) HSDDP_LQ(false, true);
+        else HSDDP_LQ(false, false);
+#undef HSDDP_LQ
     }
     LAUNCH_EL(k_terminal, dim3(p.B * p.P), dim3(64), st, p, d);
 }
