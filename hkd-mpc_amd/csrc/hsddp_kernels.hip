@@ -490,6 +490,14 @@ DEV void trial_row(const Bufs &d, const double *Ubar, long r, double eps, double
     }
 }
 
+// v of the previous lane of the wave (DPP wave_shr:1; lane 0 gets 0).  Every lane must be active.
+DEV double from_prev_lane(double v)
+{
+    const unsigned lo = __builtin_amdgcn_update_dpp(0u, (unsigned)__double2loint(v), 0x138, 0xf, 0xf, false);
+    const unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)__double2hiint(v), 0x138, 0xf, 0xf, false);
+    return __hiloint2double((int)hi, (int)lo);
+}
+
 // Only the state rows go through LDS (13 KB per wave); the control rows are read per lane
 // (trial_row), the slot's own control row stored from registers.  With both row sets in LDS
 // (26 KB per wave) only 6 waves fit a CU: 1.25 ms/step of line search vs 0.93 here.
@@ -554,24 +562,67 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     auto active = [&](int b) { return b == bA ? aA : b == bB ? aB : act(b); };
     const int nA = nom_buf(d, bA), nB = nom_buf(d, bB);
     auto nomof = [&](int b) { return b == bA ? nA : b == bB ? nB : nom_buf(d, b); };
+    // the control row before the wave's first slot (that slot's u_prev; every other slot takes its
+    // u_prev from the previous lane): lanes 0..11 load it with the state rows, stage it after them
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    __shared__ double Up0[NU];
+    d2 ua = {0, 0}, ue = {0, 0};
+    bool up0 = false;
+    {
+        const int s0 = (int)(g0 % p.S);
+        const auto L0 = layout_of<EL>(d, bA);
+        int i0, k0;
+        slot_phase(L0, s0, i0, k0);
+        up0 = aA && s0 < L0.S() && k0 > 0 && lane < NU / 2;
+        if (up0) {
+            const long r = (long)bA * p.Kc + s0 - i0 - 1;
+            ua = ((const d2 *)(d.Ub[nA] + r * NU))[lane];
+            ue = ((const d2 *)(d.du + r * NU))[lane];
+        }
+    }
     const long xr0 = g0 - 1;
     if (p.S >= RW)
         stage_trial2(Xt, d, xr0, total, p.S, eps, lane, g0, bA, aA, nA, bB, aB, nB);
     else
         stage_trial(Xt, d.Xb, d.dX, xr0, total, p.S, eps, lane, active, [&](long r) { return r >= g0; }, nomof);
+    if (up0) {
+        Up0[2 * lane] = ua.x + eps * ue.x;
+        Up0[2 * lane + 1] = ua.y + eps * ue.y;
+    }
     __syncthreads();
-    if (gid >= total) return;
-    const int b = (int)(gid / p.S), s = (int)(gid % p.S);
-    if (!active(b)) return;
+    // every lane stays active up to the u_prev exchange: lanes without a slot of their own work on a
+    // valid one (clamped) and write nothing
+    const long gc = gid < total ? gid : total - 1;
+    const int b = (int)(gc / p.S), s = (int)(gc % p.S);
     const auto L = layout_of<EL>(d, b);
-    if (s >= L.S()) return;
+    const bool mine = gid < total && active(b) && s < L.S();
     int i, k;
-    slot_phase(L, s, i, k);
+    slot_phase(L, s < L.S() ? s : L.S() - 1, i, k);
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
-    const double *x = Xt + (gid - xr0) * RS;
-    const long kq = (long)b * p.Kc + s - i;  // the slot's control row (k < N)
+    const double *x = Xt + (gc - xr0) * RS;
     const int nb = nomof(b);
+    const long kq = (long)b * p.Kc + s - i;  // the slot's control row (k < N)
+    const long kqmax = (long)p.B * p.Kc - 1;
+    // the trial control row of the slot (k < N; the terminal slot's row index is clamped and unused)
+    double u[NU];
+    trial_row(d, d.Ub[nb], kq < kqmax ? kq : kqmax, eps, u);
+    // the running cost of a control slot (the terminal cost at k = N: the boundary waves)
+    if (mine && k < L.N(i)) {
+        d2 *ug = (d2 *)(d.Ub[nb ^ 1] + kq * NU);
+#pragma unroll
+        for (int j = 0; j < NU / 2; ++j) ug[j] = d2{u[2 * j], u[2 * j + 1]};
+        finish_running(p, d, b, s, L.k0(i) + k, c, x, u);
+    }
+    // u_prev: the previous slot's control row is the previous lane's (k > 0: slot s - 1 is a
+    // control slot of the same phase), lane 0's was staged
+    double up[NU];
+#pragma unroll
+    for (int j = 0; j < NU; ++j) up[j] = from_prev_lane(u[j]);
+    if (lane == 0)
+#pragma unroll
+        for (int j = 0; j < NU; ++j) up[j] = Up0[j];
+    if (!mine) return;
     // a phase's first slot: x_init = x0, or the reset map of X_{i-1}[N] (MultiPhaseDDP.cpp:73-81),
     // whose Defect the boundary waves write
     if (k > 0 || i == 0) {
@@ -580,22 +631,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
 #pragma unroll
             for (int j = 0; j < NX; ++j) xs[j] = d.x0[(size_t)b * NX + j];
         } else {
-            double up[NU];
-            trial_row(d, d.Ub[nb], kq - 1, eps, up);
             double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
             hkd_step(x - RS, up, cd, p.dt, xs);
         }
         finish_defect(p, d, b, s, k, x, xs);
-    }
-    // the running cost of a control slot (the terminal cost at k = N: the boundary waves)
-    if (k < L.N(i)) {
-        double u[NU];
-        trial_row(d, d.Ub[nb], kq, eps, u);
-        typedef double d2 __attribute__((ext_vector_type(2)));
-        d2 *ug = (d2 *)(d.Ub[nb ^ 1] + kq * NU);
-#pragma unroll
-        for (int j = 0; j < NU / 2; ++j) ug[j] = d2{u[2 * j], u[2 * j + 1]};
-        finish_running(p, d, b, s, L.k0(i) + k, c, x, u);
     }
 }
 

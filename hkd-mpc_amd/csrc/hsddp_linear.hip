@@ -313,7 +313,6 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
     const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5;
     const bool rowl = r < NX;
     const int rr = rowl ? r : 0;
-    const real dt = p.dt;
     LSTAMP(0);
     if (more) {
         src.advance();

@@ -377,15 +377,23 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     for (int l = 0; l < 4; ++l) { bv[l] = I.pc[l]; bq[l] = I.pc[4 + l]; }
     STAMP(1);
     // ---- Gn = G + H d (SinglePhase.cpp:320), T = H B_c, M = H A (row pp) ----------------------
-    real m[NX], t[HC], ga[4] = {g, 0, 0, 0};
-#pragma unroll
-    for (int c = 0; c < NX; ++c) m[c] = h[c];
+    // T and Gn read H first; M = H + H S then accumulates over H's registers (H is not read again:
+    // the knot ends by forming the new H) from copies of the 9 entries S's rows read
+    real t[HC], ga[4] = {g, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < HC; ++q) t[q] = 0;
-    emit_SA(m, h, cf, dt);
     emit_Bc(t, h[6], h[7], h[8], h + 9, h + 12, bv, bq, cf);
     static_for<NX>([&](auto C) { vfma<V_D + C>(ga[C & 3], cf, h[C]); });
     const real gn = (ga[0] + ga[1]) + (ga[2] + ga[3]);
+    pin(t);
+    real h9[NX];  // (entries 0..8 only)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) h9[j] = h[j];
+#pragma unroll
+    for (int j = 9; j < NX; ++j) h9[j] = 0;
+    SSYNC();
+    real (&m)[NX] = h;
+    emit_SA(m, h9, cf, dt);
     pin(t);
     pin(m);
     if (L.row) {
@@ -485,9 +493,10 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     if (more) fetch(S, nrec0, ndef0, nrec1, ndef1, L.lane);
     STAMP(5);
     // ---- PSD test + Gauss-Jordan on [Quu_cc | Qux_c | Qu_c] --------------------------------------
-    real quxs[HC];  // Qux_c column pp (position 24: Qu_c), kept for G and the value update
+    // Qux_c column pp, kept for G and the value update (positions >= 24: zero, so their H row stays 0)
+    real quxs[HC];
 #pragma unroll
-    for (int q = 0; q < HC; ++q) quxs[q] = w2[q];
+    for (int q = 0; q < HC; ++q) quxs[q] = L.row ? w2[q] : (real)0;
     pin(quxs);
     unsigned long long bad = __builtin_amdgcn_ballot_w64(zl && !(qzz > (real)1e-9));
     // w2 becomes -Quu_cc^-1 [Qux_c | Qu_c] = [K_c | dU_c] (the reference's explicit inverse,
@@ -569,9 +578,7 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     // of ka (c < 16) or kb (c >= 16)); the coupled dU_c is position 24's: kb at position 8
     real ka[HC], kb[HC];
 #pragma unroll
-    for (int q = 0; q < HC; ++q) row_pair(w2[q], ka[q], kb[q]);
-#pragma unroll
-    for (int q = 0; q < HC; ++q) quxs[q] = L.row ? quxs[q] : (real)0;  // positions >= 24 keep H = 0
+    for (int q = 0; q < HC; ++q) row_pair_last(w2[q], ka[q], kb[q]);
     // G = Qx - Qux_c^T Quu_cc^-1 Qu_c = Qx + Qux_c^T dU_c (SinglePhase.cpp:359)
     real gq4[4] = {qx, 0, 0, 0};
     static_for<HC>([&](auto Q) { bfma<8>(gq4[Q & 3], kb[Q], quxs[Q]); });
@@ -598,12 +605,26 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     // knot's stores, both long complete — so no later wait counts these stores: the next knot reads
     // its images without waiting (vector memory operations complete in order).
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if HSDDP_VALUE_MFMA
     if (st && L.row) {
         real *Kg = it.K + (size_t)kc * KCW;
 #pragma unroll
         for (int q = 0; q < HC; ++q) Kg[q * NX + pp] = w2[q];
         it.dU[(size_t)kc * NX + pp] = I.du[pp];
     }
+#else
+    // from the row-pair copies (w2 is dead after the broadcast): columns 0..15 from ka by both DPP
+    // rows of the item (the two write the same value), columns 16..23 from kb
+    if (st) {
+        real *Kg = it.K + (size_t)kc * KCW;
+#pragma unroll
+        for (int q = 0; q < HC; ++q) Kg[q * NX + pos] = ka[q];
+        if (pos < NX - 16)
+#pragma unroll
+            for (int q = 0; q < HC; ++q) Kg[q * NX + 16 + pos] = kb[q];
+        if (L.row) it.dU[(size_t)kc * NX + pp] = I.du[pp];
+    }
+#endif
     SSYNC();
     STAMP(9);
 }

@@ -213,6 +213,25 @@ DEV void row_pair(double x, double &ka, double &kb)
     ka = __hiloint2double(b[0], a[0]);
     kb = __hiloint2double(b[1], a[1]);
 }
+DEV void row_pair_last_f(float x, float &ka, float &kb)
+{
+    const unsigned u = __float_as_uint(x);
+    const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    ka = __uint_as_float(a[0]);
+    kb = __uint_as_float(a[1]);
+}
+// The same when x is not used afterwards: one 64-bit copy (x's own registers take the other
+// result), not a copy per 32-bit half for each operand of the swaps
+DEV void row_pair_last(double x, double &ka, double &kb)
+{
+    double c;
+    asm volatile("v_mov_b64 %0, %1" : "=v"(c) : "v"(x));
+    const auto a = __builtin_amdgcn_permlane16_swap(__double2loint(c), __double2loint(x), false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(__double2hiint(c), __double2hiint(x), false, false);
+    ka = __hiloint2double(b[0], a[0]);
+    kb = __hiloint2double(b[1], a[1]);
+}
+DEV void row_pair_last(float x, float &ka, float &kb) { row_pair_last_f(x, ka, kb); }
 DEV void row_pair(float x, float &ka, float &kb)
 {
     const unsigned u = __float_as_uint(x);
