@@ -747,6 +747,9 @@ struct Timer {
     std::vector<hipEvent_t> *pool;  // the handle's events, handed out in order (no create / destroy per launch)
     size_t used = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[5];  // lq, riccati, forward, other, linear
+    // the last end() event, when nothing was launched since: the next begin() reuses it (an event
+    // record costs the stream a ~5 us gap, and adjacent end / begin pairs were two)
+    hipEvent_t pend = nullptr;
     hipEvent_t next()
     {
         if (used == pool->size()) {
@@ -759,16 +762,24 @@ struct Timer {
     void begin(int cat, hipEvent_t &e0)
     {
         if (!on) return;
+        (void)cat;
+        if (pend) {
+            e0 = pend;
+            pend = nullptr;
+            return;
+        }
         e0 = next();
         hipEventRecord(e0, st);
-        (void)cat;
     }
+    // launches outside the timed categories follow: the next begin() records its own event
+    void cut() { pend = nullptr; }
     void end(int cat, hipEvent_t e0)
     {
         if (!on) return;
         hipEvent_t e1 = next();
         hipEventRecord(e1, st);
         ev[cat].push_back({e0, e1});
+        pend = e1;
     }
     double total(int cat)
     {
@@ -920,6 +931,7 @@ extern "C" int hsddp_solve(hsddp_handle h, hsddp_stats *stats)
     int iters = 0, outers = 0, nbwd = 0;
     const bool checks = !h->opt.no_early_exit;
     for (int ou = 0; ou < h->opt.max_AL_iter; ++ou) {
+        tm.cut();
         launch_outer_begin(h->p, h->d, h->stream);
         outers++;
         for (int in = 0; in < h->opt.max_DDP_iter; ++in) {
@@ -928,6 +940,7 @@ extern "C" int hsddp_solve(hsddp_handle h, hsddp_stats *stats)
             nbwd++;
             if (checks) {
                 int n = 0;
+                tm.cut();
                 if ((rc = count_active(h, 1, n))) return rc;
                 if (n == 0) break;
             }
@@ -935,6 +948,7 @@ extern "C" int hsddp_solve(hsddp_handle h, hsddp_stats *stats)
         outer_end_launches(h, tm);
         if (checks) {
             int n = 0;
+            tm.cut();
             if ((rc = count_active(h, 2, n))) return rc;
             if (n == 0) break;
         }

@@ -200,6 +200,9 @@ template <bool EL>
 __global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
 {
     const int b = blockIdx.x / p.P, i = blockIdx.x % p.P, t = threadIdx.x;
+    // the parallel-retry list of the k_riccati launch that follows starts empty (its only reader
+    // before then is the previous iteration's k_riccati_select): no memset launch of its own
+    if (p.retry_cap > 0 && blockIdx.x == 0 && t == 0) *d.retry_count = 0;
     const ElemState &E = d.el[b];
     if (E.done || E.inner_done) return;
     const auto L = layout_of<EL>(d, b);
