@@ -425,7 +425,7 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         (rc = dalloc(h, d.reb_eps, B * Kc * 20)) || (rc = dalloc(h, d.al_sigma, B * P * 4)) ||
         (rc = dalloc(h, d.al_lambda, B * P * 4)) || (rc = dalloc(h, d.term_h, B * P * 4)) ||
         (rc = dalloc(h, d.slot_cost, B * S)) || (rc = dalloc(h, d.slot_feas, B * S)) || (rc = dalloc(h, d.slot_viol, B * S)) ||
-        (rc = dalloc(h, d.slot_div, B * S)) || (rc = dalloc(h, d.el, B)) || (rc = dalloc(h, d.counter, 8)) ||
+        (rc = dalloc(h, d.slot_div, B * S)) || (rc = dalloc(h, d.el, B)) || (rc = dalloc(h, d.counter, 8)) || (rc = dalloc(h, d.ls_live, LS_LIVE)) ||
         (rc = dalloc(h, (Layout *&)d.lay, B)) || (rc = dalloc(h, (int *&)d.pairs, 2 * B + 2))) {
         hsddp_destroy(h);
         return rc;
@@ -833,8 +833,8 @@ static std::vector<double> ls_steps(double alpha)
 static void begin_launches(hsddp_handle h)
 {
     launch_reset_elements(h->p, h->d, h->stream);
-    launch_rollout(h->p, h->d, 0.0, 1, h->stream);
-    launch_decide(h->p, h->d, 0.0, 0, 1, h->stream);
+    launch_rollout(h->p, h->d, 0.0, 1, -1, h->stream);
+    launch_decide(h->p, h->d, 0.0, 0, 1, -1, h->stream);
     h->slots_fresh = true;
 }
 
@@ -860,8 +860,8 @@ static void iteration_launches(hsddp_handle h, const std::vector<double> &trials
     tm.end(4, e0);
     tm.begin(2, e0);
     for (size_t t = 0; t < trials.size(); ++t) {
-        launch_rollout(p, d, trials[t], 0, st);
-        launch_decide(p, d, trials[t], t + 1 == trials.size(), 0, st);
+        launch_rollout(p, d, trials[t], 0, (int)t, st);
+        launch_decide(p, d, trials[t], t + 1 == trials.size(), 0, (int)t, st);
     }
     tm.end(2, e0);
     h->slots_fresh = true;

@@ -22,6 +22,7 @@ namespace hsddp {
 constexpr int NX = 24;
 constexpr int NN = 576;
 constexpr int MAXP = 16;
+constexpr int LS_LIVE = 128;  // line-search trials with a liveness flag (later ones run unconditionally)
 // Gains are stored for the 12 controls whose B column is non-zero: row q (0..11) is control
 // u = q when leg q/3 is in stance, u = 12 + q when it swings.  The other 12 rows of the
 // reference's 24 x 24 K are exactly zero (hsddp_sweep.hip) and are expanded on
@@ -126,6 +127,10 @@ struct Bufs {
     float *lq32, *K32, *def32;
     ElemState *el;
     int *counter;                          // [8] host-visible activity counters [0..2], stat sums [4..5]
+    // [LS_LIVE] per line-search trial t of the current inner iteration: 1 when an element is still
+    // searching after trial t (k_decide), zeroed at the iteration's start (k_lq): later trials of a
+    // batch with none left return at once
+    int *ls_live;
     // parallel regularisation retries: deferred elements [retry_cap], their count, per attempt a
     // success flag [retry_cap][retry_m] and the attempt's gains / dU rows [retry_cap][retry_m][Kc][..]
     RetryEntry *retry_list;
@@ -142,8 +147,9 @@ struct Bufs {
 };
 
 // kernel launchers (hsddp_kernels.hip)
-void launch_rollout(const Params &p, const Bufs &d, double eps, int init, hipStream_t st);
-void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, hipStream_t st);
+// tix: the trial's index in the inner iteration's line search (-1: the initial rollout)
+void launch_rollout(const Params &p, const Bufs &d, double eps, int init, int tix, hipStream_t st);
+void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, int tix, hipStream_t st);
 // nominal rows of every element into buffer 0 (Bufs::sel bit 0 cleared), for host transfers
 void launch_normalize(const Params &p, const Bufs &d, hipStream_t st);
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st);

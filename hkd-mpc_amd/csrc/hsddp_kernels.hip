@@ -3,7 +3,8 @@
 // One DDP inner iteration of MultiPhaseDDP::solve (HSDDPSolver/source/MultiPhaseDDP.cpp:304-381)
 // for B trajectories is:
 //   k_lq        knot-parallel  cost at (X, U) + compact LQ model   SinglePhase::compute_cost/LQ_approximation
-//   k_terminal  (elem, phase)  Phix, Phixx (+AL), reset Jacobian   SinglePhase.cpp:286-295; HKDReset.h:78-136
+//   (terminal)  (elem, phase)  Phix, Phixx (+AL), reset Jacobian   SinglePhase.cpp:286-295; HKDReset.h:78-136
+//                              one wave per task, the last blocks of the k_lq launch
 //   k_riccati   one wave/2 elems regularised Riccati sweep over all phases   (hsddp_sweep.hip)
 //                              MultiPhaseDDP.cpp:141-229; SinglePhase.cpp:298-367
 //   k_lin_rollout one wave/2 elems  MS linear rollout + merit                (hsddp_linear.hip)
@@ -70,6 +71,169 @@ DEV void lq_stage_store(T *wl, const long *ridx, const double *v, T *lq, int ldw
     lq_flush(wl, ridx, lq, ldw, lane, OFF, N);
 }
 
+// The terminal task of one (element, phase), one wave: Phix, Phixx (+AL, quirk A4) and the
+// reset-map Jacobian Px.  These run as the last waves of the k_lq launch (they fill its tail).
+struct TermLds {
+    double sx[NX], shx[4][NX], scoef[4][2], sh[4], sxr[NX], spf[12], ssl[8], sdd[NX], scw[12];
+    double spx[NX * (NX + 1)];
+    int sc[4], scn[4];
+};
+
+// LDS hand-over between the lanes of one wave (its LDS accesses complete in order)
+DEV void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool EL>
+DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int t)
+{
+    const int b = task / p.P, i = task % p.P;
+    const ElemState &E = d.el[b];
+    if (E.done || E.inner_done) return;
+    const auto L = layout_of<EL>(d, b);
+    const int P = L.P();
+    if (i >= P) return;
+    double *sx = S.sx, (*shx)[NX] = S.shx, (*scoef)[2] = S.scoef, *sh = S.sh, *sxr = S.sxr, *spf = S.spf, *ssl = S.ssl;
+    int *sc = S.sc, *scn = S.scn;
+    const int s = L.s0(i) + L.N(i);
+    const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
+    if (t < NX) sx[t] = d.Xb[work_buf(d, b)][((size_t)b * p.S + s) * NX + t];
+    // the terminal cost's other inputs, staged with X[N] (no memory round trip at the end)
+    if (t >= 32 && t < 32 + NX) sxr[t - 32] = xr[t - 32];
+    if (t >= 56 && t < 64) ssl[t - 56] = (t < 60 ? d.al_sigma : d.al_lambda)[((size_t)b * p.P + i) * 4 + (t & 3)];
+    if (t >= 4 && t < 16) spf[t - 4] = pf[t - 4];
+    if (t < 4) {
+        const int *cc = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
+        sc[t] = cc[t]; scn[t] = cc[4 + t];
+    }
+    wave_sync();
+    // Px at X_i[N] (HKDReset.h:78-136) is built in LDS from the identity (phase boundaries only)
+    double *spx = S.spx;
+    const bool bnd = i < P - 1;
+    for (int e = t; e < 4 * NX; e += 64) (&shx[0][0])[e] = 0.0;
+    if (bnd)
+        for (int e = t; e < NX * (NX + 1); e += 64) spx[e] = (e / (NX + 1) == e % (NX + 1)) ? 1.0 : 0.0;
+    wave_sync();
+    if (t < 4) {
+        // touchdown legs: foot height h, its gradient (non-zeros at 0..2, 5, 12 + 3 l + k) and, at a
+        // phase boundary, the reset map's foot-Jacobian rows — from one evaluation of the leg's
+        // kinematics (hkd_foot_height_grad_sparse's and hkd_foot_jacobian's expressions)
+        const int l = t;
+        const bool td = touchdown(sc, scn, l);
+        double h = 0.0;
+        if (td) {
+            Rot R, Dy, Dp, Dr;
+            const EulTrig tr = eul_trig(sx);
+            rot_zyx(tr, R);
+            rot_zyx_grad(tr, Dy, Dp, Dr);
+            double pb[3], dpb[3][3];
+            foot_body(l, sx + 12 + 3 * l, pb, dpb);
+            shx[l][0] = Dy.r[2][0] * pb[0] + Dy.r[2][1] * pb[1] + Dy.r[2][2] * pb[2];
+            shx[l][1] = Dp.r[2][0] * pb[0] + Dp.r[2][1] * pb[1] + Dp.r[2][2] * pb[2];
+            shx[l][2] = Dr.r[2][0] * pb[0] + Dr.r[2][1] * pb[1] + Dr.r[2][2] * pb[2];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) shx[l][12 + 3 * l + k] = R.r[2][0] * dpb[0][k] + R.r[2][1] * dpb[1][k] + R.r[2][2] * dpb[2][k];
+            shx[l][5] = 1.0;
+            h = (sx[5] + R.r[2][0] * pb[0] + R.r[2][1] * pb[1] + R.r[2][2] * pb[2]) - p.ground;
+            if (bnd) {  // rows 12 + 3 l + k, k < 2: the foot Jacobian's rows; the k = 2 row is zero
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    double *row = spx + (12 + 3 * l + k) * (NX + 1);
+                    row[12 + 3 * l + k] = 0.0;
+                    if (k == 2) continue;
+                    row[0] = Dy.r[k][0] * pb[0] + Dy.r[k][1] * pb[1] + Dy.r[k][2] * pb[2];
+                    row[1] = Dp.r[k][0] * pb[0] + Dp.r[k][1] * pb[1] + Dp.r[k][2] * pb[2];
+                    row[2] = Dr.r[k][0] * pb[0] + Dr.r[k][1] * pb[1] + Dr.r[k][2] * pb[2];
+                    row[3 + k] = 1.0;
+#pragma unroll
+                    for (int m = 0; m < 3; ++m)
+                        row[12 + 3 * l + m] = R.r[k][0] * dpb[0][m] + R.r[k][1] * dpb[1][m] + R.r[k][2] * dpb[2][m];
+                }
+            }
+        } else if (bnd && sc[l] && !scn[l]) {  // lift-off: rows 12 + 3 l + k zero
+#pragma unroll
+            for (int k = 0; k < 3; ++k) spx[(12 + 3 * l + k) * (NX + 2)] = 0.0;
+        }
+        const double sg = ssl[l], lm = ssl[4 + l];
+        scoef[l][0] = (td && p.AL_active) ? sg * h + lm : 0.0;
+        scoef[l][1] = (td && p.AL_active) ? sg * (1 + h) + lm : 0.0;
+        sh[l] = h;
+    }
+    wave_sync();
+    KParams &kp = *kparams();  // runtime-indexed weights
+    double *rec = d.term + ((size_t)b * p.P + i) * TW;
+    if (t == 0) {  // the phase's terminal cost at X[N] (SinglePhase::compute_cost's last term) for k_lq's slot sums
+        double tv;
+        d.slot_cost[(size_t)b * p.S + s] = terminal_cost_h(p, sc, scn, sx, sxr, spf, ssl, ssl + 4, sh, tv);
+    }
+    if (t < NX) { // Phix
+        const int j = t;
+        double v = kp.qf_gain * kp.qf_scale[j] * q_diag(kp, sc, j) * (sx[j] - xr[j]);
+        if (j >= 3 && j < 6) {
+            for (int l = 0; l < 4; ++l) {
+                int m = 3 * l + (j - 3);
+                double e = (sx[12 + m] - sx[j]) - (pf[m] - xr[j]);
+                v += -(p.foot_term_grad * sc[l] * foot_weight(kp, sc, m) * e);
+            }
+        } else if (j >= 12) {
+            int m = j - 12, l = m / 3;
+            double e = (sx[j] - sx[3 + m % 3]) - (pf[m] - xr[3 + m % 3]);
+            v += p.foot_term_grad * sc[l] * foot_weight(kp, sc, m) * e;
+        }
+        for (int l = 0; l < 4; ++l) v += scoef[l][0] * shx[l][j];
+        rec[TM_PHIX + j] = v;
+    }
+    // foot Hessian 20 D^T Qfoot D: weight of (leg l, axis j), entries (3 + j, 3 + j) (summed over
+    // the legs in leg order), (12 + 3 l + j, 12 + 3 l + j) and, negated, the two cross entries.
+    // Lane r < 24 forms diagonal entry r, lane 24 + m the weight of joint column 12 + m (runtime-
+    // indexed weights read once per phase, not once per entry); the 576 entries then combine them.
+    auto fw = [&](int l, int j) { return p.foot_term_grad * sc[l] * sc[l] * foot_weight(kp, sc, 3 * l + j); };
+    double *sdd = S.sdd, *scw = S.scw;
+    if (t < NX) {
+        const int r = t;
+        double v = kp.qf_gain * kp.qf_scale[r] * q_diag(kp, sc, r);
+        if (r >= 3 && r < 6) {
+            for (int l = 0; l < 4; ++l) v += fw(l, r - 3);
+        } else if (r >= 12) {
+            v += fw((r - 12) / 3, (r - 12) % 3);
+        }
+        sdd[r] = v;
+    } else if (t < NX + 12) {
+        const int m = t - NX;
+        scw[m] = fw(m / 3, m % 3);
+    }
+    wave_sync();
+    // the AL terms of the touchdown legs only (a leg's coefficient is the same on every lane; the
+    // others add exact zeros)
+    bool use[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) use[l] = scoef[l][1] != 0.0;
+    int r = t / NX, cidx = t % NX;  // entry e = t + 64 j: (r, cidx) advance by (2, 16) per step
+    for (int e = t; e < NN; e += 64) { // Phixx
+        double v = 0.0;
+        if (r == cidx)
+            v = sdd[r];
+        else if (r >= 3 && r < 6 && cidx >= 12 && (cidx - 12) % 3 == r - 3)
+            v = -scw[cidx - 12];
+        else if (cidx >= 3 && cidx < 6 && r >= 12 && (r - 12) % 3 == cidx - 3)
+            v = -scw[r - 12];
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+            if (use[l]) v += scoef[l][1] * (shx[l][r] * shx[l][cidx]);
+        rec[TM_PHIXX + e] = v;
+        if (bnd) rec[TM_PX + e] = spx[r * (NX + 1) + cidx];  // Px rows from LDS, stored coalesced
+        r += 2;
+        cidx += 16;
+        if (cidx >= NX) {
+            cidx -= NX;
+            r += 1;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_lq: per (element, state slot): cost and |Defect|^2 at the current (X, U); compact LQ model at
 // control slots (SinglePhase::compute_cost + LQ_approximation, SinglePhase.cpp:235-296).
@@ -81,9 +245,24 @@ template <bool F32, bool EL, bool SLOTS>
 __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 {
     using T = std::conditional_t<F32, float, double>;
-    __shared__ T stage[4][64 * LQ_STG];
+    // the record stage of the knot waves, or the LDS of the terminal tasks (blocks after them)
+    constexpr size_t STG = sizeof(T) * 4 * 64 * LQ_STG, TRM = 4 * sizeof(TermLds);
+    __shared__ __attribute__((aligned(16))) char lds[STG > TRM ? STG : TRM];
+    T (*stage)[64 * LQ_STG] = reinterpret_cast<T (*)[64 * LQ_STG]>(lds);
     __shared__ long sridx[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long nknot = ((long)p.B * p.S + 255) / 256;
+    if ((long)blockIdx.x >= nknot) {  // terminal tasks, one per wave
+        const long task = ((long)blockIdx.x - nknot) * 4 + w;
+        // the parallel-retry list of the k_riccati launch that follows starts empty (its only
+        // reader before then is the previous iteration's k_riccati_select): no memset launch
+        if (p.retry_cap > 0 && task == 0 && lane == 0) *d.retry_count = 0;
+        // and no element has been seen searching after any trial of this iteration yet
+        if (task == 0)
+            for (int t = lane; t < LS_LIVE; t += 64) d.ls_live[t] = 0;
+        if (task < (long)p.B * p.P) terminal_task<EL>(p, d, reinterpret_cast<TermLds *>(lds)[w], (int)task, lane);
+        return;
+    }
     sridx[w][lane] = -1; // before any early return: lanes without a record stay -1
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long)p.B * p.S) return;
@@ -114,7 +293,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
         for (int j = 0; j < NX; ++j) d32[j] = (float)dg[j];
     }
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
-    if (k == L.N(i)) return;  // the terminal cost: k_terminal (the same function, from its foot heights)
+    if (k == L.N(i)) return;  // the terminal cost: the terminal task (the same function, from its foot heights)
     const int kc = L.k0(i) + k;
     sridx[w][lane] = (long)b * p.Kc + kc;
     double u[NU];
@@ -195,146 +374,6 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     lq_stage_store<T, LQ_RB, 24>(stage[w], sridx[w], rb, lqT, ldw, lane);
 }
 
-// k_terminal: one wave per (element, phase): Phix, Phixx (+AL, quirk A4) and reset-map Jacobian Px.
-template <bool EL>
-__global__ __launch_bounds__(64) void k_terminal(Params p, Bufs d)
-{
-    const int b = blockIdx.x / p.P, i = blockIdx.x % p.P, t = threadIdx.x;
-    // the parallel-retry list of the k_riccati launch that follows starts empty (its only reader
-    // before then is the previous iteration's k_riccati_select): no memset launch of its own
-    if (p.retry_cap > 0 && blockIdx.x == 0 && t == 0) *d.retry_count = 0;
-    const ElemState &E = d.el[b];
-    if (E.done || E.inner_done) return;
-    const auto L = layout_of<EL>(d, b);
-    const int P = L.P();
-    if (i >= P) return;
-    __shared__ double sx[NX], shx[4][NX], scoef[4][2], sh[4], sxr[NX], spf[12], ssl[8];
-    __shared__ int sc[4], scn[4];
-    const int s = L.s0(i) + L.N(i);
-    const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
-    if (t < NX) sx[t] = d.Xb[work_buf(d, b)][((size_t)b * p.S + s) * NX + t];
-    // the terminal cost's other inputs, staged with X[N] (no memory round trip at the end)
-    if (t >= 32 && t < 32 + NX) sxr[t - 32] = xr[t - 32];
-    if (t >= 56 && t < 64) ssl[t - 56] = (t < 60 ? d.al_sigma : d.al_lambda)[((size_t)b * p.P + i) * 4 + (t & 3)];
-    if (t >= 4 && t < 16) spf[t - 4] = pf[t - 4];
-    if (t < 4) {
-        const int *cc = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
-        sc[t] = cc[t]; scn[t] = cc[4 + t];
-    }
-    __syncthreads();
-    // Px at X_i[N] (HKDReset.h:78-136) is built in LDS from the identity (phase boundaries only)
-    __shared__ double spx[NX * (NX + 1)];
-    const bool bnd = i < P - 1;
-    for (int e = t; e < 4 * NX; e += 64) (&shx[0][0])[e] = 0.0;
-    if (bnd)
-        for (int e = t; e < NX * (NX + 1); e += 64) spx[e] = (e / (NX + 1) == e % (NX + 1)) ? 1.0 : 0.0;
-    __syncthreads();
-    if (t < 4) {
-        // touchdown legs: foot height h, its gradient (non-zeros at 0..2, 5, 12 + 3 l + k) and, at a
-        // phase boundary, the reset map's foot-Jacobian rows — from one evaluation of the leg's
-        // kinematics (hkd_foot_height_grad_sparse's and hkd_foot_jacobian's expressions)
-        const int l = t;
-        const bool td = touchdown(sc, scn, l);
-        double h = 0.0;
-        if (td) {
-            Rot R, Dy, Dp, Dr;
-            const EulTrig tr = eul_trig(sx);
-            rot_zyx(tr, R);
-            rot_zyx_grad(tr, Dy, Dp, Dr);
-            double pb[3], dpb[3][3];
-            foot_body(l, sx + 12 + 3 * l, pb, dpb);
-            shx[l][0] = Dy.r[2][0] * pb[0] + Dy.r[2][1] * pb[1] + Dy.r[2][2] * pb[2];
-            shx[l][1] = Dp.r[2][0] * pb[0] + Dp.r[2][1] * pb[1] + Dp.r[2][2] * pb[2];
-            shx[l][2] = Dr.r[2][0] * pb[0] + Dr.r[2][1] * pb[1] + Dr.r[2][2] * pb[2];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) shx[l][12 + 3 * l + k] = R.r[2][0] * dpb[0][k] + R.r[2][1] * dpb[1][k] + R.r[2][2] * dpb[2][k];
-            shx[l][5] = 1.0;
-            h = (sx[5] + R.r[2][0] * pb[0] + R.r[2][1] * pb[1] + R.r[2][2] * pb[2]) - p.ground;
-            if (bnd) {  // rows 12 + 3 l + k, k < 2: the foot Jacobian's rows; the k = 2 row is zero
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    double *row = spx + (12 + 3 * l + k) * (NX + 1);
-                    row[12 + 3 * l + k] = 0.0;
-                    if (k == 2) continue;
-                    row[0] = Dy.r[k][0] * pb[0] + Dy.r[k][1] * pb[1] + Dy.r[k][2] * pb[2];
-                    row[1] = Dp.r[k][0] * pb[0] + Dp.r[k][1] * pb[1] + Dp.r[k][2] * pb[2];
-                    row[2] = Dr.r[k][0] * pb[0] + Dr.r[k][1] * pb[1] + Dr.r[k][2] * pb[2];
-                    row[3 + k] = 1.0;
-#pragma unroll
-                    for (int m = 0; m < 3; ++m)
-                        row[12 + 3 * l + m] = R.r[k][0] * dpb[0][m] + R.r[k][1] * dpb[1][m] + R.r[k][2] * dpb[2][m];
-                }
-            }
-        } else if (bnd && sc[l] && !scn[l]) {  // lift-off: rows 12 + 3 l + k zero
-#pragma unroll
-            for (int k = 0; k < 3; ++k) spx[(12 + 3 * l + k) * (NX + 2)] = 0.0;
-        }
-        const double sg = ssl[l], lm = ssl[4 + l];
-        scoef[l][0] = (td && p.AL_active) ? sg * h + lm : 0.0;
-        scoef[l][1] = (td && p.AL_active) ? sg * (1 + h) + lm : 0.0;
-        sh[l] = h;
-    }
-    __syncthreads();
-    KParams &kp = *kparams();  // runtime-indexed weights
-    double *rec = d.term + ((size_t)b * p.P + i) * TW;
-    if (t == 0) {  // the phase's terminal cost at X[N] (SinglePhase::compute_cost's last term) for k_lq's slot sums
-        double tv;
-        d.slot_cost[(size_t)b * p.S + s] = terminal_cost_h(p, sc, scn, sx, sxr, spf, ssl, ssl + 4, sh, tv);
-    }
-    if (t < NX) { // Phix
-        const int j = t;
-        double v = kp.qf_gain * kp.qf_scale[j] * q_diag(kp, sc, j) * (sx[j] - xr[j]);
-        if (j >= 3 && j < 6) {
-            for (int l = 0; l < 4; ++l) {
-                int m = 3 * l + (j - 3);
-                double e = (sx[12 + m] - sx[j]) - (pf[m] - xr[j]);
-                v += -(p.foot_term_grad * sc[l] * foot_weight(kp, sc, m) * e);
-            }
-        } else if (j >= 12) {
-            int m = j - 12, l = m / 3;
-            double e = (sx[j] - sx[3 + m % 3]) - (pf[m] - xr[3 + m % 3]);
-            v += p.foot_term_grad * sc[l] * foot_weight(kp, sc, m) * e;
-        }
-        for (int l = 0; l < 4; ++l) v += scoef[l][0] * shx[l][j];
-        rec[TM_PHIX + j] = v;
-    }
-    // foot Hessian 20 D^T Qfoot D: weight of (leg l, axis j), entries (3 + j, 3 + j) (summed over
-    // the legs in leg order), (12 + 3 l + j, 12 + 3 l + j) and, negated, the two cross entries.
-    // Lane r < 24 forms diagonal entry r, lane 24 + m the weight of joint column 12 + m (runtime-
-    // indexed weights read once per phase, not once per entry); the 576 entries then combine them.
-    auto fw = [&](int l, int j) { return p.foot_term_grad * sc[l] * sc[l] * foot_weight(kp, sc, 3 * l + j); };
-    __shared__ double sdd[NX], scw[12];
-    if (t < NX) {
-        const int r = t;
-        double v = kp.qf_gain * kp.qf_scale[r] * q_diag(kp, sc, r);
-        if (r >= 3 && r < 6) {
-            for (int l = 0; l < 4; ++l) v += fw(l, r - 3);
-        } else if (r >= 12) {
-            v += fw((r - 12) / 3, (r - 12) % 3);
-        }
-        sdd[r] = v;
-    } else if (t < NX + 12) {
-        const int m = t - NX;
-        scw[m] = fw(m / 3, m % 3);
-    }
-    __syncthreads();
-    for (int e = t; e < NN; e += 64) { // Phixx
-        const int r = e / NX, cidx = e % NX;
-        double v = 0.0;
-        if (r == cidx)
-            v = sdd[r];
-        else if (r >= 3 && r < 6 && cidx >= 12 && (cidx - 12) % 3 == r - 3)
-            v = -scw[cidx - 12];
-        else if (cidx >= 3 && cidx < 6 && r >= 12 && (r - 12) % 3 == cidx - 3)
-            v = -scw[r - 12];
-#pragma unroll
-        for (int l = 0; l < 4; ++l) v += scoef[l][1] * (shx[l][r] * shx[l][cidx]);
-        rec[TM_PHIXX + e] = v;
-    }
-    if (bnd)  // Px rows from LDS, stored coalesced by the wave
-        for (int e = t; e < NN; e += 64) rec[TM_PX + e] = spx[(e / NX) * (NX + 1) + e % NX];
-}
-
 // ---------------------------------------------------------------------------------------------
 // Per-slot outputs of one rollout trial from the slot's state x = X[k], simulated state xs =
 // Xsim[k] and control u = U[k] (k < N): Defect, |Defect|^2, divergence flag, running or terminal
@@ -390,6 +429,14 @@ DEV void finish_slot(const Params &p, const Bufs &d, const L_ &L, int b, int s, 
         finish_terminal(p, d, b, s, i, c, cn, x);
     else
         finish_running(p, d, b, s, L.k0(i) + k, c, x, u);
+}
+
+// trial tix > 0 of an inner iteration runs only when an element is still searching after trial
+// tix - 1 (Bufs::ls_live, written by the previous launch; a batch with none left returns at once)
+DEV bool ls_skip(const Bufs &d, int tix)
+{
+    if (tix <= 0 || tix > LS_LIVE) return false;
+    return __builtin_amdgcn_readfirstlane(d.ls_live[tix - 1]) == 0;
 }
 
 // k_rollout: one line-search trial (eps) per (element, state slot).  All knots are shooting states
@@ -544,8 +591,9 @@ DEV void rollout_boundary(const Params &p, const Bufs &d, double eps, int init, 
 }
 
 template <bool EL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOUT_WAVES))) void k_rollout(Params p, Bufs d, double eps, int init)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOUT_WAVES))) void k_rollout(Params p, Bufs d, double eps, int init, int tix)
 {
+    if (ls_skip(d, tix)) return;
     __shared__ double Xt[RW * RS];
     const int lane = threadIdx.x;
     const long total = (long)p.B * p.S;
@@ -647,8 +695,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
 // (X[0] = x_init when the set is empty) and U[k] = Ubar[k] + eps dU[k] + K[k] (X[k] - Xbar[k]),
 // then the slot outputs of those states.  One thread per element; rare (a few states per element).
 template <bool EL>
-__global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double eps, int init)
+__global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double eps, int init, int tix)
 {
+    if (ls_skip(d, tix)) return;
     const int b = blockIdx.x * 64 + threadIdx.x;
     if (b >= p.B) return;
     const ElemState &E = d.el[b];
@@ -712,8 +761,9 @@ __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double ep
 // slots in order, and the phase sums are added in phase order — the reference's summation order
 // (compute_cost, MultiPhaseDDP.cpp:431-440; SinglePhase.cpp:235-262).
 template <bool EL>
-__global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int last, int init)
+__global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int last, int init, int tix)
 {
+    if (ls_skip(d, tix)) return;
     const int lane = threadIdx.x, g = lane & 15, base = lane & ~15;
     const int b = blockIdx.x * 4 + (lane >> 4);
     const bool valid = b < p.B;
@@ -783,6 +833,7 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
         E.accepted = 0; E.ls_active = 0; E.cost = E.cost_prev; E.merit = E.merit_prev; fin = true;
         d.sel[b] = nb | ((nb ^ 1) << 1);  // quirk A2: the last trial stays the working trajectory
     }
+    if (!fin && tix >= 0 && tix < LS_LIVE) d.ls_live[tix] = 1;  // still searching (same value from every writer)
     if (fin) {
         // the later-termination test breaks before the iteration's entry is buffered (:358-371)
         if (!p.no_early_exit && fabs((E.cost_prev - E.cost) / E.cost_prev) < p.cost_thresh && E.feas <= p.feas_thresh)
@@ -1173,16 +1224,16 @@ static inline unsigned blocks_for(long n, int bs) { return (unsigned)((n + bs - 
         else hipLaunchKernelGGL(kern<false>, grid, block, 0, st, __VA_ARGS__);                      \
     } while (0)
 
-void launch_rollout(const Params &p, const Bufs &d, double eps, int init, hipStream_t st)
+void launch_rollout(const Params &p, const Bufs &d, double eps, int init, int tix, hipStream_t st)
 {
     // slot waves, then the phase-boundary waves (k_rollout, rollout_boundary)
     LAUNCH_EL(k_rollout, dim3(blocks_for((long)p.B * p.S, 64) + blocks_for((long)p.B * p.P, 64)), dim3(64), st, p, d,
-              eps, init);
-    if (p.has_tail) LAUNCH_EL(k_rollout_tail, dim3((p.B + 63) / 64), dim3(64), st, p, d, eps, init);
+              eps, init, tix);
+    if (p.has_tail) LAUNCH_EL(k_rollout_tail, dim3((p.B + 63) / 64), dim3(64), st, p, d, eps, init, tix);
 }
-void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, hipStream_t st)
+void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, int tix, hipStream_t st)
 {
-    LAUNCH_EL(k_decide, dim3((p.B + 3) / 4), dim3(64), st, p, d, eps, last, init);
+    LAUNCH_EL(k_decide, dim3((p.B + 3) / 4), dim3(64), st, p, d, eps, last, init, tix);
 }
 void launch_normalize(const Params &p, const Bufs &d, hipStream_t st)
 {
@@ -1191,7 +1242,8 @@ void launch_normalize(const Params &p, const Bufs &d, hipStream_t st)
 }
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
 {
-    const dim3 g(blocks_for((long)p.B * p.S, 256));
+    // the knot blocks, then the terminal tasks (four per block)
+    const dim3 g(blocks_for((long)p.B * p.S, 256) + blocks_for((long)p.B * p.P, 4));
     if (p.fp32) {
 #define HSDDP_LQ(f, e)                                                          \
     do {                                                                        \
@@ -1205,7 +1257,6 @@ void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
         else HSDDP_LQ(false, false);
 #undef HSDDP_LQ
     }
-    LAUNCH_EL(k_terminal, dim3(p.B * p.P), dim3(64), st, p, d);
 }
 
 __global__ __launch_bounds__(256) void k_broadcast(double *dst, const double *src, size_t n, size_t total)

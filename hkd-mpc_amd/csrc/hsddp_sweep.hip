@@ -978,7 +978,7 @@ __global__ __launch_bounds__(64) void k_riccati_select(Params p, Bufs d)
 
 void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
 {
-    // (the retry list count is zeroed by k_terminal, launched just before with the LQ model)
+    // (the retry list count is zeroed by the k_lq launch just before, in its first terminal task)
     const dim3 g1((unsigned)(p.elem_layout ? p.n_pairs : (p.B + 1) / 2));
     if (p.fp32) {
         if (p.elem_layout) hipLaunchKernelGGL((k_riccati<float, true>), g1, dim3(64), 0, st, p, d);
