@@ -347,7 +347,10 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     for (int j = 0; j < NU; ++j) lu[j] = p.dt * r_diag(p, j) * (u[j] - ur[j]);
 #pragma unroll
     for (int j = 0; j < 24; ++j) rb[j] = 0.0;
-    if (p.ReB_active) {
+    // uniform ReB parameters (the default schedule) and per-knot ones as separate code: in the
+    // uniform case no per-row (delta, eps) load and no per-row 1 / delta division is issued
+    auto reb = [&](auto uniform) {
+        constexpr bool U = decltype(uniform)::value;
         const double inv_du = 1.0 / p.grf_delta;
 #pragma unroll
         for (int lg = 0; lg < 4; ++lg) {
@@ -358,9 +361,9 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
                 double row[3], d1, d2;
                 grf_row(p.mu, r, row);
                 double g = row[0] * u[3 * lg] + row[1] * u[3 * lg + 1] + row[2] * u[3 * lg + 2];
-                const double dlr = p.reb_uniform ? p.grf_delta : dl[5 * lg + r];
-                reb_derivs(g, dlr, p.reb_uniform ? inv_du : 1.0 / dlr, d1, d2);
-                double e = p.reb_uniform ? p.grf_eps : ep[5 * lg + r];
+                const double dlr = U ? p.grf_delta : dl[5 * lg + r];
+                reb_derivs(g, dlr, U ? inv_du : 1.0 / dlr, d1, d2);
+                double e = U ? p.grf_eps : ep[5 * lg + r];
                 for (int a = 0; a < 3; ++a) gu[a] += e * d1 * row[a];
                 hu[0] += e * (d2 * row[0] * row[0]); hu[1] += e * (d2 * row[0] * row[1]);
                 hu[2] += e * (d2 * row[0] * row[2]); hu[3] += e * (d2 * row[1] * row[1]);
@@ -369,6 +372,10 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
             for (int a = 0; a < 3; ++a) lu[3 * lg + a] += p.dt * gu[a];
             for (int a = 0; a < 6; ++a) rb[6 * lg + a] = p.dt * hu[a];
         }
+    };
+    if (p.ReB_active) {
+        if (p.reb_uniform) reb(std::true_type{});
+        else reb(std::false_type{});
     }
     lq_stage_store<T, LQ_LU, NU>(stage[w], sridx[w], lu, lqT, ldw, lane);
     lq_stage_store<T, LQ_RB, 24>(stage[w], sridx[w], rb, lqT, ldw, lane);
