@@ -742,25 +742,43 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
 }
 
 // ElemState cost / feasibility of element b at the start of the inner iteration
-// (MultiPhaseDDP.cpp:306-307; the reference's summation order)
+// (MultiPhaseDDP.cpp:306-307; the reference's summation order): the half-wave's 32 lanes stage the
+// element's slot costs and |Defect|^2 in `stg` (the item's LDS, not yet in use; every load in flight
+// at once), then lane g < P sums phase g's slots in slot order and every lane adds the phase sums in
+// phase order (compute_cost's order).  stg == nullptr (horizons too long for it): the lanes read
+// global memory directly, ten slots' loads in flight.
 template <bool EL>
-DEV void element_cost(const Params &p, const Bufs &d, int b, int lane, double &cost, double &feas)
+DEV void element_cost(const Params &p, const Bufs &d, int b, int lane, double *stg, double &cost, double &feas)
 {
-    // lane g < P of the half sums phase g's slots in slot order (unrolled: ten loads in flight),
-    // then every lane adds the phase sums in phase order (compute_cost's order)
     const auto LY = layout_of<EL>(d, b);
     const int P = LY.P(), g = lane & 31;
+    const double *c = d.slot_cost + (size_t)b * p.S, *f = d.slot_feas + (size_t)b * p.S;
+    if (stg) {  // (p.S <= 512: the fp64 item holds two arrays of 509)
+        const int Sel = LY.S();
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int sl = g + 32 * t;
+            if (sl < Sel) {
+                stg[sl] = c[sl];
+                stg[p.S + sl] = f[sl];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        c = stg;
+        f = stg + p.S;
+    }
     double ci = 0.0, fi = 0.0;
     if (g < P) {
-        const int N = LY.N(g);
-        const double *c = d.slot_cost + (size_t)b * p.S + LY.s0(g), *f = d.slot_feas + (size_t)b * p.S + LY.s0(g);
+        const int N = LY.N(g), s0 = LY.s0(g);
 #pragma unroll 10
         for (int k = 0; k < N; ++k) {
-            ci += c[k];
-            fi += f[k];
+            ci += c[s0 + k];
+            fi += f[s0 + k];
         }
-        ci += c[N];
-        fi += f[N];
+        ci += c[s0 + N];
+        fi += f[s0 + N];
     }
     cost = 0.0; feas = 0.0;
     for (int i = 0; i < P; ++i) {
@@ -830,7 +848,12 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
     if (!__builtin_amdgcn_ballot_w64(act)) return;
     // the slot sums come from k_lq's pass: taken here, all lanes active
     double ecost, efeas;
-    element_cost<EL>(p, d, bv, L.lane, ecost, efeas);
+    {
+        // the slot values staged in this item's LDS (free until the sweep starts), two arrays of p.S
+        double *stg = 2 * (size_t)p.S * sizeof(double) <= sizeof(S.it[0]) ? reinterpret_cast<double *>(&S.it[L.e]) : nullptr;
+        element_cost<EL>(p, d, bv, L.lane, stg, ecost, efeas);
+        SSYNC();
+    }
     double reg = E.reg;
     Item<real> it;
     it.b = bv;
