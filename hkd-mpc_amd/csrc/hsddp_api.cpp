@@ -336,6 +336,8 @@ static void fill_params(hsddp_handle h)
     // (delta, eps) at its initial value (ConstraintsBase.h:168-183): the kernels then read the two
     // scalars instead of the per-knot arrays.
     p.reb_uniform = o.update_ReB == 1.0 && o.update_relax == 1.0 && p.grf_delta >= p.grf_delta_min;
+    p.grf_inv_delta = 1.0 / p.grf_delta;
+    p.grf_log_delta = std::log(p.grf_delta);
     // attempts of backward_sweep_regularized after the first, at most (from mu = 0: 1e-3, then
     // x update_regularization while <= 1e2); the parallel retry holds that many per deferred element
     int M = 0;

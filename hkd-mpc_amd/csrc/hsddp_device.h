@@ -143,7 +143,7 @@ DEV double running_cost(const Params &p, const int *c, const double *x, const do
         if constexpr (decltype(uniform)::value) {
             // uniform parameters (the default schedule): the rows with g > delta of one leg share one
             // log of their product (sum of -log g = -log of the product), the others the quadratic branch
-            const double dl = p.grf_delta, e = p.grf_eps, log_du = log(dl), inv_dl = 1.0 / dl;
+            const double dl = p.grf_delta, e = p.grf_eps, log_du = p.grf_log_delta, inv_dl = p.grf_inv_delta;
 #pragma unroll
             for (int lg = 0; lg < 4; ++lg) {
                 if (!c[lg]) continue;

@@ -78,6 +78,7 @@ struct Params {
     double cost_thresh, tconstr_thresh, pconstr_thresh, feas_thresh, merit_scale, merit_offset;
     int AL_active, ReB_active, no_early_exit;
     int reb_uniform;  // every ReB (delta, eps) equals (grf_delta, grf_eps): per-knot arrays not read
+    double grf_inv_delta, grf_log_delta;  // 1 / grf_delta, log(grf_delta): the uniform ReB terms' constants
     int lq_slots;     // k_lq recomputes the running costs and |Defect|^2 of the slots (0: the last
                       // rollout's values still hold for the working trajectory and the cost parameters)
     int fp32;         // fp32 Riccati mode (config C5): LQ records, sweep, gains and linear rollout in fp32

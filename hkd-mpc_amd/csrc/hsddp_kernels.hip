@@ -351,7 +351,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     // uniform case no per-row (delta, eps) load and no per-row 1 / delta division is issued
     auto reb = [&](auto uniform) {
         constexpr bool U = decltype(uniform)::value;
-        const double inv_du = 1.0 / p.grf_delta;
+        const double inv_du = p.grf_inv_delta;
 #pragma unroll
         for (int lg = 0; lg < 4; ++lg) {
             if (!c[lg]) continue;
