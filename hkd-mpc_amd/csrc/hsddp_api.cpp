@@ -213,6 +213,16 @@ struct hsddp_handle_t {
     hipStream_t stream = nullptr;
     int *host_counter = nullptr;                // [8]: k_count's activity counts, stat sums
     std::vector<hipEvent_t> events;             // the stats timer's pool (reused, destroyed with the handle)
+    // hsddp_solve's inner iteration + activity count as replayed hipGraphs (early-exit mode), keyed
+    // by the launch arguments they froze; a small cache so the receding-horizon tick's recurring
+    // layouts and swapped warm-start buffers find theirs again (round-robin eviction)
+    struct IterGraph {
+        hipGraphExec_t exec = nullptr;
+        Params p;
+        Bufs d;
+        double alpha = 0;
+    } iter_graph[8];
+    int iter_graph_next = 0;
     std::vector<void *> allocs;
     size_t bytes = 0;
     int Bref = 1;
@@ -491,6 +501,8 @@ extern "C" int hsddp_destroy(hsddp_handle h)
     if (h->hist) hipFree(h->hist);
     if (h->value0) hipFree(h->value0);
 
+    for (auto &g : h->iter_graph)
+        if (g.exec) hipGraphExecDestroy(g.exec);
     if (h->host_counter) hipHostFree(h->host_counter);
     for (hipEvent_t e : h->events) hipEventDestroy(e);
     if (h->stream) hipStreamDestroy(h->stream);
@@ -869,6 +881,61 @@ static void iteration_launches(hsddp_handle h, const std::vector<double> &trials
     h->slots_fresh = true;
 }
 
+// One early-exit inner iteration of hsddp_solve (MultiPhaseDDP.cpp:304-381 and the `n == 0` test)
+// replayed from a hipGraph: the ~15 launches, the count memset and the pinned read-back of the
+// activity count go to the device as one submission.  At B = 1 (BASELINE config 1) the iteration's
+// kernels are a few microseconds each and the host's per-launch cost was the critical path.  The
+// graph freezes the launch arguments (Params, Bufs, the step sizes): it is re-captured whenever
+// they differ from the ones it was built with.  The per-phase timers are not recorded in this mode
+// (hsddp_stats carries ms_total only); HSDDP_NO_GRAPH=1 restores launch-by-launch issue.
+static bool graphs_enabled()
+{
+    const char *e = std::getenv("HSDDP_NO_GRAPH");  // read per solve: a test switches it in-process
+    return !(e && *e && *e != '0');
+}
+
+static int graph_iteration(hsddp_handle h, const std::vector<double> &trials, int &n_active)
+{
+    Params pl = h->p;
+    pl.lq_slots = h->slots_fresh ? 0 : 1;
+    hsddp_handle_t::IterGraph *hit = nullptr;
+    for (auto &c : h->iter_graph)
+        if (c.exec && !std::memcmp(&c.p, &pl, sizeof(Params)) && !std::memcmp(&c.d, &h->d, sizeof(Bufs)) &&
+            c.alpha == h->opt.alpha)
+            hit = &c;
+    if (!hit) {
+        auto &g = h->iter_graph[h->iter_graph_next];
+        h->iter_graph_next = (h->iter_graph_next + 1) % 8;
+        if (g.exec) HIPCHK(hipGraphExecDestroy(g.exec));
+        g.exec = nullptr;
+        HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+        Timer off{h->stream, false, &h->events};
+        iteration_launches(h, trials, off);
+        hipError_t e = hipMemsetAsync(h->d.counter, 0, 4 * sizeof(int), h->stream);
+        launch_count(h->p, h->d, 1, h->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(h->host_counter, h->d.counter, 4 * sizeof(int), hipMemcpyDeviceToHost, h->stream);
+        hipGraph_t graph = nullptr;
+        const hipError_t ec = hipStreamEndCapture(h->stream, &graph);
+        if (e == hipSuccess) e = ec;
+        if (e == hipSuccess) e = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+        if (graph) hipGraphDestroy(graph);
+        if (e != hipSuccess) {
+            g.exec = nullptr;
+            return fail(HSDDP_ERR_DEVICE, std::string("iteration graph: ") + hipGetErrorString(e));
+        }
+        std::memcpy(&g.p, &pl, sizeof(Params));
+        std::memcpy(&g.d, &h->d, sizeof(Bufs));
+        g.alpha = h->opt.alpha;
+        hit = &g;
+    }
+    HIPCHK(hipGraphLaunch(hit->exec, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->slots_fresh = true;
+    n_active = h->host_counter[1];
+    return HSDDP_OK;
+}
+
 static void outer_end_launches(hsddp_handle h, Timer &tm)
 {
     hipEvent_t e0;
@@ -932,11 +999,21 @@ extern "C" int hsddp_solve(hsddp_handle h, hsddp_stats *stats)
     begin_launches(h);
     int iters = 0, outers = 0, nbwd = 0;
     const bool checks = !h->opt.no_early_exit;
+    const bool graph = checks && graphs_enabled();
     for (int ou = 0; ou < h->opt.max_AL_iter; ++ou) {
         tm.cut();
         launch_outer_begin(h->p, h->d, h->stream);
         outers++;
         for (int in = 0; in < h->opt.max_DDP_iter; ++in) {
+            if (graph) {
+                int n = 0;
+                tm.cut();
+                if ((rc = graph_iteration(h, trials, n))) return rc;
+                iters++;
+                nbwd++;
+                if (n == 0) break;
+                continue;
+            }
             iteration_launches(h, trials, tm);
             iters++;
             nbwd++;

@@ -1,0 +1,62 @@
+"""hsddp_solve's graph-replayed inner iteration (early-exit mode) against launch-by-launch issue.
+
+The graph freezes each launch's arguments at capture, so it must be re-captured whenever Params,
+the device buffers or the step sizes change; the results of both modes must be bit-identical
+(same kernels, same inputs, same order).  HSDDP_NO_GRAPH is read at every solve.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import hsddp
+from hsddp import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(prob, opt, graph, changes=()):
+    prev = os.environ.get("HSDDP_NO_GRAPH")
+    os.environ["HSDDP_NO_GRAPH"] = "0" if graph else "1"
+    try:
+        s = hsddp.Solver(prob, opt)
+        out = []
+        st = s.solve()
+        out.append(({**s.trajectory(), **s.element_info()}, st.inner_iterations))
+        for change in changes:  # a second solve on the same handle after a change
+            change(s)
+            st = s.solve()
+            out.append(({**s.trajectory(), **s.element_info()}, st.inner_iterations))
+        s.close()
+        return out
+    finally:
+        if prev is None:
+            os.environ.pop("HSDDP_NO_GRAPH", None)
+        else:
+            os.environ["HSDDP_NO_GRAPH"] = prev
+
+
+def _equal(a, b):
+    for (ga, ia), (gb, ib) in zip(a, b):
+        assert ia == ib
+        for f in ("Xbar", "Ubar", "cost", "iters", "outer_iters", "status", "n_ls_trials"):
+            assert np.array_equal(ga[f], gb[f]), f
+
+
+@pytest.mark.parametrize("B,P,N,gait", [(1, 1, 50, "trot"), (16, 8, 25, "jump"), (16, 4, 50, "trot")])
+def test_graph_solve_equals_launches(B, P, N, gait):
+    prob = syn.make_batch(B, P, N, gait)
+    opt = hsddp.load_settings()
+    prob2 = syn.make_batch(B, P, N, gait, seed=7)
+
+    def new_x0(s):  # same layout, new inputs: the graph is replayed as captured
+        s.upload_problem(prob2["contacts"], prob2["x0"], prob2["ref_x"], prob2["ref_u"], prob2["ref_foot"])
+
+    def new_alpha(s):  # other step sizes: the graph must be re-captured
+        o = hsddp.load_settings()
+        o.alpha = 0.5
+        s.set_options(o)
+        new_x0(s)
+
+    changes = (new_x0, new_alpha)
+    _equal(_solve(prob, opt, True, changes), _solve(prob, opt, False, changes))
