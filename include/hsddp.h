@@ -184,6 +184,10 @@ int hsddp_upload_problem(hsddp_handle h, const int *contacts, const double *x0, 
  * resets X = Xbar, U = Ubar, dX = 0 and the ReB/AL parameters to their initial values. */
 int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const double *Ubar, const double *K);
 
+/* MultiPhaseDDP::solve (MultiPhaseDDP.cpp:232-428) for every element.  With early exits on, each
+ * inner iteration is replayed from a cached hipGraph and stats carries ms_total but no per-phase
+ * times (ms_lq, ms_backward, ms_linear, ms_forward stay 0); the environment variable
+ * HSDDP_NO_GRAPH=1, read at every call, issues launch by launch with the per-phase timers. */
 int hsddp_solve(hsddp_handle h, hsddp_stats *stats);
 /* Split form of hsddp_solve for timing a fixed number of inner iterations (throughput mode):
  * begin = initial rollout + first outer prologue; iterate = n inner iterations of every active
