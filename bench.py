@@ -193,11 +193,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # the RCCL leg runs whenever this is a torch.distributed.run rank — world size 1 included, so a
+    # one-GPU box executes the same init / all_gather / gather path the N-GPU run takes
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
-        if world > 1:
+        if distributed:
             dist.barrier()
 
     B = args.batch
@@ -228,7 +231,7 @@ def main():
         cmd = torch.empty(B * hsddp.MPC_COMMAND.itemsize, dtype=torch.uint8, device=dev)
         solver.extract_commands_device(cmd.data_ptr())
     gather = {"summary_bytes_per_element": 48, "command_bytes_per_element": hsddp.MPC_COMMAND.itemsize if cmd is not None else 0}
-    if world > 1:
+    if distributed:
         allr = [torch.zeros_like(red) for _ in range(world)]
         dist.all_gather(allr, red)
         rank_ms = [float(r[0]) / args.steps * 1e3 for r in allr]
@@ -313,7 +316,7 @@ def main():
                                   "kernel_GBps": gbs}},
             "extra": {"batch_iterations_per_s": total_iters / elapsed / (B * world),
                       "mean_ls_trials": mean_ls, "device_ms_per_step": dms,
-                      "rank_ms_per_step": rank_ms, "rccl_world_size": world, "gathered_elements": gathered_rows,
+                      "rank_ms_per_step": rank_ms, "rccl_world_size": world if distributed else 0, "gathered_elements": gathered_rows,
                       "final_gather": gather,
                       "all_costs_finite": finite, "device_bytes": solver.device_bytes()},
         }
@@ -321,7 +324,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     solver.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -57,3 +57,24 @@ def test_two_rank_gpu_shards_equal_single_process(tmp_path):
     assert np.array_equal(np.load(tmp_path / "summ.npy"), shard.summary_rows(info))
     assert np.array_equal(np.load(tmp_path / "cmds.npy"), shard.command_bytes(cmds))  # device extraction, gathered
     assert np.array_equal(np.load(tmp_path / "xbar.npy"), tr["Xbar"])
+
+
+def test_bench_rccl_leg_world1():
+    """bench.py as a torch.distributed.run rank on the box's one GPU: RCCL (backend "nccl")
+    initialises, the timing all_gather and the final gather of summaries and command blocks
+    (HKDMPC.cpp:254-286) run through it, and rank 0's line reports the gathered shard."""
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.join(root, "bench.py"),
+           "--gpus", "1", "--batch", "256", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    import json
+    out = json.loads(line)
+    ex = out["extra"]
+    assert ex["rccl_world_size"] == 1
+    assert ex["gathered_elements"] == 256
+    assert ex["final_gather"]["commands_ok"] and "ms" in ex["final_gather"]
+    assert ex["all_costs_finite"]
