@@ -211,7 +211,7 @@ struct hsddp_handle_t {
     Params p;
     Bufs d;
     hipStream_t stream = nullptr;
-    int *host_counter = nullptr;                // [8]: k_count's activity counts, stat sums
+    int *host_counter = nullptr;                // [16]: k_count's activity counts, stat sums, the graphs' counts
     std::vector<hipEvent_t> events;             // the stats timer's pool (reused, destroyed with the handle)
     // hsddp_solve's inner iteration + activity count as replayed hipGraphs (early-exit mode), keyed
     // by the launch arguments they froze; a small cache so the receding-horizon tick's recurring
@@ -221,8 +221,10 @@ struct hsddp_handle_t {
         Params p;
         Bufs d;
         double alpha = 0;
+        int par = 0;  // which host count slot (host_counter[8 + 4 * par + 1]) its copy fills
     } iter_graph[8];
     int iter_graph_next = 0;
+    hipEvent_t iter_done[2] = {nullptr, nullptr};  // recorded after each replay, by parity
     std::vector<void *> allocs;
     size_t bytes = 0;
     int Bref = 1;
@@ -472,7 +474,7 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         }
     }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void **)&h->host_counter, 8 * sizeof(int), 0) != hipSuccess) {
+        hipHostMalloc((void **)&h->host_counter, 16 * sizeof(int), 0) != hipSuccess) {
         hsddp_destroy(h);
         return fail(HSDDP_ERR_DEVICE, "stream / pinned allocation failed");
     }
@@ -503,6 +505,8 @@ extern "C" int hsddp_destroy(hsddp_handle h)
 
     for (auto &g : h->iter_graph)
         if (g.exec) hipGraphExecDestroy(g.exec);
+    for (hipEvent_t e : h->iter_done)
+        if (e) hipEventDestroy(e);
     if (h->host_counter) hipHostFree(h->host_counter);
     for (hipEvent_t e : h->events) hipEventDestroy(e);
     if (h->stream) hipStreamDestroy(h->stream);
@@ -894,14 +898,14 @@ static bool graphs_enabled()
     return !(e && *e && *e != '0');
 }
 
-static int graph_iteration(hsddp_handle h, const std::vector<double> &trials, int &n_active)
+static int graph_launch(hsddp_handle h, const std::vector<double> &trials, int par)
 {
     Params pl = h->p;
     pl.lq_slots = h->slots_fresh ? 0 : 1;
     hsddp_handle_t::IterGraph *hit = nullptr;
     for (auto &c : h->iter_graph)
-        if (c.exec && !std::memcmp(&c.p, &pl, sizeof(Params)) && !std::memcmp(&c.d, &h->d, sizeof(Bufs)) &&
-            c.alpha == h->opt.alpha)
+        if (c.exec && c.par == par && !std::memcmp(&c.p, &pl, sizeof(Params)) &&
+            !std::memcmp(&c.d, &h->d, sizeof(Bufs)) && c.alpha == h->opt.alpha)
             hit = &c;
     if (!hit) {
         auto &g = h->iter_graph[h->iter_graph_next];
@@ -914,7 +918,8 @@ static int graph_iteration(hsddp_handle h, const std::vector<double> &trials, in
         hipError_t e = hipMemsetAsync(h->d.counter, 0, 4 * sizeof(int), h->stream);
         launch_count(h->p, h->d, 1, h->stream);
         if (e == hipSuccess)
-            e = hipMemcpyAsync(h->host_counter, h->d.counter, 4 * sizeof(int), hipMemcpyDeviceToHost, h->stream);
+            e = hipMemcpyAsync(h->host_counter + 8 + 4 * par, h->d.counter, 4 * sizeof(int), hipMemcpyDeviceToHost,
+                               h->stream);
         hipGraph_t graph = nullptr;
         const hipError_t ec = hipStreamEndCapture(h->stream, &graph);
         if (e == hipSuccess) e = ec;
@@ -927,12 +932,20 @@ static int graph_iteration(hsddp_handle h, const std::vector<double> &trials, in
         std::memcpy(&g.p, &pl, sizeof(Params));
         std::memcpy(&g.d, &h->d, sizeof(Bufs));
         g.alpha = h->opt.alpha;
+        g.par = par;
         hit = &g;
     }
+    if (!h->iter_done[par]) HIPCHK(hipEventCreateWithFlags(&h->iter_done[par], hipEventDisableTiming));
     HIPCHK(hipGraphLaunch(hit->exec, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipEventRecord(h->iter_done[par], h->stream));
     h->slots_fresh = true;
-    n_active = h->host_counter[1];
+    return HSDDP_OK;
+}
+
+static int graph_wait(hsddp_handle h, int par, int &n_active)
+{
+    HIPCHK(hipEventSynchronize(h->iter_done[par]));
+    n_active = h->host_counter[8 + 4 * par + 1];
     return HSDDP_OK;
 }
 
@@ -1006,9 +1019,16 @@ extern "C" int hsddp_solve(hsddp_handle h, hsddp_stats *stats)
         outers++;
         for (int in = 0; in < h->opt.max_DDP_iter; ++in) {
             if (graph) {
+                // iteration `in` was launched by the step before (or here, for the first); the next
+                // one is queued before waiting for this one's count, so the GPU never waits on the
+                // host's round trip.  When the count comes back 0 the queued iteration finds every
+                // element inner_done / done and returns at once (the kernels' own early exits), as
+                // the reference's loop would not have run it; it is never queued past max_DDP_iter.
                 int n = 0;
                 tm.cut();
-                if ((rc = graph_iteration(h, trials, n))) return rc;
+                if (in == 0 && (rc = graph_launch(h, trials, 0))) return rc;
+                if (in + 1 < h->opt.max_DDP_iter && (rc = graph_launch(h, trials, (in + 1) & 1))) return rc;
+                if ((rc = graph_wait(h, in & 1, n))) return rc;
                 iters++;
                 nbwd++;
                 if (n == 0) break;
