@@ -886,7 +886,7 @@ static void iteration_launches(hsddp_handle h, const std::vector<double> &trials
 }
 
 // One early-exit inner iteration of hsddp_solve (MultiPhaseDDP.cpp:304-381 and the `n == 0` test)
-// replayed from a hipGraph: the ~15 launches, the count memset and the pinned read-back of the
+// replayed from a hipGraph: the ~15 launches, the count kernel and the pinned read-back of the
 // activity count go to the device as one submission.  At B = 1 (BASELINE config 1) the iteration's
 // kernels are a few microseconds each and the host's per-launch cost was the critical path.  The
 // graph freezes the launch arguments (Params, Bufs, the step sizes): it is re-captured whenever
@@ -915,10 +915,8 @@ static int graph_launch(hsddp_handle h, const std::vector<double> &trials, int p
         HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
         Timer off{h->stream, false, &h->events};
         iteration_launches(h, trials, off);
-        hipError_t e = hipMemsetAsync(h->d.counter, 0, 4 * sizeof(int), h->stream);
-        launch_count(h->p, h->d, 1, h->stream);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(h->host_counter + 8 + 4 * par, h->d.counter, 4 * sizeof(int), hipMemcpyDeviceToHost,
+        launch_count(h->p, h->d, 1, h->stream);  // (k_lq's first terminal task zeroed the counts)
+        hipError_t e = hipMemcpyAsync(h->host_counter + 8 + 4 * par, h->d.counter, 4 * sizeof(int), hipMemcpyDeviceToHost,
                                h->stream);
         hipGraph_t graph = nullptr;
         const hipError_t ec = hipStreamEndCapture(h->stream, &graph);

@@ -260,6 +260,9 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
         // and no element has been seen searching after any trial of this iteration yet
         if (task == 0)
             for (int t = lane; t < LS_LIVE; t += 64) d.ls_live[t] = 0;
+        // k_count's activity counts at the end of this iteration start from zero (the
+        // graph-replayed iteration of hsddp_solve has no memset launch before k_count)
+        if (task == 0 && lane < 4) d.counter[lane] = 0;
         if (task < (long)p.B * p.P) terminal_task<EL>(p, d, reinterpret_cast<TermLds *>(lds)[w], (int)task, lane);
         return;
     }
