@@ -206,6 +206,9 @@ struct hsddp_handle_t {
     // the slot costs / |Defect|^2 of the last rollout (k_rollout's per-slot outputs) belong to the
     // working trajectory under the current cost parameters: k_lq need not recompute them
     bool slots_fresh = false;
+    // every per-knot ReB (delta, eps) still equals the descriptor's initial pair, so the kernels may
+    // read the two scalars (Params::reb_uniform) when the schedule keeps them there
+    bool reb_at_init = true;
     hsddp_problem_desc desc;
     hsddp_options opt;
     Params p;
@@ -240,6 +243,9 @@ struct hsddp_handle_t {
     size_t S_cap = 0;
     double *spare_Xbar = nullptr, *spare_Ubar = nullptr;
     void *spare_K = nullptr;
+    // ... and of the constraint parameters the phases carry (ReB per knot, touchdown constraints)
+    double *spare_reb_delta = nullptr, *spare_reb_eps = nullptr, *spare_al_sigma = nullptr, *spare_al_lambda = nullptr;
+    int *spare_td_mask = nullptr;
     bool need_inputs = false;   // a shift changed the layout: update_problem before solving
     double *ref_table = nullptr;  // reference samples [n][RT_W] (hsddp_set_reference_table)
     int ref_n = 0;
@@ -347,7 +353,7 @@ static void fill_params(hsddp_handle h)
     // With update_ReB = update_relax = 1 (the shipped settings) update_REB_params leaves every
     // (delta, eps) at its initial value (ConstraintsBase.h:168-183): the kernels then read the two
     // scalars instead of the per-knot arrays.
-    p.reb_uniform = o.update_ReB == 1.0 && o.update_relax == 1.0 && p.grf_delta >= p.grf_delta_min;
+    p.reb_uniform = o.update_ReB == 1.0 && o.update_relax == 1.0 && p.grf_delta >= p.grf_delta_min && h->reb_at_init;
     p.grf_inv_delta = 1.0 / p.grf_delta;
     p.grf_log_delta = std::log(p.grf_delta);
     // attempts of backward_sweep_regularized after the first, at most (from mu = 0: 1e-3, then
@@ -436,8 +442,9 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
                    (rc = dalloc(h, d.def32, B * S * NX)))
                 : ((rc = dalloc(h, d.K, B * Kc * KCW)) || (rc = dalloc(h, d.lq, B * Kc * LQW)))) ||
         (rc = dalloc(h, d.term, B * P * TW)) || (rc = dalloc(h, d.reb_delta, B * Kc * 20)) ||
-        (rc = dalloc(h, d.reb_eps, B * Kc * 20)) || (rc = dalloc(h, d.al_sigma, B * P * 4)) ||
-        (rc = dalloc(h, d.al_lambda, B * P * 4)) || (rc = dalloc(h, d.term_h, B * P * 4)) ||
+        (rc = dalloc(h, d.reb_eps, B * Kc * 20)) || (rc = dalloc(h, d.al_sigma, B * P * MTD * 4)) ||
+        (rc = dalloc(h, d.al_lambda, B * P * MTD * 4)) || (rc = dalloc(h, d.td_mask, B * P * MTD)) ||
+        (rc = dalloc(h, d.term_h, B * P * 4)) ||
         (rc = dalloc(h, d.slot_cost, B * S)) || (rc = dalloc(h, d.slot_feas, B * S)) || (rc = dalloc(h, d.slot_viol, B * S)) ||
         (rc = dalloc(h, d.slot_div, B * S)) || (rc = dalloc(h, d.el, B)) || (rc = dalloc(h, d.counter, 8)) || (rc = dalloc(h, d.ls_live, LS_LIVE)) ||
         (rc = dalloc(h, (Layout *&)d.lay, B)) || (rc = dalloc(h, (int *&)d.pairs, 2 * B + 2))) {
@@ -703,6 +710,8 @@ extern "C" int hsddp_upload_problem(hsddp_handle h, const int *contacts, const d
     return hsddp_upload_warm_start(h, nullptr, nullptr, nullptr);
 }
 
+static int reset_working(hsddp_handle h, bool params);
+
 extern "C" int hsddp_update_problem(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
                                     const double *ref_u, const double *ref_foot)
 {
@@ -711,9 +720,38 @@ extern "C" int hsddp_update_problem(hsddp_handle h, const int *contacts, const d
     int rc = upload_inputs(h, contacts, x0, ref_x, ref_u, ref_foot);
     if (rc) return rc;
     h->need_inputs = false;
-    // keeps Xbar / Ubar / K; resets X, U, dX, the ReB / AL parameters (reset_params,
-    // HKDProblem.cpp:209) and the per-element solver state
-    return hsddp_upload_warm_start(h, nullptr, nullptr, nullptr);
+    // keeps Xbar / Ubar / K and the constraint parameters (HKDProblem::update's reset_params is a
+    // no-op, ConstraintsBase.h:165-167,341-348: the ReB / AL parameters carry over to the next
+    // tick); resets X, U, dX and the per-element solver state; touchdown constraints added by the
+    // shift take their legs from the new contact rows
+    return reset_working(h, false);
+}
+
+// the working trajectory restarts at the warm start (X = Xbar, U = Ubar, dX = du = dU = Defect = 0,
+// per-element solver state cleared); params: the ReB / AL parameters and touchdown constraints
+// return to their initial values (a new problem) — else they are kept.  Pending touchdown masks
+// are resolved from the contact rows either way.
+static int reset_working(hsddp_handle h, bool params)
+{
+    const Params &p = h->p;
+    const size_t B = p.B, S = p.S, Kc = p.Kc;
+    Bufs &d = h->d;
+    launch_normalize(p, d, h->stream);
+    HIPCHK(hipMemsetAsync(d.sel, 0, B * sizeof(int), h->stream));  // X = Xbar, U = Ubar: one buffer
+    HIPCHK(hipMemsetAsync(d.dX, 0, B * S * NX * sizeof(double), h->stream));
+    HIPCHK(hipMemsetAsync(d.du, 0, B * Kc * NX * sizeof(double), h->stream));
+    HIPCHK(hipMemsetAsync(d.dU, 0, B * Kc * NX * sizeof(double), h->stream));
+    HIPCHK(hipMemsetAsync(d.Defect, 0, B * S * NX * sizeof(double), h->stream));
+    if (params) {
+        launch_init_params(p, d, h->stream);
+        h->reb_at_init = true;
+        fill_params(h);
+    }
+    launch_resolve_td(p, d, h->stream);
+    launch_reset_elements(p, d, h->stream);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->slots_fresh = false;
+    return HSDDP_OK;
 }
 
 extern "C" int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const double *Ubar, const double *K)
@@ -746,14 +784,57 @@ extern "C" int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const
         }
         HIPCHK(hipStreamSynchronize(h->stream));
     }
-    HIPCHK(hipMemsetAsync(d.sel, 0, B * sizeof(int), h->stream));  // X = Xbar, U = Ubar: one buffer
-    HIPCHK(hipMemsetAsync(d.dX, 0, B * S * NX * sizeof(double), h->stream));
-    HIPCHK(hipMemsetAsync(d.du, 0, B * Kc * NX * sizeof(double), h->stream));
-    HIPCHK(hipMemsetAsync(d.dU, 0, B * Kc * NX * sizeof(double), h->stream));
-    HIPCHK(hipMemsetAsync(d.Defect, 0, B * S * NX * sizeof(double), h->stream));
-    launch_init_params(p, d, h->stream);
-    launch_reset_elements(p, d, h->stream);
+    return reset_working(h, true);
+}
+
+static_assert(MTD == HSDDP_MAX_TD, "touchdown constraint slots");
+
+extern "C" int hsddp_upload_constraint_params(hsddp_handle h, const double *reb_delta, const double *reb_eps,
+                                              const int *td_legs, const double *al_sigma, const double *al_lambda)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
+    const Params &p = h->p;
+    const size_t nr = (size_t)p.B * p.Kc * 20, nt = (size_t)p.B * p.P * MTD;
+    if (td_legs)
+        for (size_t q = 0; q < nt; ++q)
+            if (td_legs[q] < 0 || td_legs[q] > 15) return fail(HSDDP_ERR_ARG, "td_legs entries are 4-bit leg masks");
+    HIPCHK(hipSetDevice(h->desc.device));
+    const Bufs &d = h->d;
+    int rc;
+    if ((reb_delta && (rc = h2d(d.reb_delta, reb_delta, nr * sizeof(double), h->stream))) ||
+        (reb_eps && (rc = h2d(d.reb_eps, reb_eps, nr * sizeof(double), h->stream))) ||
+        (td_legs && (rc = h2d(d.td_mask, td_legs, nt * sizeof(int), h->stream))) ||
+        (al_sigma && (rc = h2d(d.al_sigma, al_sigma, nt * 4 * sizeof(double), h->stream))) ||
+        (al_lambda && (rc = h2d(d.al_lambda, al_lambda, nt * 4 * sizeof(double), h->stream))))
+        return rc;
     HIPCHK(hipStreamSynchronize(h->stream));
+    if (reb_delta || reb_eps) {  // the uniform-ReB shortcut holds only while every knot has the initial pair
+        bool at = true;
+        for (size_t q = 0; q < nr && at; ++q)
+            at = (!reb_delta || reb_delta[q] == p.grf_delta) && (!reb_eps || reb_eps[q] == p.grf_eps);
+        h->reb_at_init = at && h->reb_at_init;
+        if (at && reb_delta && reb_eps) h->reb_at_init = true;
+        fill_params(h);
+    }
+    h->slots_fresh = false;  // the running / terminal costs change with the parameters
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_download_constraint_params(hsddp_handle h, double *reb_delta, double *reb_eps, int *td_legs,
+                                                double *al_sigma, double *al_lambda)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    const Params &p = h->p;
+    const size_t nr = (size_t)p.B * p.Kc * 20, nt = (size_t)p.B * p.P * MTD;
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const Bufs &d = h->d;
+    if (reb_delta) HIPCHK(hipMemcpy(reb_delta, d.reb_delta, nr * sizeof(double), hipMemcpyDeviceToHost));
+    if (reb_eps) HIPCHK(hipMemcpy(reb_eps, d.reb_eps, nr * sizeof(double), hipMemcpyDeviceToHost));
+    if (td_legs) HIPCHK(hipMemcpy(td_legs, d.td_mask, nt * sizeof(int), hipMemcpyDeviceToHost));
+    if (al_sigma) HIPCHK(hipMemcpy(al_sigma, d.al_sigma, nt * 4 * sizeof(double), hipMemcpyDeviceToHost));
+    if (al_lambda) HIPCHK(hipMemcpy(al_lambda, d.al_lambda, nt * 4 * sizeof(double), hipMemcpyDeviceToHost));
     return HSDDP_OK;
 }
 
@@ -910,7 +991,12 @@ static int graph_launch(hsddp_handle h, const std::vector<double> &trials, int p
     if (!hit) {
         auto &g = h->iter_graph[h->iter_graph_next];
         h->iter_graph_next = (h->iter_graph_next + 1) % 8;
-        if (g.exec) HIPCHK(hipGraphExecDestroy(g.exec));
+        if (g.exec) {
+            // the victim may be the iteration queued last (still on the stream): drain the stream
+            // before its exec goes away (evictions are rare: 8 keys cover an MPC tick's recurring ones)
+            HIPCHK(hipStreamSynchronize(h->stream));
+            HIPCHK(hipGraphExecDestroy(g.exec));
+        }
         g.exec = nullptr;
         HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
         Timer off{h->stream, false, &h->events};
@@ -952,7 +1038,10 @@ static void outer_end_launches(hsddp_handle h, Timer &tm)
     hipEvent_t e0;
     tm.begin(3, e0);
     // update_REB_params moves per-knot (delta, eps) unless they stay uniform: the running costs change
-    if (h->opt.ReB_active && !h->p.reb_uniform) h->slots_fresh = false;
+    if (h->opt.ReB_active && !h->p.reb_uniform) {
+        h->slots_fresh = false;
+        h->reb_at_init = false;
+    }
     if (h->opt.ReB_active) launch_reb_update(h->p, h->d, h->stream);
     launch_outer_end(h->p, h->d, h->stream);
     tm.end(3, e0);
@@ -1578,6 +1667,9 @@ namespace {
 struct ShiftPhase {
     int N, ss, reach;
     std::vector<int> xs, us;
+    int src = -1;         // the old phase it continues (-1: added by this shift)
+    int add = 0;          // touchdown constraints appended by this shift (add_tconstr_one_phase)
+    std::vector<int> rs;  // per control slot: the old slot its ReB parameters come from (-1: initial)
 };
 }  // namespace
 
@@ -1590,8 +1682,10 @@ static int shift_phases(const Layout &L, const int *reach, int n_steps, const in
     ph.assign(L.P, ShiftPhase{});
     for (int i = 0; i < L.P; ++i) {
         ph[i].N = L.N[i]; ph[i].ss = L.ss[i]; ph[i].reach = reach[i];
+        ph[i].src = i;
         for (int k = 0; k <= L.N[i]; ++k) ph[i].xs.push_back(L.s0[i] + k);
         for (int k = 0; k < L.N[i]; ++k) ph[i].us.push_back(L.k0[i] + k);
+        ph[i].rs = ph[i].us;
     }
     for (int j = 0; j < n_steps; ++j) {
         const int change = cc[(size_t)j * cstride];
@@ -1605,6 +1699,7 @@ static int shift_phases(const Layout &L, const int *reach, int n_steps, const in
             ShiftPhase &f = ph.front();
             f.xs.erase(f.xs.begin());
             f.us.erase(f.us.begin());
+            f.rs.erase(f.rs.begin());
             f.N--;
         }
         // back: a contact change after the last phase reached its end starts a new phase of one
@@ -1618,14 +1713,19 @@ static int shift_phases(const Layout &L, const int *reach, int n_steps, const in
             n.N = 1; n.ss = 0; n.reach = 0;
             n.xs = {-1, -1};
             n.us = {-1};
+            n.rs = {-1};  // a new GRF constraint: initial ReB parameters (HKDProblem.cpp:255-263)
             ph.push_back(n);
         } else {
             const int last = l.xs.back();
             l.xs.push_back(last >= 0 ? -2 - last : last);
             l.us.push_back(-1);
+            l.rs.push_back(l.rs.back());  // PathConstraintBase::push_back copies params.back()
             l.N++;
             if (change) l.reach = 1;
         }
+        // add_tconstr_one_phase on a last phase that has reached its end, at every step
+        // (HKDProblem.cpp:199-202): one more touchdown constraint with initial AL parameters
+        if (ph.back().reach) ph.back().add++;
     }
     // update_SS_config after the steps (HKDProblem.cpp:203-217): every phase but a last one of
     // horizon <= 2 gets all its states as shooting states
@@ -1642,10 +1742,10 @@ static int shift_phases(const Layout &L, const int *reach, int n_steps, const in
 // element ends on one layout the handle keeps (or returns to) the shared layout.
 static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride, size_t sstride)
 {
-    h->slots_fresh = false;
     if (!h || (n_steps > 0 && !cc)) return fail(HSDDP_ERR_ARG, "null argument");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     if (n_steps < 0) return fail(HSDDP_ERR_ARG, "n_steps must be >= 0");
+    h->slots_fresh = false;
     Params &p = h->p;
     const size_t B = p.B;
     const bool elem = !h->lays.empty();
@@ -1692,13 +1792,19 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
         Snew = std::max(Snew, s);
         Pnew = std::max(Pnew, L.P);
     }
-    // slot maps [nk][Snew] (padding rows: zero) and [nk][Kc]
-    std::vector<int> smap((size_t)nk * Snew, -1), cmap((size_t)nk * p.Kc);
+    // slot maps [nk][Snew] (padding rows: zero) and [nk][Kc]; constraint-parameter maps: ReB source
+    // per control slot [nk][Kc], phase source and appended touchdown constraints [nk][16]
+    std::vector<int> smap((size_t)nk * Snew, -1), cmap((size_t)nk * p.Kc), rmap((size_t)nk * p.Kc);
+    std::vector<int> pmap((size_t)nk * HSDDP_MAX_PHASES, -1), nadd((size_t)nk * HSDDP_MAX_PHASES, 0);
     for (int q = 0; q < nk; ++q) {
-        size_t s = 0, k = 0;
-        for (auto &f : phs[q]) {
+        size_t s = 0, k = 0, r = 0;
+        for (size_t i = 0; i < phs[q].size(); ++i) {
+            const auto &f = phs[q][i];
             for (int v : f.xs) smap[(size_t)q * Snew + s++] = v;
             for (int v : f.us) cmap[(size_t)q * p.Kc + k++] = v;
+            for (int v : f.rs) rmap[(size_t)q * p.Kc + r++] = v;
+            pmap[(size_t)q * HSDDP_MAX_PHASES + i] = f.src;
+            nadd[(size_t)q * HSDDP_MAX_PHASES + i] = f.add;
         }
     }
     HIPCHK(hipSetDevice(h->desc.device));
@@ -1712,13 +1818,36 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
         else { double *k64; if ((rc = dalloc(h, k64, B * p.Kc * KCW))) return rc; sk = k64; }
         h->spare_Xbar = sx; h->spare_Ubar = su; h->spare_K = sk;
     }
+    if (!h->spare_reb_delta) {
+        if ((rc = dalloc(h, h->spare_reb_delta, B * p.Kc * 20)) || (rc = dalloc(h, h->spare_reb_eps, B * p.Kc * 20)) ||
+            (rc = dalloc(h, h->spare_al_sigma, B * HSDDP_MAX_PHASES * MTD * 4)) ||
+            (rc = dalloc(h, h->spare_al_lambda, B * HSDDP_MAX_PHASES * MTD * 4)) ||
+            (rc = dalloc(h, h->spare_td_mask, B * HSDDP_MAX_PHASES * MTD)))
+            return rc;
+    }
     char *buf;
-    if ((rc = scratch(h, (smap.size() + cmap.size() + (nk > 1 ? B : 0)) * sizeof(int), &buf))) return rc;
-    int *dsm = (int *)buf, *dcm = dsm + smap.size(), *did = dcm + cmap.size();
+    const size_t nmaps = smap.size() + cmap.size() + rmap.size() + pmap.size() + nadd.size();
+    if ((rc = scratch(h, (nmaps + (nk > 1 ? B : 0)) * sizeof(int), &buf))) return rc;
+    int *dsm = (int *)buf, *dcm = dsm + smap.size(), *drm = dcm + cmap.size(), *dpm = drm + rmap.size(),
+        *dna = dpm + pmap.size(), *did = dna + nadd.size();
     if ((rc = h2d(dsm, smap.data(), smap.size() * sizeof(int), h->stream)) ||
         (rc = h2d(dcm, cmap.data(), cmap.size() * sizeof(int), h->stream)) ||
+        (rc = h2d(drm, rmap.data(), rmap.size() * sizeof(int), h->stream)) ||
+        (rc = h2d(dpm, pmap.data(), pmap.size() * sizeof(int), h->stream)) ||
+        (rc = h2d(dna, nadd.data(), nadd.size() * sizeof(int), h->stream)) ||
         (nk > 1 && (rc = h2d(did, map_id.data(), B * sizeof(int), h->stream))))
         return rc;
+    // the constraint parameters first (they read the old layout's strides)
+    ShiftParamArgs pa;
+    pa.Kc = p.Kc; pa.P_old = p.P; pa.P_new = Pnew;
+    pa.rmap = drm; pa.pmap = dpm; pa.nadd = dna;
+    pa.map_id = nk > 1 ? did : nullptr;
+    pa.reb_delta0 = p.grf_delta; pa.reb_eps0 = p.grf_eps; pa.td_sigma0 = p.td_sigma; pa.td_lambda0 = p.td_lambda;
+    pa.overflow = d.counter + 6;
+    HIPCHK(hipMemsetAsync(d.counter + 6, 0, sizeof(int), h->stream));
+    launch_shift_params(p.B, pa, d, h->spare_reb_delta, h->spare_reb_eps, h->spare_al_sigma, h->spare_al_lambda,
+                        h->spare_td_mask, h->stream);
+    HIPCHK(hipMemcpyAsync(h->host_counter + 6, d.counter + 6, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     ShiftArgs a;
     a.S_old = p.S; a.S_new = Snew; a.Kc = p.Kc;
     a.smap = dsm; a.cmap = dcm;
@@ -1730,6 +1859,12 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     HIPCHK(hipStreamSynchronize(h->stream));
     std::swap(d.Xb[0], h->spare_Xbar);
     std::swap(d.Ub[0], h->spare_Ubar);
+    std::swap(d.reb_delta, h->spare_reb_delta);
+    std::swap(d.reb_eps, h->spare_reb_eps);
+    std::swap(d.al_sigma, h->spare_al_sigma);
+    std::swap(d.al_lambda, h->spare_al_lambda);
+    std::swap(d.td_mask, h->spare_td_mask);
+    const bool td_overflow = h->host_counter[6] != 0;
     HIPCHK(hipMemset(d.sel, 0, B * sizeof(int)));  // the gathered warm start is buffer 0's
     if (p.fp32) { float *t = d.K32; d.K32 = (float *)h->spare_K; h->spare_K = t; }
     else { double *t = d.K; d.K = (double *)h->spare_K; h->spare_K = t; }
@@ -1762,6 +1897,8 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     h->need_inputs = true;
     h->refs_on_device = false;  // built for the old layout
     h->contacts_current = false;
+    if (td_overflow)  // the shift itself is complete; the constraints past HSDDP_MAX_TD were not added
+        return fail(HSDDP_ERR_UNSUPPORTED, "a phase would carry more than HSDDP_MAX_TD touchdown constraints");
     return HSDDP_OK;
 }
 
@@ -1786,6 +1923,59 @@ extern "C" int hsddp_get_layout(hsddp_handle h, int *n_phases, int *horizons, in
         if (shooting) shooting[i] = p.ss[i];
         if (reach_end) reach_end[i] = h->reach_end[i];
     }
+    return HSDDP_OK;
+}
+
+// The caller's own receding-horizon bookkeeping applied to a live handle (the C++ facade's
+// MultiPhaseDDP after HKDProblem::update, HKDProblem.cpp:117-222): a new shared layout of the same
+// Kc, with each phase's shooting states SS_set = {0 .. shooting[i] - 1} (SinglePhase.h:161-164).
+// Host only; the inputs and warm start of the new layout are uploaded next.
+extern "C" int hsddp_set_layout(hsddp_handle h, int n_phases, const int *horizons, const int *shooting,
+                                const int *reach_end)
+{
+    if (!h || !horizons) return fail(HSDDP_ERR_ARG, "null argument");
+    if (n_phases < 1 || n_phases > HSDDP_MAX_PHASES) return fail(HSDDP_ERR_ARG, "n_phases must lie in 1..16");
+    Params &p = h->p;
+    int s = 0, k = 0, tail = 0;
+    for (int i = 0; i < n_phases; ++i) {
+        const int N = horizons[i], ss = shooting ? shooting[i] : N + 1;
+        if (N < 1) return fail(HSDDP_ERR_ARG, "phase horizons must be >= 1");
+        if (ss < 0 || ss > N + 1) return fail(HSDDP_ERR_ARG, "shooting states must lie in 0 .. N_i + 1");
+        // the knot-parallel rollout simulates non-shooting states after the shooting ones, and only
+        // in the last phase (the one HKDProblem::update leaves with horizon <= 2)
+        if (ss < N + 1 && i < n_phases - 1)
+            return fail(HSDDP_ERR_UNSUPPORTED, "non-shooting states outside the last phase");
+        tail |= ss < N + 1;
+        s += N + 1;
+        k += N;
+    }
+    if (k != p.Kc) return fail(HSDDP_ERR_ARG, "the layout's horizons must sum to the handle's Kc");
+    if ((size_t)s > h->S_cap) return fail(HSDDP_ERR_ARG, "layout exceeds the handle's state-slot capacity");
+    h->slots_fresh = false;
+    s = k = 0;
+    for (int i = 0; i < HSDDP_MAX_PHASES; ++i) {
+        const bool in = i < n_phases;
+        p.N[i] = in ? horizons[i] : 0;
+        p.s0[i] = in ? s : 0;
+        p.k0[i] = in ? k : 0;
+        p.ss[i] = in ? (shooting ? shooting[i] : horizons[i] + 1) : 0;
+        if (in) { s += horizons[i] + 1; k += horizons[i]; }
+    }
+    p.P = n_phases;
+    p.S = s;
+    p.has_tail = tail;
+    p.elem_layout = 0;
+    h->lays.clear();
+    h->reach_el.clear();
+    h->reach_end.assign(n_phases, 0);
+    if (reach_end)
+        for (int i = 0; i < n_phases; ++i) h->reach_end[i] = reach_end[i] ? 1 : 0;
+    h->desc.n_phases = n_phases;
+    for (int i = 0; i < HSDDP_MAX_PHASES; ++i) h->desc.horizons[i] = i < n_phases ? horizons[i] : 0;
+    h->have_problem = false;  // inputs of the new layout next (hsddp_upload_problem)
+    h->need_inputs = false;
+    h->contacts_current = false;
+    h->refs_on_device = false;
     return HSDDP_OK;
 }
 

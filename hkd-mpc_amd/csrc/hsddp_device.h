@@ -178,10 +178,30 @@ DEV double running_cost(const Params &p, const int *c, const double *x, const do
     return l;
 }
 
-// terminal cost Phi (tracking Qf + 10 * foot + AL) from the touchdown legs' foot heights h[l]
-// (hkd_foot_height_grad - ground; any value for other legs), and max |h|
-DEV double terminal_cost_h(const Params &p, const int *c, const int *cn, const double *x, const double *xr,
-                           const double *pf, const double *sig, const double *lam, const double *hl, double &tviol)
+// the legs of the phase's touchdown constraints (union of the slot masks; TD_PENDING slots are
+// resolved before any solve)
+DEV unsigned td_union(const int *mask)
+{
+    unsigned u = 0;
+#pragma unroll
+    for (int j = 0; j < MTD; ++j) u |= (unsigned)mask[j];
+    return u & 15u;
+}
+// the touchdown legs from contact c to cn as a mask (add_tconstr_one_phase, HKDProblem.cpp:270-276)
+DEV int td_bits(const int *c, const int *cn)
+{
+    int m = 0;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) m |= touchdown(c, cn, l) ? 1 << l : 0;
+    return m;
+}
+
+// terminal cost Phi (tracking Qf + 10 * foot + AL) from the constraint legs' foot heights h[l]
+// (hkd_foot_height_grad - ground; any value for other legs), and max |h|.  The AL terms are
+// summed per touchdown constraint (slot j: legs mask[j], parameters sig / lam [j][4]) and added
+// constraint by constraint, as update_terminal_cost_with_tconstr (SinglePhase.cpp:402-411).
+DEV double terminal_cost_h(const Params &p, const int *c, const double *x, const double *xr, const double *pf,
+                           const int *mask, const double *sig, const double *lam, const double *hl, double &tviol)
 {
     double phi = 0.0, fc = 0.0;
 #pragma unroll
@@ -196,27 +216,33 @@ DEV double terminal_cost_h(const Params &p, const int *c, const int *cn, const d
         fc += e * foot_weight(p, c, j) * e;
     }
     phi = phi + p.foot_term_cost * fc;
-    double al = 0.0, tv = 0.0;
+    double tv = 0.0;
+    for (int q = 0; q < MTD; ++q) {
+        const int m = mask[q];
+        if (!m) continue;
+        double al = 0.0;
 #pragma unroll
-    for (int l = 0; l < 4; ++l) {
-        if (!touchdown(c, cn, l)) continue;
-        const double h = hl[l];
-        tv = fmax(tv, fabs(h));
-        al += 0.5 * sig[l] * h * h;
-        al += lam[l] * h;
+        for (int l = 0; l < 4; ++l) {
+            if (!((m >> l) & 1)) continue;
+            const double h = hl[l];
+            tv = fmax(tv, fabs(h));
+            al += 0.5 * sig[4 * q + l] * h * h;
+            al += lam[4 * q + l] * h;
+        }
+        if (p.AL_active) phi += al;
     }
-    if (p.AL_active) phi += al;
     tviol = tv;
     return phi;
 }
 
-// terminal cost Phi (tracking Qf + 10 * foot + AL), max |h| and h per touchdown leg
-DEV double terminal_cost(const Params &p, const int *c, const int *cn, const double *x, const double *xr,
-                         const double *pf, const double *sig, const double *lam, double &tviol, double *h_out)
+// terminal cost Phi (tracking Qf + 10 * foot + AL), max |h| and h per constraint leg
+DEV double terminal_cost(const Params &p, const int *c, const double *x, const double *xr, const double *pf,
+                         const int *mask, const double *sig, const double *lam, double &tviol, double *h_out)
 {
+    const unsigned u = td_union(mask);
 #pragma unroll
-    for (int l = 0; l < 4; ++l) h_out[l] = touchdown(c, cn, l) ? hkd_foot_height_grad(l, x, nullptr) - p.ground : 0.0;
-    return terminal_cost_h(p, c, cn, x, xr, pf, sig, lam, h_out, tviol);
+    for (int l = 0; l < 4; ++l) h_out[l] = ((u >> l) & 1) ? hkd_foot_height_grad(l, x, nullptr) - p.ground : 0.0;
+    return terminal_cost_h(p, c, x, xr, pf, mask, sig, lam, h_out, tviol);
 }
 
 

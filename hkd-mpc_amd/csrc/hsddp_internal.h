@@ -7,7 +7,9 @@
 //   lq                                [B][Kc][LQW]    compact LQ model of one knot (below)
 //   term                              [B][P][TW]      Phix | Phixx | Px (reset-map Jacobian at X_i[N])
 //   reb_delta, reb_eps                [B][Kc][20]     ReB params, index leg*5 + row
-//   al_sigma, al_lambda, term_h       [B][P][4]
+//   td_mask                           [B][P][MTD]     touchdown constraints of each phase (bit l = leg l)
+//   al_sigma, al_lambda               [B][P][MTD][4]  their AL parameters, per constraint and leg
+//   term_h                            [B][P][4]       foot heights at the phase end (constraint legs)
 //   slot_cost, slot_feas, slot_viol   [B][S]          per-slot partial sums for per-element reductions
 //   fp32 Riccati mode (Params::fp32): lq32 [B][Kc][LQW32], K32 [B][Kc][12][24], def32 [B][S][24]
 //   replace lq and K (the fp64 copies are not allocated) and mirror Defect for the sweep
@@ -23,6 +25,13 @@ constexpr int NX = 24;
 constexpr int NN = 576;
 constexpr int MAXP = 16;
 constexpr int LS_LIVE = 128;  // line-search trials with a liveness flag (later ones run unconditionally)
+// TouchDownConstraint objects per phase (HSDDP_MAX_TD): HKDProblem::initialization registers one
+// per phase and HKDProblem::update one more at every step the last phase has reached its end
+// (HKDProblem.cpp:104,199-202); each keeps its own AL parameters, which persist across MPC ticks
+// (reset_params is a no-op, ConstraintsBase.h:341-348).  A mask of TD_PENDING is resolved to the
+// touchdown legs of the phase's contact rows (c_i -> c_{i+1}) when the next contacts are uploaded.
+constexpr int MTD = 4;
+constexpr int TD_PENDING = 0x10;
 // Gains are stored for the 12 controls whose B column is non-zero: row q (0..11) is control
 // u = q when leg q/3 is in stance, u = 12 + q when it swings.  The other 12 rows of the
 // reference's 24 x 24 K are exactly zero (hsddp_sweep.hip) and are expanded on
@@ -122,6 +131,7 @@ struct Bufs {
     int *sel;                              // [B]
     double *K, *lq, *term;
     double *reb_delta, *reb_eps, *al_sigma, *al_lambda, *term_h;
+    int *td_mask;                          // [B][P][MTD] (0: no constraint in that slot)
     double *slot_cost, *slot_feas, *slot_viol;
     int *slot_div;
     // fp32 Riccati mode only: LQ records [B][Kc][LQW32], gains [B][Kc][KCW], Defect copy [B][S][24]
@@ -161,6 +171,8 @@ void launch_reb_update(const Params &p, const Bufs &d, hipStream_t st);
 void launch_outer_end(const Params &p, const Bufs &d, hipStream_t st);
 void launch_reset_elements(const Params &p, const Bufs &d, hipStream_t st);
 void launch_init_params(const Params &p, const Bufs &d, hipStream_t st);
+// TD_PENDING touchdown masks resolved from the contact rows (after new contacts are uploaded)
+void launch_resolve_td(const Params &p, const Bufs &d, hipStream_t st);
 void launch_count(const Params &p, const Bufs &d, int which, hipStream_t st);
 void launch_stat_sums(const Params &p, const Bufs &d, hipStream_t st);
 // dst[c][n] = src[n] for c < copies

@@ -74,9 +74,9 @@ DEV void lq_stage_store(T *wl, const long *ridx, const double *v, T *lq, int ldw
 // The terminal task of one (element, phase), one wave: Phix, Phixx (+AL, quirk A4) and the
 // reset-map Jacobian Px.  These run as the last waves of the k_lq launch (they fill its tail).
 struct TermLds {
-    double sx[NX], shx[4][NX], scoef[4][2], sh[4], sxr[NX], spf[12], ssl[8], sdd[NX], scw[12];
+    double sx[NX], shx[4][NX], scoef[4][2], sh[4], sxr[NX], spf[12], ssl[2 * MTD * 4], sdd[NX], scw[12];
     double spx[NX * (NX + 1)];
-    int sc[4], scn[4];
+    int sc[4], scn[4], smask[MTD];
 };
 
 // LDS hand-over between the lanes of one wave (its LDS accesses complete in order)
@@ -97,13 +97,15 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
     const int P = L.P();
     if (i >= P) return;
     double *sx = S.sx, (*shx)[NX] = S.shx, (*scoef)[2] = S.scoef, *sh = S.sh, *sxr = S.sxr, *spf = S.spf, *ssl = S.ssl;
-    int *sc = S.sc, *scn = S.scn;
+    int *sc = S.sc, *scn = S.scn, *smask = S.smask;
     const int s = L.s0(i) + L.N(i);
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
     if (t < NX) sx[t] = d.Xb[work_buf(d, b)][((size_t)b * p.S + s) * NX + t];
     // the terminal cost's other inputs, staged with X[N] (no memory round trip at the end)
     if (t >= 32 && t < 32 + NX) sxr[t - 32] = xr[t - 32];
-    if (t >= 56 && t < 64) ssl[t - 56] = (t < 60 ? d.al_sigma : d.al_lambda)[((size_t)b * p.P + i) * 4 + (t & 3)];
+    // the phase's touchdown constraints: AL parameters [slot][leg] (sigma, then lambda) and leg masks
+    if (t < 2 * MTD * 4) ssl[t] = (t < MTD * 4 ? d.al_sigma : d.al_lambda)[((size_t)b * p.P + i) * MTD * 4 + (t & (MTD * 4 - 1))];
+    if (t >= 60 && t < 60 + MTD) smask[t - 60] = d.td_mask[((size_t)b * p.P + i) * MTD + t - 60];
     if (t >= 4 && t < 16) spf[t - 4] = pf[t - 4];
     if (t < 4) {
         const int *cc = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
@@ -118,13 +120,14 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
         for (int e = t; e < NX * (NX + 1); e += 64) spx[e] = (e / (NX + 1) == e % (NX + 1)) ? 1.0 : 0.0;
     wave_sync();
     if (t < 4) {
-        // touchdown legs: foot height h, its gradient (non-zeros at 0..2, 5, 12 + 3 l + k) and, at a
-        // phase boundary, the reset map's foot-Jacobian rows — from one evaluation of the leg's
-        // kinematics (hkd_foot_height_grad_sparse's and hkd_foot_jacobian's expressions)
+        // legs of the touchdown constraints: foot height h and its gradient (non-zeros at 0..2, 5,
+        // 12 + 3 l + k); legs touching down at a phase boundary: the reset map's foot-Jacobian rows
+        // — from one evaluation of the leg's kinematics (hkd_foot_height_grad_sparse's and
+        // hkd_foot_jacobian's expressions)
         const int l = t;
-        const bool td = touchdown(sc, scn, l);
+        const bool tdc = (td_union(smask) >> l) & 1, tdr = touchdown(sc, scn, l);
         double h = 0.0;
-        if (td) {
+        if (tdc || (bnd && tdr)) {
             Rot R, Dy, Dp, Dr;
             const EulTrig tr = eul_trig(sx);
             rot_zyx(tr, R);
@@ -138,7 +141,12 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
             for (int k = 0; k < 3; ++k) shx[l][12 + 3 * l + k] = R.r[2][0] * dpb[0][k] + R.r[2][1] * dpb[1][k] + R.r[2][2] * dpb[2][k];
             shx[l][5] = 1.0;
             h = (sx[5] + R.r[2][0] * pb[0] + R.r[2][1] * pb[1] + R.r[2][2] * pb[2]) - p.ground;
-            if (bnd) {  // rows 12 + 3 l + k, k < 2: the foot Jacobian's rows; the k = 2 row is zero
+            if (!tdc) {  // a reset-map leg without a constraint: no AL gradient
+                h = 0.0;
+#pragma unroll
+                for (int j = 0; j < NX; ++j) shx[l][j] = 0.0;
+            }
+            if (bnd && tdr) {  // rows 12 + 3 l + k, k < 2: the foot Jacobian's rows; the k = 2 row is zero
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     double *row = spx + (12 + 3 * l + k) * (NX + 1);
@@ -157,9 +165,18 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
 #pragma unroll
             for (int k = 0; k < 3; ++k) spx[(12 + 3 * l + k) * (NX + 2)] = 0.0;
         }
-        const double sg = ssl[l], lm = ssl[4 + l];
-        scoef[l][0] = (td && p.AL_active) ? sg * h + lm : 0.0;
-        scoef[l][1] = (td && p.AL_active) ? sg * (1 + h) + lm : 0.0;
+        // AL gradient / Hessian coefficients of the leg, summed over the constraints holding it
+        // (quirk A4: (sigma (1 + h) + lambda) hx hx^T, ConstraintsBase.h:374-399)
+        double c0 = 0.0, c1 = 0.0;
+        if (tdc && p.AL_active)
+            for (int q = 0; q < MTD; ++q)
+                if ((smask[q] >> l) & 1) {
+                    const double sg = ssl[4 * q + l], lm = ssl[MTD * 4 + 4 * q + l];
+                    c0 += sg * h + lm;
+                    c1 += sg * (1 + h) + lm;
+                }
+        scoef[l][0] = c0;
+        scoef[l][1] = c1;
         sh[l] = h;
     }
     wave_sync();
@@ -167,7 +184,7 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
     double *rec = d.term + ((size_t)b * p.P + i) * TW;
     if (t == 0) {  // the phase's terminal cost at X[N] (SinglePhase::compute_cost's last term) for k_lq's slot sums
         double tv;
-        d.slot_cost[(size_t)b * p.S + s] = terminal_cost_h(p, sc, scn, sx, sxr, spf, ssl, ssl + 4, sh, tv);
+        d.slot_cost[(size_t)b * p.S + s] = terminal_cost_h(p, sc, sx, sxr, spf, smask, ssl, ssl + MTD * 4, sh, tv);
     }
     if (t < NX) { // Phix
         const int j = t;
@@ -411,8 +428,9 @@ DEV void finish_terminal(const Params &p, const Bufs &d, int b, int s, int i, co
     const size_t sb = (size_t)b * p.S;
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
     double tv, h[4];
-    const double *sg = d.al_sigma + ((size_t)b * p.P + i) * 4, *lm = d.al_lambda + ((size_t)b * p.P + i) * 4;
-    d.slot_cost[sb + s] = terminal_cost(p, c, cn, x, xr, pf, sg, lm, tv, h);
+    const size_t q = ((size_t)b * p.P + i) * MTD;
+    (void)cn;
+    d.slot_cost[sb + s] = terminal_cost(p, c, x, xr, pf, d.td_mask + q, d.al_sigma + q * 4, d.al_lambda + q * 4, tv, h);
     d.slot_viol[sb + s] = tv;
 #pragma unroll
     for (int l = 0; l < 4; ++l) d.term_h[((size_t)b * p.P + i) * 4 + l] = h[l];
@@ -936,22 +954,24 @@ __global__ void k_outer_end(Params p, Bufs d)
     if (E.done) return;
     if (p.AL_active) {
         const int P = layout_of<EL>(d, b).P();
-        for (int i = 0; i < P; ++i) {
-            int c[4], cn[4];
-            load_contacts(d, p, b, i, c, cn);
-            for (int l = 0; l < 4; ++l) {
-                if (!touchdown(c, cn, l)) continue;
-                const size_t q = ((size_t)b * p.P + i) * 4 + l;
-                double h = d.term_h[q];
-                if (fabs(h) < p.tconstr_thresh) continue;
-                if (fabs(h) > 0.005) {
-                    d.al_sigma[q] *= p.update_penalty;
-                    d.al_sigma[q] = fmin(d.al_sigma[q], p.td_sigma_max);
-                } else {
-                    d.al_lambda[q] += h * d.al_sigma[q];
+        // TerminalConstraintBase::update_params (ConstraintsBase.h:354-372) of every touchdown
+        // constraint of every phase, leg by leg
+        for (int i = 0; i < P; ++i)
+            for (int j = 0; j < MTD; ++j) {
+                const int m = d.td_mask[((size_t)b * p.P + i) * MTD + j];
+                for (int l = 0; l < 4; ++l) {
+                    if (!((m >> l) & 1)) continue;
+                    const double h = d.term_h[((size_t)b * p.P + i) * 4 + l];
+                    const size_t q = (((size_t)b * p.P + i) * MTD + j) * 4 + l;
+                    if (fabs(h) < p.tconstr_thresh) continue;
+                    if (fabs(h) > 0.005) {
+                        d.al_sigma[q] *= p.update_penalty;
+                        d.al_sigma[q] = fmin(d.al_sigma[q], p.td_sigma_max);
+                    } else {
+                        d.al_lambda[q] += h * d.al_sigma[q];
+                    }
                 }
             }
-        }
     }
     if (p.no_early_exit) return;
     if (E.max_t < p.tconstr_thresh && fabs(E.max_p) < p.pconstr_thresh && E.feas <= p.feas_thresh) E.done = 1;
@@ -972,7 +992,25 @@ __global__ __launch_bounds__(256) void k_init_params(Params p, Bufs d)
 {
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid < (long)p.B * p.Kc * 20) { d.reb_delta[gid] = p.grf_delta; d.reb_eps[gid] = p.grf_eps; }
-    if (gid < (long)p.B * p.P * 4) { d.al_sigma[gid] = p.td_sigma; d.al_lambda[gid] = p.td_lambda; }
+    if (gid < (long)p.B * p.P * MTD * 4) { d.al_sigma[gid] = p.td_sigma; d.al_lambda[gid] = p.td_lambda; }
+    // one touchdown constraint per phase towards the next phase's contact (HKDProblem::
+    // initialization's add_tconstr_one_phase, HKDProblem.cpp:104), resolved from the contact rows
+    if (gid < (long)p.B * p.P * MTD) d.td_mask[gid] = gid % MTD == 0 ? TD_PENDING : 0;
+}
+
+// TD_PENDING slots take the touchdown legs of their phase's contact rows (0: no constraint)
+template <bool EL>
+__global__ __launch_bounds__(256) void k_resolve_td(Params p, Bufs d)
+{
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)p.B * p.P * MTD) return;
+    const int b = (int)(gid / ((long)p.P * MTD)), i = (int)(gid / MTD % p.P);
+    int &m = d.td_mask[gid];
+    if (i >= layout_of<EL>(d, b).P()) { m = 0; return; }
+    if (m != TD_PENDING) return;
+    int c[4], cn[4];
+    load_contacts(d, p, b, i, c, cn);
+    m = td_bits(c, cn);
 }
 
 // which: 0 = elements with ls_active, 1 = elements still iterating (!done && !inner_done), 2 = !done
@@ -1299,8 +1337,12 @@ void launch_reset_elements(const Params &p, const Bufs &d, hipStream_t st)
 void launch_init_params(const Params &p, const Bufs &d, hipStream_t st)
 {
     long n = (long)p.B * p.Kc * 20;
-    if ((long)p.B * p.P * 4 > n) n = (long)p.B * p.P * 4;
+    if ((long)p.B * p.P * MTD * 4 > n) n = (long)p.B * p.P * MTD * 4;
     hipLaunchKernelGGL(k_init_params, dim3(blocks_for(n, 256)), dim3(256), 0, st, p, d);
+}
+void launch_resolve_td(const Params &p, const Bufs &d, hipStream_t st)
+{
+    LAUNCH_EL(k_resolve_td, dim3(blocks_for((long)p.B * p.P * MTD, 256)), dim3(256), st, p, d);
 }
 void launch_stat_sums(const Params &p, const Bufs &d, hipStream_t st)
 {

@@ -28,6 +28,19 @@ struct ShiftArgs {
 };
 void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, double *Xbar_new, double *Ubar_new, void *K_new,
                          hipStream_t st);
+// constraint parameters through the shift: ReB rows by control-slot source (rmap: old slot, -1 =
+// initial), touchdown constraints by phase source (pmap: old phase, -1 = new) plus nadd appended
+// pending ones per new phase; overflow counts phases past MTD constraints
+struct ShiftParamArgs {
+    int Kc, P_old, P_new;
+    const int *rmap;          // [n_maps][Kc]
+    const int *pmap, *nadd;   // [n_maps][MAXP]
+    const int *map_id;        // [B] (null: one map)
+    double reb_delta0, reb_eps0, td_sigma0, td_lambda0;
+    int *overflow;
+};
+void launch_shift_params(int B, const ShiftParamArgs &a, const Bufs &d, double *reb_delta, double *reb_eps,
+                         double *al_sigma, double *al_lambda, int *td_mask, hipStream_t st);
 
 // reference sample table on the device: [n][RT_W] doubles per sample
 constexpr int RT_BODY = 0, RT_QJ = 12, RT_QJD = 24, RT_FOOT = 36, RT_GRF = 48, RT_C = 60, RT_W = 64;

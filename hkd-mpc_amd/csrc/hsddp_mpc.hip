@@ -129,6 +129,62 @@ void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, double *Xbar_
                            (double *)K_new);
 }
 
+// The constraint parameters the phases carry through HKDProblem::update (HKDProblem.cpp:117-222):
+// per-knot ReB (delta, eps) follow their knots (PathConstraintBase::pop_front / push_back,
+// ConstraintsBase.h:147-158: a pushed knot copies the last one's; a new phase starts from the
+// initial values), and each phase keeps its touchdown constraints with their AL parameters; the
+// update's add_tconstr_one_phase appends one more (initial parameters, legs resolved from the next
+// contact rows: TD_PENDING) at every step its last phase has reached its end.  One thread per
+// (element, control slot, row) and per (element, new phase).
+__global__ __launch_bounds__(256) void k_shift_params(int B, ShiftParamArgs a, Bufs d, double *rd, double *re,
+                                                      double *sg, double *lm, int *mk)
+{
+    const long nr = (long)B * a.Kc * 20, gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid < nr) {
+        const long b = gid / ((long)a.Kc * 20);
+        const int k = (int)(gid / 20 % a.Kc), r = (int)(gid % 20);
+        const int m = a.map_id ? a.map_id[b] : 0, lab = a.rmap[(size_t)m * a.Kc + k];
+        rd[gid] = lab >= 0 ? d.reb_delta[(b * a.Kc + lab) * 20 + r] : a.reb_delta0;
+        re[gid] = lab >= 0 ? d.reb_eps[(b * a.Kc + lab) * 20 + r] : a.reb_eps0;
+        return;
+    }
+    const long g = gid - nr;
+    if (g >= (long)B * a.P_new) return;
+    const long b = g / a.P_new;
+    const int i = (int)(g % a.P_new), m = a.map_id ? a.map_id[b] : 0;
+    const int src = a.pmap[m * MAXP + i], add = a.nadd[m * MAXP + i];
+    const size_t o = ((size_t)b * a.P_new + i) * MTD, q = ((size_t)b * a.P_old + src) * MTD;
+    int mask[MTD];
+    for (int j = 0; j < MTD; ++j) {
+        mask[j] = src >= 0 ? d.td_mask[q + j] : 0;
+        for (int l = 0; l < 4; ++l) {
+            sg[(o + j) * 4 + l] = src >= 0 ? d.al_sigma[(q + j) * 4 + l] : a.td_sigma0;
+            lm[(o + j) * 4 + l] = src >= 0 ? d.al_lambda[(q + j) * 4 + l] : a.td_lambda0;
+        }
+    }
+    for (int n = 0; n < add; ++n) {  // appended constraints take the first free slots
+        int j = 0;
+        while (j < MTD && mask[j]) ++j;
+        if (j == MTD) {
+            atomicAdd(a.overflow, 1);
+            break;
+        }
+        mask[j] = TD_PENDING;
+        for (int l = 0; l < 4; ++l) {
+            sg[(o + j) * 4 + l] = a.td_sigma0;
+            lm[(o + j) * 4 + l] = a.td_lambda0;
+        }
+    }
+    for (int j = 0; j < MTD; ++j) mk[o + j] = mask[j];
+}
+
+void launch_shift_params(int B, const ShiftParamArgs &a, const Bufs &d, double *rd, double *re, double *sg, double *lm,
+                         int *mk, hipStream_t st)
+{
+    const long n = (long)B * a.Kc * 20 + (long)B * a.P_new;
+    hipLaunchKernelGGL(k_shift_params, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, B, a, d, rd, re, sg, lm, mk);
+}
+
 // HKDSinglePhaseReference::get_reference_at_t (HKDReference.cpp:8-57) at state slot s of reference
 // element b: one thread per (b, s); the slot -> sample offset map is shared (host-built with the
 // reference's float time rounding), the window start is per element.

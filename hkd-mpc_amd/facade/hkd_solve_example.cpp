@@ -95,6 +95,7 @@ int main(int argc, char **argv)
             if (phase_contact[0] + phase_contact[1] + phase_contact[2] + phase_contact[3] > 0)  // HKDProblem.cpp:255-263
                 phase->add_pathConstraint(std::make_shared<hkd::GRFConstraint>(phase_contact));
             phase->add_terminalConstraint(std::make_shared<hkd::TouchDownConstraint>(td_proto));
+            phase->update_SS_config(N[i] + 1);  // every state a shooting state (HKDProblem.cpp:104)
             phases.push_back(phase);
             trajs.push_back(traj);
         }

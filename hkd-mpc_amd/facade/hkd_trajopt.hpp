@@ -78,7 +78,8 @@ public:
     void dynamics(StateType &xnext, OutputType &y, StateType &x, ContrlType &u, T t, CtactStatusType &ctact_status, T &dt)
     {
         (void)y; (void)t;
-        if (hsddp_facade::probe_record(hsddp_facade::PROBE_DYNAMICS, ctact_status, (const CtactStatusType *)nullptr, dt))
+        if (hsddp_facade::probe_record(hsddp_facade::PROBE_DYNAMICS, ctact_status, (const CtactStatusType *)nullptr, dt,
+                                       &xnext, nullptr, &x, &u))
             return;
         static_assert(std::is_same<T, double>::value, "the device model computes in fp64");
         const double c[4] = {(double)ctact_status[0], (double)ctact_status[1], (double)ctact_status[2], (double)ctact_status[3]};
@@ -95,7 +96,7 @@ public:
     {
         (void)C; (void)D; (void)t;
         if (hsddp_facade::probe_record(hsddp_facade::PROBE_DYNAMICS_PARTIAL, ctact_status, (const CtactStatusType *)nullptr,
-                                       dt))
+                                       dt, &A, &B, &x, &u))
             return;
         static_assert(std::is_same<T, double>::value, "the device model computes in fp64");
         const double c[4] = {(double)ctact_status[0], (double)ctact_status[1], (double)ctact_status[2], (double)ctact_status[3]};
@@ -139,7 +140,7 @@ public:
     // touching down its foot position projected onto the ground plane
     void resetmap(DVec<T> &xnext, DVec<T> &x, VecM<int, 4> &c, VecM<int, 4> &cn)
     {
-        if (hsddp_facade::probe_record(hsddp_facade::PROBE_RESET, c, &cn, 0.0)) return;
+        if (hsddp_facade::probe_record(hsddp_facade::PROBE_RESET, c, &cn, 0.0, &xnext, nullptr, &x, nullptr)) return;
         static_assert(std::is_same<T, double>::value, "the device model computes in fp64");
         int ci[4], cni[4];
         for (int l = 0; l < 4; ++l) { ci[l] = c[l]; cni[l] = cn[l]; }
@@ -153,7 +154,7 @@ public:
     // its Jacobian Px (24 x 24, column-major)
     void resetmap_partial(DMat<T> &Px, DVec<T> &x, VecM<int, 4> &c, VecM<int, 4> &cn)
     {
-        if (hsddp_facade::probe_record(hsddp_facade::PROBE_RESET_PARTIAL, c, &cn, 0.0)) return;
+        if (hsddp_facade::probe_record(hsddp_facade::PROBE_RESET_PARTIAL, c, &cn, 0.0, &Px, nullptr, &x, nullptr)) return;
         static_assert(std::is_same<T, double>::value, "the device model computes in fp64");
         int ci[4], cni[4];
         for (int l = 0; l < 4; ++l) { ci[l] = c[l]; cni[l] = cn[l]; }

@@ -22,12 +22,14 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <deque>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -365,15 +367,20 @@ struct Probe {
     int kind = PROBE_OFF, hits = 0;
     int c[4] = {0, 0, 0, 0}, cn[4] = {0, 0, 0, 0};
     double dt = 0;
+    // the objects the model call received (outputs, inputs): a callback that is exactly the HKD
+    // registration forwards the solver's own arguments (std::bind forwards references)
+    const void *out[2] = {nullptr, nullptr}, *in[2] = {nullptr, nullptr};
 };
 inline Probe &probe()
 {
     thread_local Probe p;
     return p;
 }
-// record the bound arguments when probing for `kind`; true = do not evaluate
+// record the bound arguments and the forwarded objects when probing for `kind`; true = do not
+// evaluate (the outputs stay untouched)
 template <typename CV, typename DT>
-inline bool probe_record(int kind, const CV &c, const CV *cn, DT dt)
+inline bool probe_record(int kind, const CV &c, const CV *cn, DT dt, const void *out0, const void *out1,
+                         const void *in0, const void *in1)
 {
     Probe &p = probe();
     if (p.kind != kind) return false;
@@ -383,6 +390,8 @@ inline bool probe_record(int kind, const CV &c, const CV *cn, DT dt)
         p.cn[l] = cn ? (int)(*cn)[l] : 0;
     }
     p.dt = (double)dt;
+    p.out[0] = out0; p.out[1] = out1;
+    p.in[0] = in0; p.in[1] = in1;
     return true;
 }
 
@@ -401,6 +410,9 @@ struct CostSpec {
     // foot placements and the body position they are taken relative to (pcom NULL: x_ref's)
     std::function<void(int k, float t, double *pf, double *pcom)> foot_ref;
     bool foot_pcom = false;  // foot_ref writes pcom
+    // per-knot reference tables the term holds (-1: looked up by time, any horizon): the solve
+    // refuses tables that do not cover the phase (x / foot: N + 1 rows, u: at least N)
+    int x_rows = -1, u_rows = -1, foot_rows = -1;
 };
 struct DeviceCost {
     virtual ~DeviceCost() = default;
@@ -1116,17 +1128,20 @@ struct HKDCostTerm : CostBase<double, 24, 24, 0>, HKDCostRefs, hsddp_facade::Dev
             spec.foot_term_cost = weights.foot_term_cost;
             spec.foot_term_grad = weights.foot_term_grad;
         }
-        const std::string nm = cost_name;
-        if (TERMS & HSDDP_TERM_TRACKING)
-            spec.track_ref = [this, nm](int k, float, double *xr, double *ur) {
-                if (k >= (int)x_ref.size()) throw std::runtime_error(nm + ": reference lengths must match the horizon");
+        // row counts checked against the phase horizon by the solve (describe) before any lookup
+        if (TERMS & HSDDP_TERM_TRACKING) {
+            spec.x_rows = (int)x_ref.size();
+            spec.u_rows = (int)u_ref.size();
+            spec.track_ref = [this](int k, float, double *xr, double *ur) {
                 for (int j = 0; j < 24; ++j) { xr[j] = x_ref[k][j]; ur[j] = k < (int)u_ref.size() ? u_ref[k][j] : 0.0; }
             };
-        if (TERMS & HSDDP_TERM_FOOT)
-            spec.foot_ref = [this, nm](int k, float, double *pf, double *) {
-                if (k >= (int)foot_ref.size()) throw std::runtime_error(nm + ": reference lengths must match the horizon");
+        }
+        if (TERMS & HSDDP_TERM_FOOT) {
+            spec.foot_rows = (int)foot_ref.size();
+            spec.foot_ref = [this](int k, float, double *pf, double *) {
                 for (int j = 0; j < 12; ++j) pf[j] = foot_ref[k][j];
             };
+        }
     }
 
     void running_cost(RCost &rc, const State &x, const Contrl &u, const Output &, double dt, float t) override
@@ -1333,6 +1348,11 @@ public:
     struct Problem {
         hsddp_problem_desc desc;
         int S = 0, Kc = 0;
+        std::vector<int> shooting;  // [P]: SS_set = {0 .. shooting[i] - 1}
+        // constraint parameters (hsddp_upload_constraint_params): touchdown legs [P][HSDDP_MAX_TD],
+        // AL sigma / lambda [P][HSDDP_MAX_TD][4], ReB delta / eps [Kc][20]
+        std::vector<int> td_legs;
+        std::vector<double> al_sigma, al_lambda, reb_delta, reb_eps;
         std::vector<int> contacts;
         std::vector<double> ref_x, ref_u, ref_foot, Xbar, Ubar, K;
     };
@@ -1359,10 +1379,61 @@ private:
         int c[4] = {0, 0, 0, 0}, cn[4] = {0, 0, 0, 0};
         double dt = 0;
     };
+    // Device handles outlive the solver object: HKDMPCSolver::update builds a new MultiPhaseDDP for
+    // every MPC tick (HKDMPC.cpp:127-131), so a released handle is parked in a small process-wide
+    // pool and the next solver with the same descriptor (weights, parameters, Kc, device; any
+    // layout) takes it over instead of allocating and capturing again.  The pool is never torn
+    // down (no HIP calls during static destruction); it holds at most kPoolSize handles.
+    struct PoolEntry {
+        hsddp_problem_desc key;
+        int Kc;
+        hsddp_handle h;
+    };
+    static constexpr size_t kPoolSize = 2;
+    static std::mutex &pool_mutex()
+    {
+        static std::mutex *m = new std::mutex;
+        return *m;
+    }
+    static std::vector<PoolEntry> &pool()
+    {
+        static std::vector<PoolEntry> *p = new std::vector<PoolEntry>;
+        return *p;
+    }
+    static std::atomic<int> &creations()
+    {
+        static std::atomic<int> *n = new std::atomic<int>(0);
+        return *n;
+    }
     void release()
     {
-        if (handle) hsddp_destroy(handle);
+        if (!handle) return;
+        std::lock_guard<std::mutex> lk(pool_mutex());
+        auto &pl = pool();
+        if (pl.size() < kPoolSize) pl.push_back({handle_desc, handle_Kc, handle});
+        else hsddp_destroy(handle);
         handle = nullptr;
+    }
+    // a pooled handle for (key, Kc), or a new one
+    void acquire(const hsddp_problem_desc &full, const hsddp_problem_desc &key, int Kc)
+    {
+        {
+            std::lock_guard<std::mutex> lk(pool_mutex());
+            auto &pl = pool();
+            for (size_t j = 0; j < pl.size(); ++j)
+                if (pl[j].Kc == Kc && !std::memcmp(&pl[j].key, &key, sizeof key)) {
+                    handle = pl[j].h;
+                    pl.erase(pl.begin() + j);
+                    break;
+                }
+        }
+        if (!handle) {
+            check(hsddp_create(&full, &handle));
+            ++creations();
+            check(hsddp_set_value_export(handle, 1));  // G[0], H[0] per phase for get_value_approx
+        }
+        handle_desc = key;
+        handle_Kc = Kc;
     }
     static void check(int rc)
     {
@@ -1372,9 +1443,16 @@ private:
     {
         throw std::runtime_error("phase " + std::to_string(i) + ": " + what);
     }
-    // call a registered callback once in probe mode: true when it reached the HKD model / reset
+    // call a registered callback once in probe mode: true when it is exactly the HKD model / reset
+    // registration — it reaches the model once, forwards the solver's own output and input objects
+    // (outs, ins: what the model call must receive) and leaves the outputs as they were (the model
+    // does not evaluate in probe mode, so any write is the callback's own logic).  A callback that
+    // transforms x / u or post-processes the model's result would be dropped by the device solve,
+    // so it is refused.
     template <typename F, typename... A>
-    static bool probe_call(int kind, const F &f, Bound &out, A &...args)
+    static bool probe_call(int kind, const F &f, Bound &out, std::array<const void *, 2> outs,
+                           std::array<const void *, 2> ins, const std::function<bool()> &outputs_untouched,
+                           A &...args)
     {
         if (!f) return false;
         struct Guard {
@@ -1389,13 +1467,32 @@ private:
             return false;
         }
         if (p.hits != 1) return false;
+        for (int j = 0; j < 2; ++j)
+            if (p.out[j] != outs[j] || p.in[j] != ins[j]) return false;
+        if (!outputs_untouched()) return false;
         for (int l = 0; l < 4; ++l) { out.c[l] = p.c[l]; out.cn[l] = p.cn[l]; }
         out.dt = p.dt;
+        return true;
+    }
+    // a recognisable fill for the probe's output objects (alternating signs, so that clamps in
+    // either direction show up)
+    static double probe_fill(size_t j) { return (j & 1 ? -1234.5678125 : 1234.5678125) * (1.0 + j / 64.0); }
+    template <typename M>
+    static void fill(M &m, size_t n)
+    {
+        for (size_t j = 0; j < n; ++j) m.data()[j] = probe_fill(j);
+    }
+    template <typename M>
+    static bool filled(const M &m, size_t n)
+    {
+        for (size_t j = 0; j < n; ++j)
+            if (m.data()[j] != probe_fill(j)) return false;
         return true;
     }
     static bool read_dynamics(const Phase &ph, Bound &b);
     static bool read_dynamics_partial(const Phase &ph, Bound &b);
     static int read_reset(const Phase &ph, Bound &b);  // 0: none registered, 1: read, -1: not HKDReset
+    void write_back_constraints(const Problem &pr);
     static hsddp_hkd_weights derive_weights(const std::vector<hsddp_facade::CostSpec> &track,
                                             const std::vector<hsddp_facade::CostSpec> &foot,
                                             const std::vector<int> &contacts);
@@ -1407,7 +1504,12 @@ private:
     std::vector<float> cost_buffer, dyn_feas_buffer, eqn_feas_buffer, ineq_feas_buffer;
     hsddp_element_info info{};
     hsddp_handle handle = nullptr;
-    hsddp_problem_desc handle_desc{};
+    hsddp_problem_desc handle_desc{};  // the live handle's descriptor without its layout
+    int handle_Kc = 0;
+
+public:
+    // extension: device handles the process's solvers have created so far
+    static int handle_creations() { return creations().load(); }
 };
 
 template <typename T>
@@ -1422,7 +1524,9 @@ bool MultiPhaseDDP<T>::read_dynamics(const Phase &ph, Bound &b)
     typename Phase::Output y;
     typename Phase::Contrl u;
     double t = 0;
-    return probe_call(hsddp_facade::PROBE_DYNAMICS, ph.dynamics, b, xn, y, x, u, t);
+    fill(xn, 24);
+    return probe_call(hsddp_facade::PROBE_DYNAMICS, ph.dynamics, b, {&xn, nullptr}, {&x, &u},
+                      [&] { return filled(xn, 24); }, xn, y, x, u, t);
 }
 
 template <typename T>
@@ -1440,7 +1544,10 @@ bool MultiPhaseDDP<T>::read_dynamics_partial(const Phase &ph, Bound &b)
     typename Phase::State x;
     typename Phase::Contrl u;
     double t = 0;
-    return probe_call(hsddp_facade::PROBE_DYNAMICS_PARTIAL, ph.dynamics_partial, b, A, B, C, D, x, u, t);
+    fill(A, 576);
+    fill(B, 576);
+    return probe_call(hsddp_facade::PROBE_DYNAMICS_PARTIAL, ph.dynamics_partial, b, {&A, &B}, {&x, &u},
+                      [&] { return filled(A, 576) && filled(B, 576); }, A, B, C, D, x, u, t);
 }
 
 template <typename T>
@@ -1454,14 +1561,20 @@ int MultiPhaseDDP<T>::read_reset(const Phase &ph, Bound &b)
         for (int l = 0; l < 4; ++l) { b.c[l] = r->contact[l]; b.cn[l] = r->next_contact[l]; }
     } else {
         DVec<double> xn(24), x(24);
-        if (!probe_call(hsddp_facade::PROBE_RESET, f, b, xn, x)) return -1;
+        fill(xn, 24);
+        if (!probe_call(hsddp_facade::PROBE_RESET, f, b, {&xn, nullptr}, {&x, nullptr},
+                        [&] { return xn.size() == 24 && filled(xn, 24); }, xn, x))
+            return -1;
     }
     if (const auto *r = fp.template target<hkd::ResetmapPartial>()) {
         for (int l = 0; l < 4; ++l) { bp.c[l] = r->contact[l]; bp.cn[l] = r->next_contact[l]; }
     } else {
         DMat<double> Px(24, 24);
         DVec<double> x(24);
-        if (!probe_call(hsddp_facade::PROBE_RESET_PARTIAL, fp, bp, Px, x)) return -1;
+        fill(Px, 576);
+        if (!probe_call(hsddp_facade::PROBE_RESET_PARTIAL, fp, bp, {&Px, nullptr}, {&x, nullptr},
+                        [&] { return Px.rows() == 24 && Px.cols() == 24 && filled(Px, 576); }, Px, x))
+            return -1;
     }
     for (int l = 0; l < 4; ++l)
         if (b.c[l] != bp.c[l] || b.cn[l] != bp.cn[l]) return -1;
@@ -1590,45 +1703,67 @@ typename MultiPhaseDDP<T>::Problem MultiPhaseDDP<T>::describe()
             for (int l = 0; l < 4; ++l)
                 if (rst[i].c[l] != dyn[i].c[l]) refuse(i, "the resetmap's current contact differs from the dynamics'");
     }
-    // terminal constraints: touchdown legs and AL parameters per phase
-    std::vector<int> td_impact(4 * P, 0), has_td(P, 0);
+    // terminal constraints: every phase's TouchDownConstraint objects in registration order, each
+    // with its legs and its current AL parameters (TerminalConstraintBase::params, one row per leg in
+    // leg order).  HKDProblem::update registers one more on the last phase at every step after it
+    // has reached its end (HKDProblem.cpp:199-202), and the parameters evolve across MPC ticks
+    // (reset_params is a no-op), so the solve uploads them and writes the updated ones back.
+    hsddp_constraint_params cp0;
+    hsddp_default_constraint_params(&cp0);
+    pr.td_legs.assign((size_t)P * HSDDP_MAX_TD, 0);
+    pr.al_sigma.assign((size_t)P * HSDDP_MAX_TD * 4, cp0.td_sigma);
+    pr.al_lambda.assign((size_t)P * HSDDP_MAX_TD * 4, cp0.td_lambda);
     hsddp_facade::TdSpec td0;
     bool td_seen = false;
-    for (int i = 0; i < P; ++i)
+    for (int i = 0; i < P; ++i) {
+        int slot = 0;
         for (auto &c : ph[i]->tconstraints) {
             const auto *dc = dynamic_cast<const hsddp_facade::DeviceTerminalConstraint *>(c.get());
             if (!dc) refuse(i, "terminal constraint '" + c->name + "' cannot run on the device");
             hsddp_facade::TdSpec s;
             dc->device_spec(s);
-            bool any = false;
-            for (int l = 0; l < 4; ++l) { td_impact[4 * i + l] |= s.impact[l]; any |= s.impact[l] != 0; }
-            if (has_td[i] && any) refuse(i, "more than one touchdown constraint");
-            has_td[i] |= any;
-            if (!any) continue;
-            if (td_seen && (s.sigma != td0.sigma || s.lambda != td0.lambda || s.sigma_max != td0.sigma_max ||
-                            s.ground != td0.ground))
-                refuse(i, "touchdown AL parameters / ground height differ from another phase's (one set per handle)");
-            td0 = s;
+            int mask = 0, rows = 0;
+            for (int l = 0; l < 4; ++l)
+                if (s.impact[l]) { mask |= 1 << l; ++rows; }
+            if (!mask) continue;  // no rows: no AL terms
+            if (slot == HSDDP_MAX_TD)
+                refuse(i, "more than " + std::to_string(HSDDP_MAX_TD) + " touchdown constraints on one phase");
+            if (td_seen && (s.sigma_max != td0.sigma_max || s.ground != td0.ground))
+                refuse(i, "touchdown sigma_max / ground height differ from another constraint's (one set per handle)");
+            if (!td_seen) td0 = s;
             td_seen = true;
+            const bool own = c->params.size() == (size_t)rows;  // initialize_params ran (else the defaults)
+            if (!own && !c->params.empty()) refuse(i, "touchdown constraint parameters do not match its rows");
+            pr.td_legs[(size_t)i * HSDDP_MAX_TD + slot] = mask;
+            for (int l = 0, r = 0; l < 4; ++l) {
+                if (!((mask >> l) & 1)) continue;
+                const size_t q = ((size_t)i * HSDDP_MAX_TD + slot) * 4 + l;
+                pr.al_sigma[q] = own ? (double)c->params[r].sigma : s.sigma;
+                pr.al_lambda[q] = own ? (double)c->params[r].lambda : s.lambda;
+                ++r;
+            }
+            ++slot;
         }
+    }
     if (td_seen) {
         desc.cparams.td_sigma = td0.sigma; desc.cparams.td_lambda = td0.lambda;
         desc.cparams.td_sigma_max = td0.sigma_max; desc.cparams.ground_height = td0.ground;
     }
     // the contact after the horizon: the last phase's reset target, else the touchdown legs' stance
-    for (int l = 0; l < 4; ++l)
-        pr.contacts[4 * P + l] = has_reset[P - 1] ? rst[P - 1].cn[l]
-                                                  : (td_impact[4 * (P - 1) + l] ? 1 : pr.contacts[4 * (P - 1) + l]);
+    for (int l = 0; l < 4; ++l) {
+        int td = 0;
+        for (int j = 0; j < HSDDP_MAX_TD; ++j) td |= (pr.td_legs[(size_t)(P - 1) * HSDDP_MAX_TD + j] >> l) & 1;
+        pr.contacts[4 * P + l] = has_reset[P - 1] ? rst[P - 1].cn[l] : (td ? 1 : pr.contacts[4 * (P - 1) + l]);
+    }
     for (int i = 0; i < P; ++i)
         for (int l = 0; l < 4; ++l) {
             const int c = pr.contacts[4 * i + l], cn = pr.contacts[4 * (i + 1) + l];
             if (has_reset[i] && rst[i].cn[l] != cn) refuse(i, "the resetmap's next contact differs from the next phase's");
             if (!has_reset[i] && c != cn && i < P - 1)
                 refuse(i, "the contact changes at the phase end but no resetmap (HKDReset) is registered");
-            if ((c == 0 && cn == 1) != (td_impact[4 * i + l] != 0))
-                refuse(i, "touchdown constraint legs differ from the legs touching down at the phase end");
         }
-    // path constraints: GRF friction pyramids with their ReB parameters
+    // path constraints: GRF friction pyramids with their per-knot ReB parameters
+    // (PathConstraintBase::params [knot][row], 5 rows per stance leg in leg order)
     hsddp_facade::GrfSpec g0;
     bool grf_seen = false;
     for (int i = 0; i < P; ++i) {
@@ -1642,9 +1777,9 @@ typename MultiPhaseDDP<T>::Problem MultiPhaseDDP<T>::describe()
             for (int l = 0; l < 4; ++l)
                 if (s.contact[l] != pr.contacts[4 * i + l]) refuse(i, "GRF constraint contact differs from the phase's");
             ++n_grf;
-            if (grf_seen && (s.mu != g0.mu || s.delta != g0.delta || s.delta_min != g0.delta_min || s.eps != g0.eps))
-                refuse(i, "GRF friction / ReB parameters differ from another phase's (one set per handle)");
-            g0 = s;
+            if (grf_seen && (s.mu != g0.mu || s.delta_min != g0.delta_min))
+                refuse(i, "GRF friction coefficient / ReB delta_min differ from another phase's (one set per handle)");
+            if (!grf_seen) g0 = s;
             grf_seen = true;
         }
         if (stance > 0 && n_grf != 1) refuse(i, "a phase with stance legs needs exactly one GRF constraint");
@@ -1668,9 +1803,64 @@ typename MultiPhaseDDP<T>::Problem MultiPhaseDDP<T>::describe()
         if (nt != 1 || nf != 1)
             refuse(i, "needs one HKD tracking cost and one foot-placement regularisation (HKDTrackingCost / "
                       "HKDFootPlaceReg, or hkd::TrackingCost / hkd::FootPlaceReg)");
+        const int N = trajs[i]->horizon;
+        if ((track[i].x_rows >= 0 && track[i].x_rows != N + 1) || (track[i].u_rows >= 0 && track[i].u_rows < N) ||
+            (foot[i].foot_rows >= 0 && foot[i].foot_rows != N + 1))
+            refuse(i, "reference tables must match the horizon (x_ref and foot_ref: N + 1 rows, u_ref: at least N)");
     }
     desc.weights = derive_weights(track, foot, pr.contacts);
     hsddp_pack::layout(trajs, desc.horizons, desc.dt, pr.S, pr.Kc);
+    // per-knot ReB parameters of the GRF constraints (initialize_params ran: its own, else the spec's)
+    pr.reb_delta.assign((size_t)pr.Kc * 20, desc.cparams.grf_delta);
+    pr.reb_eps.assign((size_t)pr.Kc * 20, desc.cparams.grf_eps);
+    for (int i = 0, k0 = 0; i < P; k0 += desc.horizons[i], ++i)
+        for (auto &c : ph[i]->pconstraints) {
+            hsddp_facade::GrfSpec s;
+            dynamic_cast<const hsddp_facade::DevicePathConstraint *>(c.get())->device_spec(s);
+            const int N = desc.horizons[i];
+            if (c->params.empty()) {
+                for (int k = 0; k < N; ++k)
+                    for (int r = 0; r < 20; ++r) {
+                        pr.reb_delta[(size_t)(k0 + k) * 20 + r] = s.delta;
+                        pr.reb_eps[(size_t)(k0 + k) * 20 + r] = s.eps;
+                    }
+                continue;
+            }
+            if ((int)c->params.size() != N) refuse(i, "GRF constraint parameters do not cover the phase horizon");
+            for (int k = 0; k < N; ++k) {
+                const auto &row = c->params[k];
+                if (row.size() != c->size) refuse(i, "GRF constraint parameters do not match its rows");
+                for (int l = 0, q = 0; l < 4; ++l) {
+                    if (!s.contact[l]) continue;
+                    for (int r = 0; r < 5; ++r, ++q) {
+                        pr.reb_delta[(size_t)(k0 + k) * 20 + 5 * l + r] = row[q].delta;
+                        pr.reb_eps[(size_t)(k0 + k) * 20 + 5 * l + r] = row[q].eps;
+                    }
+                }
+            }
+        }
+    // shooting states: SinglePhase::SS_set (update_SS_config, SinglePhase.h:161-164), read as the
+    // rollout reads it (find(k) for k = 0 .. N, SinglePhase.cpp:187-220): entries past N are never
+    // queried.  The device holds SS_set = {0 .. m - 1}; the knot-parallel rollout simulates the
+    // states after the last shooting one in the last phase only — HKDProblem::update leaves a new
+    // last phase of horizon <= 2 with an empty set (HKDProblem.cpp:203-217), every other phase full.
+    pr.shooting.assign(P, 0);
+    for (int i = 0; i < P; ++i) {
+        const int N = desc.horizons[i];
+        std::vector<int> in;
+        for (int s : ph[i]->SS_set)
+            if (s >= 0 && s <= N) in.push_back(s);
+        std::sort(in.begin(), in.end());
+        in.erase(std::unique(in.begin(), in.end()), in.end());
+        for (size_t j = 0; j < in.size(); ++j)
+            if (in[j] != (int)j)
+                refuse(i, "shooting states (SS_set) other than {0 .. m-1} cannot run on the device");
+        pr.shooting[i] = (int)in.size();
+        if (i < P - 1 && pr.shooting[i] != N + 1)
+            refuse(i, "has non-shooting states (SS_set covers " + std::to_string(pr.shooting[i]) + " of " +
+                          std::to_string(N + 1) + " states; call update_SS_config(N + 1) as HKDProblem.cpp:104 does): "
+                          "the device rollout simulates non-shooting states in the last phase only");
+    }
     // references at every knot's time t = t_offset + k dt (SinglePhase.cpp:243-287)
     hsddp_pack::pack_references(P, desc.horizons, [&](int i, int k, double *xr, double *ur, double *pf) {
         const float t = (float)(ph[i]->t_offset + k * trajs[i]->timeStep);
@@ -1685,6 +1875,46 @@ typename MultiPhaseDDP<T>::Problem MultiPhaseDDP<T>::describe()
     return pr;
 }
 
+// the solve's AL / ReB parameters back into the phases' constraint objects (their params rows,
+// in the order describe() read them); objects whose params were never initialised stay as they are
+template <typename T>
+void MultiPhaseDDP<T>::write_back_constraints(const Problem &pr)
+{
+    for (int i = 0, k0 = 0; i < n_phases; k0 += pr.desc.horizons[i], ++i) {
+        Phase *ph = dynamic_cast<Phase *>(phases[i].get());
+        int slot = 0;
+        for (auto &c : ph->tconstraints) {
+            hsddp_facade::TdSpec s;
+            dynamic_cast<const hsddp_facade::DeviceTerminalConstraint *>(c.get())->device_spec(s);
+            int mask = 0;
+            for (int l = 0; l < 4; ++l) mask |= s.impact[l] ? 1 << l : 0;
+            if (!mask) continue;
+            if (!c->params.empty())
+                for (int l = 0, r = 0; l < 4; ++l) {
+                    if (!((mask >> l) & 1)) continue;
+                    const size_t q = ((size_t)i * HSDDP_MAX_TD + slot) * 4 + l;
+                    c->params[r].sigma = (T)pr.al_sigma[q];
+                    c->params[r].lambda = (T)pr.al_lambda[q];
+                    ++r;
+                }
+            ++slot;
+        }
+        for (auto &c : ph->pconstraints) {
+            if (c->params.empty()) continue;
+            hsddp_facade::GrfSpec s;
+            dynamic_cast<const hsddp_facade::DevicePathConstraint *>(c.get())->device_spec(s);
+            for (int k = 0; k < pr.desc.horizons[i]; ++k)
+                for (int l = 0, q = 0; l < 4; ++l) {
+                    if (!s.contact[l]) continue;
+                    for (int r = 0; r < 5; ++r, ++q) {
+                        c->params[k][q].delta = (T)pr.reb_delta[(size_t)(k0 + k) * 20 + 5 * l + r];
+                        c->params[k][q].eps = (T)pr.reb_eps[(size_t)(k0 + k) * 20 + 5 * l + r];
+                    }
+                }
+        }
+    }
+}
+
 template <typename T>
 void MultiPhaseDDP<T>::solve(HSDDP_OPTION option)
 {
@@ -1692,19 +1922,31 @@ void MultiPhaseDDP<T>::solve(HSDDP_OPTION option)
     const int P = n_phases, S = pr.S, Kc = pr.Kc;
     std::vector<std::shared_ptr<Trajectory<double, 24, 24, 0>>> trajs(P);
     for (int i = 0; i < P; ++i) trajs[i] = dynamic_cast<Phase *>(phases[i].get())->traj;
-    // one handle while the problem's shape, weights and parameters stay the same (an MPC loop)
-    if (!handle || std::memcmp(&pr.desc, &handle_desc, sizeof handle_desc) != 0) {
+    // One handle while the weights, parameters and the total knot count stay the same: the MPC
+    // loop's receding-horizon updates (HKDProblem::update) move knots between phases and add or
+    // drop phases, which the live handle takes as a new layout (hsddp_set_layout, no device
+    // allocation and no re-capture of anything but the iteration graphs of the new layout).
+    hsddp_problem_desc key = pr.desc;
+    key.n_phases = 0;
+    std::memset(key.horizons, 0, sizeof key.horizons);
+    if (!handle || std::memcmp(&key, &handle_desc, sizeof handle_desc) != 0 || Kc != handle_Kc) {
         release();
-        check(hsddp_create(&pr.desc, &handle));
-        handle_desc = pr.desc;
-        check(hsddp_set_value_export(handle, 1));  // G[0], H[0] per phase for get_value_approx
+        acquire(pr.desc, key, Kc);
     }
+    check(hsddp_set_layout(handle, P, pr.desc.horizons, pr.shooting.data(), nullptr));
     const hsddp_options o = option.to_c();
     check(hsddp_set_options(handle, &o));
     check(hsddp_upload_problem(handle, pr.contacts.data(), x0.data(), pr.ref_x.data(), pr.ref_u.data(), pr.ref_foot.data()));
     check(hsddp_upload_warm_start(handle, pr.Xbar.data(), pr.Ubar.data(), pr.K.data()));
+    check(hsddp_upload_constraint_params(handle, pr.reb_delta.data(), pr.reb_eps.data(), pr.td_legs.data(),
+                                         pr.al_sigma.data(), pr.al_lambda.data()));
     hsddp_stats st;
     check(hsddp_solve(handle, &st));
+    // the constraint objects keep the parameters the solve's AL / ReB updates left (the next MPC
+    // tick starts from them, as the reference's objects do)
+    check(hsddp_download_constraint_params(handle, pr.reb_delta.data(), pr.reb_eps.data(), nullptr,
+                                           pr.al_sigma.data(), pr.al_lambda.data()));
+    write_back_constraints(pr);
     // solution, working trajectory, LQ model, terminal data, value function, solver info
     std::vector<double> &Xb = pr.Xbar, &Ub = pr.Ubar, &K = pr.K;
     check(hsddp_download_trajectory(handle, Xb.data(), Ub.data(), K.data()));

@@ -10,7 +10,7 @@
 // Device part (argument "gpu"): the hkd:: plugins' virtuals equal the batched C-ABI primitives.
 #include <cstdio>
 
-#include "hsddp_facade.hpp"
+#include "hkd_trajopt.hpp"  // hsddp_facade.hpp + the HKD-TrajOpt classes (HKD::Model, HKDReset)
 
 #define CHECK(c)                                                                    \
     do {                                                                            \
@@ -238,6 +238,7 @@ static int host_checks()
         ph->add_cost(tc);
         ph->add_cost(fr);
         ph->add_pathConstraint(std::make_shared<hkd::GRFConstraint>(c));
+        ph->update_SS_config(N + 1);  // every state a shooting state (HKDProblem.cpp:104)
         return ph;
     };
     std::shared_ptr<hkd::TrackingCost> tc0, tc1;
@@ -283,6 +284,77 @@ static int host_checks()
         mixed = std::string(e.what()).find("no resetmap") != std::string::npos;
     }
     CHECK(mixed);
+
+    // shooting states (SinglePhase::SS_set): the last phase may keep an empty set (HKDProblem::update
+    // leaves a new last phase of <= 2 knots without one), any other phase must be all shooting
+    auto refused_with = [&](const std::string &needle) {
+        try {
+            ws.describe();
+        } catch (const std::runtime_error &e) {
+            return std::string(e.what()).find(needle) != std::string::npos;
+        }
+        return false;
+    };
+    auto s0 = hkd_phase(4, trot_a, trot_a, tc0, fr0), s1 = hkd_phase(2, trot_a, trot_a, tc1, fr1);
+    fr0->weights = fr1->weights;
+    s1->SS_set.clear();
+    ws.set_multiPhaseProblem({s0, s1});
+    const auto pr = ws.describe();
+    CHECK(pr.shooting.size() == 2 && pr.shooting[0] == 5 && pr.shooting[1] == 0);
+    s1->update_SS_config(7);  // entries past N are never queried (SinglePhase.cpp:187-220)
+    CHECK(ws.describe().shooting[1] == 3);
+    s0->SS_set.clear();
+    CHECK(refused_with("phase 0: has non-shooting states"));
+    s0->SS_set = {0, 2, 3, 4, 5};
+    CHECK(refused_with("phase 0: shooting states (SS_set) other than"));
+    s0->update_SS_config(5);
+    // per-knot reference tables must cover the phase
+    tc0->x_ref.pop_back();
+    CHECK(refused_with("phase 0: reference tables must match the horizon"));
+    tc0->x_ref.push_back({});
+    fr1->foot_ref.push_back({});
+    CHECK(refused_with("phase 1: reference tables must match the horizon"));
+    fr1->foot_ref.pop_back();
+    tc1->u_ref.resize(1);
+    CHECK(refused_with("phase 1: reference tables must match the horizon"));
+    tc1->u_ref.resize(2);  // u_ref needs N rows (the last state slot's control reference is unused)
+    CHECK(ws.describe().shooting[0] == 5);
+
+    // dynamics / reset callbacks: exactly the HKD::Model / HKDReset registration (std::bind forwards
+    // the solver's own objects) is accepted; a callback that transforms its inputs or post-processes
+    // the model's result would be dropped by the device solve, so it is refused
+    namespace pc = std::placeholders;
+    typedef SinglePhase<double, 24, 24, 0> Ph;
+    HKD::Model<double> model;
+    VecM<int, 4> cv;
+    for (int l = 0; l < 4; ++l) cv[l] = trot_a[l];
+    double dtb = 0.01;
+    s0->set_dynamics(std::bind(&HKD::Model<double>::dynamics, &model, pc::_1, pc::_2, pc::_3, pc::_4, pc::_5, cv, dtb));
+    CHECK(ws.describe().shooting[0] == 5);
+    s0->set_dynamics([&](Ph::State &xn, Ph::Output &y, Ph::State &x, Ph::Contrl &u, double t) {
+        model.dynamics(xn, y, x, u, t, cv, dtb);
+        xn[5] = std::max(xn[5], 0.0);  // user post-processing
+    });
+    CHECK(refused_with("phase 0: Dynamics is not the HKD registration"));
+    s0->set_dynamics([&](Ph::State &xn, Ph::Output &y, Ph::State &x, Ph::Contrl &u, double t) {
+        Ph::Contrl u2 = u;  // user-transformed input
+        u2[2] += 1;
+        model.dynamics(xn, y, x, u2, t, cv, dtb);
+    });
+    CHECK(refused_with("phase 0: Dynamics is not the HKD registration"));
+    s0->set_dynamics([&](Ph::State &xn, Ph::Output &y, Ph::State &x, Ph::Contrl &u, double t) {
+        model.dynamics(xn, y, x, u, t, cv, dtb);  // a plain forwarding lambda is the registration
+    });
+    CHECK(ws.describe().shooting[0] == 5);
+    HKDReset<double> reset;
+    s0->set_resetmap([&](DVec<double> &xn, DVec<double> &x) {
+        reset.resetmap(xn, x, cv, cv);
+        xn[0] = 0;
+    });
+    CHECK(refused_with("phase 0: resetmap / resetmap_partial is not the HKD registration"));
+    s0->set_resetmap(std::bind(&HKDReset<double>::resetmap, &reset, pc::_1, pc::_2, cv, cv));
+    s0->set_resetmap_partial(std::bind(&HKDReset<double>::resetmap_partial, &reset, pc::_1, pc::_2, cv, cv));
+    CHECK(ws.describe().shooting[0] == 5);
     return 0;
 }
 

@@ -239,6 +239,27 @@ class Solver:
         check(lib().hsddp_download_terminal(self._h, *(out[k].ctypes.data for k in ("Phi", "Phix", "Phixx", "Px"))))
         return out
 
+    MAX_TD = 4  # HSDDP_MAX_TD
+
+    def constraint_params(self) -> dict:
+        """The ReB / AL parameters the solve reads and updates: reb_delta, reb_eps [B][Kc][20];
+        td_mask [B][P][MAX_TD] (each phase's touchdown constraints, bit l = leg l); al_sigma,
+        al_lambda [B][P][MAX_TD][4]."""
+        B, P, Kc, T = self.B, self.P, self.Kc, self.MAX_TD
+        out = {"reb_delta": np.empty((B, Kc, 20)), "reb_eps": np.empty((B, Kc, 20)),
+               "td_mask": np.empty((B, P, T), np.int32), "al_sigma": np.empty((B, P, T, 4)),
+               "al_lambda": np.empty((B, P, T, 4))}
+        check(lib().hsddp_download_constraint_params(self._h, *(out[k].ctypes.data for k in
+                                                               ("reb_delta", "reb_eps", "td_mask", "al_sigma", "al_lambda"))))
+        return out
+
+    def upload_constraint_params(self, reb_delta=None, reb_eps=None, td_mask=None, al_sigma=None, al_lambda=None):
+        """hsddp_upload_constraint_params (None keeps a field)"""
+        arrs = [None if a is None else np.ascontiguousarray(a, dtype=t) for a, t in
+                ((reb_delta, np.float64), (reb_eps, np.float64), (td_mask, np.int32), (al_sigma, np.float64),
+                 (al_lambda, np.float64))]
+        check(lib().hsddp_upload_constraint_params(self._h, *(None if a is None else a.ctypes.data for a in arrs)))
+
     def set_value_export(self, on: bool = True) -> None:
         """Store G[0], H[0] of every phase in each sweep (SinglePhase::get_value_approx)."""
         check(lib().hsddp_set_value_export(self._h, int(bool(on))))

@@ -106,6 +106,7 @@ EXPORTS = [
     "hsddp_get_phase_info", "hsddp_hkd_running_cost", "hsddp_hkd_terminal_cost", "hsddp_hkd_grf_constraint",
     "hsddp_hkd_touchdown_constraint", "hsddp_set_element_layouts",
     "hsddp_shift_elements", "hsddp_get_element_layouts", "hsddp_extract_commands_device",
+    "hsddp_set_layout", "hsddp_upload_constraint_params", "hsddp_download_constraint_params",
 ]
 
 
@@ -179,6 +180,9 @@ def lib():
     L.hsddp_extract_commands.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_void_p, C.c_int,
                                          C.c_void_p, C.c_int, C.c_float, C.c_void_p]
     L.hsddp_extract_commands_device.argtypes = L.hsddp_extract_commands.argtypes
+    L.hsddp_set_layout.argtypes = [V, C.c_int, IP, IP, IP]
+    L.hsddp_upload_constraint_params.argtypes = [V] * 6
+    L.hsddp_download_constraint_params.argtypes = [V] * 6
     _lib = L
     return L
 

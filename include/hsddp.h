@@ -16,6 +16,8 @@
  *   hsddp_upload_problem (x0, references)     MultiPhaseDDP::set_initial_condition  MultiPhaseDDP.h:384;
  *                                             HKDSinglePhaseReference::get_reference_at_t HKDReference.cpp:8-57
  *   hsddp_upload_warm_start                   Trajectory::Xbar/Ubar/K warm start    TrajectoryManagement.h:54-77
+ *   hsddp_upload/download_constraint_params   PathConstraintBase / TerminalConstraintBase params (ReB, AL)
+ *                                             ConstraintsBase.h:88-183, 329-405
  *   hsddp_solve                               MultiPhaseDDP::solve                  MultiPhaseDDP.cpp:232-428
  *   hsddp_solve_begin/_iterate/_end           the same loop split at its inner iterations (:257-303 / :304-381 / :383-408)
  *   hsddp_download_trajectory                 Trajectory fields read by the caller  HKDMPC.cpp:243-298
@@ -27,6 +29,8 @@
  *   hsddp_advance / hsddp_get_phase_info      HKDProblem::update from the reference table   HKDProblem.cpp:117-222
  *   hsddp_shift / hsddp_update_problem        HKDProblem::update + HKDMPCSolver::update's re-solve
  *                                             setup (warm start reused)  HKDProblem.cpp:117-222; HKDMPC.cpp:96-143
+ *   hsddp_set_layout                          a caller-side HKDProblem::update's layout + SinglePhase::
+ *                                             update_SS_config (SS_set)  HKDProblem.cpp:203-217; SinglePhase.h:161-164
  *   hsddp_extract_commands                    update_foot_placement + publish_mpc_cmd HKDMPC.cpp:207-298
  *   hsddp_hkd_dynamics                        HKD::Model::dynamics (hkinodyn)       HKDModel.h:33-45
  *   hsddp_hkd_dynamics_partial                HKD::Model::dynamics_partial          HKDModel.h:46-61
@@ -63,6 +67,10 @@ extern "C" {
 #define HSDDP_NX 24
 #define HSDDP_NU 24
 #define HSDDP_MAX_PHASES 16
+/* TouchDownConstraint objects one phase can carry: HKDProblem::initialization registers one per
+ * phase and HKDProblem::update one more at every step its last phase has reached its end
+ * (HKDProblem.cpp:104,199-202); each keeps its own AL parameters. */
+#define HSDDP_MAX_TD 4
 /* longest regularisation schedule accepted: mu = max(mu * update_regularization, 1e-3) retries
  * of one failed backward sweep until mu > 1e2 (MultiPhaseDDP.cpp:150-167) */
 #define HSDDP_MAX_REG_ATTEMPTS 64
@@ -181,8 +189,22 @@ int hsddp_upload_problem(hsddp_handle h, const int *contacts, const double *x0, 
                          const double *ref_u, const double *ref_foot);
 /* Xbar [B][S][24], Ubar [B][Kc][24], K [B][Kc][24][24]; NULL keeps the current value (initially
  * Xbar = ref_x, Ubar = 0, K = 0 as HKDProblem.cpp:84-90 / TrajectoryManagement.cpp:5-35).  Also
- * resets X = Xbar, U = Ubar, dX = 0 and the ReB/AL parameters to their initial values. */
+ * resets X = Xbar, U = Ubar, dX = 0 and the constraint parameters to those of a new problem: ReB
+ * (delta, eps) = desc->cparams at every knot, one touchdown constraint per phase (the touchdown legs
+ * from contact row i to row i + 1, none when there are none) with the initial AL parameters. */
 int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const double *Ubar, const double *K);
+/* The constraint parameters the solve reads and updates (its update_AL_params / update_REB_params,
+ * ConstraintsBase.h:160-176, 354-372), for callers that keep their constraint objects themselves
+ * (the C++ facade's PathConstraintBase::params / TerminalConstraintBase::params):
+ * reb_delta, reb_eps [B][Kc][20] (row 5 l + r of stance leg l, GRFConstraint row order);
+ * td_legs [B][P][HSDDP_MAX_TD]: the touchdown constraints of each phase in registration order,
+ * bit l = leg l (0: no constraint in that slot); al_sigma, al_lambda [B][P][HSDDP_MAX_TD][4] per
+ * constraint and leg (entries of legs outside the mask are ignored).  Any pointer may be NULL
+ * (kept / not read).  Upload after the problem's contacts (hsddp_upload_problem). */
+int hsddp_upload_constraint_params(hsddp_handle h, const double *reb_delta, const double *reb_eps, const int *td_legs,
+                                   const double *al_sigma, const double *al_lambda);
+int hsddp_download_constraint_params(hsddp_handle h, double *reb_delta, double *reb_eps, int *td_legs,
+                                     double *al_sigma, double *al_lambda);
 
 /* MultiPhaseDDP::solve (MultiPhaseDDP.cpp:232-428) for every element.  With early exits on, each
  * inner iteration is replayed from a cached hipGraph and stats carries ms_total but no per-phase
@@ -303,8 +325,20 @@ int hsddp_get_element_layouts(hsddp_handle h, int *n_phases, int *horizons, int 
 /* current layout: n_phases, horizons[16], shooting states[16], is_phase_reach_end[16] (any NULL);
  * HSDDP_ERR_UNSUPPORTED with per-element layouts (hsddp_get_element_layouts) */
 int hsddp_get_layout(hsddp_handle h, int *n_phases, int *horizons, int *shooting, int *reach_end);
+/* A new shared layout on a live handle, for callers that run HKDProblem::update's bookkeeping
+ * themselves (the C++ facade: SinglePhase::pop_front / push_back_default on the host Trajectory,
+ * HKDProblem.cpp:117-222; update_SS_config, SinglePhase.h:161-164): n_phases phases of horizons[i]
+ * knots summing to the handle's Kc, shooting[i] = the size of phase i's SS_set {0 .. shooting[i]-1}
+ * (NULL: N_i + 1 each; below N_i + 1 only in the last phase — HSDDP_ERR_UNSUPPORTED elsewhere),
+ * reach_end[i] = is_phase_reach_end (NULL: 0).  No device work and no reallocation; the handle then
+ * needs hsddp_upload_problem (and a warm start) of the new layout before it solves. */
+int hsddp_set_layout(hsddp_handle h, int n_phases, const int *horizons, const int *shooting, const int *reach_end);
 /* as hsddp_upload_problem, but keeps the warm start Xbar / Ubar / K (the MPC update's reuse of the
- * previous solution); resets X = Xbar, U = Ubar and the ReB / AL parameters (reset_params) */
+ * previous solution) and the constraint parameters: HKDProblem::update's reset_params is a no-op
+ * (ConstraintsBase.h:165-167, 341-348), so the per-knot ReB parameters and every touchdown
+ * constraint's AL parameters carry over from the previous solve (shifted with their knots and phases
+ * by hsddp_shift / hsddp_advance, which also append the touchdown constraints add_tconstr_one_phase
+ * registers: their legs are the new contact rows' touchdown legs).  Resets X = Xbar, U = Ubar. */
 int hsddp_update_problem(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
                          const double *ref_u, const double *ref_foot);
 

@@ -56,6 +56,8 @@ typedef struct {
     double foot_term_cost, foot_term_grad;                /* HKDCost.cpp:49,63-64 */
 } orc_weights;
 
+#define ORC_MAX_TD 4 /* touchdown constraints per phase (HSDDP_MAX_TD) */
+
 typedef struct {
     int n_phases;
     const int *horizons;      /* [P] */
@@ -81,7 +83,10 @@ typedef struct {
     double *Ubar, *U, *dU;                       /* [Kc][24] */
     double *K;                                   /* [Kc][24][24] */
     double *reb_delta, *reb_eps;                 /* [Kc][20] (leg*5+row) */
-    double *al_sigma, *al_lambda;                /* [P][4] */
+    /* TouchDownConstraint objects of each phase, in registration order (HKDProblem.cpp:104,
+       199-202): legs (bit l = leg l, 0 = no constraint) and AL parameters per constraint and leg */
+    double *al_sigma, *al_lambda;                /* [P][ORC_MAX_TD][4] */
+    int *td_mask;                                /* [P][ORC_MAX_TD] */
     /* outputs */
     double cost, feas, merit, max_tconstr, max_pconstr;
     int iters, outer_iters, status, n_ls_trials;
@@ -108,7 +113,9 @@ int orc_solve_batch(const orc_problem *p, const orc_options *o, orc_element *ele
 int orc_riccati_lq(int N, const double *A, const double *B, const double *lxx, const double *luu, const double *lx,
                    const double *lu, const double *Phix, const double *Phixx, double reg, double *K0, double *dU0,
                    double *G0, double *H0);
-void orc_init_element(const orc_problem *p, orc_element *e); /* default ReB/AL params */
+/* a new problem's constraint parameters: ReB at every knot, one touchdown constraint per phase
+   (contact row i -> i + 1, HKDProblem.cpp:104) with the initial AL parameters; needs e->contacts */
+void orc_init_element(const orc_problem *p, orc_element *e);
 
 #ifdef __cplusplus
 }

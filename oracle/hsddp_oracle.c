@@ -85,6 +85,13 @@ typedef struct {
 } ctx_t;
 
 static int n_stance(const int *c) { return c[0] + c[1] + c[2] + c[3]; }
+/* the legs of phase i's touchdown constraints (union of their masks) */
+static int td_legs(const orc_element *e, int i)
+{
+    int u = 0;
+    for (int j = 0; j < ORC_MAX_TD; ++j) u |= e->td_mask[i * ORC_MAX_TD + j];
+    return u & 15;
+}
 static int n_touchdown(const int *c, const int *cn)
 {
     int n = 0;
@@ -201,11 +208,13 @@ static int phase_hybrid_rollout(ctx_t *C, int i, double eps, const double *x_ini
         }
     }
     C->pviol[i] = pv;
-    /* TouchDownConstraint::compute_violation at X[N] (HKDConstraints.cpp:69-118) */
+    /* TouchDownConstraint::compute_violation at X[N] (HKDConstraints.cpp:69-118) of every
+       touchdown constraint of the phase: the foot heights of their legs */
     double tv = 0;
     const double *xN = X + (size_t)(s0 + N) * NX;
+    const int tdu = td_legs(C->e, i);
     for (int l = 0; l < 4; ++l) {
-        if (!(C->c[i][l] == 0 && C->c[i + 1][l] == 1)) continue;
+        if (!((tdu >> l) & 1)) continue;
         double pf[3];
         orc_foot_position(l, xN + 3, xN, xN + 12 + 3 * l, pf);
         C->h[i][l] = pf[2] - C->p->ground_height;
@@ -281,15 +290,21 @@ static void phase_compute_cost(ctx_t *C, int i)
     foot_residual(C, s, x, d);
     for (int j = 0; j < 12; ++j) pf += d[j] * C->Qfoot[i][j] * d[j];
     phi = 0 + phi + C->p->w.foot_term_cost * pf;
-    if (C->o->AL_active) { /* update_terminal_cost_with_tconstr (SinglePhase.cpp:401-411) */
-        double al = 0;
-        for (int l = 0; l < 4; ++l) {
-            if (!(C->c[i][l] == 0 && C->c[i + 1][l] == 1)) continue;
-            double sg = e->al_sigma[i * 4 + l], lm = e->al_lambda[i * 4 + l], hh = C->h[i][l];
-            al += 0.5 * sg * hh * hh;
-            al += lm * hh;
+    if (C->o->AL_active) { /* update_terminal_cost_with_tconstr (SinglePhase.cpp:401-411): per
+                               constraint, compute_AL_cost (ConstraintsBase.h:374-382), Phi += */
+        for (int j = 0; j < ORC_MAX_TD; ++j) {
+            const int m = e->td_mask[i * ORC_MAX_TD + j];
+            if (!m) continue;
+            double al = 0;
+            for (int l = 0; l < 4; ++l) {
+                if (!((m >> l) & 1)) continue;
+                const int q = (i * ORC_MAX_TD + j) * 4 + l;
+                double sg = e->al_sigma[q], lm = e->al_lambda[q], hh = C->h[i][l];
+                al += 0.5 * sg * hh * hh;
+                al += lm * hh;
+            }
+            phi += al;
         }
-        phi += al;
     }
     C->Phi[i] = phi;
     C->phase_cost[i] = cost + phi;
@@ -353,21 +368,39 @@ static void phase_LQ(ctx_t *C, int i)
     foot_residual(C, s, x, d);
     foot_grad(C->c[i], C->Qfoot[i], d, C->p->w.foot_term_grad, Px_);
     foot_hess(C->c[i], C->Qfoot[i], C->p->w.foot_term_grad, Pxx);
-    if (C->o->AL_active) { /* TouchDownConstraint::compute_partial + AL partials */
+    if (C->o->AL_active) { /* TouchDownConstraint::compute_partial (HKDConstraints.cpp:120-171) of the
+                               constraint legs, then per constraint compute_AL_partials
+                               (ConstraintsBase.h:383-399) and Phix += grad, Phixx += hess
+                               (update_terminal_cost_par_with_tconstr, SinglePhase.cpp:414-426) */
+        const int tdu = td_legs(e, i);
         for (int l = 0; l < 4; ++l) {
-            if (!(C->c[i][l] == 0 && C->c[i + 1][l] == 1)) continue;
+            if (!((tdu >> l) & 1)) continue;
             double J[54], hxv[NX];
             orc_foot_jacobian(l, x + 3, x, x + 12 + 3 * l, J);
             memset(hxv, 0, sizeof(hxv));
             for (int j = 0; j < 3; ++j) { hxv[j] = J[2 * 18 + 3 + j]; hxv[3 + j] = J[2 * 18 + j]; }
             for (int j = 0; j < 12; ++j) hxv[12 + j] = J[2 * 18 + 6 + j];
             memcpy(C->hx[i][l], hxv, sizeof(hxv));
-            double sg = e->al_sigma[i * 4 + l], lm = e->al_lambda[i * 4 + l], hh = C->h[i][l];
-            double a1 = sg * hh + lm, a2 = sg * (1 + hh) + lm; /* quirk A4 */
-            for (int a = 0; a < NX; ++a) {
-                Px_[a] += a1 * hxv[a];
-                for (int b = 0; b < NX; ++b) Pxx[a * NX + b] += a2 * (hxv[a] * hxv[b]);
+        }
+        for (int j = 0; j < ORC_MAX_TD; ++j) {
+            const int m = e->td_mask[i * ORC_MAX_TD + j];
+            if (!m) continue;
+            double grad[NX], hess[NN];
+            memset(grad, 0, sizeof grad);
+            memset(hess, 0, sizeof hess);
+            for (int l = 0; l < 4; ++l) {
+                if (!((m >> l) & 1)) continue;
+                const int q = (i * ORC_MAX_TD + j) * 4 + l;
+                const double *hxv = C->hx[i][l];
+                double sg = e->al_sigma[q], lm = e->al_lambda[q], hh = C->h[i][l];
+                double a1 = sg * hh + lm, a2 = sg * (1 + hh) + lm; /* quirk A4 */
+                for (int a = 0; a < NX; ++a) {
+                    grad[a] += a1 * hxv[a];
+                    for (int b = 0; b < NX; ++b) hess[a * NX + b] += a2 * (hxv[a] * hxv[b]);
+                }
             }
+            for (int a = 0; a < NX; ++a) Px_[a] += grad[a];
+            for (int a = 0; a < NN; ++a) Pxx[a] += hess[a];
         }
     }
 }
@@ -774,14 +807,19 @@ static void mp_update_AL(ctx_t *C)
 {
     orc_element *e = C->e;
     const orc_options *o = C->o;
+    /* update_al_params of every touchdown constraint (ConstraintsBase.h:354-372) */
     for (int i = 0; i < C->P; ++i)
-        for (int l = 0; l < 4; ++l) {
-            if (!(C->c[i][l] == 0 && C->c[i + 1][l] == 1)) continue;
-            double hh = C->h[i][l];
-            if (fabs(hh) < o->tconstr_thresh) continue;
-            double *sg = &e->al_sigma[i * 4 + l];
-            if (fabs(hh) > 0.005) { *sg *= o->update_penalty; *sg = fmin(*sg, C->p->td_sigma_max); }
-            else e->al_lambda[i * 4 + l] += hh * *sg;
+        for (int j = 0; j < ORC_MAX_TD; ++j) {
+            const int m = e->td_mask[i * ORC_MAX_TD + j];
+            for (int l = 0; l < 4; ++l) {
+                if (!((m >> l) & 1)) continue;
+                double hh = C->h[i][l];
+                if (fabs(hh) < o->tconstr_thresh) continue;
+                const int q = (i * ORC_MAX_TD + j) * 4 + l;
+                double *sg = &e->al_sigma[q];
+                if (fabs(hh) > 0.005) { *sg *= o->update_penalty; *sg = fmin(*sg, C->p->td_sigma_max); }
+                else e->al_lambda[q] += hh * *sg;
+            }
         }
 }
 
@@ -810,7 +848,15 @@ void orc_init_element(const orc_problem *p, orc_element *e)
     int P = p->n_phases, Kc = 0;
     for (int i = 0; i < P; ++i) Kc += p->horizons[i];
     for (int q = 0; q < Kc * 20; ++q) { e->reb_delta[q] = p->grf_delta; e->reb_eps[q] = p->grf_eps; }
-    for (int q = 0; q < P * 4; ++q) { e->al_sigma[q] = p->td_sigma; e->al_lambda[q] = p->td_lambda; }
+    for (int q = 0; q < P * ORC_MAX_TD * 4; ++q) { e->al_sigma[q] = p->td_sigma; e->al_lambda[q] = p->td_lambda; }
+    for (int i = 0; i < P; ++i)
+        for (int j = 0; j < ORC_MAX_TD; ++j) {
+            int m = 0;
+            if (j == 0)  /* add_tconstr_one_phase at initialization: legs with c = 0 -> cn = 1 */
+                for (int l = 0; l < 4; ++l)
+                    if (e->contacts[i * 4 + l] == 0 && e->contacts[(i + 1) * 4 + l] == 1) m |= 1 << l;
+            e->td_mask[i * ORC_MAX_TD + j] = m;
+        }
 }
 
 /* One knot and one phase end, evaluated alone (test infrastructure for the known-answer and
@@ -832,21 +878,22 @@ void orc_knot_eval(const orc_problem *p, const orc_options *o, const int *c, con
     p1.horizons = hz;
     p1.shooting = NULL;
     double X[2 * NX], Xbar[2 * NX], U[NX], Ubar[NX], D[2 * NX], Db[2 * NX], dX[2 * NX], dU[NX], K[NN];
-    double RX[2 * NX], RU[2 * NX], RF[24], rd[20], re[20], as[4], al[4];
-    int cc[8];
+    double RX[2 * NX], RU[2 * NX], RF[24], rd[20], re[20], as[ORC_MAX_TD * 4], al[ORC_MAX_TD * 4];
+    int cc[8], tdm[ORC_MAX_TD] = {0, 0, 0, 0};
     memcpy(X, x, sizeof(double) * NX); memcpy(X + NX, x_end, sizeof(double) * NX);
     memcpy(U, u, sizeof(double) * NX);
     memcpy(RX, xr, sizeof(double) * NX); memcpy(RX + NX, xr_end, sizeof(double) * NX);
     memcpy(RU, ur, sizeof(double) * NX); memset(RU + NX, 0, sizeof(double) * NX);
     memcpy(RF, pf, sizeof(double) * 12); memcpy(RF + 12, pf_end, sizeof(double) * 12);
     memcpy(rd, reb_delta, sizeof rd); memcpy(re, reb_eps, sizeof re);
-    memcpy(as, sigma, sizeof as); memcpy(al, lambda, sizeof al);
-    for (int l = 0; l < 4; ++l) { cc[l] = c[l]; cc[4 + l] = cn[l]; }
+    memset(as, 0, sizeof as); memset(al, 0, sizeof al);
+    memcpy(as, sigma, 4 * sizeof(double)); memcpy(al, lambda, 4 * sizeof(double));
+    for (int l = 0; l < 4; ++l) { cc[l] = c[l]; cc[4 + l] = cn[l]; tdm[0] |= (c[l] == 0 && cn[l] == 1) << l; }
     orc_element e;
     memset(&e, 0, sizeof e);
     e.contacts = cc; e.x0 = x; e.ref_x = RX; e.ref_u = RU; e.ref_foot = RF;
     e.X = X; e.Xbar = Xbar; e.U = U; e.Ubar = Ubar; e.Defect = D; e.Defect_bar = Db; e.dX = dX; e.dU = dU; e.K = K;
-    e.reb_delta = rd; e.reb_eps = re; e.al_sigma = as; e.al_lambda = al;
+    e.reb_delta = rd; e.reb_eps = re; e.al_sigma = as; e.al_lambda = al; e.td_mask = tdm;
     ctx_t *C = (ctx_t *)calloc(1, sizeof(ctx_t));
     double *pool = (double *)calloc(8 * NN + 4 * NX + 64, sizeof(double));
     C->p = &p1; C->o = o; C->e = &e; C->P = 1; C->S = 2; C->Kc = 1;

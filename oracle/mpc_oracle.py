@@ -121,3 +121,70 @@ def shift(horizons, shooting, reach_end, Xbar, X, Ubar, K, contact_change):
     ub[0][0] = np.zeros_like(ub[0][0])
     flat = lambda L: np.array([r for ph in L for r in ph])
     return hz, ss, re, flat(xb), flat(ub), flat(kk)
+
+
+# ---- the constraint objects through the receding-horizon update --------------------------------
+MAX_TD = 4          # touchdown constraints per phase (HSDDP_MAX_TD)
+TD_PENDING = 0x10   # a constraint registered by the update whose legs come from the next contact rows
+
+
+def td_bits(c, cn):
+    """legs with contact 0 -> 1 (add_tconstr_one_phase's touchdown_status, HKDProblem.cpp:270-276)"""
+    return sum(1 << l for l in range(4) if c[l] == 0 and cn[l] == 1)
+
+
+def shift_constraints(horizons, reach_end, cons, contact_change, grf_delta, grf_eps, td_sigma, td_lambda):
+    """HKDProblem::update (HKDProblem.cpp:117-222) on one element's constraint objects, which live on
+    in the phases across MPC ticks (HKDProblem::update's reset_params is a no-op, ConstraintsBase.h:
+    165-167, 341-348).  cons: reb_delta, reb_eps [Kc][20]; td_mask [P][MAX_TD]; al_sigma, al_lambda
+    [P][MAX_TD][4].  Per step: the front knot's ReB row leaves with it (PathConstraintBase::pop_front)
+    or the whole first phase is dropped; a pushed-back knot copies the last knot's ReB row
+    (PathConstraintBase::push_back, ConstraintsBase.h:147-158); a new phase's GRF constraint starts
+    from the initial ReB parameters and carries no touchdown constraint; at every step whose last
+    phase has reached its end, add_tconstr_one_phase appends one more touchdown constraint with the
+    initial AL parameters (HKDProblem.cpp:199-202) — its legs follow from the next contact rows
+    (TD_PENDING, resolve_td).  Returns the new cons."""
+    hz, re = list(horizons), list(reach_end)
+    rd = split_phases(cons["reb_delta"], hz, False)
+    rs = split_phases(cons["reb_eps"], hz, False)
+    td = [list(zip([int(m) for m in cons["td_mask"][i]], [np.array(v) for v in cons["al_sigma"][i]],
+                   [np.array(v) for v in cons["al_lambda"][i]])) for i in range(len(hz))]
+    init_row = lambda v: np.full(20, v)  # noqa: E731
+    for cc in contact_change:
+        if hz[0] <= 1:
+            for L in (hz, re, rd, rs, td):
+                L.pop(0)
+        else:
+            rd[0].pop(0); rs[0].pop(0)
+            hz[0] -= 1
+        if cc and re[-1]:
+            hz.append(1); re.append(0)
+            rd.append([init_row(grf_delta)]); rs.append([init_row(grf_eps)])
+            td.append([(0, np.full(4, td_sigma), np.full(4, td_lambda)) for _ in range(MAX_TD)])
+        else:
+            rd[-1].append(np.array(rd[-1][-1])); rs[-1].append(np.array(rs[-1][-1]))
+            hz[-1] += 1
+            if cc:
+                re[-1] = 1
+        if re[-1]:  # one more touchdown constraint on the last phase, in its first free slot
+            slots = td[-1]
+            j = next((q for q, s in enumerate(slots) if s[0] == 0), None)
+            assert j is not None, "more than MAX_TD touchdown constraints on one phase"
+            slots[j] = (TD_PENDING, np.full(4, td_sigma), np.full(4, td_lambda))
+    flat = lambda L: np.array([r for ph in L for r in ph])  # noqa: E731
+    return {"reb_delta": flat(rd), "reb_eps": flat(rs),
+            "td_mask": np.array([[s[0] for s in ph] for ph in td], np.int32),
+            "al_sigma": np.array([[s[1] for s in ph] for ph in td]),
+            "al_lambda": np.array([[s[2] for s in ph] for ph in td])}
+
+
+def resolve_td(cons, contacts):
+    """TD_PENDING constraints take the touchdown legs of their phase's contact rows (i -> i + 1)"""
+    out = dict(cons)
+    m = np.array(cons["td_mask"], copy=True)
+    for i in range(m.shape[0]):
+        for j in range(m.shape[1]):
+            if m[i, j] == TD_PENDING:
+                m[i, j] = td_bits(contacts[i], contacts[i + 1])
+    out["td_mask"] = m
+    return out

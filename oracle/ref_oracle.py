@@ -193,6 +193,16 @@ class ProblemTracker:
         self.durations = [np.asarray(d) for d in plan["durations"]]
         self.reach_end = [0] * len(self.horizons)
         self.t_cur = F32(0)
+        # HKDProblemData's float phase clock and the phases' shooting sets (update_SS_config(N + 1)
+        # at initialization, HKDProblem.cpp:104)
+        self.start_times = [F32(v) for v in plan["start_times"]]
+        self.end_times = [F32(v) for v in plan["end_times"]]
+        self.shooting = [n + 1 for n in self.horizons]
+        # each phase's TouchDownConstraint objects (their legs), in registration order: one per phase
+        # at initialization (add_tconstr_one_phase, HKDProblem.cpp:104: registered when some leg
+        # touches down towards the next phase, or towards the contact at plan + dt_mpc for the last)
+        rows = self.contacts + [self.next]
+        self.td = [[m] if (m := _td_bits(rows[i], rows[i + 1])) else [] for i in range(len(self.horizons))]
 
     def _sample(self, t):
         k = min(self.start + sample_at(t, self.dt, self.sz), len(self.table) - 1)
@@ -208,31 +218,68 @@ class ProblemTracker:
             self.t_cur = F32(self.t_cur + self.dt)
             self.start += 1
             i += 1
-        if self.horizons[0] <= 1:
-            for a in (self.horizons, self.reach_end, self.contacts, self.durations):
+        new_start, new_end = self.t_cur, F32(self.t_cur + self.T)  # get_start_time / get_end_time
+        # front (HKDProblem.cpp:126-143): the phase clock and the knot count agree on when the first
+        # phase has shrunk to a point
+        pop = self.end_times[0] < new_start or _approx_eq(self.end_times[0], new_start)
+        assert pop == (self.horizons[0] <= 1), "phase clock and knot count disagree"
+        if pop:
+            for a in (self.horizons, self.reach_end, self.contacts, self.durations, self.start_times,
+                      self.end_times, self.shooting, self.td):
                 a.pop(0)
         else:
             self.horizons[0] -= 1
-        rel = F32(F32(self.t_cur + self.T) - self.t_cur)
+            self.start_times[0] = new_start
+        rel = F32(new_end - new_start)
         q = self._sample(rel)
         new = tuple(int(v) for v in q["contact"])
         cc = new != self.contacts[-1]
         if cc and self.reach_end[-1]:
-            self.horizons.append(1)
+            qn = float(F32(F32(new_end - self.end_times[-1]) / self.dt_sim))
+            hz_new = int(math.copysign(math.floor(abs(qn) + 0.5), qn))  # (int) round(...)
+            assert hz_new == 1, "a new phase starts with one knot"
+            self.start_times.append(self.end_times[-1])
+            self.end_times.append(new_end)
+            self.horizons.append(hz_new)
             self.reach_end.append(0)
             self.contacts.append(new)
             self.durations.append(q["status_dur"].copy())
+            self.shooting.append(0)  # SinglePhase::initialization clears SS_set
+            self.td.append([])       # create_problem_one_phase registers no terminal constraint
             self.next = new
         else:
+            self.end_times[-1] = new_end
             self.horizons[-1] += 1
             if cc:
                 self.reach_end[-1] = 1
-        if self.reach_end[-1]:
+        if self.reach_end[-1]:  # add_tconstr_one_phase at every step (HKDProblem.cpp:199-202)
             self.next = tuple(int(v) for v in self._sample(F32(self.T + self.dt_mpc))["contact"])
+            m = _td_bits(self.contacts[-1], self.next)
+            if m:
+                self.td[-1].append(m)
         return int(cc)
+
+    def update(self, n_steps=1):
+        """HKDProblem::update (:117-222): n_steps simulation steps, then update_SS_config for every
+        phase but a last one of horizon <= 2 (:203-217); returns the step flags"""
+        flags = [self.step() for _ in range(n_steps)]
+        P = len(self.horizons)
+        for i in range(P):
+            if i < P - 1 or self.horizons[i] > 2:
+                self.shooting[i] = self.horizons[i] + 1
+        return flags
+
+    def time_offsets(self):
+        """set_time_offset(phase_start_times[i] - phase_start_times[0]) (HKDProblem.cpp:206)"""
+        return [F32(s - self.start_times[0]) for s in self.start_times]
 
     def contact_rows(self):
         return np.array(self.contacts + [self.next], np.int32)
+
+
+def _td_bits(c, cn):
+    """legs with contact 0 -> 1 (touchdown_status, HKDProblem.cpp:270-276) as a mask"""
+    return sum(1 << l for l in range(4) if c[l] == 0 and cn[l] == 1)
 
 
 def reference_at(sample):

@@ -1,25 +1,28 @@
-// hkd_problem_example — HKDProblem's own problem assembly, registration for registration, solved
-// through the facade on the GPU.  The phases are built exactly as HKD-TrajOpt builds them
-// (HKDProblem.cpp): a std::bind of HKD::Model<T>::dynamics / dynamics_partial with the phase
-// contact and dt, HKDTrackingCost<T>(contact) on an HKDSinglePhaseReference, HKDFootPlaceReg<T>
-// (contact) on the QuadReference, GRFConstraint<T>(contact) with the GRF ReB parameters, a
-// std::bind of HKDReset<T>::resetmap(_partial) with (contact, next contact) and
-// TouchDownConstraint<T>(touchdown legs) with the TD AL parameters; HKDMPC's initial state and
-// solve follow (HKDMPC.cpp:18-70), then `ticks` receding-horizon updates (HKDProblem::update,
-// HKDProblem.cpp:117-222) each re-solved with max_AL_iter = 2, max_DDP_iter = 1 (HKDMPC.cpp:102-103).
+// hkd_problem_example — test driver (not product code): HKDProblem's own problem assembly,
+// registration for registration, solved through the facade on the GPU.  The phases are built
+// exactly as HKD-TrajOpt builds them (HKDProblem.cpp): a std::bind of HKD::Model<T>::dynamics /
+// dynamics_partial with the phase contact and dt, HKDTrackingCost<T>(contact) on an
+// HKDSinglePhaseReference, HKDFootPlaceReg<T>(contact) on the QuadReference, GRFConstraint<T>(contact)
+// with the GRF ReB parameters, a std::bind of HKDReset<T>::resetmap(_partial) with (contact, next
+// contact) and TouchDownConstraint<T>(touchdown legs) with the TD AL parameters; HKDMPC's initial
+// state and solve follow (HKDMPC.cpp:18-70), then `ticks` receding-horizon updates
+// (HKDProblem::update, HKDProblem.cpp:117-222), each re-solved by a new MultiPhaseDDP with
+// max_AL_iter = 2, max_DDP_iter = 1 (HKDMPCSolver::update, HKDMPC.cpp:96-143).
 //
-//   hkd_problem_example <quad_reference.csv> <ddp_setting.info> <constraint_params.info> <out_dir> [ticks]
+//   hkd_problem_example <quad_reference.csv> <ddp_setting.info> <constraint_params.info> <out_dir> [ticks] [describe]
 //
-// Writes per solve n = 0 .. ticks into out_dir: layout_<n>.txt (P, horizons, contacts), x0_<n>.f64,
-// Xbar_<n>.f64 [S][24], Ubar_<n>.f64 [Kc][24], K_<n>.f64 [Kc][24][24], A_<n>.f64, lx_<n>.f64,
-// G0_<n>.f64, H0_<n>.f64 (Trajectory exports) and info_<n>.txt (cost, feas, iters, status, n_ls).
+// Writes per solve n = 0 .. ticks into out_dir: layout_<n>.txt (P, horizons, shooting states),
+// x0_<n>.f64, Xbar_<n>.f64 [S][24], Ubar_<n>.f64 [Kc][24], K_<n>.f64 [Kc][24][24], A_<n>.f64,
+// lx_<n>.f64, G0_<n>.f64, H0_<n>.f64 (Trajectory exports), info_<n>.txt (cost, feas, iters, status,
+// n_ls) and handles.txt (device handles created over the run).  With `describe`: desc_<n>.txt and
+// the references / warm start each tick's solve would upload (no device work).
 #include <cstdio>
 #include <fstream>
 #include <functional>
 #include <iostream>
 #include <memory>
 
-#include "hkd_trajopt.hpp"
+#include "../../hkd-mpc_amd/facade/hkd_trajopt.hpp"
 
 namespace pc = std::placeholders;
 using std::make_shared;
@@ -238,6 +241,8 @@ static void dump(const std::string &dir, int n, HKDProblemData<double> &pdata, M
     std::ofstream lay(dir + "/layout" + sfx + ".txt");
     lay << pdata.n_phases;
     for (int i = 0; i < pdata.n_phases; ++i) lay << " " << pdata.phase_horizons[i];
+    for (int i = 0; i < pdata.n_phases; ++i)
+        lay << " " << std::dynamic_pointer_cast<SinglePhase<double, 24, 24, 0>>(pdata.phase_ptrs[i])->SS_set.size();
     lay << "\n";
     std::vector<double> x(x0.data(), x0.data() + 24), Xb, Ub, K, A, lx, G0, H0;
     for (int i = 0; i < pdata.n_phases; ++i) {
@@ -278,6 +283,7 @@ static void dump_problem(const std::string &dir, int n, const MultiPhaseDDP<doub
     f.precision(17);
     f << d.n_phases << " " << d.dt;
     for (int i = 0; i < d.n_phases; ++i) f << " " << d.horizons[i];
+    for (int i = 0; i < d.n_phases; ++i) f << " " << pr.shooting[i];
     f << "\n";
     for (int v : pr.contacts) f << v << " ";
     f << "\n";
@@ -286,6 +292,8 @@ static void dump_problem(const std::string &dir, int n, const MultiPhaseDDP<doub
     f << "\n";
     const double *c = (const double *)&d.cparams;
     for (size_t j = 0; j < sizeof d.cparams / sizeof(double); ++j) f << c[j] << " ";
+    f << "\n";
+    for (int v : pr.td_legs) f << v << " ";  // touchdown constraints per phase [P][HSDDP_MAX_TD]
     f << "\n";
     write_bin(dir + "/ref_x" + sfx + ".f64", pr.ref_x);
     write_bin(dir + "/ref_u" + sfx + ".f64", pr.ref_u);
@@ -310,9 +318,9 @@ int main(int argc, char **argv)
             HKDProblem<double> opt_problem;
             opt_problem.set_problem_data(&pdata, HKDPlanConfig{.6f, 0.01f, 1});
             opt_problem.initialization(argv[3]);
-            MultiPhaseDDP<double> solver;
             for (int n = 0; n <= ticks; ++n) {
                 if (n > 0) opt_problem.update();
+                MultiPhaseDDP<double> solver;
                 std::deque<shared_ptr<SinglePhaseBase<double>>> multiple_phases(pdata.phase_ptrs.begin(), pdata.phase_ptrs.end());
                 solver.set_multiPhaseProblem(multiple_phases);
                 solver.set_initial_condition(DVec<double>(24));
@@ -342,7 +350,7 @@ int main(int argc, char **argv)
         for (int a = 0; a < 3; ++a) xinit[3 + a] = pos[a];
         for (int j = 0; j < 12; ++j) xinit[12 + j] = qdummy[j];
 
-        MultiPhaseDDP<double> solver;
+        double last_cost = 0;
         for (int n = 0; n <= ticks; ++n) {
             if (n > 0) {
                 // HKDMPCSolver::update (HKDMPC.cpp:96-143): the receding-horizon update, the state
@@ -352,14 +360,19 @@ int main(int argc, char **argv)
                 ddp_options.max_AL_iter = 2;
                 ddp_options.max_DDP_iter = 1;
             }
+            // a new solver per tick, as HKDMPCSolver::update builds one (HKDMPC.cpp:127-131)
+            MultiPhaseDDP<double> solver;
             std::deque<shared_ptr<SinglePhaseBase<double>>> multiple_phases;
             for (auto phase : pdata.phase_ptrs) multiple_phases.push_back(phase);
             solver.set_multiPhaseProblem(multiple_phases);
             solver.set_initial_condition(xinit);
             solver.solve(ddp_options);
             dump(dir, n, pdata, solver, xinit);
+            last_cost = solver.get_actual_cost();
         }
-        std::printf("hkd_problem_example ok: %d phases, cost %.17g\n", pdata.n_phases, solver.get_actual_cost());
+        std::ofstream(dir + "/handles.txt") << MultiPhaseDDP<double>::handle_creations() << "\n";
+        std::printf("hkd_problem_example ok: %d phases, cost %.17g, %d device handle(s)\n", pdata.n_phases, last_cost,
+                    MultiPhaseDDP<double>::handle_creations());
     } catch (const std::exception &ex) {
         std::cerr << "error: " << ex.what() << "\n";
         return 1;

@@ -2,8 +2,8 @@
 """Fixtures for the reference-construction tests: the first samples of
 three of the reference's own trajectory data files, unchanged (data, not source):
 
-    Reference/Data/trot/quad_reference.csv            -> ref_trot.csv      (100 samples)
-    Reference/Data/flytrot/quad_reference.csv         -> ref_flytrot.csv   (80 samples)
+    Reference/Data/trot/quad_reference.csv            -> ref_trot.csv      (130 samples)
+    Reference/Data/flytrot/quad_reference.csv         -> ref_flytrot.csv   (110 samples)
     Reference/Data/gaitLib/run_jump/quad_reference.csv -> ref_run_jump.csv (40 samples; its dt is NaN, quirk A16)
 
 Run in the build container (where /root/reference exists):  python tests/golden/make_ref_fixtures.py
@@ -12,7 +12,7 @@ import os
 
 SRC = "/root/reference/Reference/Data"
 HERE = os.path.dirname(os.path.abspath(__file__))
-FILES = [("trot/quad_reference.csv", "ref_trot.csv", 100), ("flytrot/quad_reference.csv", "ref_flytrot.csv", 80),
+FILES = [("trot/quad_reference.csv", "ref_trot.csv", 130), ("flytrot/quad_reference.csv", "ref_flytrot.csv", 110),
          ("gaitLib/run_jump/quad_reference.csv", "ref_run_jump.csv", 40)]
 
 for src, dst, n in FILES:

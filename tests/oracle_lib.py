@@ -50,7 +50,7 @@ class OrcElement(C.Structure):
     _fields_ = [("contacts", IP), ("x0", DP), ("ref_x", DP), ("ref_u", DP), ("ref_foot", DP),
                 ("Xbar", DP), ("X", DP), ("Defect", DP), ("Defect_bar", DP), ("dX", DP),
                 ("Ubar", DP), ("U", DP), ("dU", DP), ("K", DP),
-                ("reb_delta", DP), ("reb_eps", DP), ("al_sigma", DP), ("al_lambda", DP),
+                ("reb_delta", DP), ("reb_eps", DP), ("al_sigma", DP), ("al_lambda", DP), ("td_mask", IP),
                 ("cost", C.c_double), ("feas", C.c_double), ("merit", C.c_double),
                 ("max_tconstr", C.c_double), ("max_pconstr", C.c_double),
                 ("iters", C.c_int), ("outer_iters", C.c_int), ("status", C.c_int),
@@ -202,10 +202,17 @@ def riccati_lq(N, A, B, lxx, luu, lx=None, lu=None, Phix=None, Phixx=None, reg=0
 
 
 # ---- solver -----------------------------------------------------------------------------------
+MAX_TD = 4  # ORC_MAX_TD / HSDDP_MAX_TD
+CONSTRAINT_FIELDS = ("reb_delta", "reb_eps", "al_sigma", "al_lambda", "td_mask")
+
+
 def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 1,
-                elements=None, weights: dict | None = None) -> dict:
+                elements=None, weights: dict | None = None, constraints: dict | None = None) -> dict:
     """Run the oracle solve on (a subset of) a synthetic batch; returns per-element outputs.
-    weights: HKD cost-weight overrides by field name (e.g. {"r_qJd": -0.5})."""
+    weights: HKD cost-weight overrides by field name (e.g. {"r_qJd": -0.5}).
+    constraints: the elements' constraint parameters (CONSTRAINT_FIELDS, [B] leading axis) to start
+    from instead of a new problem's (orc_init_element) — an MPC tick's carried-over ReB / AL
+    parameters and touchdown constraints; the outputs carry them after the solve."""
     options = options or default_options()
     B = prob["batch"]
     idx = list(range(B)) if elements is None else list(elements)
@@ -226,7 +233,8 @@ def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 
         "U": np.ascontiguousarray(prob["Ubar"][idx]).copy(), "dU": np.zeros((n, Kc, 24)),
         "K": (np.zeros((n, Kc, 24, 24)) if prob.get("K") is None else np.ascontiguousarray(prob["K"][idx]).copy()),
         "reb_delta": np.zeros((n, Kc, 20)), "reb_eps": np.zeros((n, Kc, 20)),
-        "al_sigma": np.zeros((n, P, 4)), "al_lambda": np.zeros((n, P, 4)),
+        "al_sigma": np.zeros((n, P, MAX_TD, 4)), "al_lambda": np.zeros((n, P, MAX_TD, 4)),
+        "td_mask": np.zeros((n, P, MAX_TD), np.int32),
     }
     contacts = np.ascontiguousarray(prob["contacts"][idx])
     x0 = np.ascontiguousarray(prob["x0"][idx])
@@ -243,8 +251,11 @@ def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 
         keep += [rx, ru, rf]
         e.ref_x, e.ref_u, e.ref_foot = dp(rx), dp(ru), dp(rf)
         for k in st:
-            setattr(e, k, dp(st[k][j]))
+            setattr(e, k, ip(st[k][j]) if st[k].dtype == np.int32 else dp(st[k][j]))
         lib().orc_init_element(C.byref(p), C.byref(e))
+        if constraints is not None:
+            for k in CONSTRAINT_FIELDS:
+                st[k][j] = constraints[k][b]
     hcap = 1 + options.max_AL_iter * options.max_DDP_iter
     hist = np.zeros((n, hcap, 4), np.float32)
     for j in range(n):

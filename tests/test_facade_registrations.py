@@ -35,14 +35,18 @@ import ref_oracle as R  # noqa: E402
 F32 = np.float32
 
 
+DRIVERS = os.path.join(ROOT, "tests", "drivers")
+
+
 def _make():
-    r = subprocess.run(["make", "-C", os.path.join(PKG, "facade")], capture_output=True, text=True)
-    assert r.returncode == 0, r.stdout + r.stderr
+    for d in (os.path.join(PKG, "facade"), DRIVERS):
+        r = subprocess.run(["make", "-C", d], capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
 
 
 def _run(out, csv, ticks=0, describe=False):
     _make()
-    cmd = [os.path.join(PKG, "hkd_problem_example"), csv, SETTINGS, CPARAMS, str(out), str(ticks)]
+    cmd = [os.path.join(DRIVERS, "hkd_problem_example"), csv, SETTINGS, CPARAMS, str(out), str(ticks)]
     if describe:
         cmd.append("describe")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
@@ -147,3 +151,103 @@ def test_reference_registrations_solve_equals_ctypes_path(tmp_path, name):
     assert float(cost) == info["cost"][0]
     assert (int(iters), int(outer), int(status), int(nls)) == (
         info["iters"][0], info["outer_iters"][0], info["status"][0], info["n_ls_trials"][0])
+
+
+def _layout(out, n):
+    v = [int(t) for t in open(os.path.join(out, f"layout_{n}.txt")).read().split()]
+    P = v[0]
+    return v[1:1 + P], v[1 + P:1 + 2 * P]
+
+
+TICKS = 30
+
+
+@pytest.mark.parametrize("name", ["trot", "flytrot"])
+def test_describe_ticks_equal_reference_update(tmp_path, name):
+    """Ticks 1..24 (HKDProblem::update, HKDProblem.cpp:117-222, on the facade's phases): every tick's
+    device problem — layout, shooting states (SS_set: a new last phase of <= 2 knots keeps an empty
+    one, SinglePhase.cpp:34 / HKDProblem.cpp:214-218), contacts, references at the phases' float
+    time offsets and the shifted warm start — equals the restated bookkeeping (oracle
+    ProblemTracker + mpc_oracle.shift).  Bit-exact."""
+    import mpc_oracle as M
+    csv = os.path.join(GOLD, f"ref_{name}.csv")
+    _run(tmp_path, csv, ticks=TICKS, describe=True)
+    table, dt_ref = R.load_quad_reference(csv)
+    n_win = int(round(0.6 / float(dt_ref))) + 2
+    tk = R.ProblemTracker(table, 0, dt_ref)
+    xb = None
+    tails = multi = 0
+    for n in range(TICKS + 1):
+        flags = tk.update(1) if n > 0 else []
+        d = _desc(tmp_path, n)
+        P = d["P"]
+        shooting = [int(v) for v in open(os.path.join(tmp_path, f"desc_{n}.txt")).readline().split()[2 + P:2 + 2 * P]]
+        assert d["horizons"] == tk.horizons and sum(d["horizons"]) == 60, n
+        assert shooting == tk.shooting, n
+        tails += shooting[-1] < d["horizons"][-1] + 1
+        assert np.array_equal(d["contacts"], tk.contact_rows()), n
+        td = [int(v) for v in open(os.path.join(tmp_path, f"desc_{n}.txt")).read().split("\n")[4].split()]
+        assert [[m for m in td[4 * i:4 * i + 4] if m] for i in range(P)] == tk.td, n
+        multi += max(len(t) for t in tk.td) > 1
+        S = sum(h + 1 for h in d["horizons"])
+        rx, ru, rf = R.reference_slots(table, tk.start, n_win, dt_ref, d["horizons"], 0.01, tk.start_times)
+        got = lambda f, w: np.fromfile(os.path.join(tmp_path, f"{f}_{n}.f64")).reshape(S, w)  # noqa: E731
+        assert np.array_equal(got("ref_x", 24), rx), n
+        assert np.array_equal(got("ref_u", 24), ru), n
+        assert np.array_equal(got("ref_foot", 12), rf), n
+        if n == 0:
+            xb = got("Xbar", 24)
+            hz, ss, re = list(d["horizons"]), list(shooting), [0] * P
+            ub, kk = np.zeros((60, 24)), np.zeros((60, 24, 24))
+        else:  # no solve in between: the warm start is the initial one, shifted (X = Xbar)
+            hz, ss, re, xb, ub, kk = M.shift(hz, ss, re, xb, xb, ub, kk, flags)
+            assert hz == d["horizons"] and ss == shooting, n
+            assert np.array_equal(got("Xbar", 24), xb), n
+    assert tails >= 1  # the run crosses ticks whose new last phase has no shooting states
+    if name == "trot":  # ... and ticks with a phase carrying more than one touchdown constraint
+        assert multi >= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["trot", "flytrot"])
+def test_facade_ticks_equal_capi_mpc_path(tmp_path, name):
+    """HKDMPCSolver's loop through the facade — HKDProblem::update on the host Trajectory deques,
+    a new MultiPhaseDDP per tick (HKDMPC.cpp:96-143) — equals the C-ABI MPC path on one handle
+    (hsddp_advance: the same bookkeeping and the warm-start shift on the device, then
+    hsddp_update_problem + hsddp_solve) bit for bit at every tick: Xbar, Ubar, K, the LQ model,
+    G[0] / H[0], cost and iteration counts.  The facade keeps one device handle over all ticks."""
+    csv = os.path.join(GOLD, f"ref_{name}.csv")
+    _run(tmp_path, csv, ticks=TICKS)
+    assert open(os.path.join(tmp_path, "handles.txt")).read().split() == ["1"]
+    table, dt_ref = hsddp.load_quad_reference(csv)
+    rd = lambda f, n, shape: np.fromfile(os.path.join(tmp_path, f"{f}_{n}.f64")).reshape(shape)  # noqa: E731
+    x0 = rd("x0", 0, (1, 24))
+    p = hsddp.reference_problem(table, dt_ref, [0], x0)
+    s = hsddp.Solver(p, hsddp.load_settings(SETTINGS))
+    s.set_value_export(True)
+    tails = 0
+    for n in range(TICKS + 1):
+        if n > 0:
+            s.advance(None)
+            s.update_problem(None, rd("x0", n, (1, 24)))
+            s.set_options(hsddp.load_settings(SETTINGS, max_AL_iter=2, max_DDP_iter=1))
+        s.solve()
+        lay = s.layout()
+        hz, ss = _layout(tmp_path, n)
+        assert lay["horizons"] == hz and lay["shooting"] == ss, n
+        tails += ss[-1] < hz[-1] + 1
+        S, Kc, P = sum(h + 1 for h in hz), sum(hz), len(hz)
+        tr, info, lq, val = s.trajectory(), s.element_info(), s.lq(), s.value()
+        assert np.array_equal(rd("Xbar", n, (S, 24)), tr["Xbar"][0]), n
+        assert np.array_equal(rd("Ubar", n, (Kc, 24)), tr["Ubar"][0]), n
+        assert np.array_equal(rd("K", n, (Kc, 24, 24)), tr["K"][0]), n
+        assert np.array_equal(rd("A", n, (Kc, 24, 24)), lq["A"][0]), n
+        assert np.array_equal(rd("lx", n, (Kc, 24)), lq["lx"][0]), n
+        assert np.array_equal(rd("G0", n, (P, 24)), val["G"][0]), n
+        assert np.array_equal(rd("H0", n, (P, 24, 24)), val["H"][0]), n
+        cost, feas, iters, outer, status, nls = open(os.path.join(tmp_path, f"info_{n}.txt")).read().split()
+        assert float(cost) == info["cost"][0], n
+        assert (int(iters), int(outer), int(status), int(nls)) == (
+            info["iters"][0], info["outer_iters"][0], info["status"][0], info["n_ls_trials"][0]), n
+    s.close()
+    assert tails >= 1

@@ -60,3 +60,41 @@ def test_graph_solve_equals_launches(B, P, N, gait):
 
     changes = (new_x0, new_alpha)
     _equal(_solve(prob, opt, True, changes), _solve(prob, opt, False, changes))
+
+
+def test_graph_cache_eviction_equals_launches():
+    """More distinct (alpha, Params) keys than the handle's 8 cached graphs: every miss past the
+    eighth evicts a graph that may be the iteration queued last; the results must still equal
+    launch-by-launch issue (eviction drains the stream before destroying the exec)."""
+    prob = syn.make_batch(4, 2, 10, "trot")
+    opt = hsddp.load_settings()
+
+    def with_alpha(a):
+        def ch(s):
+            o = hsddp.load_settings()
+            o.alpha = a
+            s.set_options(o)
+            s.upload_problem(prob["contacts"], prob["x0"], prob["ref_x"], prob["ref_u"], prob["ref_foot"])
+        return ch
+
+    changes = tuple(with_alpha(a) for a in (0.5, 0.3, 0.2, 0.15, 0.25, 0.35, 0.45, 0.55, 0.6, 0.5, 0.1, 0.3))
+    _equal(_solve(prob, opt, True, changes), _solve(prob, opt, False, changes))
+
+
+@pytest.mark.parametrize("gait,P,N", [("trot", 4, 10), ("jump", 8, 5)])
+def test_graph_nonuniform_reb_schedule_equals_launches(gait, P, N):
+    """update_ReB = 7, update_relax = 0.1 with several outer iterations and early exits on: the
+    second and later outer iterations run k_lq's slot-recompute variant (lq_slots = 1) inside the
+    captured graph."""
+    prob = syn.make_batch(8, P, N, gait)
+    opt = hsddp.load_settings(max_AL_iter=3, update_ReB=7.0, update_relax=0.1)
+    _equal(_solve(prob, opt, True), _solve(prob, opt, False))
+
+
+def test_graph_mixed_layouts_equals_launches():
+    """Per-element layouts (trot-like n x N beside jumps on 2n x N/2) with early exits."""
+    names = ["trot", "jump", "pace", "jump", "bound", "pronk", "jump"]
+    lays = [(g, 8, 5) if g == "jump" else (g, 4, 10) for g in (names[b % len(names)] for b in range(11))]
+    prob = syn.make_layout_batch(lays)
+    opt = hsddp.load_settings(max_AL_iter=3)
+    _equal(_solve(prob, opt, True), _solve(prob, opt, False))

@@ -110,7 +110,8 @@ def test_mpc_loop_matches_oracle():
     assert _rel(g["Xbar"], r["Xbar"]) < 1e-9
     kw = dict(max_AL_iter=2, max_DDP_iter=1)
     s.set_options(hsddp.load_settings(**kw))
-    tails = 0
+    tails = n_td = 0
+    op, _ = O.default_problem(prob["horizons"], prob["dt"])  # the initial ReB / AL parameters
     for it in range(9):
         lay0 = s.layout()
         flags = sc.step(1)
@@ -119,6 +120,13 @@ def test_mpc_loop_matches_oracle():
         sh = [M.shift(lay0["horizons"], lay0["shooting"], lay0["reach_end"], r["Xbar"][b], r["X"][b],
                       r["Ubar"][b], r["K"][b], flags) for b in range(B)]
         inp = sc.inputs(np.stack([q[3][0] for q in sh]))
+        # the constraint objects live on: ReB / AL parameters carried over, one more touchdown
+        # constraint on a last phase that has reached its end (HKDProblem.cpp:199-202)
+        cons = [M.resolve_td(M.shift_constraints(lay0["horizons"], lay0["reach_end"],
+                                                 {k: r[k][b] for k in O.CONSTRAINT_FIELDS}, flags, op.grf_delta,
+                                                 op.grf_eps, op.td_sigma, op.td_lambda), inp["contacts"][b])
+                for b in range(B)]
+        cons = {k: np.stack([c[k] for c in cons]) for k in O.CONSTRAINT_FIELDS}
         s.update_problem(inp["contacts"], inp["x0"], inp["ref_x"], inp["ref_u"], inp["ref_foot"])
         s.solve()
         g = {**s.trajectory(), **s.working(), **s.element_info()}
@@ -126,10 +134,16 @@ def test_mpc_loop_matches_oracle():
               "S": sum(n + 1 for n in lay["horizons"]), "Kc": sum(lay["horizons"]), **inp,
               "Xbar": np.stack([q[3] for q in sh]), "Ubar": np.stack([q[4] for q in sh]),
               "K": np.stack([q[5] for q in sh])}
-        r = O.solve_batch(p2, O.default_options(**kw), n_threads=8)
+        r = O.solve_batch(p2, O.default_options(**kw), n_threads=8, constraints=cons)
+        dc = s.constraint_params()
+        assert np.array_equal(dc["td_mask"], r["td_mask"]), it
+        n_td = max(n_td, int((dc["td_mask"] != 0).sum(axis=2).max()))
+        for f in ("al_sigma", "al_lambda", "reb_delta", "reb_eps"):
+            assert _rel(dc[f], r[f]) < 1e-9, (it, f)
         for f in ("Xbar", "Ubar", "X", "K"):
             assert _rel(g[f], r[f]) < 1e-8, (it, f)
         assert np.array_equal(g["n_ls_trials"], r["n_ls_trials"]), it
         assert _rel(g["cost"], r["cost"]) < 1e-9, it
     assert tails >= 2  # the loop passed through last phases without shooting states
+    assert n_td >= 1   # (phases carrying two touchdown constraints: test_gpu_reference.py's file-driven loop)
     s.close()

@@ -204,3 +204,63 @@ def test_advance_matches_tracker(name, start, steps, n):
             assert np.all(cmd["N_mpcsteps"] == 8)
     assert n_new >= 2  # the window crossed contact switches
     dev.close(); host.close()
+
+
+def test_advance_loop_matches_oracle():
+    """HKDMPCSolver's loop on the reference's trot file (HKDMPC.cpp:57-165): the initial solve with
+    the shipped settings, then 25 ticks of hsddp_advance + re-solve (max_AL_iter = 2, max_DDP_iter =
+    1), against the oracle doing the same with the restated bookkeeping — warm start
+    (mpc_oracle.shift), references, and the constraint objects that live on in the phases: per-knot
+    ReB and per-constraint AL parameters carried over (reset_params is a no-op) and one more
+    touchdown constraint at every step a last phase has reached its end (mpc_oracle.
+    shift_constraints; HKDProblem.cpp:199-202).  The run crosses phases carrying two touchdown
+    constraints."""
+    import mpc_oracle as M
+    tab, ref, dt = _load("trot")
+    B = 2
+    p = hsddp.reference_problem(tab, dt, [0], _x0(B))
+    dev = hsddp.Solver(p, hsddp.load_settings())
+    dev.solve()
+    q = _host_prob(p, ref, dt)
+    r = O.solve_batch(q, O.default_options(), n_threads=2)
+    g = dev.trajectory()
+    for f in ("Xbar", "Ubar", "K"):
+        assert np.max(np.abs(g[f] - r[f])) <= 1e-8 * np.max(np.abs(r[f])), f
+    kw = dict(max_AL_iter=2, max_DDP_iter=1)
+    dev.set_options(hsddp.load_settings(**kw))
+    op, _ = O.default_problem(p["horizons"], p["dt"])
+    tk = R.ProblemTracker(ref, 0, dt)
+    n_td = 0
+    for it in range(25):
+        lay0 = dev.layout()
+        x0 = _x0(B, 100 + it)
+        flags = dev.advance(x0, 1)
+        assert flags == tk.update(1), it
+        lay = dev.layout()
+        assert lay["horizons"] == tk.horizons and lay["shooting"] == tk.shooting, it
+        rows = tk.contact_rows()
+        sh = [M.shift(lay0["horizons"], lay0["shooting"], lay0["reach_end"], r["Xbar"][b], r["X"][b], r["Ubar"][b],
+                      r["K"][b], flags) for b in range(B)]
+        cons = [M.resolve_td(M.shift_constraints(lay0["horizons"], lay0["reach_end"],
+                                                 {k: r[k][b] for k in O.CONSTRAINT_FIELDS}, flags, op.grf_delta,
+                                                 op.grf_eps, op.td_sigma, op.td_lambda), rows) for b in range(B)]
+        cons = {k: np.stack([c[k] for c in cons]) for k in O.CONSTRAINT_FIELDS}
+        rx, ru, rf = _oracle_refs(ref, [tk.start], tk.horizons, dt)
+        p2 = {"batch": B, "horizons": tk.horizons, "shooting": tk.shooting, "dt": p["dt"],
+              "S": sum(n + 1 for n in tk.horizons), "Kc": sum(tk.horizons), "x0": x0,
+              "contacts": np.repeat(rows[None], B, axis=0), "ref_x": rx, "ref_u": ru, "ref_foot": rf,
+              "Xbar": np.stack([s[3] for s in sh]), "Ubar": np.stack([s[4] for s in sh]), "K": np.stack([s[5] for s in sh])}
+        dc = dev.constraint_params()
+        assert np.array_equal(dc["td_mask"], cons["td_mask"]), it
+        assert [[m for m in dc["td_mask"][0, i] if m] for i in range(len(tk.horizons))] == tk.td, it
+        n_td = max(n_td, max(len(t) for t in tk.td))
+        dev.solve()
+        r = O.solve_batch(p2, O.default_options(**kw), n_threads=2, constraints=cons)
+        g, dc = {**dev.trajectory(), **dev.working(), **dev.element_info()}, dev.constraint_params()
+        for f in ("al_sigma", "al_lambda", "reb_delta", "reb_eps"):
+            assert np.max(np.abs(dc[f] - r[f])) <= 1e-9 * max(1.0, np.max(np.abs(r[f]))), (it, f)
+        for f in ("Xbar", "Ubar", "X", "K"):
+            assert np.max(np.abs(g[f] - r[f])) <= 1e-8 * np.max(np.abs(r[f])), (it, f)
+        assert np.array_equal(g["n_ls_trials"], r["n_ls_trials"]), it
+    assert n_td >= 2
+    dev.close()

@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
 import ref_oracle as R  # noqa: E402
 
 GOLD = os.path.join(HERE, "golden")
-FILES = {"trot": 100, "flytrot": 80, "run_jump": 40}
+FILES = {"trot": 130, "flytrot": 110, "run_jump": 40}
 
 
 def path(name):
