@@ -266,6 +266,12 @@ struct hsddp_handle_t {
     std::vector<Layout> lays;
     std::vector<int> reach_el;  // [B][16] is_phase_reach_end per element (with per-element layouts)
     double *value0 = nullptr;  // G[0], H[0] per phase [B][16][600] (hsddp_set_value_export)
+    // asynchronous command extraction (hsddp_extract_commands_async): two device record buffers, two
+    // pinned host buffers, a copy stream and per buffer the event of its last copy
+    hsddp_mpc_command *cmd_dev[2] = {nullptr, nullptr}, *cmd_host[2] = {nullptr, nullptr};
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t cmd_ready[2] = {nullptr, nullptr}, cmd_copied[2] = {nullptr, nullptr};
+    int cmd_next = 0;
 };
 
 // device staging area of at least `bytes` (contents not preserved when it grows)
@@ -515,6 +521,14 @@ extern "C" int hsddp_destroy(hsddp_handle h)
     for (hipEvent_t e : h->iter_done)
         if (e) hipEventDestroy(e);
     if (h->host_counter) hipHostFree(h->host_counter);
+    if (h->copy_stream) hipStreamSynchronize(h->copy_stream);
+    for (int q = 0; q < 2; ++q) {
+        if (h->cmd_dev[q]) hipFree(h->cmd_dev[q]);
+        if (h->cmd_host[q]) hipHostFree(h->cmd_host[q]);
+        if (h->cmd_ready[q]) hipEventDestroy(h->cmd_ready[q]);
+        if (h->cmd_copied[q]) hipEventDestroy(h->cmd_copied[q]);
+    }
+    if (h->copy_stream) hipStreamDestroy(h->copy_stream);
     for (hipEvent_t e : h->events) hipEventDestroy(e);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
@@ -1590,7 +1604,8 @@ extern "C" int hsddp_device_synchronize(int device)
 // ---- MPC command extraction (HKDMPCSolver::update_foot_placement + publish_mpc_cmd) ----------
 static int extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
                             const double *status_durations, int durations_per_element, const float *foot_placements,
-                            int feet_per_element, float solve_time, hsddp_mpc_command *out, bool out_on_device);
+                            int feet_per_element, float solve_time, hsddp_mpc_command *out, bool out_on_device,
+                            int ticket = -1);
 
 extern "C" int hsddp_extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
                                       const double *status_durations, int durations_per_element,
@@ -1610,13 +1625,16 @@ extern "C" int hsddp_extract_commands_device(hsddp_handle h, int nsteps_between_
                             foot_placements, feet_per_element, solve_time, (hsddp_mpc_command *)out_device, true);
 }
 
+// ticket >= 0 (asynchronous form): the records go to device buffer `ticket` and from there to its
+// pinned host buffer on the copy stream; out is unused
 static int extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
                             const double *status_durations, int durations_per_element, const float *foot_placements,
-                            int feet_per_element, float solve_time, hsddp_mpc_command *out, bool out_on_device)
+                            int feet_per_element, float solve_time, hsddp_mpc_command *out, bool out_on_device,
+                            int ticket)
 {
     if (h && !h->lays.empty())
         return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts (hsddp_set_element_layouts): the MPC-side steps need the handle's shared layout");
-    if (!h || !out) return fail(HSDDP_ERR_ARG, "null argument");
+    if (!h || (!out && ticket < 0)) return fail(HSDDP_ERR_ARG, "null argument");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     const Params &p = h->p;
     CmdArgs a{};
@@ -1643,7 +1661,7 @@ static int extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_t
     char *buf;
     int rc;
     if ((rc = scratch(h, cmd_bytes + dur_bytes + feet_bytes, &buf))) return rc;
-    hsddp_mpc_command *dcmd = out_on_device ? out : (hsddp_mpc_command *)buf;
+    hsddp_mpc_command *dcmd = ticket >= 0 ? h->cmd_dev[ticket] : out_on_device ? out : (hsddp_mpc_command *)buf;
     if (status_durations) {
         a.durations = (const double *)(buf + cmd_bytes);
         if ((rc = h2d((void *)a.durations, status_durations, (a.dur_per_elem ? B : 1) * p.P * 4 * sizeof(double), h->stream))) return rc;
@@ -1652,10 +1670,56 @@ static int extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_t
         a.feet = (const float *)(buf + cmd_bytes + dur_bytes);
         if ((rc = h2d((void *)a.feet, foot_placements, feet_bytes, h->stream))) return rc;
     }
+    if (ticket >= 0)  // the buffer's previous copy (two extractions ago) has left it
+        HIPCHK(hipStreamWaitEvent(h->stream, h->cmd_copied[ticket], 0));
     launch_extract_commands(p, h->d, a, dcmd, h->stream);
     HIPCHK(hipGetLastError());
+    if (ticket >= 0) {  // D2H on the copy stream, behind the kernel: the handle's stream moves on
+        HIPCHK(hipEventRecord(h->cmd_ready[ticket], h->stream));
+        HIPCHK(hipStreamWaitEvent(h->copy_stream, h->cmd_ready[ticket], 0));
+        HIPCHK(hipMemcpyAsync(h->cmd_host[ticket], dcmd, B * sizeof(hsddp_mpc_command), hipMemcpyDeviceToHost,
+                              h->copy_stream));
+        HIPCHK(hipEventRecord(h->cmd_copied[ticket], h->copy_stream));
+        return HSDDP_OK;
+    }
     if (!out_on_device) HIPCHK(hipMemcpyAsync(out, dcmd, B * sizeof(hsddp_mpc_command), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_extract_commands_async(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
+                                            const double *status_durations, int durations_per_element,
+                                            const float *foot_placements, int feet_per_element, float solve_time,
+                                            int *ticket)
+{
+    if (!h || !ticket) return fail(HSDDP_ERR_ARG, "null argument");
+    HIPCHK(hipSetDevice(h->desc.device));
+    const size_t bytes = (size_t)h->p.B * sizeof(hsddp_mpc_command);
+    if (!h->copy_stream) {  // first use: two record buffers on each side, the copy stream, events
+        HIPCHK(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+        for (int q = 0; q < 2; ++q) {
+            HIPCHK(hipMalloc((void **)&h->cmd_dev[q], bytes));
+            HIPCHK(hipHostMalloc((void **)&h->cmd_host[q], bytes, 0));
+            HIPCHK(hipEventCreateWithFlags(&h->cmd_ready[q], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&h->cmd_copied[q], hipEventDisableTiming));
+            HIPCHK(hipEventRecord(h->cmd_copied[q], h->copy_stream));
+        }
+    }
+    const int t = h->cmd_next;
+    const int rc = extract_commands(h, nsteps_between_mpc, mpc_time, dt_mpc, status_durations, durations_per_element,
+                                    foot_placements, feet_per_element, solve_time, nullptr, false, t);
+    if (rc) return rc;
+    h->cmd_next ^= 1;
+    *ticket = t;
+    return HSDDP_OK;
+}
+
+extern "C" int hsddp_commands_wait(hsddp_handle h, int ticket, const hsddp_mpc_command **records)
+{
+    if (!h || !records) return fail(HSDDP_ERR_ARG, "null argument");
+    if (ticket < 0 || ticket > 1 || !h->copy_stream) return fail(HSDDP_ERR_ARG, "no such extraction ticket");
+    HIPCHK(hipEventSynchronize(h->cmd_copied[ticket]));
+    *records = h->cmd_host[ticket];
     return HSDDP_OK;
 }
 

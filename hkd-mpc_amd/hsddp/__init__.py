@@ -285,6 +285,30 @@ class Solver:
             float(solve_time), out.ctypes.data))
         return out
 
+    def extract_commands_async(self, nsteps_between_mpc: int = 1, mpc_time: float = 0.0, dt_mpc: float = 0.01,
+                               status_durations=None, foot_placements=None, solve_time: float = 0.0) -> int:
+        """hsddp_extract_commands_async: the records cross PCIe on the handle's copy stream while the
+        caller goes on (the next tick's advance / solve); returns the ticket for commands_wait."""
+        dur = None if status_durations is None else np.ascontiguousarray(status_durations, dtype=np.float64)
+        feet = None if foot_placements is None else np.ascontiguousarray(foot_placements, dtype=np.float32)
+        self._cmd_keep = (dur, feet)
+        t = C.c_int()
+        check(lib().hsddp_extract_commands_async(
+            self._h, int(nsteps_between_mpc), float(mpc_time), float(dt_mpc),
+            None if dur is None else dur.ctypes.data, int(dur is not None and dur.ndim == 3),
+            None if feet is None else feet.ctypes.data, int(feet is not None and feet.ndim == 2),
+            float(solve_time), C.byref(t)))
+        return t.value
+
+    def commands_wait(self, ticket: int, copy: bool = True) -> np.ndarray:
+        """the [B] records of an asynchronous extraction (a copy, or a view of the pinned buffer that
+        the extraction after next overwrites)"""
+        ptr = C.c_void_p()
+        check(lib().hsddp_commands_wait(self._h, int(ticket), C.byref(ptr)))
+        buf = (C.c_char * (self.B * MPC_COMMAND.itemsize)).from_address(ptr.value)
+        v = np.frombuffer(buf, dtype=MPC_COMMAND, count=self.B)
+        return v.copy() if copy else v
+
     def extract_commands_device(self, out_ptr: int, nsteps_between_mpc: int = 1, mpc_time: float = 0.0,
                                 dt_mpc: float = 0.01, solve_time: float = 0.0) -> None:
         """extract_commands into device memory at out_ptr ([B] hsddp_mpc_command on the handle's

@@ -31,7 +31,7 @@
  *                                             setup (warm start reused)  HKDProblem.cpp:117-222; HKDMPC.cpp:96-143
  *   hsddp_set_layout                          a caller-side HKDProblem::update's layout + SinglePhase::
  *                                             update_SS_config (SS_set)  HKDProblem.cpp:203-217; SinglePhase.h:161-164
- *   hsddp_extract_commands                    update_foot_placement + publish_mpc_cmd HKDMPC.cpp:207-298
+ *   hsddp_extract_commands(_async)            update_foot_placement + publish_mpc_cmd HKDMPC.cpp:207-298
  *   hsddp_hkd_dynamics                        HKD::Model::dynamics (hkinodyn)       HKDModel.h:33-45
  *   hsddp_hkd_dynamics_partial                HKD::Model::dynamics_partial          HKDModel.h:46-61
  *   hsddp_hkd_resetmap(_partial)              HKDReset::resetmap(_partial)          HKDReset.h:41-136
@@ -383,6 +383,16 @@ int hsddp_extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_ti
                            const double *status_durations, int durations_per_element,
                            const float *foot_placements, int feet_per_element, float solve_time,
                            hsddp_mpc_command *out);
+/* hsddp_extract_commands without waiting for the records: the kernel runs on the handle's stream
+ * and the [B] records (7.8 KB each) cross PCIe into one of two pinned host buffers of the handle on a
+ * copy stream of their own, so the copy overlaps whatever the caller issues next (the next tick's
+ * hsddp_advance / hsddp_solve).  ticket receives the buffer (0 or 1); hsddp_commands_wait(h,
+ * ticket, &records) waits for that copy and points records at the buffer, which stays valid until
+ * the extraction after next reuses it. */
+int hsddp_extract_commands_async(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
+                                 const double *status_durations, int durations_per_element,
+                                 const float *foot_placements, int feet_per_element, float solve_time, int *ticket);
+int hsddp_commands_wait(hsddp_handle h, int ticket, const hsddp_mpc_command **records);
 /* The same into device memory: out_device [B] hsddp_mpc_command on the handle's device (no host
  * copy) — the optional first-knots command block of the final multi-GPU gather (SURVEY.md §8(e),
  * HKDMPC.cpp:254-286), gathered by the caller's collective straight from HBM. */

@@ -46,6 +46,39 @@ def test_commands_match_oracle(P, N, mixed, fp32, nsteps):
                 assert np.array_equal(g[f], r[f]), (b, f)
 
 
+def test_async_commands_equal_sync_across_ticks():
+    """hsddp_extract_commands_async: the records of tick t, copied on the handle's copy stream while
+    tick t + 1 is shifted and re-solved, equal the synchronous extraction of tick t field for field;
+    the two pinned buffers alternate and a buffer is reused only after its copy completed."""
+    B, P, N = 19, 4, 5
+    sc, prob = _scenario_batch(B, P, N)
+    s = hsddp.Solver(prob, hsddp.load_settings(max_AL_iter=2, max_DDP_iter=1))
+    s.solve()
+    rng = np.random.default_rng(11)
+    pending = None
+    for it in range(7):
+        dur = rng.uniform(0.1, 0.4, (B, len(s.layout()["horizons"]), 4))
+        feet = rng.standard_normal((B, 12)).astype(np.float32)
+        want = s.extract_commands(1, 0.01 * it, 0.01, dur, feet, 0.5)
+        ticket = s.extract_commands_async(1, 0.01 * it, 0.01, dur, feet, 0.5)
+        assert ticket == it % 2
+        if pending is not None:  # the previous tick's records, copied during this tick's work
+            _same_records(s.commands_wait(pending[0]), pending[1], it)
+        pending = (ticket, want)
+        flags = sc.step(1)
+        s.shift(flags)
+        inp = sc.inputs(prob["x0"])
+        s.update_problem(inp["contacts"], inp["x0"], inp["ref_x"], inp["ref_u"], inp["ref_foot"])
+        s.solve()
+    _same_records(s.commands_wait(pending[0]), pending[1], "last")
+    s.close()
+
+
+def _same_records(a, b, where):
+    for f in a.dtype.names:  # field by field (the record has padding bytes nothing writes)
+        assert np.array_equal(a[f], b[f]), (where, f)
+
+
 # ---- receding-horizon update (HKDProblem::update, HKDProblem.cpp:117-222) --------------------
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import oracle_lib as O  # noqa: E402

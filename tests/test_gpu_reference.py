@@ -73,7 +73,8 @@ def test_per_element_windows_match_oracle():
     tab = np.concatenate([t1, t2])
     ref = r1 + r2
     p0 = hsddp.plan_phases(tab[3:3 + N_WIN], dt)
-    starts = [3, 103, 3, 103, 3, 103]
+    n1 = len(t1)
+    starts = [3, n1 + 3, 3, n1 + 3, 3, n1 + 3]
     p = hsddp.reference_problem(tab, dt, starts, _x0(6))
     assert p["horizons"] == p0["horizons"]
     s = hsddp.Solver(p)
@@ -82,11 +83,12 @@ def test_per_element_windows_match_oracle():
     assert got["ref_x"].shape[0] == 6
     assert np.array_equal(got["ref_x"], rx) and np.array_equal(got["ref_u"], ru) and np.array_equal(got["ref_foot"], rf)
     # samples past the table's end read its last sample
-    s.build_references([150] * 6, N_WIN, None, 0.01)
-    rx3, _, _ = _oracle_refs(ref, [150] * 6, p["horizons"], dt)
+    late = len(tab) - 10
+    s.build_references([late] * 6, N_WIN, None, 0.01)
+    rx3, _, _ = _oracle_refs(ref, [late] * 6, p["horizons"], dt)
     assert np.array_equal(s.references()["ref_x"], rx3)
     with pytest.raises(hsddp.HSDDPError):
-        s.build_references([400] * 6, N_WIN, None, 0.01)  # window outside the table
+        s.build_references([len(tab) + 40] * 6, N_WIN, None, 0.01)  # window outside the table
     s.close()
 
 
