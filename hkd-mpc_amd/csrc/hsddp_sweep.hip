@@ -433,22 +433,15 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     }
     SSYNC();
     // lxx + reg I into the Z image: each row lane adds its diagonal and lxx cross terms to its own
-    // row (read, add, write back: no two lanes touch one entry; absent terms add 0 to column 25)
+    // row by LDS atomic adds behind its row's stores (a wave's LDS operations complete in order, so
+    // no read-back round trip; no two lanes touch one entry; the add is the IEEE add of the value
+    // stored, as a read-add-write would form it)
     if (L.row) {
         real *zr = I.MI + pp * MS;
-        int col[4];
+        lds_add(zr + pp, ph.lxd + reg);
 #pragma unroll
-        for (int t2 = 0; t2 < 4; ++t2) col[t2] = L.xkind == 1 ? L.xc0 + 3 * t2 : (L.xkind == 2 && t2 == 0) ? L.xc0 : MS - 1;
-        real v[5];
-        v[0] = zr[pp];
-#pragma unroll
-        for (int t2 = 0; t2 < 4; ++t2) v[1 + t2] = zr[col[t2]];
-        v[0] += ph.lxd + reg;
-#pragma unroll
-        for (int t2 = 0; t2 < 4; ++t2) v[1 + t2] += ((ph.xmask >> t2) & 1) ? -ph.xw : (real)0;
-        zr[pp] = v[0];
-#pragma unroll
-        for (int t2 = 0; t2 < 4; ++t2) zr[col[t2]] = v[1 + t2];
+        for (int t2 = 0; t2 < 4; ++t2)
+            if ((ph.xmask >> t2) & 1) lds_add(zr + (L.xkind == 1 ? L.xc0 + 3 * t2 : L.xc0), -ph.xw);
     }
     SSYNC();
     const real *zrow = L.row ? I.MI + pp * MS : S.zero;

@@ -183,6 +183,14 @@ DEV void lds_dma16(const void *src, unsigned m0)
                  : "memory");
 }
 
+// LDS atomic add without return (ds_add_f64 / ds_add_f32): the IEEE round-to-nearest add of v to
+// the stored value, queued behind the wave's earlier LDS operations
+template <typename real>
+DEV void lds_add(real *p, real v)
+{
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 }  // namespace hsddp
 
 namespace hsddp {
