@@ -225,11 +225,10 @@ def main():
     red = torch.tensor([t1 - t0, elem_iters, float(st.ls_trials)], dtype=torch.float64, device=dev)
     rank_ms = [(t1 - t0) / args.steps * 1e3]
     # after the timed region: every element's command block (hkd_command_lcmt, HKDMPC.cpp:232-298)
-    # extracted on the device into the tensor the final gather sends (not for per-element layouts)
-    cmd = None
-    if not args.mixed:
-        cmd = torch.empty(B * hsddp.MPC_COMMAND.itemsize, dtype=torch.uint8, device=dev)
-        solver.extract_commands_device(cmd.data_ptr())
+    # extracted on the device into the tensor the final gather sends (per-element layouts: each
+    # element's own knot walk)
+    cmd = torch.empty(B * hsddp.MPC_COMMAND.itemsize, dtype=torch.uint8, device=dev)
+    solver.extract_commands_device(cmd.data_ptr())
     gather = {"summary_bytes_per_element": 48, "command_bytes_per_element": hsddp.MPC_COMMAND.itemsize if cmd is not None else 0}
     if distributed:
         allr = [torch.zeros_like(red) for _ in range(world)]

@@ -1632,8 +1632,6 @@ static int extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_t
                             int feet_per_element, float solve_time, hsddp_mpc_command *out, bool out_on_device,
                             int ticket)
 {
-    if (h && !h->lays.empty())
-        return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts (hsddp_set_element_layouts): the MPC-side steps need the handle's shared layout");
     if (!h || (!out && ticket < 0)) return fail(HSDDP_ERR_ARG, "null argument");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     const Params &p = h->p;
@@ -1641,13 +1639,15 @@ static int extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_t
     a.n = nsteps_between_mpc + 7;  // HKDMPC.cpp:232-233
     if (nsteps_between_mpc < 1 || a.n > HSDDP_CMD_STEPS || a.n > p.Kc)
         return fail(HSDDP_ERR_ARG, "nsteps_between_mpc + 7 must fit the command (10 rows) and the horizon");
-    // the knot walk of publish_mpc_cmd (HKDMPC.cpp:239-246): s runs over phase i's controls
-    for (int k = 0, i = 0, s = 0; k < a.n; ++k, ++s) {
-        if (s >= p.N[i]) { s = 0; ++i; }
-        a.kc[k] = p.k0[i] + s;
-        a.xs[k] = p.s0[i] + s;
-        a.ph[k] = i;
-    }
+    // the knot walk of publish_mpc_cmd (HKDMPC.cpp:239-246): s runs over phase i's controls (per-
+    // element layouts: each workgroup walks its element's own)
+    if (h->lays.empty())
+        for (int k = 0, i = 0, s = 0; k < a.n; ++k, ++s) {
+            if (s >= p.N[i]) { s = 0; ++i; }
+            a.kc[k] = p.k0[i] + s;
+            a.xs[k] = p.s0[i] + s;
+            a.ph[k] = i;
+        }
     a.mpc_time = mpc_time;
     a.dt_mpc = dt_mpc;
     a.solve_time = solve_time;
@@ -2084,8 +2084,6 @@ extern "C" int hsddp_build_references(hsddp_handle h, const int *window_start, i
                                       const float *phase_start_times, float dt_sim)
 {
     if (h) h->slots_fresh = false;  // new reference rows: the running costs change
-    if (h && !h->lays.empty())
-        return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts (hsddp_set_element_layouts): the MPC-side steps need the handle's shared layout");
     return build_refs(h, window_start, window_len, phase_start_times, dt_sim, true);
 }
 
@@ -2100,39 +2098,63 @@ static int build_refs(hsddp_handle h, const int *window_start, int window_len, c
     if (window_len < 1 || !(dt_sim > 0)) return fail(HSDDP_ERR_ARG, "window_len >= 1 and dt_sim > 0 required");
     const Params &p = h->p;
     const int Br = h->Bref;
+    const bool elem = !h->lays.empty();
     for (int b = 0; b < Br; ++b)
         if (window_start[b] < 0 || window_start[b] >= h->ref_n) return fail(HSDDP_ERR_ARG, "window start outside the table");
+    if (elem && phase_start_times)
+        return fail(HSDDP_ERR_ARG, "per-element layouts: the phase start times follow each element's own float clock (NULL)");
     // slot times as the reference forms them: t_offset (float, phase start relative to the first
     // phase) + k dt (double), passed on as float (SinglePhase.cpp:243-287; set_time_offset,
-    // HKDProblem.cpp:103,208), snapped to a sample (QuadReference.cpp:60-76)
-    std::vector<float> start(p.P);
-    if (phase_start_times) {
-        for (int i = 0; i < p.P; ++i) start[i] = phase_start_times[i] - phase_start_times[0];
-    } else {  // the float clock of HKDProblem::initialization (t += dt_sim per knot)
-        float t = 0.0f;
-        for (int i = 0; i < p.P; ++i) {
-            start[i] = t;
-            for (int k = 0; k < p.N[i]; ++k) t += dt_sim;
+    // HKDProblem.cpp:103,208), snapped to a sample (QuadReference.cpp:60-76); per layout
+    auto starts_of = [&](const Layout &L) {
+        std::vector<float> start(L.P);
+        if (phase_start_times) {
+            for (int i = 0; i < L.P; ++i) start[i] = phase_start_times[i] - phase_start_times[0];
+        } else {  // the float clock of HKDProblem::initialization (t += dt_sim per knot)
+            float t = 0.0f;
+            for (int i = 0; i < L.P; ++i) {
+                start[i] = t;
+                for (int k = 0; k < L.N[i]; ++k) t += dt_sim;
+            }
         }
-    }
-    std::vector<int> idx(p.S);
+        return start;
+    };
     const int sz = window_len - 1;
-    for (int i = 0; i < p.P; ++i)
-        for (int k = 0; k <= p.N[i]; ++k) {
-            const float t = (float)((double)start[i] + k * (double)dt_sim);
-            int q = (int)std::floor(t / h->ref_dt);
-            if (t - q * h->ref_dt > 0.5 * h->ref_dt) q++;
-            idx[p.s0[i] + k] = q > sz ? sz : q;
+    // one slot map per distinct layout ([n_maps][S], padding slots repeat the last sample)
+    std::map<std::vector<int>, int> keys;
+    std::vector<int> idx, map_id(elem ? p.B : 0);
+    std::vector<std::vector<float>> map_starts;
+    for (int b = 0; b < (elem ? p.B : 1); ++b) {
+        const Layout L = layout_of(h, b);
+        std::vector<int> key(L.N, L.N + L.P);
+        auto it = keys.find(key);
+        if (it == keys.end()) {
+            const std::vector<float> start = starts_of(L);
+            std::vector<int> row(p.S, 0);
+            for (int i = 0; i < L.P; ++i)
+                for (int k = 0; k <= L.N[i]; ++k) {
+                    const float t = (float)((double)start[i] + k * (double)dt_sim);
+                    int q = (int)std::floor(t / h->ref_dt);
+                    if (t - q * h->ref_dt > 0.5 * h->ref_dt) q++;
+                    row[L.s0[i] + k] = q > sz ? sz : q;
+                }
+            for (int sl = L.S; sl < p.S; ++sl) row[sl] = row[L.S - 1];
+            it = keys.emplace(key, (int)map_starts.size()).first;
+            idx.insert(idx.end(), row.begin(), row.end());
+            map_starts.push_back(start);
         }
+        if (elem) map_id[b] = it->second;
+    }
     HIPCHK(hipSetDevice(h->desc.device));
     char *buf;
     int rc;
-    if ((rc = scratch(h, (Br + p.S) * sizeof(int), &buf))) return rc;
-    int *dstart = (int *)buf, *didx = dstart + Br;
+    if ((rc = scratch(h, (Br + idx.size() + map_id.size()) * sizeof(int), &buf))) return rc;
+    int *dstart = (int *)buf, *didx = dstart + Br, *dmap = didx + idx.size();
     if ((rc = h2d(dstart, window_start, Br * sizeof(int), h->stream)) ||
-        (rc = h2d(didx, idx.data(), p.S * sizeof(int), h->stream)))
+        (rc = h2d(didx, idx.data(), idx.size() * sizeof(int), h->stream)) ||
+        (elem && (rc = h2d(dmap, map_id.data(), map_id.size() * sizeof(int), h->stream))))
         return rc;
-    RefArgs a{h->ref_table, h->ref_n, dstart, didx};
+    RefArgs a{h->ref_table, h->ref_n, dstart, didx, elem ? dmap : nullptr};
     launch_build_refs(p, h->d, Br, a, h->stream);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -2143,11 +2165,13 @@ static int build_refs(hsddp_handle h, const int *window_start, int window_len, c
     if (initial) {
         h->t_cur = 0;
         h->durations.assign((size_t)p.B * p.P * 4, 0.0);
-        for (int b = 0; b < p.B; ++b)
-            for (int i = 0; i < p.P; ++i) {
+        for (int b = 0; b < p.B; ++b) {
+            const std::vector<float> &start = map_starts[elem ? map_id[b] : 0];
+            for (int i = 0; i < (int)start.size(); ++i) {
                 const int k = std::min(window_start[Br == 1 ? 0 : b] + ref_sample(start[i], h->ref_dt, sz), h->ref_n - 1);
                 for (int l = 0; l < 4; ++l) h->durations[((size_t)b * p.P + i) * 4 + l] = h->table_host[k].status_dur[l];
             }
+        }
     }
     return HSDDP_OK;
 }
@@ -2163,8 +2187,6 @@ static int build_refs(hsddp_handle h, const int *window_start, int window_len, c
 extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, float dt_mpc, const double *x0,
                              int *contact_change)
 {
-    if (h && !h->lays.empty())
-        return fail(HSDDP_ERR_UNSUPPORTED, "per-element layouts (hsddp_set_element_layouts): the MPC-side steps need the handle's shared layout");
     if (!h) return fail(HSDDP_ERR_ARG, "null handle");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     if (h->need_inputs) return fail(HSDDP_ERR_ARG, "the previous shift awaits hsddp_update_problem");
@@ -2173,28 +2195,17 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     if (n_steps < 0) return fail(HSDDP_ERR_ARG, "n_steps must be >= 0");
     const Params &p = h->p;
     const int B = p.B, Br = h->Bref, sz = h->win_len - 1;
+    const bool elem = !h->lays.empty();
     const float dt = h->ref_dt, dts = h->dt_sim;
     auto leq = [](float a, float b) { return a < b || std::abs(a - b) <= 1e-6f; };
     int adv = 0;  // samples per simulation step
     for (int i = 1; leq(i * dt, dts); ++i) adv++;
-    // The edits are the same for every element (the layout is shared), so they are tracked once as
-    // a source per phase: an old phase (index >= 0) or the sample a new phase starts from (step
-    // j: -1 - j); the next-contact row likewise.  Per-element values are read at the end.
-    const int P0 = p.P;
-    std::vector<int> hz(p.N, p.N + p.P), reach(h->reach_end), ws(h->win_start), flags(n_steps), src(P0);
-    for (int i = 0; i < P0; ++i) src[i] = i;
+    // QuadReference::step for every step: the window starts and the clock (shared by the batch)
+    const int P0 = p.P;  // stride of the current contact rows [B][P0 + 1][4] and durations [B][P0][4]
     std::vector<std::vector<int>> wsj(n_steps);  // window starts at each step
     std::vector<float> relj(n_steps);            // new_end - new_start at each step
-    int next_kind = 0, next_step = -1;           // row P: 0 old row, 1 contact at relj, 2 at plan + dt_mpc
+    std::vector<int> ws(h->win_start);
     float t_cur = h->t_cur;
-    auto sample_w = [&](const std::vector<int> &w, int b, float t) -> const hsddp_quad_state & {
-        const int k = w[Br == 1 ? 0 : b] + ref_sample(t, dt, sz);
-        return h->table_host[std::min(k, h->ref_n - 1)];
-    };
-    auto phase_contact = [&](int sc, int b, int l) {
-        return sc >= 0 ? h->contacts[((size_t)b * (P0 + 1) + sc) * 4 + l]
-                       : sample_w(wsj[-1 - sc], b, relj[-1 - sc]).contact[l];
-    };
     for (int j = 0; j < n_steps; ++j) {
         for (int a = 0; a < adv; ++a) {
             t_cur += dt;
@@ -2203,61 +2214,108 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
         for (int &w : ws)
             if (w >= h->ref_n) return fail(HSDDP_ERR_ARG, "the reference window ran past the table");
         wsj[j] = ws;
-        if (hz.front() <= 1) {  // pop_front_phase (HKDProblem.h:56-66)
-            if (hz.size() == 1) return fail(HSDDP_ERR_ARG, "advance would remove the only phase");
-            hz.erase(hz.begin());
-            reach.erase(reach.begin());
-            src.erase(src.begin());
-        } else {
-            hz.front()--;
-        }
         relj[j] = (t_cur + plan_duration) - t_cur;  // new_end_time - new_start_time
-        int cc = -1;
-        for (int b = 0; b < B; ++b) {
-            const int *nc = sample_w(ws, b, relj[j]).contact;
-            int cb = 0;
-            for (int l = 0; l < 4; ++l) cb |= nc[l] != phase_contact(src.back(), b, l);
-            if (cc >= 0 && cb != cc)
-                return fail(HSDDP_ERR_UNSUPPORTED, "elements disagree on a contact change (the layout is shared)");
-            cc = cb;
-        }
-        if (cc && reach.back()) {
-            if ((int)hz.size() >= HSDDP_MAX_PHASES) return fail(HSDDP_ERR_ARG, "advance exceeds HSDDP_MAX_PHASES phases");
-            hz.push_back(1);
-            reach.push_back(0);
-            src.push_back(-1 - j);
-            next_kind = 1;  // a new phase carries no terminal constraint (identity reset)
-            next_step = j;
-        } else {
-            hz.back()++;
-            if (cc) reach.back() = 1;
-        }
-        if (reach.back()) { next_kind = 2; next_step = j; }
-        flags[j] = cc;
     }
-    int rc;
-    if ((rc = hsddp_shift(h, n_steps, flags.data()))) return rc;
-    if (p.P != (int)hz.size() || !std::equal(hz.begin(), hz.end(), p.N) || h->reach_end != reach)
-        return fail(HSDDP_ERR_ARG, "internal: advance and shift disagree on the layout");
-    if ((rc = build_refs(h, ws.data(), h->win_len, nullptr, dts, false))) return rc;
-    const int P = p.P;
-    std::vector<int> contacts((size_t)B * (P + 1) * 4);
-    std::vector<double> dur((size_t)B * P * 4);
+    auto sample_w = [&](const std::vector<int> &w, int b, float t) -> const hsddp_quad_state & {
+        const int k = w[Br == 1 ? 0 : b] + ref_sample(t, dt, sz);
+        return h->table_host[std::min(k, h->ref_n - 1)];
+    };
+    // HKDProblem::update's bookkeeping (HKDProblem.cpp:126-202) of every element over the steps: its
+    // phases as sources — an old phase (index >= 0) or the sample a new phase starts from (step j:
+    // -1 - j) — the step flags and where its next-contact row comes from
+    struct Track {
+        std::vector<int> hz, reach, src, flags;
+        int P_old = 0;                       // the element's phases before the steps
+        int next_kind = 0, next_step = -1;  // row P: 0 old row, 1 contact at relj, 2 at plan + dt_mpc
+    };
+    std::vector<Track> tr(B);
     for (int b = 0; b < B; ++b) {
-        for (int i = 0; i < P; ++i) {
-            const int sc = src[i];
+        Track &T = tr[b];
+        const Layout L = layout_of(h, b);
+        const int *reach0 = elem ? &h->reach_el[(size_t)b * HSDDP_MAX_PHASES] : h->reach_end.data();
+        T.hz.assign(L.N, L.N + L.P);
+        T.P_old = L.P;
+        T.reach.assign(reach0, reach0 + L.P);
+        for (int i = 0; i < L.P; ++i) T.src.push_back(i);
+        T.flags.assign(n_steps, 0);
+        auto phase_contact = [&](int sc, int l) {
+            return sc >= 0 ? h->contacts[((size_t)b * (P0 + 1) + sc) * 4 + l]
+                           : sample_w(wsj[-1 - sc], b, relj[-1 - sc]).contact[l];
+        };
+        for (int j = 0; j < n_steps; ++j) {
+            if (T.hz.front() <= 1) {  // pop_front_phase (HKDProblem.h:56-66)
+                if (T.hz.size() == 1) return fail(HSDDP_ERR_ARG, "advance would remove the only phase");
+                T.hz.erase(T.hz.begin());
+                T.reach.erase(T.reach.begin());
+                T.src.erase(T.src.begin());
+            } else {
+                T.hz.front()--;
+            }
+            const int *nc = sample_w(wsj[j], b, relj[j]).contact;
+            int cc = 0;
+            for (int l = 0; l < 4; ++l) cc |= nc[l] != phase_contact(T.src.back(), l);
+            if (cc && T.reach.back()) {
+                if ((int)T.hz.size() >= HSDDP_MAX_PHASES) return fail(HSDDP_ERR_ARG, "advance exceeds HSDDP_MAX_PHASES phases");
+                T.hz.push_back(1);
+                T.reach.push_back(0);
+                T.src.push_back(-1 - j);
+                T.next_kind = 1;  // a new phase carries no terminal constraint (identity reset)
+                T.next_step = j;
+            } else {
+                T.hz.back()++;
+                if (cc) T.reach.back() = 1;
+            }
+            if (T.reach.back()) { T.next_kind = 2; T.next_step = j; }
+            T.flags[j] = cc;
+        }
+    }
+    // the shift: one set of flags for the batch when it agrees (the shared layout stays shared),
+    // else every element's own (per-element layouts; they need per-element references)
+    bool agree = !elem;
+    for (int b = 1; b < B && agree; ++b) agree = tr[b].flags == tr[0].flags;
+    int rc;
+    if (agree) {
+        if ((rc = hsddp_shift(h, n_steps, tr[0].flags.data()))) return rc;
+    } else {
+        if (B > 1 && Br == 1)
+            return fail(HSDDP_ERR_UNSUPPORTED, "elements disagree on a contact change, which takes per-element layouts "
+                                               "and per-element references (ref_per_element = 1)");
+        std::vector<int> cc((size_t)B * n_steps);
+        for (int b = 0; b < B; ++b) std::copy(tr[b].flags.begin(), tr[b].flags.end(), cc.begin() + (size_t)b * n_steps);
+        if ((rc = hsddp_shift_elements(h, n_steps, cc.data()))) return rc;
+    }
+    for (int b = 0; b < B; ++b) {
+        const Layout L = layout_of(h, b);
+        const int *re = h->lays.empty() ? h->reach_end.data() : &h->reach_el[(size_t)b * HSDDP_MAX_PHASES];
+        if (L.P != (int)tr[b].hz.size() || !std::equal(tr[b].hz.begin(), tr[b].hz.end(), L.N) ||
+            !std::equal(tr[b].reach.begin(), tr[b].reach.end(), re))
+            return fail(HSDDP_ERR_ARG, "internal: advance and shift disagree on the layout");
+    }
+    if ((rc = build_refs(h, ws.data(), h->win_len, nullptr, dts, false))) return rc;
+    const int P = p.P;  // the new stride (the largest layout's with per-element layouts)
+    std::vector<int> contacts((size_t)B * (P + 1) * 4, 0);
+    std::vector<double> dur((size_t)B * P * 4, 0.0);
+    for (int b = 0; b < B; ++b) {
+        const Track &T = tr[b];
+        const int Pb = (int)T.hz.size();
+        auto phase_contact = [&](int sc, int l) {
+            return sc >= 0 ? h->contacts[((size_t)b * (P0 + 1) + sc) * 4 + l]
+                           : sample_w(wsj[-1 - sc], b, relj[-1 - sc]).contact[l];
+        };
+        for (int i = 0; i < Pb; ++i) {
+            const int sc = T.src[i];
             const double *dv = sc >= 0 ? &h->durations[((size_t)b * P0 + sc) * 4]
                                        : sample_w(wsj[-1 - sc], b, relj[-1 - sc]).status_dur;
             for (int l = 0; l < 4; ++l) {
-                contacts[((size_t)b * (P + 1) + i) * 4 + l] = phase_contact(sc, b, l);
+                contacts[((size_t)b * (P + 1) + i) * 4 + l] = phase_contact(sc, l);
                 dur[((size_t)b * P + i) * 4 + l] = dv[l];
             }
         }
         for (int l = 0; l < 4; ++l)
-            contacts[((size_t)b * (P + 1) + P) * 4 + l] =
-                next_kind == 0 ? h->contacts[((size_t)b * (P0 + 1) + P0) * 4 + l]
-                : next_kind == 1 ? sample_w(wsj[next_step], b, relj[next_step]).contact[l]
-                                 : sample_w(wsj[next_step], b, plan_duration + dt_mpc).contact[l];
+            contacts[((size_t)b * (P + 1) + Pb) * 4 + l] =
+                T.next_kind == 0 ? h->contacts[((size_t)b * (P0 + 1) + T.P_old) * 4 + l]
+                : T.next_kind == 1 ? sample_w(wsj[T.next_step], b, relj[T.next_step]).contact[l]
+                                   : sample_w(wsj[T.next_step], b, plan_duration + dt_mpc).contact[l];
     }
     if (x0) {
         if ((rc = hsddp_update_problem(h, contacts.data(), x0, nullptr, nullptr, nullptr))) return rc;
@@ -2267,7 +2325,12 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     }
     h->durations.swap(dur);
     h->t_cur = t_cur;
-    if (contact_change) std::copy(flags.begin(), flags.end(), contact_change);
+    if (contact_change)  // per step: some element saw a contact change (the batch's flag when it agrees)
+        for (int j = 0; j < n_steps; ++j) {
+            int f = 0;
+            for (int b = 0; b < B; ++b) f |= tr[b].flags[j];
+            contact_change[j] = f;
+        }
     return HSDDP_OK;
 }
 

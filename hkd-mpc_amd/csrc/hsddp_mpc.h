@@ -48,7 +48,8 @@ struct RefArgs {
     const double *table;   // [n][RT_W]
     int n;
     const int *start;      // [Bw] window start sample per element (Bw = Bref)
-    const int *slot_idx;   // [S] sample offset of each state slot within the window
+    const int *slot_idx;   // [n_maps][S] sample offset of each state slot within the window
+    const int *map_id;     // [B] slot map of each element (per-element layouts), or null: map 0
 };
 void launch_build_refs(const Params &p, const Bufs &d, int Bref, const RefArgs &a, hipStream_t st);
 

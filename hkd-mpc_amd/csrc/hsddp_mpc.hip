@@ -18,30 +18,48 @@
 namespace hsddp {
 
 // One element per workgroup.  The knot walk of publish_mpc_cmd (phase i, knot s; HKDMPC.cpp:
-// 239-246) depends only on the horizons, which the batch shares, so the host passes it resolved
-// (a.kc[k], a.ph[k]).
+// 239-246) depends only on the horizons: with the handle's shared layout the host passes it
+// resolved (a.kc[k], a.xs[k], a.ph[k]); with per-element layouts (EL) the workgroup walks its
+// element's own layout first.
+template <bool EL>
 __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdArgs a, hsddp_mpc_command *out)
 {
     const int b = blockIdx.x, t = threadIdx.x;
     hsddp_mpc_command &o = out[b];
+    const auto L = layout_of<EL>(d, b);
+    __shared__ int wkc[HSDDP_CMD_STEPS], wxs[HSDDP_CMD_STEPS], wph[HSDDP_CMD_STEPS];
+    if (t == 0) {
+        if constexpr (EL) {
+            for (int k = 0, i = 0, s = 0; k < a.n; ++k, ++s) {
+                if (s >= L.N(i)) { s = 0; ++i; }
+                wkc[k] = L.k0(i) + s;
+                wxs[k] = L.s0(i) + s;
+                wph[k] = i;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < HSDDP_CMD_STEPS; ++k) { wkc[k] = a.kc[k]; wxs[k] = a.xs[k]; wph[k] = a.ph[k]; }
+        }
+    }
+    __syncthreads();
     const int *cb = d.contacts + (size_t)b * (p.P + 1) * 4;
     const double *Xbar = d.Xb[nom_buf(d, b)], *Ubar = d.Ub[nom_buf(d, b)];
     // controls, body states, feedback rows (zero past N_mpcsteps, as a fresh message)
     for (int e = t; e < HSDDP_CMD_STEPS * 24; e += blockDim.x) {
         const int k = e / 24, j = e % 24;
-        o.hkd_controls[k][j] = k < a.n ? (float)Ubar[((size_t)b * p.Kc + a.kc[k]) * NX + j] : 0.f;
+        o.hkd_controls[k][j] = k < a.n ? (float)Ubar[((size_t)b * p.Kc + wkc[k]) * NX + j] : 0.f;
     }
     for (int e = t; e < HSDDP_CMD_STEPS * 12; e += blockDim.x) {
         const int k = e / 12, j = e % 12;
-        o.des_body_state[k][j] = k < a.n ? (float)Xbar[((size_t)b * p.S + a.xs[k]) * NX + j] : 0.f;
+        o.des_body_state[k][j] = k < a.n ? (float)Xbar[((size_t)b * p.S + wxs[k]) * NX + j] : 0.f;
     }
     // K(m, n), m, n < 12: control m is leg m/3's GRF; its gain row is compact row m when the leg
     // is in stance and exactly zero when it swings (KCW layout, hsddp_internal.h)
     for (int e = t; e < HSDDP_CMD_STEPS * 144; e += blockDim.x) {
         const int k = e / 144, m = (e / 12) % 12, n = e % 12;
         float v = 0.f;
-        if (k < a.n && cb[a.ph[k] * 4 + m / 3]) {
-            const size_t idx = ((size_t)b * p.Kc + a.kc[k]) * KCW + m * NX + n;
+        if (k < a.n && cb[wph[k] * 4 + m / 3]) {
+            const size_t idx = ((size_t)b * p.Kc + wkc[k]) * KCW + m * NX + n;
             v = p.fp32 ? d.K32[idx] : (float)d.K[idx];
         }
         o.feedback[k][m][n] = v;
@@ -49,8 +67,8 @@ __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdA
     for (int e = t; e < HSDDP_CMD_STEPS * 4; e += blockDim.x) {
         const int k = e / 4, l = e % 4;
         const bool on = k < a.n;
-        o.contacts[k][l] = on ? cb[a.ph[k] * 4 + l] : 0;
-        const double *dur = a.durations ? a.durations + ((size_t)(a.dur_per_elem ? b : 0) * p.P + a.ph[k]) * 4 : nullptr;
+        o.contacts[k][l] = on ? cb[wph[k] * 4 + l] : 0;
+        const double *dur = a.durations ? a.durations + ((size_t)(a.dur_per_elem ? b : 0) * p.P + wph[k]) * 4 : nullptr;
         o.statusTimes[k][l] = (on && dur) ? dur[l] : 0.0;
     }
     // mpc_time + k dt_mpc rounded twice, as written (no fused multiply-add)
@@ -61,9 +79,9 @@ __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdA
     if (t < 12) {
         const int l = t / 3, ax = t % 3;
         float pf = a.feet ? a.feet[(size_t)(a.feet_per_elem ? b : 0) * 12 + t] : 0.f;
-        for (int i = 0; i < p.P - 1 && i <= 4; ++i) {
+        for (int i = 0; i < L.P() - 1 && i <= 4; ++i) {
             if (cb[i * 4 + l] == 0 && cb[(i + 1) * 4 + l] == 1) {
-                pf = (float)Xbar[((size_t)b * p.S + p.s0[i + 1]) * NX + 12 + 3 * l + ax];
+                pf = (float)Xbar[((size_t)b * p.S + L.s0(i + 1)) * NX + 12 + 3 * l + ax];
                 break;
             }
         }
@@ -193,7 +211,7 @@ __global__ __launch_bounds__(256) void k_build_refs(Params p, Bufs d, int Bref, 
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long)Bref * p.S) return;
     const int b = (int)(gid / p.S), s = (int)(gid % p.S);
-    int k = a.start[b] + a.slot_idx[s];
+    int k = a.start[b] + a.slot_idx[(size_t)(a.map_id ? a.map_id[b] : 0) * p.S + s];
     k = k < a.n ? k : a.n - 1;  // past the loaded data: its last sample
     const double *q = a.table + (size_t)k * RT_W;
     double *rx = (double *)d.ref_x + gid * NX, *ru = (double *)d.ref_u + gid * NX, *rf = (double *)d.ref_foot + gid * 12;
@@ -217,7 +235,8 @@ void launch_build_refs(const Params &p, const Bufs &d, int Bref, const RefArgs &
 void launch_extract_commands(const Params &p, const Bufs &d, const CmdArgs &a, hsddp_mpc_command *out,
                              hipStream_t st)
 {
-    hipLaunchKernelGGL(k_extract_commands, dim3(p.B), dim3(256), 0, st, p, d, a, out);
+    if (p.elem_layout) hipLaunchKernelGGL(k_extract_commands<true>, dim3(p.B), dim3(256), 0, st, p, d, a, out);
+    else hipLaunchKernelGGL(k_extract_commands<false>, dim3(p.B), dim3(256), 0, st, p, d, a, out);
 }
 
 }  // namespace hsddp

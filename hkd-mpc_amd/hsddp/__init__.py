@@ -86,17 +86,24 @@ def reference_problem(table: np.ndarray, dt_ref: float, window_start, x0: np.nda
     n_win = int(round(plan_duration / dt_ref)) + 2  # QuadReference::initialize: sz + 1 samples, sz = round(T/dt) + 1
     plans = [plan_phases(table[w:w + n_win], dt_ref, plan_duration, dt_sim, dt_mpc) for w in ws]
     hz = plans[0]["horizons"]
-    for q in plans[1:]:
-        if q["horizons"] != hz:
-            raise HSDDPError("per-element windows must share the phase layout")
-    contacts = np.stack([q["contacts"] for q in plans]).astype(np.int32)
+    shared = all(q["horizons"] == hz for q in plans[1:])
+    Kc = sum(hz)
+    if any(sum(q["horizons"]) != Kc for q in plans):
+        raise HSDDPError("every window's plan must have the same number of knots")
+    Pmax = max(len(q["horizons"]) for q in plans)
+    contacts = np.zeros((len(plans), Pmax + 1, 4), np.int32)
+    for b, q in enumerate(plans):  # [B][Pmax + 1][4]: element b's rows 0 .. P_b
+        contacts[b, :len(q["horizons"]) + 1] = q["contacts"]
     if contacts.shape[0] == 1 and B > 1:
         contacts = np.repeat(contacts, B, axis=0)
-    S, Kc = sum(n + 1 for n in hz), sum(hz)
+    S = Kc + Pmax
     # dt: HKDProblem's float dt_sim widened to double by Trajectory(dt_sim, N) (HKDProblem.cpp:81)
-    return {"batch": B, "horizons": hz, "S": S, "Kc": Kc, "dt": float(np.float32(dt_sim)), "x0": x0, "contacts": contacts,
-            "shooting": [n + 1 for n in hz], "ref_table": table, "dt_ref": dt_ref, "window_start": ws,
-            "window_len": n_win, "phase_start_times": plans[0]["start_times"], "plan": plans[0]}
+    out = {"batch": B, "horizons": hz, "S": S, "Kc": Kc, "dt": float(np.float32(dt_sim)), "x0": x0, "contacts": contacts,
+           "shooting": [n + 1 for n in hz], "ref_table": table, "dt_ref": dt_ref, "window_start": ws,
+           "window_len": n_win, "phase_start_times": plans[0]["start_times"], "plan": plans[0]}
+    if not shared:  # windows of different gaits: every element segmented by its own (HKDProblem.cpp:40-68)
+        out.update(layouts=[q["horizons"] for q in plans], phase_start_times=None, plans=plans)
+    return out
 
 
 class Solver:
@@ -394,9 +401,13 @@ class Solver:
         flags = np.zeros(max(1, n_steps), np.int32)
         check(lib().hsddp_advance(self._h, int(n_steps), float(plan_duration), float(dt_mpc),
                                   None if x0 is None else dp(np.ascontiguousarray(x0, dtype=np.float64)), ip(flags)))
-        lay = self.layout()
-        self.P = len(lay["horizons"])
-        self.S = sum(n + 1 for n in lay["horizons"])
+        el = self.element_layouts()
+        if any(h != el["horizons"][0] for h in el["horizons"]):  # per-element layouts
+            self.P = int(el["n_phases"].max())
+            self.S = self.Kc + self.P
+        else:
+            self.P = len(el["horizons"][0])
+            self.S = sum(n + 1 for n in el["horizons"][0])
         return [int(f) for f in flags[:n_steps]]
 
     def phase_info(self) -> dict:

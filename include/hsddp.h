@@ -179,8 +179,8 @@ int hsddp_validate_options(const hsddp_options *opt);
  * layout as their stride: contacts [B][Pmax+1][4] (element b: rows 0 .. n_phases[b], row
  * n_phases[b] = the contact after its horizon), state-slot arrays [B][Smax][..] (element b: its
  * first S_b = Kc + n_phases[b] rows), per-phase arrays [B][Pmax][..]; the problem must be uploaded
- * again.  The MPC-side steps (hsddp_shift, _advance, _build_references, _extract_commands) keep
- * requiring the shared layout. */
+ * again.  The MPC-side steps take every element's own layout (hsddp_shift_elements,
+ * hsddp_advance, hsddp_build_references with phase_start_times NULL, hsddp_extract_commands). */
 int hsddp_set_element_layouts(hsddp_handle h, const int *n_phases, const int *horizons);
 
 /* contacts int32 [B][P+1][4] (row P: contact after the horizon, for the last phase's touchdown
@@ -344,11 +344,13 @@ int hsddp_update_problem(hsddp_handle h, const int *contacts, const double *x0, 
 
 /* HKDProblem::update (HKDProblem.cpp:117-222) driven by the reference table, for handles whose
  * references were built by hsddp_build_references: n_steps simulation steps of the window
- * (QuadReference::step), each with the contact at the new horizon end deciding the phase growth
- * (the batch must agree on it), the last phase's next contact at plan_duration + dt_mpc once it
- * has reached its end (add_tconstr_one_phase), new phases' contact durations; then hsddp_shift,
- * the new layout's references and hsddp_update_problem with these contacts and x0 [B][24].
- * contact_change [n_steps] (may be NULL) receives the step flags.  x0 NULL: the inputs are left
+ * (QuadReference::step), each with the contact at the new horizon end of every element's own
+ * window deciding that element's phase growth, the last phase's next contact at plan_duration +
+ * dt_mpc once it has reached its end (add_tconstr_one_phase), new phases' contact durations; then
+ * the shift (hsddp_shift when the batch agrees on every step's flag, else hsddp_shift_elements:
+ * per-element layouts, which need per-element references), the new layouts' references and
+ * hsddp_update_problem with these contacts and x0 [B][24].  contact_change [n_steps] (may be NULL)
+ * receives, per step, whether any element saw a contact change.  x0 NULL: the inputs are left
  * pending — read the new first phase's contact (hsddp_get_phase_info), form x0 from it
  * (compute_hkd_state, HKDMPC.cpp:132-134) and call hsddp_update_problem(h, NULL, x0, NULL, NULL,
  * NULL), where NULL contacts are the ones derived here.  The caller's whole MPC tick is

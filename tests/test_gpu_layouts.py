@@ -100,8 +100,8 @@ def test_layouts_validation():
         hsddp.Solver(bad, hsddp.load_settings())
     s = hsddp.Solver(prob, hsddp.load_settings())
     s.solve()
-    with pytest.raises(hsddp.HSDDPError, match="shared layout"):
-        s.extract_commands()
+    cmd = s.extract_commands()  # each element's own knot walk (per-element layouts)
+    assert np.all(cmd["N_mpcsteps"] == 8) and np.all(np.isfinite(cmd["hkd_controls"]))
     s.close()
 
 
@@ -196,3 +196,72 @@ def test_diverging_shift_with_shared_references_fails_and_keeps_the_handle():
     with pytest.raises(hsddp.HSDDPError, match="value export is off"):
         s.value()
     s.close()
+
+
+def test_mixed_gait_mpc_loop_equals_uniform_handles():
+    """HKDMPCSolver's loop for robots on different gaits in one handle (SURVEY.md §8 config C4's
+    MPC side): windows into the reference's trot and flytrot files (one table, per-element window
+    starts) segment into different phase layouts at initialization (HKDProblem.cpp:40-68); then 16
+    ticks of hsddp_advance — each element's own contact changes, per-element shifts — re-solve and
+    command extraction (each element's own knot walk, HKDMPC.cpp:207-298).  Every element's layout,
+    warm start, solution and command record equal, bit for bit, those of a uniform handle of the
+    elements of its file alone."""
+    import os
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    ta, dt = hsddp.load_quad_reference(os.path.join(gold, "ref_trot.csv"))
+    tb, _ = hsddp.load_quad_reference(os.path.join(gold, "ref_flytrot.csv"))
+    tab = np.concatenate([ta, tb])
+    B = 6
+    starts = [0 if b % 2 == 0 else len(ta) + 2 for b in range(B)]
+    rng = np.random.default_rng(4)
+    x0 = np.zeros((B, 24))
+    x0[:, 5] = 0.25
+    x0[:, 12:] = np.float32([.2, -.14, 0, .2, .14, 0, -.2, -.14, 0, -.2, .14, 0])
+    x0[:, 6:12] += rng.uniform(-.2, .2, (B, 6))
+    p = hsddp.reference_problem(tab, dt, starts, x0)
+    assert p.get("layouts") is not None  # the two files segment the 60 knots differently
+    opt, kw = hsddp.load_settings(), dict(max_AL_iter=2, max_DDP_iter=1)
+    m = hsddp.Solver(p, opt)
+    m.solve()
+    groups = [list(range(0, B, 2)), list(range(1, B, 2))]
+    uni = []
+    for idx in groups:
+        q = hsddp.reference_problem(tab, dt, [starts[i] for i in idx], x0[idx])
+        assert q.get("layouts") is None
+        u = hsddp.Solver(q, opt)
+        u.solve()
+        uni.append(u)
+    m.set_options(hsddp.load_settings(**kw))
+    for u in uni:
+        u.set_options(hsddp.load_settings(**kw))
+    feet = rng.standard_normal((B, 12)).astype(np.float32)
+    diverged = 0
+    for it in range(16):
+        xt = x0 + rng.uniform(-.01, .01, x0.shape)
+        m.advance(xt, 1)
+        lay = m.element_layouts()
+        diverged += any(h != lay["horizons"][0] for h in lay["horizons"])
+        m.solve()
+        g = {**m.trajectory(), **m.element_info()}
+        info = m.phase_info()
+        cm = m.extract_commands(1, 0.01 * (it + 1), 0.01, info["durations"], feet, 0.5)
+        for idx, u in zip(groups, uni):
+            u.advance(xt[idx], 1)
+            ul = u.layout()
+            u.solve()
+            gu = {**u.trajectory(), **u.element_info()}
+            cu = u.extract_commands(1, 0.01 * (it + 1), 0.01, u.phase_info()["durations"], feet[idx], 0.5)
+            S = u.S
+            for j, b in enumerate(idx):
+                assert lay["horizons"][b] == ul["horizons"] and lay["shooting"][b] == ul["shooting"], (it, b)
+                assert np.array_equal(g["Xbar"][b, :S], gu["Xbar"][j]), (it, b)
+                for f in ("Ubar", "K"):
+                    assert np.array_equal(g[f][b], gu[f][j]), (it, b, f)
+                for f in ("cost", "iters", "status", "n_ls_trials"):
+                    assert g[f][b] == gu[f][j], (it, b, f)
+                for f in cm.dtype.names:
+                    assert np.array_equal(cm[f][b], cu[f][j]), (it, b, f)
+    assert diverged >= 4  # the loop ran on per-element layouts
+    m.close()
+    for u in uni:
+        u.close()

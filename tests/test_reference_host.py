@@ -143,8 +143,14 @@ def test_reference_problem_host_side():
     assert p["batch"] == 3 and p["window_len"] == 62
     assert p["S"] == sum(n + 1 for n in p["horizons"]) and p["Kc"] == 60
     assert p["contacts"].shape == (3, len(p["horizons"]) + 1, 4)
-    with pytest.raises(hsddp.HSDDPError):  # per-element windows whose layouts differ
-        hsddp.reference_problem(tab, 0.01, [0, 1, 2], x0)
+    # per-element windows whose layouts differ: every element segmented by its own window
+    # (HKDProblem.cpp:40-68), contacts strided by the largest layout, phase starts by each clock
+    q = hsddp.reference_problem(tab, 0.01, [0, 1, 2], x0)
+    assert [list(h) for h in q["layouts"]] == [hsddp.plan_phases(tab[w:w + 62], 0.01)["horizons"] for w in (0, 1, 2)]
+    Pm = max(len(h) for h in q["layouts"])
+    assert q["S"] == 60 + Pm and q["contacts"].shape == (3, Pm + 1, 4) and q["phase_start_times"] is None
+    for b, h in enumerate(q["layouts"]):
+        assert np.array_equal(q["contacts"][b, :len(h) + 1], hsddp.plan_phases(tab[b:b + 62], 0.01)["contacts"])
 
 
 def test_tracker_invariants():
