@@ -278,7 +278,7 @@ def main():
         gait = "mixed" if args.mixed else args.gait
         metric_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 4096)
         c2_cfg = (gait, args.phases, args.knots, B) == ("trot", 4, 50, 1024)
-        label = ("config C5: fp32 Riccati" if args.riccati_fp32 else "BASELINE metric config" if metric_cfg
+        label = ("config C5: fp32 Riccati (a trot-gait mode: DESIGN.md §5)" if args.riccati_fp32 else "BASELINE metric config" if metric_cfg
                  else "config C2: batch 1024" if c2_cfg
                  else "config C3: jump with resets" if gait == "jump" else "config C4 shard: mixed gaits, 4x50 / 8x25 layouts" if args.mixed
                  else "custom")

@@ -2,12 +2,19 @@
 sweep, gains and linear rollout; fp64 dynamics, costs, line search and AL/ReB outer loop) against
 the fp64 oracle and the fp64 GPU path.
 
-Tolerances (measured on MI355X, tools/fp32_tolerance.py -> profiles/round1_fp32_tolerance.json, with
-about 10x margin): one inner iteration K / dU / dX / Xbar / Ubar within 5e-5 relative to the
-largest entry (measured <= 4.6e-6), cost within 5e-6 (5.3e-7), identical line-search decisions;
-full solves with the shipped settings on trot: identical statuses, median final-cost difference
-below 1e-6.  Impact-heavy jump schedules are not held to a tolerance here: fp32 rounding flips
-the PSD test on some elements (DESIGN.md §5, fp32 mode).
+C5 is a trot-gait mode.  Tolerances (measured on MI355X, tools/fp32_tolerance.py ->
+profiles/round3_fp32_tolerance.json, with about 10x margin): one inner iteration K / dU / dX / Xbar /
+Ubar within 5e-5 relative to the largest entry (measured <= 6.6e-6), cost within 5e-6, identical
+line-search decisions; full solves with the shipped settings on trot: identical statuses, median
+final-cost difference below 1e-6.
+
+Impact-heavy jump schedules are a known limitation, bounded here but not held to the trot tolerance:
+fp32 rounding moves some elements' branch decisions (a Quu pivot across the PSD threshold, a merit
+comparison across acceptance), and jump elements amplify any rounding chaotically — the fp64 oracle
+itself moves ~1e-9 under a 1e-15 change of x0 — so after a few iterations a flipped element follows
+another, equally valid trajectory (three iterations: 0.07 % flipped, 99th percentile 2.7e-3 on K;
+full jump solves: 91 % equal statuses).  test_fp32_jump_flip_rate_and_tolerance bounds the flip rate
+and the distribution of the others.
 """
 import numpy as np
 import pytest
