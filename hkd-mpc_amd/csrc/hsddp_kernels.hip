@@ -23,6 +23,18 @@ namespace hsddp {
 
 using namespace hkd;
 
+#ifndef HSDDP_TERM_KERNEL
+#define HSDDP_TERM_KERNEL 0  // > 0: the terminal tasks as their own launch at this many blocks per CU
+#endif
+#ifndef HSDDP_RO_DEFSTAGE
+#define HSDDP_RO_DEFSTAGE 0  // 1: k_rollout stores the Defect rows through LDS (see k_rollout)
+#endif
+#ifndef HSDDP_RO_EXP
+#define HSDDP_RO_EXP 0  // timing experiments only: 1 no Defect row stores, 2 no trial U row stores (k_rollout)
+#endif
+#ifndef HSDDP_LQ_EXP
+#define HSDDP_LQ_EXP 0  // timing experiments only: 1 no terminal tasks, 2 no A - I / B arithmetic
+#endif
 #ifndef FWD_MINB
 #define FWD_MINB 2  // 256-thread blocks per CU for the knot-parallel kernels (k_lq, k_rollout)
 #endif
@@ -269,7 +281,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     __shared__ long sridx[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long nknot = ((long)p.B * p.S + 255) / 256;
-    if ((long)blockIdx.x >= nknot) {  // terminal tasks, one per wave
+    if (!HSDDP_TERM_KERNEL && (long)blockIdx.x >= nknot) {  // terminal tasks, one per wave
         const long task = ((long)blockIdx.x - nknot) * 4 + w;
         // the parallel-retry list of the k_riccati launch that follows starts empty (its only
         // reader before then is the previous iteration's k_riccati_select): no memset launch
@@ -280,6 +292,9 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
         // k_count's activity counts at the end of this iteration start from zero (the
         // graph-replayed iteration of hsddp_solve has no memset launch before k_count)
         if (task == 0 && lane < 4) d.counter[lane] = 0;
+#if HSDDP_LQ_EXP == 1
+        return;
+#endif
         if (task < (long)p.B * p.P) terminal_task<EL>(p, d, reinterpret_cast<TermLds *>(lds)[w], (int)task, lane);
         return;
     }
@@ -340,6 +355,13 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     T *wl = stage[w];
     constexpr int CH_LO[6] = {0, 16, 40, 64, 72, 88}, CH_N[6] = {16, 24, 24, 8, 16, 16};
     wl[lane * LQ_STG + 15] = 0;
+#if HSDDP_LQ_EXP == 2
+    for (int ch = 0; ch < 6; ++ch) {
+        for (int j = 0; j < CH_N[ch]; ++j) wl[lane * LQ_STG + j] = (T)x[j];
+        lq_flush(wl, sridx[w], lqT, ldw, lane, CH_LO[ch], CH_N[ch]);
+    }
+    if (0)
+#endif
     hkd_partial_emit(x, u, cd, p.dt, [&](int piece, int j, double v) {
         const int pos = piece == 0 ? LQ_SE + j : piece == 1 ? sw_at(j / 17, j % 17) : bw_at(j / 12, j % 12);
         const int ch = pos < 16 ? 0 : pos < 40 ? 1 : pos < 64 ? 2 : pos < 72 ? 3 : pos < 88 ? 4 : 5;
@@ -416,7 +438,11 @@ DEV void finish_defect(const Params &p, const Bufs &d, int b, int s, int k, cons
         nrm += xs[j] * xs[j];
         const double df = xs[j] - x[j];
         fs += df * df;
+#if HSDDP_RO_EXP == 1
+        if (df == 12345.678) Dg[j] = df;
+#else
         Dg[j] = df;
+#endif
     }
     d.slot_feas[sb + s] = fs;
     d.slot_div[sb + s] = (k > 0 && sqrt(nrm) > 1e6) ? 1 : 0;
@@ -689,6 +715,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     // the running cost of a control slot (the terminal cost at k = N: the boundary waves)
     if (mine && k < L.N(i)) {
         d2 *ug = (d2 *)(d.Ub[nb ^ 1] + kq * NU);
+#if HSDDP_RO_EXP == 2
+        if (u[0] == 12345.678)
+#endif
 #pragma unroll
         for (int j = 0; j < NU / 2; ++j) ug[j] = d2{u[2 * j], u[2 * j + 1]};
         finish_running(p, d, b, s, L.k0(i) + k, c, x, u);
@@ -701,6 +730,50 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     if (lane == 0)
 #pragma unroll
         for (int j = 0; j < NU; ++j) up[j] = Up0[j];
+#if HSDDP_RO_DEFSTAGE
+    // Defect rows through LDS: each slot's row replaces its own staged state row once every lane's
+    // dynamics have read theirs, then the wave stores the 64 rows as one contiguous range (16-byte
+    // pieces over lanes) instead of one row per lane
+    __shared__ int wflag[64];
+    const bool wr = mine && (k > 0 || i == 0);
+    if (wr) {
+        double xs[NX];
+        if (k == 0) {
+#pragma unroll
+            for (int j = 0; j < NX; ++j) xs[j] = d.x0[(size_t)b * NX + j];
+        } else {
+            double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
+            hkd_step(x - RS, up, cd, p.dt, xs);
+        }
+        wave_sync();  // (no lane writes a row before every lane's dynamics have read the previous one)
+        double *xw = Xt + (gc - xr0) * RS;
+        double nrm = 0.0, fs = 0.0;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) {
+            nrm += xs[j] * xs[j];
+            const double df = xs[j] - xw[j];
+            fs += df * df;
+            xw[j] = df;
+        }
+        const size_t q = (size_t)b * p.S + s;
+        d.slot_feas[q] = fs;
+        d.slot_div[q] = (k > 0 && sqrt(nrm) > 1e6) ? 1 : 0;
+    } else {
+        wave_sync();
+    }
+    wflag[lane] = wr;
+    wave_sync();
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    constexpr int CH = NX / 2;
+#pragma unroll 4
+    for (int f = lane; f < 64 * CH; f += 64) {
+        const int row = f / CH, cc = 2 * (f % CH);
+        if (wflag[row]) {
+            const double *src = Xt + (row + 1) * RS + cc;
+            *(d2 *)(d.Defect + (g0 + row) * NX + cc) = d2{src[0], src[1]};
+        }
+    }
+#else
     if (!mine) return;
     // a phase's first slot: x_init = x0, or the reset map of X_{i-1}[N] (MultiPhaseDDP.cpp:73-81),
     // whose Defect the boundary waves write
@@ -715,6 +788,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
         }
         finish_defect(p, d, b, s, k, x, xs);
     }
+#endif
 }
 
 // k_rollout_tail: the non-shooting states of a phase (k >= ss; HKDProblem::update leaves a new
@@ -1288,10 +1362,33 @@ void launch_normalize(const Params &p, const Bufs &d, hipStream_t st)
     hipLaunchKernelGGL(k_normalize, dim3(blocks_for((long)p.B * p.S * (NX / 2), 256)), dim3(256), 0, st, p, d);
     hipLaunchKernelGGL(k_normalize_sel, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);
 }
+#if HSDDP_TERM_KERNEL
+// the terminal tasks as a launch of their own (registers for more waves per SIMD than k_lq's)
+template <bool EL>
+__global__ __launch_bounds__(256, HSDDP_TERM_KERNEL) void k_terminal(Params p, Bufs d)
+{
+    __shared__ TermLds S[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long task = (long)blockIdx.x * 4 + w;
+    if (p.retry_cap > 0 && task == 0 && lane == 0) *d.retry_count = 0;
+    if (task == 0)
+        for (int t = lane; t < LS_LIVE; t += 64) d.ls_live[t] = 0;
+    if (task == 0 && lane < 4) d.counter[lane] = 0;
+    if (task < (long)p.B * p.P) terminal_task<EL>(p, d, S[w], (int)task, lane);
+}
+#endif
+
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
 {
+#if HSDDP_TERM_KERNEL
+    const dim3 gt(blocks_for((long)p.B * p.P, 4));
+    if (p.elem_layout) hipLaunchKernelGGL((k_terminal<true>), gt, dim3(256), 0, st, p, d);
+    else hipLaunchKernelGGL((k_terminal<false>), gt, dim3(256), 0, st, p, d);
+    const dim3 g(blocks_for((long)p.B * p.S, 256));
+#else
     // the knot blocks, then the terminal tasks (four per block)
     const dim3 g(blocks_for((long)p.B * p.S, 256) + blocks_for((long)p.B * p.P, 4));
+#endif
     if (p.fp32) {
 #define HSDDP_LQ(f, e)                                                          \
     do {                                                                        \

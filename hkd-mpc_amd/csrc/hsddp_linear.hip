@@ -16,6 +16,18 @@ constexpr int HC = 12;  // coupled controls per knot
 #ifndef HSDDP_STAMPS
 #define HSDDP_STAMPS 0
 #endif
+#ifndef HSDDP_LIN_AHEAD
+#define HSDDP_LIN_AHEAD 1  // knots whose images are requested ahead of the one computing (1 or 2)
+#endif
+#ifndef HSDDP_LIN_STORE
+#define HSDDP_LIN_STORE 1  // dX / du stores: 1 each knot's one knot later, 2 two knots at a time, 3 as 1, non-temporal
+#endif
+#if HSDDP_LIN_AHEAD == 2 && HSDDP_LIN_STORE == 2
+#error "paired stores are counted for one knot ahead only"
+#endif
+#ifndef HSDDP_LIN_EXP
+#define HSDDP_LIN_EXP 0  // timing experiments only (tools/lin_exp.sh): 1 no dX / du stores, 2 no arithmetic
+#endif
 // Diagnostic build (make stamps): s_memtime at the stage boundaries of a knot, differences summed
 // per stage into LDS and written to Bufs::dbg of the wave's second element (tools/stamps.py)
 #if HSDDP_STAMPS
@@ -242,7 +254,22 @@ DEV void vm_wait()
     else if constexpr (W == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else if constexpr (W == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if constexpr (W == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if constexpr (W == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (W == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     else static_assert(W < 0, "wait count");
+}
+
+// wait until at most n vector memory operations are outstanding, n in {0, 2, 4, NI2, NI2 + 2,
+// NI2 + 4} (a runtime choice among immediates; larger n: the conservative 0)
+template <int NI2>
+DEV void vm_wait_n(int n)
+{
+    if (n == NI2 + 4) vm_wait<NI2 + 4>();
+    else if (n == NI2 + 2) vm_wait<NI2 + 2>();
+    else if (n == NI2) vm_wait<NI2>();
+    else if (n == 4) vm_wait<4>();
+    else if (n == 2) vm_wait<2>();
+    else vm_wait<0>();
 }
 
 // per-lane constants of one phase: every row's terms as one branch-free formula, a structurally
@@ -294,19 +321,65 @@ DEV void lin_row(const Params &p, LinRow<real> &R, int r)
     R.cq = (r >= 12 && r < NX) ? pick4(R.pc.bq, (rr - 12) / 3) : (real)0;
 }
 
-// a knot's results, stored one knot later
+// a knot's results, stored one knot later (HSDDP_LIN_STORE 2: two knots at a time)
 template <typename real>
 struct LinOut {
-    double *du, *dx;  // this lane's entries of the pending knot
-    real vu, vx;
+    double *du, *dx;  // this lane's entries of the first pending knot
+    real vu, vx;      // pending knot values
+    real vu1, vx1;    // (the second pending knot, store mode 2)
+    int n;            // pending knots
 };
 
-// one knot of SinglePhase::linear_rollout (SinglePhase.cpp:144-178) from the LDS images `cur`;
-// when `more`, the next knot's images are requested into `nxt` first; when `pend`, the previous
-// knot's stores follow them
+template <typename real>
+DEV void lin_push(LinOut<real> &out, real du, real nx)
+{
+    if (out.n == 0) {
+        out.vu = du;
+        out.vx = nx;
+    } else {
+        out.vu1 = du;
+        out.vx1 = nx;
+    }
+    out.n += 1;
+}
+
+template <typename T>
+DEV void lin_st(double *p, T v)
+{
+#if HSDDP_LIN_STORE == 3
+    __builtin_nontemporal_store((double)v, p);
+#else
+    *p = (double)v;
+#endif
+}
+
+// the pending knots' rows (when `go`); returns the store instructions issued
+template <typename real>
+DEV int lin_store_pending(bool go, bool st, LinOut<real> &out)
+{
+#if HSDDP_LIN_EXP == 1
+    go = false;
+#endif
+    if (!go || out.n == 0) return 0;
+    if (st) {
+        lin_st(out.du, out.vu);
+        lin_st(out.dx, out.vx);
+        if (out.n == 2) {
+            lin_st(out.du + NX, out.vu1);
+            lin_st(out.dx + NX, out.vx1);
+        }
+    }
+    const int n = out.n;
+    out.du += n * NX;
+    out.dx += n * NX;
+    out.n = 0;
+    return 2 * n;
+}
+
 template <typename real>
 DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<real> &nxt, bool more, bool pend,
-                  LinSrc<real> &src, const LinRow<real> &R, bool st, LinOut<real> &out, real &dx, real &q1s, real &q2s)
+                  LinSrc<real> &src, const LinRow<real> &R, bool st, LinOut<real> &out, real &dx, real &q1s, real &q2s,
+                  int wait = 0, bool more2 = false, bool first = true)
 {
     using I = LinImg<real>;
     constexpr int NI2 = 2 * I::NI;
@@ -314,28 +387,32 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
     const bool rowl = r < NX;
     const int rr = rowl ? r : 0;
     LSTAMP(0);
+#if HSDDP_LIN_AHEAD == 2
+    (void)nxt;
+    (void)more;
+    vm_wait_n<NI2>(wait);
+#else
+    (void)wait;
+    (void)more2;
     if (more) {
         src.advance();
         lin_fetch(nxt, src);
     }
-    if (pend) {
-        if (st) {
-            *out.du = out.vu;
-            *out.dx = out.vx;
-        }
-        out.du += NX;
-        out.dx += NX;
-    }
-    // all but what was just issued: the 2 NI DMA of the next knot, the 2 stores of the previous
-    if (more) {
-        if (pend) vm_wait<NI2 + 2>();
-        else vm_wait<NI2>();
-    } else {
-        if (pend) vm_wait<2>();
-        else vm_wait<0>();
-    }
+    // store mode 2: the two pending knots at the first knot of a pair
+    const int ns = lin_store_pending(HSDDP_LIN_STORE == 2 ? pend && first : pend, st, out);
+    // all but what was just issued: the 2 NI DMA of the next knot, the previous knots' stores
+    vm_wait_n<NI2>((more ? NI2 : 0) + ns);
+#endif
     LSYNC();
     LSTAMP(1);
+#if HSDDP_LIN_EXP == 2
+    {
+        const real v = ((const real *)cur.v[hf])[r];
+        lin_push(out, v, v);
+        dx = v;
+        return;
+    }
+#endif
     const char *img = cur.v[hf];
     const real *kimg = (const real *)(img + I::K), *lq = (const real *)(img + I::LQ), *dd = (const real *)(img + I::D);
     const double *dUi = (const double *)(img + I::DU);
@@ -378,6 +455,17 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
     for (int q = 0; q < 12; ++q) cbw[q] = bwp[3 * q];
 #pragma unroll
     for (int b = 0; b < 3; ++b) crb[b] = rbp[R.rbi[b]];
+#if HSDDP_LIN_AHEAD == 2
+    // the image's last reads are in flight: once they land the buffer takes knot k + 2's image
+    pin(cbw);
+    pin(crb);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (more2) {
+        src.advance();
+        lin_fetch(cur, src);
+    }
+    lin_store_pending(pend, st, out);
+#endif
     if (rowl) sduv[r] = du;
     // dX terms with lane-dependent columns (rows 3..5: dt dX[r + 6]; lxx cross terms)
     const real x3 = sdxv[R.i3];
@@ -423,8 +511,7 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
     const real nx = rowl ? ((dx + sdx) + bdu) + ddr : (real)0;
     q1s += lxr * dx + lur * du;
     q2s += dx * lxd + du * lud;
-    out.vu = du;
-    out.vx = nx;
+    lin_push(out, du, nx);
     dx = nx;
     LSYNC();
     LSTAMP(4);
@@ -474,6 +561,12 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         LinSrc<real> src;
         src.init(p, d, eb, s0, k0, lane);
         lin_fetch(B0, src);  // the phase's first knot (its wait is in lin_knot)
+#if HSDDP_LIN_AHEAD == 2
+        if (N > 1) {  // and the second
+            src.advance();
+            lin_fetch(B1, src);
+        }
+#endif
         LinRow<real> R;
         load_phase(p, d, eb, hf, i, R.pc);
         if (i > 0) { // dx_init = Px dX_end
@@ -500,16 +593,28 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         R.cpl = rowl && (rr < HC ? stl : !stl);
         R.krow0 = (rr % HC) * NX;
         lin_row(p, R, r);
-        LinOut<real> out{d.du + (b * p.Kc + k0) * NX + rr, d.dX + (b * p.S + s0 + 1) * NX + rr, 0, 0};
+        LinOut<real> out{d.du + (b * p.Kc + k0) * NX + rr, d.dX + (b * p.S + s0 + 1) * NX + rr, 0, 0, 0, 0, 0};
         real q1s = 0, q2s = 0;
+#if HSDDP_LIN_AHEAD == 2
+        // operations issued after knot k's image request: knot k - 3's stores and knot k + 1's image
+        // (both during knot k - 1... k - 2), knot k - 2's stores; knots 0 and 1: the two phase-start requests
+        constexpr int NI2 = 2 * LinImg<real>::NI;
+        auto wait_of = [&](int k) {
+            if (k == 0) return N > 1 ? NI2 : 0;
+            if (k == 1) return k + 1 < N ? NI2 : 0;
+            return (k >= 3 ? 2 : 0) + (k + 1 < N ? NI2 : 0) + 2;
+        };
         for (int k = 0; k < N; k += 2) {
-            lin_knot(p, S, B0, B1, k + 1 < N, k > 0, src, R, st, out, dx, q1s, q2s);
-            if (k + 1 < N) lin_knot(p, S, B1, B0, k + 2 < N, true, src, R, st, out, dx, q1s, q2s);
+            lin_knot(p, S, B0, B1, false, k > 0, src, R, st, out, dx, q1s, q2s, wait_of(k), k + 2 < N);
+            if (k + 1 < N) lin_knot(p, S, B1, B0, false, true, src, R, st, out, dx, q1s, q2s, wait_of(k + 1), k + 3 < N);
         }
-        if (st) {  // the phase's last knot
-            *out.du = out.vu;
-            *out.dx = out.vx;
+#else
+        for (int k = 0; k < N; k += 2) {
+            lin_knot(p, S, B0, B1, k + 1 < N, k > 0, src, R, st, out, dx, q1s, q2s, 0, false, true);
+            if (k + 1 < N) lin_knot(p, S, B1, B0, k + 2 < N, true, src, R, st, out, dx, q1s, q2s, 0, false, false);
         }
+#endif
+        lin_store_pending(true, st, out);  // the phase's last knots
         const double *rec = d.term + (b * p.P + i) * TW;
         if (rowl) S.dx[hf][r] = dx;
         LSYNC();
