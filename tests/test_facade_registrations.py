@@ -164,7 +164,7 @@ TICKS = 30
 
 @pytest.mark.parametrize("name", ["trot", "flytrot"])
 def test_describe_ticks_equal_reference_update(tmp_path, name):
-    """Ticks 1..24 (HKDProblem::update, HKDProblem.cpp:117-222, on the facade's phases): every tick's
+    """Ticks 1..30 (HKDProblem::update, HKDProblem.cpp:117-222, on the facade's phases): every tick's
     device problem — layout, shooting states (SS_set: a new last phase of <= 2 knots keeps an empty
     one, SinglePhase.cpp:34 / HKDProblem.cpp:214-218), contacts, references at the phases' float
     time offsets and the shifted warm start — equals the restated bookkeeping (oracle
