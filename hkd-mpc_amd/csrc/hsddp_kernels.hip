@@ -23,6 +23,9 @@ namespace hsddp {
 
 using namespace hkd;
 
+#ifndef HSDDP_LQ_ALIGN
+#define HSDDP_LQ_ALIGN 0  // 1: k_lq writes fp64 records in 128-byte chunks (see k_lq)
+#endif
 #ifndef HSDDP_TERM_KERNEL
 #define HSDDP_TERM_KERNEL 0  // > 0: the terminal tasks as their own launch at this many blocks per CU
 #endif
@@ -263,6 +266,46 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
     }
 }
 
+// lu + ReB gradient / Hessian of one knot (SinglePhase.cpp:380-394)
+DEV void lq_lu_reb(const Params &p, const int *c, const double *u, const double *ur, const double *dl, const double *ep,
+                   double *lu, double *rb)
+{
+#pragma unroll
+    for (int j = 0; j < NU; ++j) lu[j] = p.dt * r_diag(p, j) * (u[j] - ur[j]);
+#pragma unroll
+    for (int j = 0; j < 24; ++j) rb[j] = 0.0;
+    // uniform ReB parameters (the default schedule) and per-knot ones as separate code: in the
+    // uniform case no per-row (delta, eps) load and no per-row 1 / delta division is issued
+    auto reb = [&](auto uniform) {
+        constexpr bool U = decltype(uniform)::value;
+        const double inv_du = p.grf_inv_delta;
+#pragma unroll
+        for (int lg = 0; lg < 4; ++lg) {
+            if (!c[lg]) continue;
+            double gu[3] = {0, 0, 0}, hu[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int r = 0; r < 5; ++r) {
+                double row[3], d1, d2;
+                grf_row(p.mu, r, row);
+                double g = row[0] * u[3 * lg] + row[1] * u[3 * lg + 1] + row[2] * u[3 * lg + 2];
+                const double dlr = U ? p.grf_delta : dl[5 * lg + r];
+                reb_derivs(g, dlr, U ? inv_du : 1.0 / dlr, d1, d2);
+                double e = U ? p.grf_eps : ep[5 * lg + r];
+                for (int a = 0; a < 3; ++a) gu[a] += e * d1 * row[a];
+                hu[0] += e * (d2 * row[0] * row[0]); hu[1] += e * (d2 * row[0] * row[1]);
+                hu[2] += e * (d2 * row[0] * row[2]); hu[3] += e * (d2 * row[1] * row[1]);
+                hu[4] += e * (d2 * row[1] * row[2]); hu[5] += e * (d2 * row[2] * row[2]);
+            }
+            for (int a = 0; a < 3; ++a) lu[3 * lg + a] += p.dt * gu[a];
+            for (int a = 0; a < 6; ++a) rb[6 * lg + a] = p.dt * hu[a];
+        }
+    };
+    if (p.ReB_active) {
+        if (p.reb_uniform) reb(std::true_type{});
+        else reb(std::false_type{});
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_lq: per (element, state slot): cost and |Defect|^2 at the current (X, U); compact LQ model at
 // control slots (SinglePhase::compute_cost + LQ_approximation, SinglePhase.cpp:235-296).
@@ -353,6 +396,54 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     // a line written in two partial pieces at different times cost a second line write (PMC: 11 %
     // more WRITE_SIZE than the records).
     T *wl = stage[w];
+#if HSDDP_LQ_ALIGN
+    if constexpr (!F32) {
+        // 128-byte chunks (16 values): every line of a record is written once, whole.  Positions
+        // 96 .. 103 (the last B values) wait in the stage for lx[0 .. 8); lu and the ReB Hessian
+        // share the chunk [144, 160).
+        auto put = [&](int col, double v) { wl[lane * LQ_STG + col] = (T)v; };
+        put(15, 0.0);
+        hkd_partial_emit(x, u, cd, p.dt, [&](int piece, int j, double v) {
+            const int pos = piece == 0 ? LQ_SE + j : piece == 1 ? sw_at(j / 17, j % 17) : bw_at(j / 12, j % 12);
+            const int ch = pos >> 4;
+            put(pos & 15, v);
+            if (ch < 6 && pos == 16 * ch + (ch == 0 ? 14 : 15)) {  // the chunk's last value
+                lq_flush(wl, sridx[w], lqT, ldw, lane, 16 * ch, 16);
+                if (ch == 3) put(67 - 64, 0.0);
+            }
+        });
+        double lx[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) lx[j] = p.dt * q_diag(p, c, j) * (x[j] - xr[j]);
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            double e = (x[12 + j] - x[3 + j % 3]) - (pf[j] - xr[3 + j % 3]);
+            double v = p.dt * c[j / 3] * foot_weight(p, c, j) * e;
+            lx[3 + j % 3] += -v;
+            lx[12 + j] += v;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) put(8 + j, lx[j]);
+        lq_flush(wl, sridx[w], lqT, ldw, lane, 96, 16);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) put(j, lx[8 + j]);
+        lq_flush(wl, sridx[w], lqT, ldw, lane, 112, 16);
+        double lu[NU], rb[24];
+        lq_lu_reb(p, c, u, ur, dl, ep, lu, rb);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) put(j, lu[j]);
+        lq_flush(wl, sridx[w], lqT, ldw, lane, 128, 16);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) put(j, lu[16 + j]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) put(8 + j, rb[j]);
+        lq_flush(wl, sridx[w], lqT, ldw, lane, 144, 16);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) put(j, rb[8 + j]);
+        lq_flush(wl, sridx[w], lqT, ldw, lane, 160, 16);
+        return;
+    }
+#endif
     constexpr int CH_LO[6] = {0, 16, 40, 64, 72, 88}, CH_N[6] = {16, 24, 24, 8, 16, 16};
     wl[lane * LQ_STG + 15] = 0;
 #if HSDDP_LQ_EXP == 2
@@ -385,40 +476,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     lq_stage_store<T, LQ_LX, NX>(stage[w], sridx[w], lx, lqT, ldw, lane);
     // lu + ReB gradient / Hessian (SinglePhase.cpp:380-394)
     double lu[NU], rb[24];
-#pragma unroll
-    for (int j = 0; j < NU; ++j) lu[j] = p.dt * r_diag(p, j) * (u[j] - ur[j]);
-#pragma unroll
-    for (int j = 0; j < 24; ++j) rb[j] = 0.0;
-    // uniform ReB parameters (the default schedule) and per-knot ones as separate code: in the
-    // uniform case no per-row (delta, eps) load and no per-row 1 / delta division is issued
-    auto reb = [&](auto uniform) {
-        constexpr bool U = decltype(uniform)::value;
-        const double inv_du = p.grf_inv_delta;
-#pragma unroll
-        for (int lg = 0; lg < 4; ++lg) {
-            if (!c[lg]) continue;
-            double gu[3] = {0, 0, 0}, hu[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-            for (int r = 0; r < 5; ++r) {
-                double row[3], d1, d2;
-                grf_row(p.mu, r, row);
-                double g = row[0] * u[3 * lg] + row[1] * u[3 * lg + 1] + row[2] * u[3 * lg + 2];
-                const double dlr = U ? p.grf_delta : dl[5 * lg + r];
-                reb_derivs(g, dlr, U ? inv_du : 1.0 / dlr, d1, d2);
-                double e = U ? p.grf_eps : ep[5 * lg + r];
-                for (int a = 0; a < 3; ++a) gu[a] += e * d1 * row[a];
-                hu[0] += e * (d2 * row[0] * row[0]); hu[1] += e * (d2 * row[0] * row[1]);
-                hu[2] += e * (d2 * row[0] * row[2]); hu[3] += e * (d2 * row[1] * row[1]);
-                hu[4] += e * (d2 * row[1] * row[2]); hu[5] += e * (d2 * row[2] * row[2]);
-            }
-            for (int a = 0; a < 3; ++a) lu[3 * lg + a] += p.dt * gu[a];
-            for (int a = 0; a < 6; ++a) rb[6 * lg + a] = p.dt * hu[a];
-        }
-    };
-    if (p.ReB_active) {
-        if (p.reb_uniform) reb(std::true_type{});
-        else reb(std::false_type{});
-    }
+    lq_lu_reb(p, c, u, ur, dl, ep, lu, rb);
     lq_stage_store<T, LQ_LU, NU>(stage[w], sridx[w], lu, lqT, ldw, lane);
     lq_stage_store<T, LQ_RB, 24>(stage[w], sridx[w], rb, lqT, ldw, lane);
 }
