@@ -2228,8 +2228,18 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
         int P_old = 0;                       // the element's phases before the steps
         int next_kind = 0, next_step = -1;  // row P: 0 old row, 1 contact at relj, 2 at plan + dt_mpc
     };
+    // with the handle's shared layout and window, an element whose contact rows equal element 0's
+    // tracks exactly as element 0 does (the MPC batch of one gait): its bookkeeping is element 0's
+    std::vector<int> rep(B);
+    for (int b = 0; b < B; ++b) {
+        const size_t n = (size_t)(P0 + 1) * 4;
+        rep[b] = (b > 0 && !elem && Br == 1 &&
+                  std::equal(h->contacts.begin() + (size_t)b * n, h->contacts.begin() + (size_t)(b + 1) * n, h->contacts.begin()))
+                     ? 0 : b;
+    }
     std::vector<Track> tr(B);
     for (int b = 0; b < B; ++b) {
+        if (rep[b] != b) continue;
         Track &T = tr[b];
         const Layout L = layout_of(h, b);
         const int *reach0 = elem ? &h->reach_el[(size_t)b * HSDDP_MAX_PHASES] : h->reach_end.data();
@@ -2272,7 +2282,7 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     // the shift: one set of flags for the batch when it agrees (the shared layout stays shared),
     // else every element's own (per-element layouts; they need per-element references)
     bool agree = !elem;
-    for (int b = 1; b < B && agree; ++b) agree = tr[b].flags == tr[0].flags;
+    for (int b = 1; b < B && agree; ++b) agree = tr[rep[b]].flags == tr[0].flags;
     int rc;
     if (agree) {
         if ((rc = hsddp_shift(h, n_steps, tr[0].flags.data()))) return rc;
@@ -2281,14 +2291,16 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
             return fail(HSDDP_ERR_UNSUPPORTED, "elements disagree on a contact change, which takes per-element layouts "
                                                "and per-element references (ref_per_element = 1)");
         std::vector<int> cc((size_t)B * n_steps);
-        for (int b = 0; b < B; ++b) std::copy(tr[b].flags.begin(), tr[b].flags.end(), cc.begin() + (size_t)b * n_steps);
+        for (int b = 0; b < B; ++b)
+            std::copy(tr[rep[b]].flags.begin(), tr[rep[b]].flags.end(), cc.begin() + (size_t)b * n_steps);
         if ((rc = hsddp_shift_elements(h, n_steps, cc.data()))) return rc;
     }
     for (int b = 0; b < B; ++b) {
         const Layout L = layout_of(h, b);
         const int *re = h->lays.empty() ? h->reach_end.data() : &h->reach_el[(size_t)b * HSDDP_MAX_PHASES];
-        if (L.P != (int)tr[b].hz.size() || !std::equal(tr[b].hz.begin(), tr[b].hz.end(), L.N) ||
-            !std::equal(tr[b].reach.begin(), tr[b].reach.end(), re))
+        const Track &T = tr[rep[b]];
+        if (L.P != (int)T.hz.size() || !std::equal(T.hz.begin(), T.hz.end(), L.N) ||
+            !std::equal(T.reach.begin(), T.reach.end(), re))
             return fail(HSDDP_ERR_ARG, "internal: advance and shift disagree on the layout");
     }
     if ((rc = build_refs(h, ws.data(), h->win_len, nullptr, dts, false))) return rc;
@@ -2296,7 +2308,7 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     std::vector<int> contacts((size_t)B * (P + 1) * 4, 0);
     std::vector<double> dur((size_t)B * P * 4, 0.0);
     for (int b = 0; b < B; ++b) {
-        const Track &T = tr[b];
+        const Track &T = tr[rep[b]];
         const int Pb = (int)T.hz.size();
         auto phase_contact = [&](int sc, int l) {
             return sc >= 0 ? h->contacts[((size_t)b * (P0 + 1) + sc) * 4 + l]
@@ -2328,7 +2340,7 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     if (contact_change)  // per step: some element saw a contact change (the batch's flag when it agrees)
         for (int j = 0; j < n_steps; ++j) {
             int f = 0;
-            for (int b = 0; b < B; ++b) f |= tr[b].flags[j];
+            for (int b = 0; b < B; ++b) f |= tr[rep[b]].flags[j];
             contact_change[j] = f;
         }
     return HSDDP_OK;

@@ -60,10 +60,13 @@ static_assert(LQ_SE + 15 < LQ_SW && LQ_SW + 51 < LQ_BW && LQ_BW + 36 == LQ_LX &&
 // longest regularisation schedule of one failed sweep (HSDDP_MAX_REG_ATTEMPTS, include/hsddp.h)
 constexpr int MAX_REG_ATTEMPTS = 64;
 
+// per-phase terminal record: Phix, Phixx, Px, each piece starting on a 128-byte line and the record
+// a whole number of lines (a line written in two halves at different times costs a second write)
 constexpr int TM_PHIX = 0;
-constexpr int TM_PHIXX = 24;
-constexpr int TM_PX = 24 + NN;
-constexpr int TW = 24 + 2 * NN;          // 1176
+constexpr int TM_PHIXX = 32;
+constexpr int TM_PX = TM_PHIXX + NN;
+constexpr int TW = TM_PX + NN;           // 1184
+static_assert(TM_PHIXX % 16 == 0 && TM_PX % 16 == 0 && TW % 16 == 0, "terminal record lines");
 
 // Phase layout of one element: P phases of N_i knots, state slots s0_i .. s0_i + N_i, control slots
 // k0_i .. k0_i + N_i - 1, shooting states ss_i; S = sum(N_i + 1).  Per-element layouts

@@ -20,10 +20,10 @@ constexpr int HC = 12;  // coupled controls per knot
 #define HSDDP_LIN_AHEAD 1  // knots whose images are requested ahead of the one computing (1 or 2)
 #endif
 #ifndef HSDDP_LIN_STORE
-#define HSDDP_LIN_STORE 1  // dX / du stores: 1 each knot's one knot later, 2 two knots at a time, 3 as 1, non-temporal
+#define HSDDP_LIN_STORE 1  // dX / du rows: 1 each knot's one knot later, 2 in aligned row pairs (LinOut)
 #endif
 #if HSDDP_LIN_AHEAD == 2 && HSDDP_LIN_STORE == 2
-#error "paired stores are counted for one knot ahead only"
+#error "the two-ahead wait counts assume one knot's rows per knot"
 #endif
 #ifndef HSDDP_LIN_EXP
 #define HSDDP_LIN_EXP 0  // timing experiments only (tools/lin_exp.sh): 1 no dX / du stores, 2 no arithmetic
@@ -321,39 +321,54 @@ DEV void lin_row(const Params &p, LinRow<real> &R, int r)
     R.cq = (r >= 12 && r < NX) ? pick4(R.pc.bq, (rr - 12) / 3) : (real)0;
 }
 
-// a knot's results, stored one knot later (HSDDP_LIN_STORE 2: two knots at a time)
+// a knot's dX / du rows, stored one knot later.  HSDDP_LIN_STORE 2: the rows go out in aligned
+// pairs — rows 2m and 2m + 1 of the element together, 384 bytes = three whole 128-byte lines (a row
+// alone covers one and a half) — the even row waiting in a register for its partner.
+template <typename real>
+struct RowPairs {
+    double *base;  // this lane's entry of the element's row 0
+    int row;       // the next row (the same on every lane)
+    real held;     // row `row - 1`, when that is even and not stored yet
+};
+template <typename real>
+DEV int rows_push(RowPairs<real> &w, bool st, real v)
+{
+    int ns = 0;
+    if (w.row & 1) {  // rows are pushed in order from row 0: the even partner is held
+        if (st) {
+            w.base[(size_t)(w.row - 1) * NX] = (double)w.held;
+            w.base[(size_t)w.row * NX] = (double)v;
+        }
+        ns = 2;
+    } else {
+        w.held = v;
+    }
+    w.row += 1;
+    return ns;
+}
+template <typename real>
+DEV void rows_flush(RowPairs<real> &w, bool st)
+{
+    if ((w.row & 1) && st) w.base[(size_t)(w.row - 1) * NX] = (double)w.held;
+}
+
 template <typename real>
 struct LinOut {
-    double *du, *dx;  // this lane's entries of the first pending knot
-    real vu, vx;      // pending knot values
-    real vu1, vx1;    // (the second pending knot, store mode 2)
-    int n;            // pending knots
+    double *du, *dx;      // store mode 1: this lane's entries of the pending knot
+    real vu, vx;          // the pending knot's values
+    int n;                // pending knots (0 or 1)
+    RowPairs<real> ru, rx;  // store mode 2: the element's du and dX rows
 };
 
 template <typename real>
 DEV void lin_push(LinOut<real> &out, real du, real nx)
 {
-    if (out.n == 0) {
-        out.vu = du;
-        out.vx = nx;
-    } else {
-        out.vu1 = du;
-        out.vx1 = nx;
-    }
-    out.n += 1;
+    out.vu = du;
+    out.vx = nx;
+    out.n = 1;
 }
 
-template <typename T>
-DEV void lin_st(double *p, T v)
-{
-#if HSDDP_LIN_STORE == 3
-    __builtin_nontemporal_store((double)v, p);
-#else
-    *p = (double)v;
-#endif
-}
-
-// the pending knots' rows (when `go`); returns the store instructions issued
+// the pending knot's rows (when `go`); returns the store instructions issued
 template <typename real>
 DEV int lin_store_pending(bool go, bool st, LinOut<real> &out)
 {
@@ -361,25 +376,24 @@ DEV int lin_store_pending(bool go, bool st, LinOut<real> &out)
     go = false;
 #endif
     if (!go || out.n == 0) return 0;
-    if (st) {
-        lin_st(out.du, out.vu);
-        lin_st(out.dx, out.vx);
-        if (out.n == 2) {
-            lin_st(out.du + NX, out.vu1);
-            lin_st(out.dx + NX, out.vx1);
-        }
-    }
-    const int n = out.n;
-    out.du += n * NX;
-    out.dx += n * NX;
     out.n = 0;
-    return 2 * n;
+#if HSDDP_LIN_STORE == 2
+    return rows_push(out.rx, st, out.vx) + rows_push(out.ru, st, out.vu);
+#else
+    if (st) {
+        *out.du = (double)out.vu;
+        *out.dx = (double)out.vx;
+    }
+    out.du += NX;
+    out.dx += NX;
+    return 2;
+#endif
 }
 
 template <typename real>
 DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<real> &nxt, bool more, bool pend,
                   LinSrc<real> &src, const LinRow<real> &R, bool st, LinOut<real> &out, real &dx, real &q1s, real &q2s,
-                  int wait = 0, bool more2 = false, bool first = true)
+                  int wait = 0, bool more2 = false)
 {
     using I = LinImg<real>;
     constexpr int NI2 = 2 * I::NI;
@@ -398,8 +412,7 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
         src.advance();
         lin_fetch(nxt, src);
     }
-    // store mode 2: the two pending knots at the first knot of a pair
-    const int ns = lin_store_pending(HSDDP_LIN_STORE == 2 ? pend && first : pend, st, out);
+    const int ns = lin_store_pending(pend, st, out);
     // all but what was just issued: the 2 NI DMA of the next knot, the previous knots' stores
     vm_wait_n<NI2>((more ? NI2 : 0) + ns);
 #endif
@@ -556,6 +569,9 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
     real v1 = 0, v2 = 0, dx = 0;
     const auto LY = layout_of<EL>(d, (int)eb[0]);
     const int P = LY.P();
+    LinOut<real> out{};
+    out.ru = RowPairs<real>{d.du + b * p.Kc * NX + rr, 0, 0};
+    out.rx = RowPairs<real>{d.dX + b * p.S * NX + rr, 0, 0};
     for (int i = 0; i < P; ++i) {
         const int N = LY.N(i), s0 = LY.s0(i), k0 = LY.k0(i);
         LinSrc<real> src;
@@ -581,10 +597,12 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         } else {
             dx = 0;
         }
-        if (rowl) {
-            dx = dx + defg[(b * p.S + s0) * NX + r];
-            if (st) d.dX[(b * p.S + s0) * NX + r] = dx;
-        }
+        if (rowl) dx = dx + defg[(b * p.S + s0) * NX + r];
+#if HSDDP_LIN_STORE == 2
+        rows_push(out.rx, st, dx);  // (its stores precede knot 0's wait: counted as complete there)
+#else
+        if (st) d.dX[(b * p.S + s0) * NX + r] = dx;
+#endif
         // lxx row r (HKDCost.cpp:32): diagonal + foot cross terms
         lxx_row(p, R.pc, r, R.lx);
         R.ru = rowl ? (real)(p.dt * r_diag(p, r)) : (real)0;
@@ -593,7 +611,8 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         R.cpl = rowl && (rr < HC ? stl : !stl);
         R.krow0 = (rr % HC) * NX;
         lin_row(p, R, r);
-        LinOut<real> out{d.du + (b * p.Kc + k0) * NX + rr, d.dX + (b * p.S + s0 + 1) * NX + rr, 0, 0, 0, 0, 0};
+        out.du = d.du + (b * p.Kc + k0) * NX + rr;
+        out.dx = d.dX + (b * p.S + s0 + 1) * NX + rr;
         real q1s = 0, q2s = 0;
 #if HSDDP_LIN_AHEAD == 2
         // operations issued after knot k's image request: knot k - 3's stores and knot k + 1's image
@@ -610,8 +629,8 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         }
 #else
         for (int k = 0; k < N; k += 2) {
-            lin_knot(p, S, B0, B1, k + 1 < N, k > 0, src, R, st, out, dx, q1s, q2s, 0, false, true);
-            if (k + 1 < N) lin_knot(p, S, B1, B0, k + 2 < N, true, src, R, st, out, dx, q1s, q2s, 0, false, false);
+            lin_knot(p, S, B0, B1, k + 1 < N, k > 0, src, R, st, out, dx, q1s, q2s);
+            if (k + 1 < N) lin_knot(p, S, B1, B0, k + 2 < N, true, src, R, st, out, dx, q1s, q2s);
         }
 #endif
         lin_store_pending(true, st, out);  // the phase's last knots
@@ -628,6 +647,10 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         v2 += half_sum(q2s);
         LSYNC();
     }
+#if HSDDP_LIN_STORE == 2
+    rows_flush(out.rx, st);
+    rows_flush(out.ru, st);
+#endif
 #if HSDDP_STAMPS
     __syncthreads();
     if (lane < 8) d.dbg[(size_t)__builtin_amdgcn_readfirstlane((int)eb[1]) * 16 + 8 + lane] += lin_stamps().st[lane];
