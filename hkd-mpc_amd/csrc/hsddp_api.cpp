@@ -374,8 +374,11 @@ static void fill_params(hsddp_handle h)
         }
     }
     p.retry_m = M;
-    // value export writes G[0], H[0] from the sweep that succeeds: the in-kernel retry loop only
-    p.retry_cap = (M > 0 && M <= h->retry_m_alloc && !p.store_value) ? h->retry_cap_alloc : 0;
+    // value export writes G[0], H[0] from the sweep that succeeds: the in-kernel retry loop only.
+    // Below 4 elements (C1: one robot) the retries run in k_riccati too: the retry and select
+    // launches (≈ 10 µs of a 340 µs inner iteration at B = 1) cost more than the rare sequential
+    // retry of a lone element saves.
+    p.retry_cap = (M > 0 && M <= h->retry_m_alloc && !p.store_value && p.B >= 4) ? h->retry_cap_alloc : 0;
 }
 
 // the solver-info history holds every entry one solve with the handle's options can push: the

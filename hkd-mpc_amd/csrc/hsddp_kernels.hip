@@ -24,13 +24,13 @@ namespace hsddp {
 using namespace hkd;
 
 #ifndef HSDDP_LQ_ALIGN
-#define HSDDP_LQ_ALIGN 0  // 1: k_lq writes fp64 records in 128-byte chunks (see k_lq)
+#define HSDDP_LQ_ALIGN 1  // 1: k_lq writes fp64 records in 128-byte chunks (see k_lq)
 #endif
 #ifndef HSDDP_TERM_KERNEL
-#define HSDDP_TERM_KERNEL 0  // > 0: the terminal tasks as their own launch at this many blocks per CU
+#define HSDDP_TERM_KERNEL 4  // > 0: the terminal tasks as their own launch at this many blocks per CU
 #endif
 #ifndef HSDDP_RO_DEFSTAGE
-#define HSDDP_RO_DEFSTAGE 0  // 1: k_rollout stores the Defect rows through LDS (see k_rollout)
+#define HSDDP_RO_DEFSTAGE 1  // 1: k_rollout stores the Defect rows through LDS (see k_rollout)
 #endif
 #ifndef HSDDP_RO_EXP
 #define HSDDP_RO_EXP 0  // timing experiments only: 1 no Defect row stores, 2 no trial U row stores (k_rollout)

@@ -20,7 +20,7 @@ constexpr int HC = 12;  // coupled controls per knot
 #define HSDDP_LIN_AHEAD 1  // knots whose images are requested ahead of the one computing (1 or 2)
 #endif
 #ifndef HSDDP_LIN_STORE
-#define HSDDP_LIN_STORE 1  // dX / du rows: 1 each knot's one knot later, 2 in aligned row pairs (LinOut)
+#define HSDDP_LIN_STORE 2  // dX / du rows: 1 each knot's one knot later, 2 in aligned row pairs (LinOut)
 #endif
 #if HSDDP_LIN_AHEAD == 2 && HSDDP_LIN_STORE == 2
 #error "the two-ahead wait counts assume one knot's rows per knot"

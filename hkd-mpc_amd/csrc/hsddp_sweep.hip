@@ -52,7 +52,7 @@ namespace sweep {
 // value update on the matrix cores (1) or by DPP-broadcast multiply-adds from the lanes holding
 // K_c (0, no LDS round trip)
 #ifndef HSDDP_DU_PAIRS
-#define HSDDP_DU_PAIRS 0
+#define HSDDP_DU_PAIRS 1
 #endif
 #ifndef HSDDP_VALUE_MFMA
 #define HSDDP_VALUE_MFMA 0
