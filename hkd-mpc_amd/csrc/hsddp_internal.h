@@ -48,7 +48,7 @@ constexpr int LQ_LX = 104;               // 24
 constexpr int LQ_LU = 128;               // 24
 constexpr int LQ_RB = 152;               // 24  dt * ReB Hessian, 4 legs x sym 3x3 (00,01,02,11,12,22)
 constexpr int LQW = 176;
-constexpr int LQW32 = 176;               // fp32 record stride (16-byte pieces)
+constexpr int LQW32 = 192;               // fp32 record stride: 6 whole 128-byte lines (176 values + zeros)
 // record position of omega-row r (0..2) x sparse column q of A - I, and of B's omega row r x GRF
 // column k: column-major, so k_lq emits the pieces in position order (hkd_partial_emit) and
 // stores them through its LDS stage in contiguous chunks

@@ -23,9 +23,6 @@ namespace hsddp {
 
 using namespace hkd;
 
-#ifndef HSDDP_LQ_ALIGN
-#define HSDDP_LQ_ALIGN 1  // 1: k_lq writes fp64 records in 128-byte chunks (see k_lq)
-#endif
 #ifndef HSDDP_TERM_KERNEL
 #define HSDDP_TERM_KERNEL 4  // > 0: the terminal tasks as their own launch at this many blocks per CU
 #endif
@@ -50,7 +47,8 @@ using namespace hkd;
 // record, so an instruction covers ~1 KB of contiguous records.  Pieces are even-sized at even
 // offsets, so every pair is aligned in HBM.  Lanes that returned early (past the batch, finished
 // element, phase-end slot) left ridx = -1 and their records are skipped.
-constexpr int LQ_STG = 25; // LDS stride per lane (pieces of 24, +1)
+// LDS stride per lane: one 128-byte line of a record (16 fp64 / 32 fp32 values) + 1
+template <typename T> constexpr int LQ_STG = 128 / (int)sizeof(T) + 1;
 
 // the wave's staged values (record positions OFF .. OFF + N - 1 at stage columns 0 .. N - 1) to the
 // records, pair by pair, by the still-active lanes
@@ -68,8 +66,8 @@ DEV void lq_flush(T *wl, const long *ridx, T *lq, int ldw, int lane, int OFF, in
         const long rr = ridx[r];
         if (rr >= 0) {
             T2 w;
-            w.x = wl[r * LQ_STG + 2 * jp];
-            w.y = wl[r * LQ_STG + 2 * jp + 1];
+            w.x = wl[r * LQ_STG<T> + 2 * jp];
+            w.y = wl[r * LQ_STG<T> + 2 * jp + 1];
             *reinterpret_cast<T2 *>(lq + rr * ldw + OFF + 2 * jp) = w;
         }
     }
@@ -78,13 +76,6 @@ DEV void lq_flush(T *wl, const long *ridx, T *lq, int ldw, int lane, int OFF, in
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <typename T, int OFF, int N>
-DEV void lq_stage_store(T *wl, const long *ridx, const double *v, T *lq, int ldw, int lane)
-{
-#pragma unroll
-    for (int j = 0; j < N; ++j) wl[lane * LQ_STG + j] = (T)v[j];
-    lq_flush(wl, ridx, lq, ldw, lane, OFF, N);
-}
 
 // The terminal task of one (element, phase), one wave: Phix, Phixx (+AL, quirk A4) and the
 // reset-map Jacobian Px.  These run as the last waves of the k_lq launch (they fill its tail).
@@ -318,9 +309,9 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 {
     using T = std::conditional_t<F32, float, double>;
     // the record stage of the knot waves, or the LDS of the terminal tasks (blocks after them)
-    constexpr size_t STG = sizeof(T) * 4 * 64 * LQ_STG, TRM = 4 * sizeof(TermLds);
+    constexpr size_t STG = sizeof(T) * 4 * 64 * LQ_STG<T>, TRM = 4 * sizeof(TermLds);
     __shared__ __attribute__((aligned(16))) char lds[STG > TRM ? STG : TRM];
-    T (*stage)[64 * LQ_STG] = reinterpret_cast<T (*)[64 * LQ_STG]>(lds);
+    T (*stage)[64 * LQ_STG<T>] = reinterpret_cast<T (*)[64 * LQ_STG<T>]>(lds);
     __shared__ long sridx[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long nknot = ((long)p.B * p.S + 255) / 256;
@@ -390,28 +381,33 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     const int ldw = F32 ? LQW32 : LQW;
     double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
     // A - I and B pieces (record positions 0 .. 103) in position order (hkd_partial_emit): each
-    // value goes to this wave's LDS stage as it is computed and the stage is stored coalesced, one
-    // contiguous chunk of the records at a time; positions 15 and 67 are the record's zero slots.
-    // Chunk bounds are multiples of 8 values (64-byte lines of the 1408-byte, line-aligned records):
-    // a line written in two partial pieces at different times cost a second line write (PMC: 11 %
-    // more WRITE_SIZE than the records).
+    // value goes to this wave's LDS stage as it is computed and the stage is stored coalesced;
+    // positions 15 and 67 are the record's zero slots.
     T *wl = stage[w];
-#if HSDDP_LQ_ALIGN
-    if constexpr (!F32) {
-        // 128-byte chunks (16 values): every line of a record is written once, whole.  Positions
-        // 96 .. 103 (the last B values) wait in the stage for lx[0 .. 8); lu and the ReB Hessian
-        // share the chunk [144, 160).
-        auto put = [&](int col, double v) { wl[lane * LQ_STG + col] = (T)v; };
-        put(15, 0.0);
-        hkd_partial_emit(x, u, cd, p.dt, [&](int piece, int j, double v) {
-            const int pos = piece == 0 ? LQ_SE + j : piece == 1 ? sw_at(j / 17, j % 17) : bw_at(j / 12, j % 12);
-            const int ch = pos >> 4;
-            put(pos & 15, v);
-            if (ch < 6 && pos == 16 * ch + (ch == 0 ? 14 : 15)) {  // the chunk's last value
-                lq_flush(wl, sridx[w], lqT, ldw, lane, 16 * ch, 16);
-                if (ch == 3) put(67 - 64, 0.0);
-            }
-        });
+    // The record leaves in 128-byte lines (W values): every line of a record is written once,
+    // whole — a line written in two pieces at different times costs a second line write (PMC:
+    // 7-11 % more WRITE_SIZE than the records; 0.47 -> 0.40 ms for lq + terminal when aligned).
+    // Positions 0 .. 95 (A - I and B) in emission order, a line leaving with its last value;
+    // positions 96 .. 103 (the last B values) then wait in the stage for lx, lu, the ReB Hessian
+    // and (fp32: the record is 192 values, 6 lines) zero padding, put in position order.
+    constexpr int W = 128 / (int)sizeof(T);
+    auto col = [&](int pos) -> T & { return wl[lane * LQ_STG<T> + (pos & (W - 1))]; };
+    auto put = [&](int pos, double v) {  // positions >= 96, in order
+        col(pos) = (T)v;
+        if ((pos & (W - 1)) == W - 1) lq_flush(wl, sridx[w], lqT, ldw, lane, pos - (W - 1), W);
+    };
+    col(15) = 0;
+    hkd_partial_emit(x, u, cd, p.dt, [&](int piece, int j, double v) {
+        const int pos = piece == 0 ? LQ_SE + j : piece == 1 ? sw_at(j / 17, j % 17) : bw_at(j / 12, j % 12);
+        col(pos) = (T)v;
+        // a line's last value (position 15 of the first fp64 line is a zero slot; 96 .. 103 wait)
+        if (pos < 96 && ((pos & (W - 1)) == W - 1 || (W == 16 && pos == 14))) {
+            lq_flush(wl, sridx[w], lqT, ldw, lane, pos & ~(W - 1), W);
+            if (pos == 63) col(67) = 0;  // the line holding the second zero slot starts
+        }
+    });
+    // lx: tracking + foot regularisation (HKDCost.cpp:22-37)
+    {
         double lx[NX];
 #pragma unroll
         for (int j = 0; j < NX; ++j) lx[j] = p.dt * q_diag(p, c, j) * (x[j] - xr[j]);
@@ -423,62 +419,18 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
             lx[12 + j] += v;
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) put(8 + j, lx[j]);
-        lq_flush(wl, sridx[w], lqT, ldw, lane, 96, 16);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) put(j, lx[8 + j]);
-        lq_flush(wl, sridx[w], lqT, ldw, lane, 112, 16);
-        double lu[NU], rb[24];
-        lq_lu_reb(p, c, u, ur, dl, ep, lu, rb);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) put(j, lu[j]);
-        lq_flush(wl, sridx[w], lqT, ldw, lane, 128, 16);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) put(j, lu[16 + j]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) put(8 + j, rb[j]);
-        lq_flush(wl, sridx[w], lqT, ldw, lane, 144, 16);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) put(j, rb[8 + j]);
-        lq_flush(wl, sridx[w], lqT, ldw, lane, 160, 16);
-        return;
+        for (int j = 0; j < NX; ++j) put(LQ_LX + j, lx[j]);
     }
-#endif
-    constexpr int CH_LO[6] = {0, 16, 40, 64, 72, 88}, CH_N[6] = {16, 24, 24, 8, 16, 16};
-    wl[lane * LQ_STG + 15] = 0;
-#if HSDDP_LQ_EXP == 2
-    for (int ch = 0; ch < 6; ++ch) {
-        for (int j = 0; j < CH_N[ch]; ++j) wl[lane * LQ_STG + j] = (T)x[j];
-        lq_flush(wl, sridx[w], lqT, ldw, lane, CH_LO[ch], CH_N[ch]);
-    }
-    if (0)
-#endif
-    hkd_partial_emit(x, u, cd, p.dt, [&](int piece, int j, double v) {
-        const int pos = piece == 0 ? LQ_SE + j : piece == 1 ? sw_at(j / 17, j % 17) : bw_at(j / 12, j % 12);
-        const int ch = pos < 16 ? 0 : pos < 40 ? 1 : pos < 64 ? 2 : pos < 72 ? 3 : pos < 88 ? 4 : 5;
-        wl[lane * LQ_STG + pos - CH_LO[ch]] = (T)v;
-        if (pos == CH_LO[ch] + CH_N[ch] - (ch == 0 ? 2 : 1)) {  // the chunk's last value
-            lq_flush(wl, sridx[w], lqT, ldw, lane, CH_LO[ch], CH_N[ch]);
-            if (ch == 2) wl[lane * LQ_STG + 67 - 64] = 0;
-        }
-    });
-    // lx: tracking + foot regularisation (HKDCost.cpp:22-37)
-    double lx[NX];
-#pragma unroll
-    for (int j = 0; j < NX; ++j) lx[j] = p.dt * q_diag(p, c, j) * (x[j] - xr[j]);
-#pragma unroll
-    for (int j = 0; j < 12; ++j) {
-        double e = (x[12 + j] - x[3 + j % 3]) - (pf[j] - xr[3 + j % 3]);
-        double v = p.dt * c[j / 3] * foot_weight(p, c, j) * e;
-        lx[3 + j % 3] += -v;
-        lx[12 + j] += v;
-    }
-    lq_stage_store<T, LQ_LX, NX>(stage[w], sridx[w], lx, lqT, ldw, lane);
     // lu + ReB gradient / Hessian (SinglePhase.cpp:380-394)
     double lu[NU], rb[24];
     lq_lu_reb(p, c, u, ur, dl, ep, lu, rb);
-    lq_stage_store<T, LQ_LU, NU>(stage[w], sridx[w], lu, lqT, ldw, lane);
-    lq_stage_store<T, LQ_RB, 24>(stage[w], sridx[w], rb, lqT, ldw, lane);
+#pragma unroll
+    for (int j = 0; j < NU; ++j) put(LQ_LU + j, lu[j]);
+#pragma unroll
+    for (int j = 0; j < 24; ++j) put(LQ_RB + j, rb[j]);
+    if constexpr (F32)
+#pragma unroll
+        for (int j = LQW; j < LQW32; ++j) put(j, 0.0);
 }
 
 // ---------------------------------------------------------------------------------------------
