@@ -29,6 +29,9 @@ using namespace hkd;
 #ifndef HSDDP_RO_DEFSTAGE
 #define HSDDP_RO_DEFSTAGE 1  // 1: k_rollout stores the Defect rows through LDS (see k_rollout)
 #endif
+#ifndef HSDDP_RO_USTAGE
+#define HSDDP_RO_USTAGE 0  // 1 (with HSDDP_RO_DEFSTAGE): k_rollout stores the trial's U rows through LDS too
+#endif
 #ifndef HSDDP_RO_EXP
 #define HSDDP_RO_EXP 0  // timing experiments only: 1 no Defect row stores, 2 no trial U row stores (k_rollout)
 #endif
@@ -724,12 +727,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     trial_row(d, d.Ub[nb], kq < kqmax ? kq : kqmax, eps, u);
     // the running cost of a control slot (the terminal cost at k = N: the boundary waves)
     if (mine && k < L.N(i)) {
+#if !(HSDDP_RO_DEFSTAGE && HSDDP_RO_USTAGE)
         d2 *ug = (d2 *)(d.Ub[nb ^ 1] + kq * NU);
 #if HSDDP_RO_EXP == 2
         if (u[0] == 12345.678)
 #endif
 #pragma unroll
         for (int j = 0; j < NU / 2; ++j) ug[j] = d2{u[2 * j], u[2 * j + 1]};
+#endif
         finish_running(p, d, b, s, L.k0(i) + k, c, x, u);
     }
     // u_prev: the previous slot's control row is the previous lane's (k > 0: slot s - 1 is a
@@ -783,6 +788,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
             *(d2 *)(d.Defect + (g0 + row) * NX + cc) = d2{src[0], src[1]};
         }
     }
+#if HSDDP_RO_USTAGE
+    // the trial's control rows the same way: re-formed from Ubar + eps du (the rows this lane read
+    // at the start, now in L2) into the slot's own LDS row once the Defect rows have left, then
+    // stored as the wave's (nearly) contiguous range of control rows
+    __shared__ long urow[64];
+    wave_sync();
+    const bool wu = mine && k < L.N(i);
+    if (wu) {
+        double uu[NU];
+        trial_row(d, d.Ub[nb], kq, eps, uu);
+        double *xw = Xt + (gc - xr0) * RS;
+#pragma unroll
+        for (int j = 0; j < NU; ++j) xw[j] = uu[j];
+    }
+    urow[lane] = wu ? kq * 2 + (nb ^ 1) : -1;  // control row and its target buffer
+    wave_sync();
+#pragma unroll 4
+    for (int f = lane; f < 64 * CH; f += 64) {
+        const int row = f / CH, cc = 2 * (f % CH);
+        const long ur = urow[row];
+        if (ur >= 0) {
+            const double *src = Xt + (row + 1) * RS + cc;
+            *(d2 *)(d.Ub[ur & 1] + (ur >> 1) * NU + cc) = d2{src[0], src[1]};
+        }
+    }
+#endif
 #else
     if (!mine) return;
     // a phase's first slot: x_init = x0, or the reset map of X_{i-1}[N] (MultiPhaseDDP.cpp:73-81),
