@@ -16,14 +16,8 @@ constexpr int HC = 12;  // coupled controls per knot
 #ifndef HSDDP_STAMPS
 #define HSDDP_STAMPS 0
 #endif
-#ifndef HSDDP_LIN_AHEAD
-#define HSDDP_LIN_AHEAD 1  // knots whose images are requested ahead of the one computing (1 or 2)
-#endif
 #ifndef HSDDP_LIN_STORE
 #define HSDDP_LIN_STORE 2  // dX / du rows: 1 each knot's one knot later, 2 in aligned row pairs (LinOut)
-#endif
-#if HSDDP_LIN_AHEAD == 2 && HSDDP_LIN_STORE == 2
-#error "the two-ahead wait counts assume one knot's rows per knot"
 #endif
 #ifndef HSDDP_LIN_EXP
 #define HSDDP_LIN_EXP 0  // timing experiments only (tools/lin_exp.sh): 1 no dX / du stores, 2 no arithmetic
@@ -392,8 +386,7 @@ DEV int lin_store_pending(bool go, bool st, LinOut<real> &out)
 
 template <typename real>
 DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<real> &nxt, bool more, bool pend,
-                  LinSrc<real> &src, const LinRow<real> &R, bool st, LinOut<real> &out, real &dx, real &q1s, real &q2s,
-                  int wait = 0, bool more2 = false)
+                  LinSrc<real> &src, const LinRow<real> &R, bool st, LinOut<real> &out, real &dx, real &q1s, real &q2s)
 {
     using I = LinImg<real>;
     constexpr int NI2 = 2 * I::NI;
@@ -401,21 +394,13 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
     const bool rowl = r < NX;
     const int rr = rowl ? r : 0;
     LSTAMP(0);
-#if HSDDP_LIN_AHEAD == 2
-    (void)nxt;
-    (void)more;
-    vm_wait_n<NI2>(wait);
-#else
-    (void)wait;
-    (void)more2;
     if (more) {
         src.advance();
         lin_fetch(nxt, src);
     }
     const int ns = lin_store_pending(pend, st, out);
-    // all but what was just issued: the 2 NI DMA of the next knot, the previous knots' stores
+    // all but what was just issued: the 2 NI DMA of the next knot, the previous knot's stores
     vm_wait_n<NI2>((more ? NI2 : 0) + ns);
-#endif
     LSYNC();
     LSTAMP(1);
 #if HSDDP_LIN_EXP == 2
@@ -468,17 +453,6 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
     for (int q = 0; q < 12; ++q) cbw[q] = bwp[3 * q];
 #pragma unroll
     for (int b = 0; b < 3; ++b) crb[b] = rbp[R.rbi[b]];
-#if HSDDP_LIN_AHEAD == 2
-    // the image's last reads are in flight: once they land the buffer takes knot k + 2's image
-    pin(cbw);
-    pin(crb);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (more2) {
-        src.advance();
-        lin_fetch(cur, src);
-    }
-    lin_store_pending(pend, st, out);
-#endif
     if (rowl) sduv[r] = du;
     // dX terms with lane-dependent columns (rows 3..5: dt dX[r + 6]; lxx cross terms)
     const real x3 = sdxv[R.i3];
@@ -577,12 +551,6 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         LinSrc<real> src;
         src.init(p, d, eb, s0, k0, lane);
         lin_fetch(B0, src);  // the phase's first knot (its wait is in lin_knot)
-#if HSDDP_LIN_AHEAD == 2
-        if (N > 1) {  // and the second
-            src.advance();
-            lin_fetch(B1, src);
-        }
-#endif
         LinRow<real> R;
         load_phase(p, d, eb, hf, i, R.pc);
         if (i > 0) { // dx_init = Px dX_end
@@ -614,25 +582,10 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         out.du = d.du + (b * p.Kc + k0) * NX + rr;
         out.dx = d.dX + (b * p.S + s0 + 1) * NX + rr;
         real q1s = 0, q2s = 0;
-#if HSDDP_LIN_AHEAD == 2
-        // operations issued after knot k's image request: knot k - 3's stores and knot k + 1's image
-        // (both during knot k - 1... k - 2), knot k - 2's stores; knots 0 and 1: the two phase-start requests
-        constexpr int NI2 = 2 * LinImg<real>::NI;
-        auto wait_of = [&](int k) {
-            if (k == 0) return N > 1 ? NI2 : 0;
-            if (k == 1) return k + 1 < N ? NI2 : 0;
-            return (k >= 3 ? 2 : 0) + (k + 1 < N ? NI2 : 0) + 2;
-        };
-        for (int k = 0; k < N; k += 2) {
-            lin_knot(p, S, B0, B1, false, k > 0, src, R, st, out, dx, q1s, q2s, wait_of(k), k + 2 < N);
-            if (k + 1 < N) lin_knot(p, S, B1, B0, false, true, src, R, st, out, dx, q1s, q2s, wait_of(k + 1), k + 3 < N);
-        }
-#else
         for (int k = 0; k < N; k += 2) {
             lin_knot(p, S, B0, B1, k + 1 < N, k > 0, src, R, st, out, dx, q1s, q2s);
             if (k + 1 < N) lin_knot(p, S, B1, B0, k + 2 < N, true, src, R, st, out, dx, q1s, q2s);
         }
-#endif
         lin_store_pending(true, st, out);  // the phase's last knots
         const double *rec = d.term + (b * p.P + i) * TW;
         if (rowl) S.dx[hf][r] = dx;
