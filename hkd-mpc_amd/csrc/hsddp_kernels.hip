@@ -23,20 +23,11 @@ namespace hsddp {
 
 using namespace hkd;
 
-#ifndef HSDDP_TERM_KERNEL
-#define HSDDP_TERM_KERNEL 4  // > 0: the terminal tasks as their own launch at this many blocks per CU
-#endif
-#ifndef HSDDP_RO_DEFSTAGE
-#define HSDDP_RO_DEFSTAGE 1  // 1: k_rollout stores the Defect rows through LDS (see k_rollout)
-#endif
-#ifndef HSDDP_RO_USTAGE
-#define HSDDP_RO_USTAGE 0  // 1 (with HSDDP_RO_DEFSTAGE): k_rollout stores the trial's U rows through LDS too
-#endif
 #ifndef HSDDP_RO_EXP
 #define HSDDP_RO_EXP 0  // timing experiments only: 1 no Defect row stores, 2 no trial U row stores (k_rollout)
 #endif
 #ifndef HSDDP_LQ_EXP
-#define HSDDP_LQ_EXP 0  // timing experiments only: 1 no terminal tasks, 2 no A - I / B arithmetic
+#define HSDDP_LQ_EXP 0  // timing experiment only: 1 no terminal tasks
 #endif
 #ifndef FWD_MINB
 #define FWD_MINB 2  // 256-thread blocks per CU for the knot-parallel kernels (k_lq, k_rollout)
@@ -311,30 +302,10 @@ template <bool F32, bool EL, bool SLOTS>
 __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 {
     using T = std::conditional_t<F32, float, double>;
-    // the record stage of the knot waves, or the LDS of the terminal tasks (blocks after them)
-    constexpr size_t STG = sizeof(T) * 4 * 64 * LQ_STG<T>, TRM = 4 * sizeof(TermLds);
-    __shared__ __attribute__((aligned(16))) char lds[STG > TRM ? STG : TRM];
-    T (*stage)[64 * LQ_STG<T>] = reinterpret_cast<T (*)[64 * LQ_STG<T>]>(lds);
+    // the record stage of the knot waves
+    __shared__ __attribute__((aligned(16))) T stage[4][64 * LQ_STG<T>];
     __shared__ long sridx[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const long nknot = ((long)p.B * p.S + 255) / 256;
-    if (!HSDDP_TERM_KERNEL && (long)blockIdx.x >= nknot) {  // terminal tasks, one per wave
-        const long task = ((long)blockIdx.x - nknot) * 4 + w;
-        // the parallel-retry list of the k_riccati launch that follows starts empty (its only
-        // reader before then is the previous iteration's k_riccati_select): no memset launch
-        if (p.retry_cap > 0 && task == 0 && lane == 0) *d.retry_count = 0;
-        // and no element has been seen searching after any trial of this iteration yet
-        if (task == 0)
-            for (int t = lane; t < LS_LIVE; t += 64) d.ls_live[t] = 0;
-        // k_count's activity counts at the end of this iteration start from zero (the
-        // graph-replayed iteration of hsddp_solve has no memset launch before k_count)
-        if (task == 0 && lane < 4) d.counter[lane] = 0;
-#if HSDDP_LQ_EXP == 1
-        return;
-#endif
-        if (task < (long)p.B * p.P) terminal_task<EL>(p, d, reinterpret_cast<TermLds *>(lds)[w], (int)task, lane);
-        return;
-    }
     sridx[w][lane] = -1; // before any early return: lanes without a record stay -1
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long)p.B * p.S) return;
@@ -727,14 +698,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     trial_row(d, d.Ub[nb], kq < kqmax ? kq : kqmax, eps, u);
     // the running cost of a control slot (the terminal cost at k = N: the boundary waves)
     if (mine && k < L.N(i)) {
-#if !(HSDDP_RO_DEFSTAGE && HSDDP_RO_USTAGE)
         d2 *ug = (d2 *)(d.Ub[nb ^ 1] + kq * NU);
 #if HSDDP_RO_EXP == 2
         if (u[0] == 12345.678)
 #endif
 #pragma unroll
         for (int j = 0; j < NU / 2; ++j) ug[j] = d2{u[2 * j], u[2 * j + 1]};
-#endif
         finish_running(p, d, b, s, L.k0(i) + k, c, x, u);
     }
     // u_prev: the previous slot's control row is the previous lane's (k > 0: slot s - 1 is a
@@ -745,7 +714,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     if (lane == 0)
 #pragma unroll
         for (int j = 0; j < NU; ++j) up[j] = Up0[j];
-#if HSDDP_RO_DEFSTAGE
     // Defect rows through LDS: each slot's row replaces its own staged state row once every lane's
     // dynamics have read theirs, then the wave stores the 64 rows as one contiguous range (16-byte
     // pieces over lanes) instead of one row per lane
@@ -788,48 +756,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
             *(d2 *)(d.Defect + (g0 + row) * NX + cc) = d2{src[0], src[1]};
         }
     }
-#if HSDDP_RO_USTAGE
-    // the trial's control rows the same way: re-formed from Ubar + eps du (the rows this lane read
-    // at the start, now in L2) into the slot's own LDS row once the Defect rows have left, then
-    // stored as the wave's (nearly) contiguous range of control rows
-    __shared__ long urow[64];
-    wave_sync();
-    const bool wu = mine && k < L.N(i);
-    if (wu) {
-        double uu[NU];
-        trial_row(d, d.Ub[nb], kq, eps, uu);
-        double *xw = Xt + (gc - xr0) * RS;
-#pragma unroll
-        for (int j = 0; j < NU; ++j) xw[j] = uu[j];
-    }
-    urow[lane] = wu ? kq * 2 + (nb ^ 1) : -1;  // control row and its target buffer
-    wave_sync();
-#pragma unroll 4
-    for (int f = lane; f < 64 * CH; f += 64) {
-        const int row = f / CH, cc = 2 * (f % CH);
-        const long ur = urow[row];
-        if (ur >= 0) {
-            const double *src = Xt + (row + 1) * RS + cc;
-            *(d2 *)(d.Ub[ur & 1] + (ur >> 1) * NU + cc) = d2{src[0], src[1]};
-        }
-    }
-#endif
-#else
-    if (!mine) return;
-    // a phase's first slot: x_init = x0, or the reset map of X_{i-1}[N] (MultiPhaseDDP.cpp:73-81),
-    // whose Defect the boundary waves write
-    if (k > 0 || i == 0) {
-        double xs[NX];
-        if (k == 0) {
-#pragma unroll
-            for (int j = 0; j < NX; ++j) xs[j] = d.x0[(size_t)b * NX + j];
-        } else {
-            double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
-            hkd_step(x - RS, up, cd, p.dt, xs);
-        }
-        finish_defect(p, d, b, s, k, x, xs);
-    }
-#endif
 }
 
 // k_rollout_tail: the non-shooting states of a phase (k >= ss; HKDProblem::update leaves a new
@@ -1403,10 +1329,14 @@ void launch_normalize(const Params &p, const Bufs &d, hipStream_t st)
     hipLaunchKernelGGL(k_normalize, dim3(blocks_for((long)p.B * p.S * (NX / 2), 256)), dim3(256), 0, st, p, d);
     hipLaunchKernelGGL(k_normalize_sel, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);
 }
-#if HSDDP_TERM_KERNEL
-// the terminal tasks as a launch of their own (registers for more waves per SIMD than k_lq's)
+// The terminal tasks, one wave per (element, phase), four per block: a launch of their own (87
+// VGPRs, five waves per SIMD; as the tail of k_lq's launch they ran at its two).  The first task
+// also resets the iteration's counters: the parallel-retry list of the k_riccati launch that
+// follows starts empty (its only reader before then is the previous iteration's
+// k_riccati_select), no element has been seen searching after any trial yet (ls_live), and
+// k_count's activity counts start from zero (the graph-replayed iteration has no memset launches).
 template <bool EL>
-__global__ __launch_bounds__(256, HSDDP_TERM_KERNEL) void k_terminal(Params p, Bufs d)
+__global__ __launch_bounds__(256, 4) void k_terminal(Params p, Bufs d)
 {
     __shared__ TermLds S[4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1415,21 +1345,18 @@ __global__ __launch_bounds__(256, HSDDP_TERM_KERNEL) void k_terminal(Params p, B
     if (task == 0)
         for (int t = lane; t < LS_LIVE; t += 64) d.ls_live[t] = 0;
     if (task == 0 && lane < 4) d.counter[lane] = 0;
+#if HSDDP_LQ_EXP == 1
+    return;
+#endif
     if (task < (long)p.B * p.P) terminal_task<EL>(p, d, S[w], (int)task, lane);
 }
-#endif
 
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
 {
-#if HSDDP_TERM_KERNEL
     const dim3 gt(blocks_for((long)p.B * p.P, 4));
     if (p.elem_layout) hipLaunchKernelGGL((k_terminal<true>), gt, dim3(256), 0, st, p, d);
     else hipLaunchKernelGGL((k_terminal<false>), gt, dim3(256), 0, st, p, d);
     const dim3 g(blocks_for((long)p.B * p.S, 256));
-#else
-    // the knot blocks, then the terminal tasks (four per block)
-    const dim3 g(blocks_for((long)p.B * p.S, 256) + blocks_for((long)p.B * p.P, 4));
-#endif
     if (p.fp32) {
 #define HSDDP_LQ(f, e)                                                          \
     do {                                                                        \

@@ -16,9 +16,6 @@ constexpr int HC = 12;  // coupled controls per knot
 #ifndef HSDDP_STAMPS
 #define HSDDP_STAMPS 0
 #endif
-#ifndef HSDDP_LIN_STORE
-#define HSDDP_LIN_STORE 2  // dX / du rows: 1 each knot's one knot later, 2 in aligned row pairs (LinOut)
-#endif
 #ifndef HSDDP_LIN_EXP
 #define HSDDP_LIN_EXP 0  // timing experiments only (tools/lin_exp.sh): 1 no dX / du stores, 2 no arithmetic
 #endif
@@ -315,43 +312,12 @@ DEV void lin_row(const Params &p, LinRow<real> &R, int r)
     R.cq = (r >= 12 && r < NX) ? pick4(R.pc.bq, (rr - 12) / 3) : (real)0;
 }
 
-// a knot's dX / du rows, stored one knot later.  HSDDP_LIN_STORE 2: the rows go out in aligned
-// pairs — rows 2m and 2m + 1 of the element together, 384 bytes = three whole 128-byte lines (a row
-// alone covers one and a half) — the even row waiting in a register for its partner.
-template <typename real>
-struct RowPairs {
-    double *base;  // this lane's entry of the element's row 0
-    int row;       // the next row (the same on every lane)
-    real held;     // row `row - 1`, when that is even and not stored yet
-};
-template <typename real>
-DEV int rows_push(RowPairs<real> &w, bool st, real v)
-{
-    int ns = 0;
-    if (w.row & 1) {  // rows are pushed in order from row 0: the even partner is held
-        if (st) {
-            w.base[(size_t)(w.row - 1) * NX] = (double)w.held;
-            w.base[(size_t)w.row * NX] = (double)v;
-        }
-        ns = 2;
-    } else {
-        w.held = v;
-    }
-    w.row += 1;
-    return ns;
-}
-template <typename real>
-DEV void rows_flush(RowPairs<real> &w, bool st)
-{
-    if ((w.row & 1) && st) w.base[(size_t)(w.row - 1) * NX] = (double)w.held;
-}
-
+// a knot's dX / du rows, stored one knot later
 template <typename real>
 struct LinOut {
-    double *du, *dx;      // store mode 1: this lane's entries of the pending knot
-    real vu, vx;          // the pending knot's values
-    int n;                // pending knots (0 or 1)
-    RowPairs<real> ru, rx;  // store mode 2: the element's du and dX rows
+    double *du, *dx;  // this lane's entries of the pending knot
+    real vu, vx;      // the pending knot's values
+    int n;            // pending knots (0 or 1)
 };
 
 template <typename real>
@@ -371,9 +337,6 @@ DEV int lin_store_pending(bool go, bool st, LinOut<real> &out)
 #endif
     if (!go || out.n == 0) return 0;
     out.n = 0;
-#if HSDDP_LIN_STORE == 2
-    return rows_push(out.rx, st, out.vx) + rows_push(out.ru, st, out.vu);
-#else
     if (st) {
         *out.du = (double)out.vu;
         *out.dx = (double)out.vx;
@@ -381,7 +344,6 @@ DEV int lin_store_pending(bool go, bool st, LinOut<real> &out)
     out.du += NX;
     out.dx += NX;
     return 2;
-#endif
 }
 
 template <typename real>
@@ -544,8 +506,6 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
     const auto LY = layout_of<EL>(d, (int)eb[0]);
     const int P = LY.P();
     LinOut<real> out{};
-    out.ru = RowPairs<real>{d.du + b * p.Kc * NX + rr, 0, 0};
-    out.rx = RowPairs<real>{d.dX + b * p.S * NX + rr, 0, 0};
     for (int i = 0; i < P; ++i) {
         const int N = LY.N(i), s0 = LY.s0(i), k0 = LY.k0(i);
         LinSrc<real> src;
@@ -566,11 +526,7 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
             dx = 0;
         }
         if (rowl) dx = dx + defg[(b * p.S + s0) * NX + r];
-#if HSDDP_LIN_STORE == 2
-        rows_push(out.rx, st, dx);  // (its stores precede knot 0's wait: counted as complete there)
-#else
         if (st) d.dX[(b * p.S + s0) * NX + r] = dx;
-#endif
         // lxx row r (HKDCost.cpp:32): diagonal + foot cross terms
         lxx_row(p, R.pc, r, R.lx);
         R.ru = rowl ? (real)(p.dt * r_diag(p, r)) : (real)0;
@@ -600,10 +556,6 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         v2 += half_sum(q2s);
         LSYNC();
     }
-#if HSDDP_LIN_STORE == 2
-    rows_flush(out.rx, st);
-    rows_flush(out.ru, st);
-#endif
 #if HSDDP_STAMPS
     __syncthreads();
     if (lane < 8) d.dbg[(size_t)__builtin_amdgcn_readfirstlane((int)eb[1]) * 16 + 8 + lane] += lin_stamps().st[lane];

@@ -51,9 +51,6 @@ namespace sweep {
 #endif
 // value update on the matrix cores (1) or by DPP-broadcast multiply-adds from the lanes holding
 // K_c (0, no LDS round trip)
-#ifndef HSDDP_DU_PAIRS
-#define HSDDP_DU_PAIRS 1
-#endif
 #ifndef HSDDP_VALUE_MFMA
 #define HSDDP_VALUE_MFMA 0
 #endif
@@ -142,14 +139,6 @@ struct Item {
     real reg;
     real *K;        // [Kc][12][24]
     double *dU;     // [Kc][24]
-};
-
-// HSDDP_DU_PAIRS: dU rows go out in aligned pairs (rows 2m, 2m + 1: three whole 128-byte lines;
-// one row alone covers one and a half).  The sweep runs backward, so an odd row waits in a
-// register for its even partner; a knot that is not written (failed PSD test) flushes it alone.
-struct DuPair {
-    double v;   // the held odd row's entry of this lane
-    bool held;  // (per half)
 };
 
 // Per-lane constants of a phase (contacts of the lane's item); the B entries of the contacts
@@ -366,7 +355,7 @@ DEV void eliminate(real (&w)[HC], real (&w2)[HC], unsigned long long &bad)
 // are requested into S.img during the elimination (nrec*/ndef*).  The expected cost change of the
 // sweep (SinglePhase.cpp:357-358) is not formed: the MS linear rollout replaces it (quirk A3).
 template <typename real>
-DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &ph, const Item<real> &it, DuPair &dp, int kc,
+DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &ph, const Item<real> &it, int kc,
               real (&h)[NX], real &g, bool &live, bool first, bool more, const real *nrec0, const real *ndef0,
               const real *nrec1, const real *ndef1)
 {
@@ -626,27 +615,8 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
         if (pos < NX - 16)
 #pragma unroll
             for (int q = 0; q < HC; ++q) Kg[q * NX + 16 + pos] = kb[q];
-#if !HSDDP_DU_PAIRS
         if (L.row) it.dU[(size_t)kc * NX + pp] = I.du[pp];
-#endif
     }
-#if HSDDP_DU_PAIRS
-    if (L.row) {
-        const double v = I.du[pp];
-        double *dr = it.dU + (size_t)kc * NX + pp;
-        if (st && (kc & 1)) {
-            dp.v = v;
-            dp.held = true;
-        } else if (st) {
-            if (dp.held) dr[NX] = dp.v;
-            dr[0] = v;
-            dp.held = false;
-        } else if (dp.held) {
-            dr[NX] = dp.v;
-            dp.held = false;
-        }
-    }
-#endif
 #endif
     SSYNC();
     STAMP(9);
@@ -664,7 +634,6 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
     const int b = it.b;
     const int b0 = __builtin_amdgcn_readlane(b, 0), b1 = __builtin_amdgcn_readlane(b, 32);  // wave-uniform (SGPRs)
     bool live = it.act;
-    DuPair dp{0.0, false};
     int fail = -1;
     real h[NX], g = 0;
     // both items share one layout (the handle's, or paired by layout: Bufs::pairs)
@@ -740,7 +709,7 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
             const bool more = k > 0;
             const int kn = more ? k - 1 : 0;
             const bool was = live;
-            knot(p, S, L, ph, it, dp, k0 + k, h, g, live, k == N - 1, more, recp(b0, kn), defp(b0, kn), recp(b1, kn),
+            knot(p, S, L, ph, it, k0 + k, h, g, live, k == N - 1, more, recp(b0, kn), defp(b0, kn), recp(b1, kn),
                  defp(b1, kn));
             if (was && !live) fail = k0 + k;
             if (!__builtin_amdgcn_ballot_w64(live)) break;
@@ -762,7 +731,6 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
             V[pp] = (double)g;
         }
     }
-    // (no row is left held: the sweep ends at control slot 0, even, or at a knot it does not write)
     return it.act ? fail : -1;
 }
 
