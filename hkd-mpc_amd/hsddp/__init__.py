@@ -350,13 +350,31 @@ class Solver:
         check(lib().hsddp_shift_elements(self._h, int(cc.shape[1]), ip(cc)))
         lay = self.element_layouts()
         self.P = int(lay["n_phases"].max())
-        self.S = int(max(self.Kc + P for P in lay["n_phases"]))
+        self.S = self.Kc + self.P
         return lay
 
-    def element_layouts(self) -> dict:
+    def _layout_arrays(self):
+        """Every element's layout as arrays: n_phases [B], horizons / shooting / reach_end [B][16]
+        (zeros past an element's phases)."""
         n = np.zeros(self.B, np.int32)
         hz, ss, re = (np.zeros((self.B, 16), np.int32) for _ in range(3))
         check(lib().hsddp_get_element_layouts(self._h, ip(n), ip(hz), ip(ss), ip(re)))
+        return n, hz, ss, re
+
+    def _follow_layout(self) -> bool:
+        """The solver's P and S after a layout change (vectorised: the per-element Python lists of
+        element_layouts cost milliseconds at B = 4096); True when the elements' layouts differ."""
+        n, hz, _, _ = self._layout_arrays()
+        if np.any(n != n[0]) or np.any(hz != hz[0]):
+            self.P = int(n.max())
+            self.S = self.Kc + self.P
+            return True
+        self.P = int(n[0])
+        self.S = int((hz[0, :self.P] + 1).sum())
+        return False
+
+    def element_layouts(self) -> dict:
+        n, hz, ss, re = self._layout_arrays()
         return {"n_phases": n, "horizons": [list(hz[b, :n[b]]) for b in range(self.B)],
                 "shooting": [list(ss[b, :n[b]]) for b in range(self.B)],
                 "reach_end": [list(re[b, :n[b]]) for b in range(self.B)]}
@@ -373,11 +391,8 @@ class Solver:
         returns the new layout.  Call update_problem with inputs of that layout before solving."""
         cc = np.ascontiguousarray(np.asarray(contact_change, dtype=np.int32).reshape(-1))
         check(lib().hsddp_shift(self._h, int(cc.size), ip(cc)))
-        el = self.element_layouts()
-        if any(h != el["horizons"][0] for h in el["horizons"]):  # per-element layouts
-            self.P = int(el["n_phases"].max())
-            self.S = int(max(self.Kc + P for P in el["n_phases"]))
-            return el
+        if self._follow_layout():  # per-element layouts
+            return self.element_layouts()
         lay = self.layout()
         self.P = len(lay["horizons"])
         self.S = sum(n + 1 for n in lay["horizons"])
@@ -401,13 +416,7 @@ class Solver:
         flags = np.zeros(max(1, n_steps), np.int32)
         check(lib().hsddp_advance(self._h, int(n_steps), float(plan_duration), float(dt_mpc),
                                   None if x0 is None else dp(np.ascontiguousarray(x0, dtype=np.float64)), ip(flags)))
-        el = self.element_layouts()
-        if any(h != el["horizons"][0] for h in el["horizons"]):  # per-element layouts
-            self.P = int(el["n_phases"].max())
-            self.S = self.Kc + self.P
-        else:
-            self.P = len(el["horizons"][0])
-            self.S = sum(n + 1 for n in el["horizons"][0])
+        self._follow_layout()
         return [int(f) for f in flags[:n_steps]]
 
     def phase_info(self) -> dict:
