@@ -291,6 +291,21 @@ DEV void lq_lu_reb(const Params &p, const int *c, const double *u, const double 
     }
 }
 
+// One terminal wave (task = (element, phase)); the first also resets the iteration's counters
+// (k_terminal's comment)
+template <bool EL>
+DEV void terminal_wave(const Params &p, const Bufs &d, TermLds &S, long task, int lane)
+{
+    if (p.retry_cap > 0 && task == 0 && lane == 0) *d.retry_count = 0;
+    if (task == 0)
+        for (int t = lane; t < LS_LIVE; t += 64) d.ls_live[t] = 0;
+    if (task == 0 && lane < 4) d.counter[lane] = 0;
+#if HSDDP_LQ_EXP == 1
+    return;
+#endif
+    if (task < (long)p.B * p.P) terminal_task<EL>(p, d, S, (int)task, lane);
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_lq: per (element, state slot): cost and |Defect|^2 at the current (X, U); compact LQ model at
 // control slots (SinglePhase::compute_cost + LQ_approximation, SinglePhase.cpp:235-296).
@@ -302,10 +317,18 @@ template <bool F32, bool EL, bool SLOTS>
 __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
 {
     using T = std::conditional_t<F32, float, double>;
-    // the record stage of the knot waves
-    __shared__ __attribute__((aligned(16))) T stage[4][64 * LQ_STG<T>];
+    // the record stage of the knot waves, or the LDS of the terminal waves (blocks after them: small
+    // batches, launch_lq)
+    constexpr size_t STG = sizeof(T) * 4 * 64 * LQ_STG<T>, TRM = 4 * sizeof(TermLds);
+    __shared__ __attribute__((aligned(16))) char lds[STG > TRM ? STG : TRM];
+    T (*stage)[64 * LQ_STG<T>] = reinterpret_cast<T (*)[64 * LQ_STG<T>]>(lds);
     __shared__ long sridx[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long nknot = ((long)p.B * p.S + 255) / 256;
+    if ((long)blockIdx.x >= nknot) {
+        terminal_wave<EL>(p, d, reinterpret_cast<TermLds *>(lds)[w], ((long)blockIdx.x - nknot) * 4 + w, lane);
+        return;
+    }
     sridx[w][lane] = -1; // before any early return: lanes without a record stay -1
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long)p.B * p.S) return;
@@ -1339,24 +1362,22 @@ template <bool EL>
 __global__ __launch_bounds__(256, 4) void k_terminal(Params p, Bufs d)
 {
     __shared__ TermLds S[4];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const long task = (long)blockIdx.x * 4 + w;
-    if (p.retry_cap > 0 && task == 0 && lane == 0) *d.retry_count = 0;
-    if (task == 0)
-        for (int t = lane; t < LS_LIVE; t += 64) d.ls_live[t] = 0;
-    if (task == 0 && lane < 4) d.counter[lane] = 0;
-#if HSDDP_LQ_EXP == 1
-    return;
-#endif
-    if (task < (long)p.B * p.P) terminal_task<EL>(p, d, S[w], (int)task, lane);
+    const int w = threadIdx.x >> 6;
+    terminal_wave<EL>(p, d, S[w], (long)blockIdx.x * 4 + w, threadIdx.x & 63);
 }
 
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
 {
-    const dim3 gt(blocks_for((long)p.B * p.P, 4));
-    if (p.elem_layout) hipLaunchKernelGGL((k_terminal<true>), gt, dim3(256), 0, st, p, d);
-    else hipLaunchKernelGGL((k_terminal<false>), gt, dim3(256), 0, st, p, d);
-    const dim3 g(blocks_for((long)p.B * p.S, 256));
+    // the terminal waves: a launch of their own (five waves per SIMD), or, for a small batch whose
+    // knot and terminal blocks all fit the chip at once (C1: one robot), the blocks after k_lq's
+    // knot blocks in the same launch — one launch less on the latency path
+    const unsigned nterm = blocks_for((long)p.B * p.P, 4);
+    const bool merged = nterm <= 256;
+    if (!merged) {
+        if (p.elem_layout) hipLaunchKernelGGL((k_terminal<true>), dim3(nterm), dim3(256), 0, st, p, d);
+        else hipLaunchKernelGGL((k_terminal<false>), dim3(nterm), dim3(256), 0, st, p, d);
+    }
+    const dim3 g(blocks_for((long)p.B * p.S, 256) + (merged ? nterm : 0));
     if (p.fp32) {
 #define HSDDP_LQ(f, e)                                                          \
     do {                                                                        \
