@@ -949,7 +949,7 @@ static std::vector<double> ls_steps(double alpha)
 static void begin_launches(hsddp_handle h)
 {
     launch_reset_elements(h->p, h->d, h->stream);
-    launch_rollout(h->p, h->d, 0.0, 1, -1, h->stream);
+    launch_rollout(h->p, h->d, 0.0, 0, 1, -1, h->stream);
     launch_decide(h->p, h->d, 0.0, 0, 1, -1, h->stream);
     h->slots_fresh = true;
 }
@@ -976,7 +976,7 @@ static void iteration_launches(hsddp_handle h, const std::vector<double> &trials
     tm.end(4, e0);
     tm.begin(2, e0);
     for (size_t t = 0; t < trials.size(); ++t) {
-        launch_rollout(p, d, trials[t], 0, (int)t, st);
+        launch_rollout(p, d, trials[t], t + 1 == trials.size(), 0, (int)t, st);
         launch_decide(p, d, trials[t], t + 1 == trials.size(), 0, (int)t, st);
     }
     tm.end(2, e0);

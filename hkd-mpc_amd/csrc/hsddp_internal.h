@@ -162,7 +162,8 @@ struct Bufs {
 
 // kernel launchers (hsddp_kernels.hip)
 // tix: the trial's index in the inner iteration's line search (-1: the initial rollout)
-void launch_rollout(const Params &p, const Bufs &d, double eps, int init, int tix, hipStream_t st);
+// (last: this trial is the search's last step size — used when the rollout launch also decides)
+void launch_rollout(const Params &p, const Bufs &d, double eps, int last, int init, int tix, hipStream_t st);
 void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, int tix, hipStream_t st);
 // nominal rows of every element into buffer 0 (Bufs::sel bit 0 cleared), for host transfers
 void launch_normalize(const Params &p, const Bufs &d, hipStream_t st);

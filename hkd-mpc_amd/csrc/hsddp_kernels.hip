@@ -652,9 +652,8 @@ DEV void rollout_boundary(const Params &p, const Bufs &d, double eps, int init, 
 }
 
 template <bool EL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOUT_WAVES))) void k_rollout(Params p, Bufs d, double eps, int init, int tix)
+DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
 {
-    if (ls_skip(d, tix)) return;
     __shared__ double Xt[RW * RS];
     const int lane = threadIdx.x;
     const long total = (long)p.B * p.S;
@@ -853,11 +852,10 @@ __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double ep
 // slots in order, and the phase sums are added in phase order — the reference's summation order
 // (compute_cost, MultiPhaseDDP.cpp:431-440; SinglePhase.cpp:235-262).
 template <bool EL>
-__global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int last, int init, int tix)
+DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int init, int tix, int group)
 {
-    if (ls_skip(d, tix)) return;
     const int lane = threadIdx.x, g = lane & 15, base = lane & ~15;
-    const int b = blockIdx.x * 4 + (lane >> 4);
+    const int b = group * 4 + (lane >> 4);
     const bool valid = b < p.B;
     const ElemState *Ep = valid ? &d.el[b] : nullptr;
     const bool act = valid && (init ? !Ep->done : Ep->ls_active);
@@ -932,6 +930,36 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
             E.inner_done = 1;
         else
             push_info();
+    }
+}
+
+template <bool EL>
+__global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int last, int init, int tix)
+{
+    if (ls_skip(d, tix)) return;
+    decide_group<EL>(p, d, eps, last, init, tix, blockIdx.x);
+}
+
+// One line-search trial: the slot and boundary blocks (rollout_block), and — FUSE, small batches
+// without non-shooting tails (launch_rollout) — the trial's decision by the last block to finish:
+// every block publishes its slot outputs (device-scope release) and takes a ticket; the block
+// holding the last ticket (acquire) runs k_decide's work for the batch, four elements at a time,
+// and resets the ticket counter.  One launch less per trial on the latency path of C1.
+template <bool EL, bool FUSE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOUT_WAVES))) void k_rollout(
+    Params p, Bufs d, double eps, int init, int tix, int last)
+{
+    if (ls_skip(d, tix)) return;
+    rollout_block<EL>(p, d, eps, init);
+    if constexpr (FUSE) {
+        __shared__ int ticket;
+        __threadfence();
+        if (threadIdx.x == 0) ticket = atomicAdd(&d.counter[7], 1);
+        __syncthreads();
+        if (ticket != (int)gridDim.x - 1) return;
+        __threadfence();
+        for (int q = 0; q < (p.B + 3) / 4; ++q) decide_group<EL>(p, d, eps, last, init, tix, q);
+        if (threadIdx.x == 0) d.counter[7] = 0;
     }
 }
 
@@ -1336,15 +1364,25 @@ static inline unsigned blocks_for(long n, int bs) { return (unsigned)((n + bs - 
         else hipLaunchKernelGGL(kern<false>, grid, block, 0, st, __VA_ARGS__);                      \
     } while (0)
 
-void launch_rollout(const Params &p, const Bufs &d, double eps, int init, int tix, hipStream_t st)
+// small batches without non-shooting tails decide each trial in its rollout launch (k_rollout FUSE)
+static bool fused_decide(const Params &p) { return p.B <= 16 && !p.has_tail; }
+
+void launch_rollout(const Params &p, const Bufs &d, double eps, int last, int init, int tix, hipStream_t st)
 {
     // slot waves, then the phase-boundary waves (k_rollout, rollout_boundary)
-    LAUNCH_EL(k_rollout, dim3(blocks_for((long)p.B * p.S, 64) + blocks_for((long)p.B * p.P, 64)), dim3(64), st, p, d,
-              eps, init, tix);
+    const dim3 g(blocks_for((long)p.B * p.S, 64) + blocks_for((long)p.B * p.P, 64));
+    if (fused_decide(p)) {
+        if (p.elem_layout) hipLaunchKernelGGL((k_rollout<true, true>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+        else hipLaunchKernelGGL((k_rollout<false, true>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+        return;
+    }
+    if (p.elem_layout) hipLaunchKernelGGL((k_rollout<true, false>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+    else hipLaunchKernelGGL((k_rollout<false, false>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
     if (p.has_tail) LAUNCH_EL(k_rollout_tail, dim3((p.B + 63) / 64), dim3(64), st, p, d, eps, init, tix);
 }
 void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, int tix, hipStream_t st)
 {
+    if (fused_decide(p)) return;  // decided by the rollout launch
     LAUNCH_EL(k_decide, dim3((p.B + 3) / 4), dim3(64), st, p, d, eps, last, init, tix);
 }
 void launch_normalize(const Params &p, const Bufs &d, hipStream_t st)
