@@ -71,13 +71,20 @@ DEV void lq_flush(T *wl, const long *ridx, T *lq, int ldw, int lane, int OFF, in
 }
 
 
-// The terminal task of one (element, phase), one wave: Phix, Phixx (+AL, quirk A4) and the
-// reset-map Jacobian Px.  These run as the last waves of the k_lq launch (they fill its tail).
+// The terminal task of one (element, phase): Phix, Phixx (+AL, quirk A4) and the reset-map
+// Jacobian Px, on TERM_TL lanes — TERM_TPW tasks share a wave (the per-task work is mostly serial:
+// the leg kinematics on four lanes, the cost on one), so the LDS per task, not the wave count,
+// bounds how many run at once.
+#ifndef HSDDP_TERM_TPW
+#define HSDDP_TERM_TPW 2
+#endif
+constexpr int TERM_TPW = HSDDP_TERM_TPW, TERM_TL = 64 / TERM_TPW;
 struct TermLds {
     double sx[NX], shx[4][NX], scoef[4][2], sh[4], sxr[NX], spf[12], ssl[2 * MTD * 4], sdd[NX], scw[12];
-    double spx[NX * (NX + 1)];
+    double spx[12 * (NX + 1)];  // Px rows 12 .. 23 (rows 0 .. 11 are the identity's)
     int sc[4], scn[4], smask[MTD];
 };
+static_assert(TERM_TL >= NX && TERM_TL >= 2 * MTD * 4 && TERM_TL >= 16, "terminal lane roles");
 
 // LDS hand-over between the lanes of one wave (its LDS accesses complete in order)
 DEV void wave_sync()
@@ -100,12 +107,15 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
     int *sc = S.sc, *scn = S.scn, *smask = S.smask;
     const int s = L.s0(i) + L.N(i);
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
-    if (t < NX) sx[t] = d.Xb[work_buf(d, b)][((size_t)b * p.S + s) * NX + t];
-    // the terminal cost's other inputs, staged with X[N] (no memory round trip at the end)
-    if (t >= 32 && t < 32 + NX) sxr[t - 32] = xr[t - 32];
+    // X[N] and the terminal cost's other inputs, staged together (no memory round trip at the end)
+    if (t < NX) {
+        sx[t] = d.Xb[work_buf(d, b)][((size_t)b * p.S + s) * NX + t];
+        sxr[t] = xr[t];
+    }
     // the phase's touchdown constraints: AL parameters [slot][leg] (sigma, then lambda) and leg masks
     if (t < 2 * MTD * 4) ssl[t] = (t < MTD * 4 ? d.al_sigma : d.al_lambda)[((size_t)b * p.P + i) * MTD * 4 + (t & (MTD * 4 - 1))];
-    if (t >= 60 && t < 60 + MTD) smask[t - 60] = d.td_mask[((size_t)b * p.P + i) * MTD + t - 60];
+    constexpr int MK = TERM_TL - MTD;
+    if (t >= MK) smask[t - MK] = d.td_mask[((size_t)b * p.P + i) * MTD + t - MK];
     if (t >= 4 && t < 16) spf[t - 4] = pf[t - 4];
     if (t < 4) {
         const int *cc = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
@@ -115,9 +125,9 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
     // Px at X_i[N] (HKDReset.h:78-136) is built in LDS from the identity (phase boundaries only)
     double *spx = S.spx;
     const bool bnd = i < P - 1;
-    for (int e = t; e < 4 * NX; e += 64) (&shx[0][0])[e] = 0.0;
+    for (int e = t; e < 4 * NX; e += TERM_TL) (&shx[0][0])[e] = 0.0;
     if (bnd)
-        for (int e = t; e < NX * (NX + 1); e += 64) spx[e] = (e / (NX + 1) == e % (NX + 1)) ? 1.0 : 0.0;
+        for (int e = t; e < 12 * (NX + 1); e += TERM_TL) spx[e] = (e / (NX + 1) + 12 == e % (NX + 1)) ? 1.0 : 0.0;
     wave_sync();
     if (t < 4) {
         // legs of the touchdown constraints: foot height h and its gradient (non-zeros at 0..2, 5,
@@ -149,7 +159,7 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
             if (bnd && tdr) {  // rows 12 + 3 l + k, k < 2: the foot Jacobian's rows; the k = 2 row is zero
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
-                    double *row = spx + (12 + 3 * l + k) * (NX + 1);
+                    double *row = spx + (3 * l + k) * (NX + 1);
                     row[12 + 3 * l + k] = 0.0;
                     if (k == 2) continue;
                     row[0] = Dy.r[k][0] * pb[0] + Dy.r[k][1] * pb[1] + Dy.r[k][2] * pb[2];
@@ -163,7 +173,7 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
             }
         } else if (bnd && sc[l] && !scn[l]) {  // lift-off: rows 12 + 3 l + k zero
 #pragma unroll
-            for (int k = 0; k < 3; ++k) spx[(12 + 3 * l + k) * (NX + 2)] = 0.0;
+            for (int k = 0; k < 3; ++k) spx[(3 * l + k) * (NX + 2) + 12] = 0.0;
         }
         // AL gradient / Hessian coefficients of the leg, summed over the constraints holding it
         // (quirk A4: (sigma (1 + h) + lambda) hx hx^T, ConstraintsBase.h:374-399)
@@ -205,8 +215,9 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
     }
     // foot Hessian 20 D^T Qfoot D: weight of (leg l, axis j), entries (3 + j, 3 + j) (summed over
     // the legs in leg order), (12 + 3 l + j, 12 + 3 l + j) and, negated, the two cross entries.
-    // Lane r < 24 forms diagonal entry r, lane 24 + m the weight of joint column 12 + m (runtime-
-    // indexed weights read once per phase, not once per entry); the 576 entries then combine them.
+    // Lane r < 24 forms diagonal entry r, lane m < 12 also the weight of joint column 12 + m
+    // (runtime-indexed weights read once per phase, not once per entry); the 576 entries then
+    // combine them.
     auto fw = [&](int l, int j) { return p.foot_term_grad * sc[l] * sc[l] * foot_weight(kp, sc, 3 * l + j); };
     double *sdd = S.sdd, *scw = S.scw;
     if (t < NX) {
@@ -218,18 +229,16 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
             v += fw((r - 12) / 3, (r - 12) % 3);
         }
         sdd[r] = v;
-    } else if (t < NX + 12) {
-        const int m = t - NX;
-        scw[m] = fw(m / 3, m % 3);
     }
+    if (t < 12) scw[t] = fw(t / 3, t % 3);
     wave_sync();
     // the AL terms of the touchdown legs only (a leg's coefficient is the same on every lane; the
     // others add exact zeros)
     bool use[4];
 #pragma unroll
     for (int l = 0; l < 4; ++l) use[l] = scoef[l][1] != 0.0;
-    int r = t / NX, cidx = t % NX;  // entry e = t + 64 j: (r, cidx) advance by (2, 16) per step
-    for (int e = t; e < NN; e += 64) { // Phixx
+    int r = t / NX, cidx = t % NX;  // entry e = t + TERM_TL j: (r, cidx) advance per step
+    for (int e = t; e < NN; e += TERM_TL) { // Phixx
         double v = 0.0;
         if (r == cidx)
             v = sdd[r];
@@ -241,9 +250,9 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
         for (int l = 0; l < 4; ++l)
             if (use[l]) v += scoef[l][1] * (shx[l][r] * shx[l][cidx]);
         rec[TM_PHIXX + e] = v;
-        if (bnd) rec[TM_PX + e] = spx[r * (NX + 1) + cidx];  // Px rows from LDS, stored coalesced
-        r += 2;
-        cidx += 16;
+        if (bnd) rec[TM_PX + e] = r < 12 ? (r == cidx ? 1.0 : 0.0) : spx[(r - 12) * (NX + 1) + cidx];  // coalesced
+        r += TERM_TL / NX;
+        cidx += TERM_TL % NX;
         if (cidx >= NX) {
             cidx -= NX;
             r += 1;
@@ -291,19 +300,21 @@ DEV void lq_lu_reb(const Params &p, const int *c, const double *u, const double 
     }
 }
 
-// One terminal wave (task = (element, phase)); the first also resets the iteration's counters
-// (k_terminal's comment)
+// One terminal wave: tasks (element, phase) TERM_TPW wave .. + TERM_TPW - 1 on S[0 ..]; the first
+// wave also resets the iteration's counters (k_terminal's comment)
 template <bool EL>
-DEV void terminal_wave(const Params &p, const Bufs &d, TermLds &S, long task, int lane)
+DEV void terminal_wave(const Params &p, const Bufs &d, TermLds *S, long wave, int lane)
 {
-    if (p.retry_cap > 0 && task == 0 && lane == 0) *d.retry_count = 0;
-    if (task == 0)
+    if (p.retry_cap > 0 && wave == 0 && lane == 0) *d.retry_count = 0;
+    if (wave == 0)
         for (int t = lane; t < LS_LIVE; t += 64) d.ls_live[t] = 0;
-    if (task == 0 && lane < 4) d.counter[lane] = 0;
+    if (wave == 0 && lane < 4) d.counter[lane] = 0;
 #if HSDDP_LQ_EXP == 1
     return;
 #endif
-    if (task < (long)p.B * p.P) terminal_task<EL>(p, d, S, (int)task, lane);
+    const int h = lane / TERM_TL;
+    const long task = wave * TERM_TPW + h;
+    if (task < (long)p.B * p.P) terminal_task<EL>(p, d, S[h], (int)task, lane % TERM_TL);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -319,14 +330,14 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     using T = std::conditional_t<F32, float, double>;
     // the record stage of the knot waves, or the LDS of the terminal waves (blocks after them: small
     // batches, launch_lq)
-    constexpr size_t STG = sizeof(T) * 4 * 64 * LQ_STG<T>, TRM = 4 * sizeof(TermLds);
+    constexpr size_t STG = sizeof(T) * 4 * 64 * LQ_STG<T>, TRM = 4 * TERM_TPW * sizeof(TermLds);
     __shared__ __attribute__((aligned(16))) char lds[STG > TRM ? STG : TRM];
     T (*stage)[64 * LQ_STG<T>] = reinterpret_cast<T (*)[64 * LQ_STG<T>]>(lds);
     __shared__ long sridx[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long nknot = ((long)p.B * p.S + 255) / 256;
     if ((long)blockIdx.x >= nknot) {
-        terminal_wave<EL>(p, d, reinterpret_cast<TermLds *>(lds)[w], ((long)blockIdx.x - nknot) * 4 + w, lane);
+        terminal_wave<EL>(p, d, reinterpret_cast<TermLds *>(lds) + w * TERM_TPW, ((long)blockIdx.x - nknot) * 4 + w, lane);
         return;
     }
     sridx[w][lane] = -1; // before any early return: lanes without a record stay -1
@@ -1390,18 +1401,18 @@ void launch_normalize(const Params &p, const Bufs &d, hipStream_t st)
     hipLaunchKernelGGL(k_normalize, dim3(blocks_for((long)p.B * p.S * (NX / 2), 256)), dim3(256), 0, st, p, d);
     hipLaunchKernelGGL(k_normalize_sel, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);
 }
-// The terminal tasks, one wave per (element, phase), four per block: a launch of their own (87
-// VGPRs, five waves per SIMD; as the tail of k_lq's launch they ran at its two).  The first task
+// The terminal tasks, TERM_TPW per wave, two waves per block: a launch of their own (87 VGPRs,
+// five waves per SIMD; as the tail of k_lq's launch they ran at its two).  The first wave
 // also resets the iteration's counters: the parallel-retry list of the k_riccati launch that
 // follows starts empty (its only reader before then is the previous iteration's
 // k_riccati_select), no element has been seen searching after any trial yet (ls_live), and
 // k_count's activity counts start from zero (the graph-replayed iteration has no memset launches).
 template <bool EL>
-__global__ __launch_bounds__(256, 4) void k_terminal(Params p, Bufs d)
+__global__ __launch_bounds__(128, 4) void k_terminal(Params p, Bufs d)
 {
-    __shared__ TermLds S[4];
+    __shared__ TermLds S[2 * TERM_TPW];
     const int w = threadIdx.x >> 6;
-    terminal_wave<EL>(p, d, S[w], (long)blockIdx.x * 4 + w, threadIdx.x & 63);
+    terminal_wave<EL>(p, d, S + w * TERM_TPW, (long)blockIdx.x * 2 + w, threadIdx.x & 63);
 }
 
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
@@ -1409,11 +1420,12 @@ void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
     // the terminal waves: a launch of their own (five waves per SIMD), or, for a small batch whose
     // knot and terminal blocks all fit the chip at once (C1: one robot), the blocks after k_lq's
     // knot blocks in the same launch — one launch less on the latency path
-    const unsigned nterm = blocks_for((long)p.B * p.P, 4);
+    const unsigned nterm = blocks_for((long)p.B * p.P, 4 * TERM_TPW);
     const bool merged = nterm <= 256;
     if (!merged) {
-        if (p.elem_layout) hipLaunchKernelGGL((k_terminal<true>), dim3(nterm), dim3(256), 0, st, p, d);
-        else hipLaunchKernelGGL((k_terminal<false>), dim3(nterm), dim3(256), 0, st, p, d);
+        const unsigned nt2 = blocks_for((long)p.B * p.P, 2 * TERM_TPW);
+        if (p.elem_layout) hipLaunchKernelGGL((k_terminal<true>), dim3(nt2), dim3(128), 0, st, p, d);
+        else hipLaunchKernelGGL((k_terminal<false>), dim3(nt2), dim3(128), 0, st, p, d);
     }
     const dim3 g(blocks_for((long)p.B * p.S, 256) + (merged ? nterm : 0));
     if (p.fp32) {
