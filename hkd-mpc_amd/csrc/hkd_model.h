@@ -356,13 +356,11 @@ HKD_FN void hkd_expand_colmajor(const double *Se, const double *Sw, const double
 }
 
 // ---- kinematics ------------------------------------------------------------------------
-HKD_FN void foot_body(int l, const double *q, double *pb, double (*dpb)[3])
+// from the sines / cosines of q0, q1 and q1 + q2 (tr: s0, c0, s1, c1, s12, c12)
+HKD_FN void foot_body_trig(int l, const double *tr, double *pb, double (*dpb)[3])
 {
     double s = leg_side(l), f = leg_front(l);
-    double c0, s0, c1, s1, c12, s12;
-    sincos(q[0], &s0, &c0);
-    sincos(q[1], &s1, &c1);
-    sincos(q[1] + q[2], &s12, &c12);
+    const double s0 = tr[0], c0 = tr[1], s1 = tr[2], c1 = tr[3], s12 = tr[4], c12 = tr[5];
     pb[0] = kHipX * f - kLower * s12 - kUpper * s1;
     pb[1] = kSideY * s + kAbad * s * c0 - kLower * s0 * c12 - kUpper * s0 * c1;
     pb[2] = kLower * c0 * c12 + kUpper * c0 * c1 + kAbad * s * s0;
@@ -373,6 +371,15 @@ HKD_FN void foot_body(int l, const double *q, double *pb, double (*dpb)[3])
         dpb[2][0] = -kLower * s0 * c12 - kUpper * s0 * c1 + kAbad * s * c0;
         dpb[2][1] = -kLower * c0 * s12 - kUpper * c0 * s1; dpb[2][2] = -kLower * c0 * s12;
     }
+}
+
+HKD_FN void foot_body(int l, const double *q, double *pb, double (*dpb)[3])
+{
+    double tr[6];
+    sincos(q[0], &tr[0], &tr[1]);
+    sincos(q[1], &tr[2], &tr[3]);
+    sincos(q[1] + q[2], &tr[4], &tr[5]);
+    foot_body_trig(l, tr, pb, dpb);
 }
 
 // foot position in world of leg l, joint angles taken from q (3)

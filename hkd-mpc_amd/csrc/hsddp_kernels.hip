@@ -80,7 +80,8 @@ DEV void lq_flush(T *wl, const long *ridx, T *lq, int ldw, int lane, int OFF, in
 #endif
 constexpr int TERM_TPW = HSDDP_TERM_TPW, TERM_TL = 64 / TERM_TPW;
 struct TermLds {
-    double sx[NX], shx[4][NX], scoef[4][2], sh[4], sxr[NX], spf[12], ssl[2 * MTD * 4], sdd[NX], scw[12];
+    double sx[NX], shx[4][NX], scoef[4][2], sh[4], sxr[NX], spf[12], ssl[2 * MTD * 4];
+    double sdw[NX + 12];  // the foot Hessian's diagonal, then its cross weights; first the 15 angles' sin / cos
     double spx[12 * (NX + 1)];  // Px rows 12 .. 23 (rows 0 .. 11 are the identity's)
     int sc[4], scn[4], smask[MTD];
 };
@@ -128,8 +129,21 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
     for (int e = t; e < 4 * NX; e += TERM_TL) (&shx[0][0])[e] = 0.0;
     if (bnd)
         for (int e = t; e < 12 * (NX + 1); e += TERM_TL) spx[e] = (e / (NX + 1) + 12 == e % (NX + 1)) ? 1.0 : 0.0;
+    // the kinematics' 15 angles, one sincos per lane: yaw, pitch, roll, then per leg q0, q1, q1 + q2
+    double *strig = S.sdw;
+    unsigned need = td_union(smask);
+#pragma unroll
+    for (int l = 0; l < 4; ++l) need |= (bnd && touchdown(sc, scn, l)) ? 1u << l : 0u;
+    if (need && t < 15) {
+        const int m = t - 3;
+        const double a = t < 3 ? sx[t] : m % 3 == 2 ? sx[11 + m] + sx[12 + m] : sx[12 + m];
+        sincos(a, &strig[2 * t], &strig[2 * t + 1]);
+    }
     wave_sync();
-    if (t < 4) {
+#ifndef HSDDP_TERM_EXP
+#define HSDDP_TERM_EXP 0
+#endif
+    if ((HSDDP_TERM_EXP & 2) == 0 && t < 4) {
         // legs of the touchdown constraints: foot height h and its gradient (non-zeros at 0..2, 5,
         // 12 + 3 l + k); legs touching down at a phase boundary: the reset map's foot-Jacobian rows
         // — from one evaluation of the leg's kinematics (hkd_foot_height_grad_sparse's and
@@ -139,11 +153,11 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
         double h = 0.0;
         if (tdc || (bnd && tdr)) {
             Rot R, Dy, Dp, Dr;
-            const EulTrig tr = eul_trig(sx);
+            const EulTrig tr{strig[1], strig[0], strig[3], strig[2], strig[5], strig[4]};
             rot_zyx(tr, R);
             rot_zyx_grad(tr, Dy, Dp, Dr);
             double pb[3], dpb[3][3];
-            foot_body(l, sx + 12 + 3 * l, pb, dpb);
+            foot_body_trig(l, strig + 6 + 6 * l, pb, dpb);
             shx[l][0] = Dy.r[2][0] * pb[0] + Dy.r[2][1] * pb[1] + Dy.r[2][2] * pb[2];
             shx[l][1] = Dp.r[2][0] * pb[0] + Dp.r[2][1] * pb[1] + Dp.r[2][2] * pb[2];
             shx[l][2] = Dr.r[2][0] * pb[0] + Dr.r[2][1] * pb[1] + Dr.r[2][2] * pb[2];
@@ -192,22 +206,22 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
     wave_sync();
     KParams &kp = *kparams();  // runtime-indexed weights
     double *rec = d.term + ((size_t)b * p.P + i) * TW;
-    if (t == 0) {  // the phase's terminal cost at X[N] (SinglePhase::compute_cost's last term) for k_lq's slot sums
+    if ((HSDDP_TERM_EXP & 1) == 0 && t == 0) {  // the phase's terminal cost at X[N] (SinglePhase::compute_cost's last term) for k_lq's slot sums
         double tv;
         d.slot_cost[(size_t)b * p.S + s] = terminal_cost_h(p, sc, sx, sxr, spf, smask, ssl, ssl + MTD * 4, sh, tv);
     }
-    if (t < NX) { // Phix
+    if ((HSDDP_TERM_EXP & 8) == 0 && t < NX) { // Phix
         const int j = t;
-        double v = kp.qf_gain * kp.qf_scale[j] * q_diag(kp, sc, j) * (sx[j] - xr[j]);
+        double v = kp.qf_gain * kp.qf_scale[j] * q_diag(kp, sc, j) * (sx[j] - sxr[j]);
         if (j >= 3 && j < 6) {
             for (int l = 0; l < 4; ++l) {
                 int m = 3 * l + (j - 3);
-                double e = (sx[12 + m] - sx[j]) - (pf[m] - xr[j]);
+                double e = (sx[12 + m] - sx[j]) - (spf[m] - sxr[j]);
                 v += -(p.foot_term_grad * sc[l] * foot_weight(kp, sc, m) * e);
             }
         } else if (j >= 12) {
             int m = j - 12, l = m / 3;
-            double e = (sx[j] - sx[3 + m % 3]) - (pf[m] - xr[3 + m % 3]);
+            double e = (sx[j] - sx[3 + m % 3]) - (spf[m] - sxr[3 + m % 3]);
             v += p.foot_term_grad * sc[l] * foot_weight(kp, sc, m) * e;
         }
         for (int l = 0; l < 4; ++l) v += scoef[l][0] * shx[l][j];
@@ -219,7 +233,7 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
     // (runtime-indexed weights read once per phase, not once per entry); the 576 entries then
     // combine them.
     auto fw = [&](int l, int j) { return p.foot_term_grad * sc[l] * sc[l] * foot_weight(kp, sc, 3 * l + j); };
-    double *sdd = S.sdd, *scw = S.scw;
+    double *sdd = S.sdw, *scw = S.sdw + NX;  // (the trig is dead: read before the last wave_sync)
     if (t < NX) {
         const int r = t;
         double v = kp.qf_gain * kp.qf_scale[r] * q_diag(kp, sc, r);
@@ -238,7 +252,7 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
 #pragma unroll
     for (int l = 0; l < 4; ++l) use[l] = scoef[l][1] != 0.0;
     int r = t / NX, cidx = t % NX;  // entry e = t + TERM_TL j: (r, cidx) advance per step
-    for (int e = t; e < NN; e += TERM_TL) { // Phixx
+    for (int e = t; e < ((HSDDP_TERM_EXP & 4) ? 0 : NN); e += TERM_TL) { // Phixx
         double v = 0.0;
         if (r == cidx)
             v = sdd[r];
@@ -250,7 +264,9 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
         for (int l = 0; l < 4; ++l)
             if (use[l]) v += scoef[l][1] * (shx[l][r] * shx[l][cidx]);
         rec[TM_PHIXX + e] = v;
-        if (bnd) rec[TM_PX + e] = r < 12 ? (r == cidx ? 1.0 : 0.0) : spx[(r - 12) * (NX + 1) + cidx];  // coalesced
+        // Px rows 12 .. 23 from LDS, stored coalesced (rows 0 .. 11 are the identity's, written once
+        // for every record at create: launch_init_params)
+        if (bnd && r >= 12) rec[TM_PX + e] = spx[(r - 12) * (NX + 1) + cidx];
         r += TERM_TL / NX;
         cidx += TERM_TL % NX;
         if (cidx >= NX) {
@@ -1101,6 +1117,18 @@ __global__ __launch_bounds__(256) void k_init_params(Params p, Bufs d)
     if (gid < (long)p.B * p.P * MTD) d.td_mask[gid] = gid % MTD == 0 ? TD_PENDING : 0;
 }
 
+// Px rows 0 .. 11 of every terminal record slot (the allocation's B x MAXP, whatever the
+// layout): the reset map leaves the orientation, position and velocity rows as the identity's
+// (HKDReset.h:78-136), so k_terminal writes only rows 12 .. 23
+__global__ __launch_bounds__(256) void k_term_identity(Params p, Bufs d)
+{
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)p.B * MAXP * 12 * NX) return;
+    const long rec = gid / (12 * NX);
+    const int e = (int)(gid % (12 * NX));
+    d.term[rec * TW + TM_PX + e] = (e / NX == e % NX) ? 1.0 : 0.0;
+}
+
 // TD_PENDING slots take the touchdown legs of their phase's contact rows (0: no constraint)
 template <bool EL>
 __global__ __launch_bounds__(256) void k_resolve_td(Params p, Bufs d)
@@ -1475,6 +1503,7 @@ void launch_init_params(const Params &p, const Bufs &d, hipStream_t st)
     long n = (long)p.B * p.Kc * 20;
     if ((long)p.B * p.P * MTD * 4 > n) n = (long)p.B * p.P * MTD * 4;
     hipLaunchKernelGGL(k_init_params, dim3(blocks_for(n, 256)), dim3(256), 0, st, p, d);
+    hipLaunchKernelGGL(k_term_identity, dim3(blocks_for((long)p.B * MAXP * 12 * NX, 256)), dim3(256), 0, st, p, d);
 }
 void launch_resolve_td(const Params &p, const Bufs &d, hipStream_t st)
 {

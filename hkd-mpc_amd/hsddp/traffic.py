@@ -19,7 +19,8 @@ NX = 24
 LQW, LQW32 = 176, 176   # compact LQ record (fp64 / fp32 stride), hsddp_internal.h
 KCW = 12 * 24           # compact gain rows
 TW_PHI = 24 + 576       # Phix + Phixx per phase end
-TW_PX = 576             # reset-map Jacobian per phase boundary
+TW_PX = 576             # reset-map Jacobian per phase boundary (read)
+TW_PX_W = 288           # its rows 12 .. 23 (written: rows 0 .. 11 are the identity's, set once at create)
 
 
 def kernel_bytes(B: int, S: int, Kc: int, P: int, fp32: bool = False, ref_per_element: bool = False,
@@ -38,8 +39,9 @@ def kernel_bytes(B: int, S: int, Kc: int, P: int, fp32: bool = False, ref_per_el
     # control knot U read and the record written
     reb = 2 * reb_rows * d  # delta and eps of the knot's stance-leg GRF rows
     out["k_lq"] = B * (S * (NX * d + (NX * d + NX * 4 if fp32 else 0)) + Kc * (NX * d + rec + reb) + ref)
-    # k_terminal: per phase end X read (+ AL sigma, lambda), Phix, Phixx, Px and the terminal cost written
-    out["k_terminal"] = B * (P * (NX + 8 + 1) * d + term)
+    # k_terminal: per phase end X read (+ AL sigma, lambda), Phix, Phixx, Px rows 12 .. 23 and the
+    # terminal cost written
+    out["k_terminal"] = B * (P * (NX + 8 + 1) * d + (P * TW_PHI + (P - 1) * TW_PX_W) * d)
     # k_riccati: per control knot the record and Defect[k+1] read, gain rows and dU written; per
     # element the terminal records and the slot cost / feasibility partial sums read
     out["k_riccati"] = B * (Kc * (rec + NX * f + KCW * f + NX * d) + term + 2 * S * d)
