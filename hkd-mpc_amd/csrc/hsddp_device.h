@@ -70,6 +70,17 @@ DEV void slot_phase(const L_ &L, int s, int &i, int &k)
     k = s - L.s0(i);
 }
 
+// phase i and knot k of control knot kc (kc = k0(i) + k)
+template <typename L_>
+DEV void knot_phase(const L_ &L, int kc, int &i, int &k)
+{
+    i = 0;
+    const int P = L.P();
+    for (int j = 1; j < P; ++j)
+        if (kc >= L.k0(j)) i = j;
+    k = kc - L.k0(i);
+}
+
 // element b's nominal (Xbar / Ubar), working (X / U) and trial-target buffers (Bufs::sel)
 DEV int nom_buf(const Bufs &d, int b) { return d.sel[b] & 1; }
 DEV int work_buf(const Bufs &d, int b) { return (d.sel[b] >> 1) & 1; }

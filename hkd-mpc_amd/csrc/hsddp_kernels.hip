@@ -351,21 +351,33 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     T (*stage)[64 * LQ_STG<T>] = reinterpret_cast<T (*)[64 * LQ_STG<T>]>(lds);
     __shared__ long sridx[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const long nknot = ((long)p.B * p.S + 255) / 256;
+    // one thread per control knot (the records' own order); the modes that also have work at the
+    // phase-end slots — |Defect|^2 (SLOTS), the fp32 Defect copy (F32) — one per state slot
+    constexpr bool BY_KNOT = !SLOTS && !F32;
+    const long nunit = (long)p.B * (BY_KNOT ? p.Kc : p.S);
+    const long nknot = (nunit + 255) / 256;
     if ((long)blockIdx.x >= nknot) {
         terminal_wave<EL>(p, d, reinterpret_cast<TermLds *>(lds) + w * TERM_TPW, ((long)blockIdx.x - nknot) * 4 + w, lane);
         return;
     }
     sridx[w][lane] = -1; // before any early return: lanes without a record stay -1
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (long)p.B * p.S) return;
-    const int b = (int)(gid / p.S), s = (int)(gid % p.S);
+    if (gid >= nunit) return;
+    const int b = (int)(gid / (BY_KNOT ? p.Kc : p.S));
     const ElemState &E = d.el[b];
     if (E.done || E.inner_done) return;
     const auto L = layout_of<EL>(d, b);
-    if (s >= L.S()) return;
-    int i, k;
-    slot_phase(L, s, i, k);
+    int i, k, s;
+    if constexpr (BY_KNOT) {
+        const int kc0 = (int)(gid % p.Kc);
+        knot_phase(L, kc0, i, k);
+        if (k >= L.N(i)) return;  // (every layout has Kc knots: none past the last phase)
+        s = L.s0(i) + k;
+    } else {
+        s = (int)(gid % p.S);
+        if (s >= L.S()) return;
+        slot_phase(L, s, i, k);
+    }
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     double x[NX];
@@ -1450,12 +1462,13 @@ void launch_lq(const Params &p, const Bufs &d, hipStream_t st)
     // knot blocks in the same launch — one launch less on the latency path
     const unsigned nterm = blocks_for((long)p.B * p.P, 4 * TERM_TPW);
     const bool merged = nterm <= 256;
+    const bool by_knot = !p.lq_slots && !p.fp32;  // k_lq's grid: control knots or state slots
     if (!merged) {
         const unsigned nt2 = blocks_for((long)p.B * p.P, 2 * TERM_TPW);
         if (p.elem_layout) hipLaunchKernelGGL((k_terminal<true>), dim3(nt2), dim3(128), 0, st, p, d);
         else hipLaunchKernelGGL((k_terminal<false>), dim3(nt2), dim3(128), 0, st, p, d);
     }
-    const dim3 g(blocks_for((long)p.B * p.S, 256) + (merged ? nterm : 0));
+    const dim3 g(blocks_for((long)p.B * (by_knot ? p.Kc : p.S), 256) + (merged ? nterm : 0));
     if (p.fp32) {
 #define HSDDP_LQ(f, e)                                                          \
     do {                                                                        \
