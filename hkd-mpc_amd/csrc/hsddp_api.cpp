@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cctype>
 #include <cmath>
 #include <cstdio>
@@ -2203,6 +2204,17 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     const int B = p.B, Br = h->Bref, sz = h->win_len - 1;
     const bool elem = !h->lays.empty();
     const float dt = h->ref_dt, dts = h->dt_sim;
+    // HSDDP_ADVANCE_TIMING=1: wall time of the advance's stages to stderr (a diagnostic)
+    static const bool timing = std::getenv("HSDDP_ADVANCE_TIMING") != nullptr;
+    using clk = std::chrono::steady_clock;
+    clk::time_point tmark = clk::now();
+    double tstage[6] = {0, 0, 0, 0, 0, 0};
+    auto stage = [&](int q) {
+        if (!timing) return;
+        const clk::time_point t = clk::now();
+        tstage[q] = std::chrono::duration<double, std::micro>(t - tmark).count();
+        tmark = t;
+    };
     auto leq = [](float a, float b) { return a < b || std::abs(a - b) <= 1e-6f; };
     int adv = 0;  // samples per simulation step
     for (int i = 1; leq(i * dt, dts); ++i) adv++;
@@ -2289,6 +2301,7 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     // else every element's own (per-element layouts; they need per-element references)
     bool agree = !elem;
     for (int b = 1; b < B && agree; ++b) agree = tr[rep[b]].flags == tr[0].flags;
+    stage(0);
     int rc;
     if (agree) {
         if ((rc = hsddp_shift(h, n_steps, tr[0].flags.data()))) return rc;
@@ -2301,6 +2314,7 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
             std::copy(tr[rep[b]].flags.begin(), tr[rep[b]].flags.end(), cc.begin() + (size_t)b * n_steps);
         if ((rc = hsddp_shift_elements(h, n_steps, cc.data()))) return rc;
     }
+    stage(1);
     for (int b = 0; b < B; ++b) {
         const Layout L = layout_of(h, b);
         const int *re = h->lays.empty() ? h->reach_end.data() : &h->reach_el[(size_t)b * HSDDP_MAX_PHASES];
@@ -2309,7 +2323,9 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
             !std::equal(T.reach.begin(), T.reach.end(), re))
             return fail(HSDDP_ERR_ARG, "internal: advance and shift disagree on the layout");
     }
+    stage(2);
     if ((rc = build_refs(h, ws.data(), h->win_len, nullptr, dts, false))) return rc;
+    stage(3);
     const int P = p.P;  // the new stride (the largest layout's with per-element layouts)
     std::vector<int> contacts((size_t)B * (P + 1) * 4, 0);
     std::vector<double> dur((size_t)B * P * 4, 0.0);
@@ -2335,6 +2351,7 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
                 : T.next_kind == 1 ? sample_w(wsj[T.next_step], b, relj[T.next_step]).contact[l]
                                    : sample_w(wsj[T.next_step], b, plan_duration + dt_mpc).contact[l];
     }
+    stage(4);
     if (x0) {
         if ((rc = hsddp_update_problem(h, contacts.data(), x0, nullptr, nullptr, nullptr))) return rc;
     } else {  // x0 follows from the new first phase's contact: hsddp_update_problem(h, NULL, x0, NULL...)
@@ -2343,6 +2360,10 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     }
     h->durations.swap(dur);
     h->t_cur = t_cur;
+    stage(5);
+    if (timing)
+        std::fprintf(stderr, "hsddp_advance us: bookkeeping %.1f shift %.1f check %.1f refs %.1f contacts %.1f update %.1f\n",
+                     tstage[0], tstage[1], tstage[2], tstage[3], tstage[4], tstage[5]);
     if (contact_change)  // per step: some element saw a contact change (the batch's flag when it agrees)
         for (int j = 0; j < n_steps; ++j) {
             int f = 0;
