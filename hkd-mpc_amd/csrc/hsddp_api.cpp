@@ -228,6 +228,11 @@ struct hsddp_handle_t {
         int par = 0;  // which host count slot (host_counter[8 + 4 * par + 1]) its copy fills
     } iter_graph[8];
     int iter_graph_next = 0;
+    // hsddp_advance's shift without its own synchronisation: the host rows its pageable copies read
+    // stay here until the advance synchronises, and the touchdown-overflow flag is read then
+    std::vector<std::vector<int>> shift_keep;
+    bool shift_overflow_pending = false;
+    size_t scratch_reserved = 0;  // scratch bytes the pending shift's maps occupy (build_refs goes after)
     hipEvent_t iter_done[2] = {nullptr, nullptr};  // recorded after each replay, by parity
     std::vector<void *> allocs;
     size_t bytes = 0;
@@ -1808,7 +1813,7 @@ static int shift_phases(const Layout &L, const int *reach, int n_steps, const in
 // the receding-horizon shift of every element: cc[b * bstride + j * sstride] is element b's flag of
 // step j.  Elements with equal (layout, reach flags, step flags) share one slot map; when every
 // element ends on one layout the handle keeps (or returns to) the shared layout.
-static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride, size_t sstride)
+static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride, size_t sstride, bool defer = false)
 {
     if (!h || (n_steps > 0 && !cc)) return fail(HSDDP_ERR_ARG, "null argument");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
@@ -1927,7 +1932,10 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     a.zero_u0 = 1;  // trajectory_ptrs.front()->Ubar[0].setZero() (HKDProblem.cpp:219)
     launch_shift_gather(p.B, a, d, h->spare_Xbar, h->spare_Ubar, h->spare_K, h->stream);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(h->stream));
+    // defer (hsddp_advance, one layout for the batch): the caller's host work runs under the gather;
+    // everything after it is ordered on the handle's stream
+    const bool async = defer && nk == 1;
+    if (!async) HIPCHK(hipStreamSynchronize(h->stream));
     std::swap(d.Xb[0], h->spare_Xbar);
     std::swap(d.Ub[0], h->spare_Ubar);
     std::swap(d.reb_delta, h->spare_reb_delta);
@@ -1935,8 +1943,8 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     std::swap(d.al_sigma, h->spare_al_sigma);
     std::swap(d.al_lambda, h->spare_al_lambda);
     std::swap(d.td_mask, h->spare_td_mask);
-    const bool td_overflow = h->host_counter[6] != 0;
-    HIPCHK(hipMemset(d.sel, 0, B * sizeof(int)));  // the gathered warm start is buffer 0's
+    const bool td_overflow = !async && h->host_counter[6] != 0;
+    HIPCHK(hipMemsetAsync(d.sel, 0, B * sizeof(int), h->stream));  // the gathered warm start is buffer 0's
     if (p.fp32) { float *t = d.K32; d.K32 = (float *)h->spare_K; h->spare_K = t; }
     else { double *t = d.K; d.K = (double *)h->spare_K; h->spare_K = t; }
     // the new layouts
@@ -1968,6 +1976,11 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     h->need_inputs = true;
     h->refs_on_device = false;  // built for the old layout
     h->contacts_current = false;
+    if (async) {
+        h->shift_overflow_pending = true;
+        h->scratch_reserved = ((nmaps + (nk > 1 ? B : 0)) * sizeof(int) + 255) & ~(size_t)255;
+        for (std::vector<int> *v : {&smap, &cmap, &rmap, &pmap, &nadd}) h->shift_keep.push_back(std::move(*v));
+    }
     if (td_overflow)  // the shift itself is complete; the constraints past HSDDP_MAX_TD were not added
         return fail(HSDDP_ERR_UNSUPPORTED, "a phase would carry more than HSDDP_MAX_TD touchdown constraints");
     return HSDDP_OK;
@@ -2155,7 +2168,8 @@ static int build_refs(hsddp_handle h, const int *window_start, int window_len, c
     HIPCHK(hipSetDevice(h->desc.device));
     char *buf;
     int rc;
-    if ((rc = scratch(h, (Br + idx.size() + map_id.size()) * sizeof(int), &buf))) return rc;
+    if ((rc = scratch(h, h->scratch_reserved + (Br + idx.size() + map_id.size()) * sizeof(int), &buf))) return rc;
+    buf += h->scratch_reserved;  // (after a pending shift's maps: hsddp_advance)
     int *dstart = (int *)buf, *didx = dstart + Br, *dmap = didx + idx.size();
     if ((rc = h2d(dstart, window_start, Br * sizeof(int), h->stream)) ||
         (rc = h2d(didx, idx.data(), idx.size() * sizeof(int), h->stream)) ||
@@ -2209,6 +2223,19 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     using clk = std::chrono::steady_clock;
     clk::time_point tmark = clk::now();
     double tstage[6] = {0, 0, 0, 0, 0, 0};
+    // the shift runs without its own synchronisation (shift_impl's defer): whatever path leaves this
+    // function, the stream is drained before the host rows its copies read are released
+    struct Drain {
+        hsddp_handle h;
+        ~Drain()
+        {
+            if (!h->shift_overflow_pending) return;
+            hipStreamSynchronize(h->stream);
+            h->shift_overflow_pending = false;
+            h->shift_keep.clear();
+            h->scratch_reserved = 0;
+        }
+    } drain{h};
     auto stage = [&](int q) {
         if (!timing) return;
         const clk::time_point t = clk::now();
@@ -2304,7 +2331,7 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     stage(0);
     int rc;
     if (agree) {
-        if ((rc = hsddp_shift(h, n_steps, tr[0].flags.data()))) return rc;
+        if ((rc = shift_impl(h, n_steps, tr[0].flags.data(), 0, 1, true))) return rc;
     } else {
         if (B > 1 && Br == 1)
             return fail(HSDDP_ERR_UNSUPPORTED, "elements disagree on a contact change, which takes per-element layouts "
@@ -2324,8 +2351,6 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
             return fail(HSDDP_ERR_ARG, "internal: advance and shift disagree on the layout");
     }
     stage(2);
-    if ((rc = build_refs(h, ws.data(), h->win_len, nullptr, dts, false))) return rc;
-    stage(3);
     const int P = p.P;  // the new stride (the largest layout's with per-element layouts)
     std::vector<int> contacts((size_t)B * (P + 1) * 4, 0);
     std::vector<double> dur((size_t)B * P * 4, 0.0);
@@ -2351,6 +2376,8 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
                 : T.next_kind == 1 ? sample_w(wsj[T.next_step], b, relj[T.next_step]).contact[l]
                                    : sample_w(wsj[T.next_step], b, plan_duration + dt_mpc).contact[l];
     }
+    stage(3);
+    if ((rc = build_refs(h, ws.data(), h->win_len, nullptr, dts, false))) return rc;
     stage(4);
     if (x0) {
         if ((rc = hsddp_update_problem(h, contacts.data(), x0, nullptr, nullptr, nullptr))) return rc;
@@ -2360,9 +2387,14 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     }
     h->durations.swap(dur);
     h->t_cur = t_cur;
+    if (h->shift_overflow_pending) {  // the shift's touchdown-overflow flag (its copy is queued)
+        HIPCHK(hipStreamSynchronize(h->stream));
+        if (h->host_counter[6] != 0)
+            rc = fail(HSDDP_ERR_UNSUPPORTED, "a phase would carry more than HSDDP_MAX_TD touchdown constraints");
+    }
     stage(5);
     if (timing)
-        std::fprintf(stderr, "hsddp_advance us: bookkeeping %.1f shift %.1f check %.1f refs %.1f contacts %.1f update %.1f\n",
+        std::fprintf(stderr, "hsddp_advance us: bookkeeping %.1f shift %.1f check %.1f contacts %.1f refs %.1f update %.1f\n",
                      tstage[0], tstage[1], tstage[2], tstage[3], tstage[4], tstage[5]);
     if (contact_change)  // per step: some element saw a contact change (the batch's flag when it agrees)
         for (int j = 0; j < n_steps; ++j) {
@@ -2370,7 +2402,7 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
             for (int b = 0; b < B; ++b) f |= tr[rep[b]].flags[j];
             contact_change[j] = f;
         }
-    return HSDDP_OK;
+    return rc;  // HSDDP_OK, or the touchdown overflow (the advance itself is complete)
 }
 
 extern "C" int hsddp_get_phase_info(hsddp_handle h, int *contacts, double *durations)
