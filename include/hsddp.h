@@ -354,7 +354,10 @@ int hsddp_update_problem(hsddp_handle h, const int *contacts, const double *x0, 
  * pending — read the new first phase's contact (hsddp_get_phase_info), form x0 from it
  * (compute_hkd_state, HKDMPC.cpp:132-134) and call hsddp_update_problem(h, NULL, x0, NULL, NULL,
  * NULL), where NULL contacts are the ones derived here.  The caller's whole MPC tick is
- * hsddp_advance + hsddp_solve + hsddp_extract_commands (HKDMPCSolver::update, HKDMPC.cpp:96-165). */
+ * hsddp_advance + hsddp_solve + hsddp_extract_commands (HKDMPCSolver::update, HKDMPC.cpp:96-165).
+ * A phase that would carry more than HSDDP_MAX_TD touchdown constraints returns
+ * HSDDP_ERR_UNSUPPORTED once the rest of the advance is done (the constraints past the limit are
+ * not added), as hsddp_shift returns it after its shift. */
 int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, float dt_mpc, const double *x0,
                   int *contact_change);
 /* The handle's phase bookkeeping: contacts [B][P+1][4] (row P: the last phase's next contact) and,
