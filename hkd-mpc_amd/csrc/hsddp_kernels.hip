@@ -1441,8 +1441,9 @@ void launch_normalize(const Params &p, const Bufs &d, hipStream_t st)
     hipLaunchKernelGGL(k_normalize, dim3(blocks_for((long)p.B * p.S * (NX / 2), 256)), dim3(256), 0, st, p, d);
     hipLaunchKernelGGL(k_normalize_sel, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);
 }
-// The terminal tasks, TERM_TPW per wave, two waves per block: a launch of their own (87 VGPRs,
-// five waves per SIMD; as the tail of k_lq's launch they ran at its two).  The first wave
+// The terminal tasks, TERM_TPW per wave, two waves per block: a launch of their own (82 VGPRs,
+// 4.3 KB of LDS per task: 4.5 waves per SIMD; as the tail of k_lq's launch they ran at its two).
+// The first wave
 // also resets the iteration's counters: the parallel-retry list of the k_riccati launch that
 // follows starts empty (its only reader before then is the previous iteration's
 // k_riccati_select), no element has been seen searching after any trial yet (ls_live), and
