@@ -362,6 +362,7 @@ static void fill_params(hsddp_handle h)
     p.cost_thresh = o.cost_thresh; p.tconstr_thresh = o.tconstr_thresh; p.pconstr_thresh = o.pconstr_thresh;
     p.feas_thresh = o.dynamics_feas_thresh; p.merit_scale = o.merit_scale; p.merit_offset = o.merit_offset;
     p.AL_active = o.AL_active; p.ReB_active = o.ReB_active; p.no_early_exit = o.no_early_exit;
+    p.ms0 = o.MS ? 0 : 1;  // single shooting (MultiPhaseDDP.cpp:326-329; SinglePhase.cpp:214)
     // With update_ReB = update_relax = 1 (the shipped settings) update_REB_params leaves every
     // (delta, eps) at its initial value (ConstraintsBase.h:168-183): the kernels then read the two
     // scalars instead of the per-knot arrays.
@@ -485,6 +486,7 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
             void *rk;
             if ((rc = dalloc(h, d.retry_list, cap)) || (rc = dalloc(h, d.retry_count, 1)) ||
                 (rc = dalloc(h, d.retry_flag, n)) || (rc = dalloc(h, d.retry_dU, n * Kc * NX)) ||
+                (rc = dalloc(h, d.retry_dv, n)) ||
                 (rc = p.fp32 ? dalloc(h, (float *&)rk, n * Kc * KCW) : dalloc(h, (double *&)rk, n * Kc * KCW))) {
                 hsddp_destroy(h);
                 return rc;
@@ -938,8 +940,6 @@ static int solve_check(hsddp_handle h)
     if (!h) return fail(HSDDP_ERR_ARG, "null handle");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     if (h->need_inputs) return fail(HSDDP_ERR_ARG, "the layout changed (hsddp_shift): call hsddp_update_problem first");
-    if (!h->opt.MS)
-        return fail(HSDDP_ERR_UNSUPPORTED, "single shooting (MS = false) is not supported by the knot-parallel rollout");
     HIPCHK(hipSetDevice(h->desc.device));
     return HSDDP_OK;
 }
@@ -977,9 +977,13 @@ static void iteration_launches(hsddp_handle h, const std::vector<double> &trials
     tm.begin(1, e0);
     launch_riccati(p, d, st);
     tm.end(1, e0);
-    tm.begin(4, e0);
-    launch_lin_rollout(p, d, st);
-    tm.end(4, e0);
+    // the linear rollout with multiple shooting only (MultiPhaseDDP.cpp:326-329); with single
+    // shooting the sweep forms dV and the merit (k_riccati's DV instantiation)
+    if (!p.ms0) {
+        tm.begin(4, e0);
+        launch_lin_rollout(p, d, st);
+        tm.end(4, e0);
+    }
     tm.begin(2, e0);
     for (size_t t = 0; t < trials.size(); ++t) {
         launch_rollout(p, d, trials[t], t + 1 == trials.size(), 0, (int)t, st);
@@ -1679,6 +1683,12 @@ static int extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_t
         a.feet = (const float *)(buf + cmd_bytes + dur_bytes);
         if ((rc = h2d((void *)a.feet, foot_placements, feet_bytes, h->stream))) return rc;
     }
+    if (ticket >= 0 && (status_durations || foot_placements)) {
+        // the caller's inputs are pageable host memory and the call returns before the kernel runs:
+        // wait for their two small copies (a few microseconds) so the caller may release them
+        HIPCHK(hipEventRecord(h->cmd_ready[ticket], h->stream));
+        HIPCHK(hipEventSynchronize(h->cmd_ready[ticket]));
+    }
     if (ticket >= 0)  // the buffer's previous copy (two extractions ago) has left it
         HIPCHK(hipStreamWaitEvent(h->stream, h->cmd_copied[ticket], 0));
     launch_extract_commands(p, h->d, a, dcmd, h->stream);
@@ -1812,8 +1822,13 @@ static int shift_phases(const Layout &L, const int *reach, int n_steps, const in
 
 // the receding-horizon shift of every element: cc[b * bstride + j * sstride] is element b's flag of
 // step j.  Elements with equal (layout, reach flags, step flags) share one slot map; when every
-// element ends on one layout the handle keeps (or returns to) the shared layout.
-static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride, size_t sstride, bool defer = false)
+// element ends on one layout the handle keeps (or returns to) the shared layout.  A phase that would
+// carry more than HSDDP_MAX_TD touchdown constraints keeps the first ones (the shift is otherwise
+// complete): HSDDP_ERR_UNSUPPORTED, or, with `overflow`, *overflow = 1 and HSDDP_OK (hsddp_advance
+// finishes the step and reports it then).  defer: no synchronisation (one layout for the batch;
+// the flag is read by hsddp_advance).
+static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride, size_t sstride, bool defer = false,
+                      int *overflow = nullptr)
 {
     if (!h || (n_steps > 0 && !cc)) return fail(HSDDP_ERR_ARG, "null argument");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
@@ -1981,8 +1996,10 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
         h->scratch_reserved = ((nmaps + (nk > 1 ? B : 0)) * sizeof(int) + 255) & ~(size_t)255;
         for (std::vector<int> *v : {&smap, &cmap, &rmap, &pmap, &nadd}) h->shift_keep.push_back(std::move(*v));
     }
-    if (td_overflow)  // the shift itself is complete; the constraints past HSDDP_MAX_TD were not added
-        return fail(HSDDP_ERR_UNSUPPORTED, "a phase would carry more than HSDDP_MAX_TD touchdown constraints");
+    if (td_overflow) {  // the shift itself is complete; the constraints past HSDDP_MAX_TD were not added
+        if (overflow) *overflow = 1;
+        else return fail(HSDDP_ERR_UNSUPPORTED, "a phase would carry more than HSDDP_MAX_TD touchdown constraints");
+    }
     return HSDDP_OK;
 }
 
@@ -2205,10 +2222,9 @@ static int build_refs(hsddp_handle h, const int *window_start, int window_len, c
 // constraint / reset map towards the contact at plan_duration + dt_mpc (add_tconstr_one_phase,
 // :199-202, 268-308).  Then the shifted warm start (hsddp_shift), the new layout's references
 // (build_refs) and the new contacts and x0 (hsddp_update_problem).
-extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, float dt_mpc, const double *x0,
-                             int *contact_change)
+static int advance_impl(hsddp_handle h, int n_steps, float plan_duration, float dt_mpc, const double *x0,
+                        int *contact_change, int &overflow)
 {
-    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
     if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
     if (h->need_inputs) return fail(HSDDP_ERR_ARG, "the previous shift awaits hsddp_update_problem");
     if (h->win_start.empty() || h->table_host.empty())
@@ -2223,19 +2239,6 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     using clk = std::chrono::steady_clock;
     clk::time_point tmark = clk::now();
     double tstage[6] = {0, 0, 0, 0, 0, 0};
-    // the shift runs without its own synchronisation (shift_impl's defer): whatever path leaves this
-    // function, the stream is drained before the host rows its copies read are released
-    struct Drain {
-        hsddp_handle h;
-        ~Drain()
-        {
-            if (!h->shift_overflow_pending) return;
-            hipStreamSynchronize(h->stream);
-            h->shift_overflow_pending = false;
-            h->shift_keep.clear();
-            h->scratch_reserved = 0;
-        }
-    } drain{h};
     auto stage = [&](int q) {
         if (!timing) return;
         const clk::time_point t = clk::now();
@@ -2331,7 +2334,7 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     stage(0);
     int rc;
     if (agree) {
-        if ((rc = shift_impl(h, n_steps, tr[0].flags.data(), 0, 1, true))) return rc;
+        if ((rc = shift_impl(h, n_steps, tr[0].flags.data(), 0, 1, true, &overflow))) return rc;
     } else {
         if (B > 1 && Br == 1)
             return fail(HSDDP_ERR_UNSUPPORTED, "elements disagree on a contact change, which takes per-element layouts "
@@ -2339,7 +2342,8 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
         std::vector<int> cc((size_t)B * n_steps);
         for (int b = 0; b < B; ++b)
             std::copy(tr[rep[b]].flags.begin(), tr[rep[b]].flags.end(), cc.begin() + (size_t)b * n_steps);
-        if ((rc = hsddp_shift_elements(h, n_steps, cc.data()))) return rc;
+        // (hsddp_shift_elements, with a touchdown overflow reported after the rest of the step)
+        if ((rc = shift_impl(h, n_steps, cc.data(), (size_t)n_steps, 1, false, &overflow))) return rc;
     }
     stage(1);
     for (int b = 0; b < B; ++b) {
@@ -2387,11 +2391,6 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
     }
     h->durations.swap(dur);
     h->t_cur = t_cur;
-    if (h->shift_overflow_pending) {  // the shift's touchdown-overflow flag (its copy is queued)
-        HIPCHK(hipStreamSynchronize(h->stream));
-        if (h->host_counter[6] != 0)
-            rc = fail(HSDDP_ERR_UNSUPPORTED, "a phase would carry more than HSDDP_MAX_TD touchdown constraints");
-    }
     stage(5);
     if (timing)
         std::fprintf(stderr, "hsddp_advance us: bookkeeping %.1f shift %.1f check %.1f contacts %.1f refs %.1f update %.1f\n",
@@ -2402,7 +2401,33 @@ extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, f
             for (int b = 0; b < B; ++b) f |= tr[rep[b]].flags[j];
             contact_change[j] = f;
         }
-    return rc;  // HSDDP_OK, or the touchdown overflow (the advance itself is complete)
+    return HSDDP_OK;
+}
+
+// hsddp_advance = advance_impl, then: the deferred shift's stream is drained before the host rows its
+// copies read are released (whatever path left advance_impl), and its touchdown-overflow flag is
+// read.  A touchdown overflow on a complete step (both shift paths) returns HSDDP_ERR_UNSUPPORTED
+// with the handle ready to solve: new layout, references, contacts, x0, durations and clock, the
+// phase keeping its first HSDDP_MAX_TD touchdown constraints.  When the step failed for another
+// reason, that error is returned and an overflow is added to its message.
+extern "C" int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, float dt_mpc, const double *x0,
+                             int *contact_change)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    int overflow = 0;
+    const int rc = advance_impl(h, n_steps, plan_duration, dt_mpc, x0, contact_change, overflow);
+    if (h->shift_overflow_pending) {  // the deferred shift's flag (its copy is queued on the stream)
+        const hipError_t e = hipStreamSynchronize(h->stream);
+        if (e == hipSuccess && h->host_counter[6] != 0) overflow = 1;
+        h->shift_overflow_pending = false;
+        h->shift_keep.clear();
+        h->scratch_reserved = 0;
+        if (e != hipSuccess && rc == HSDDP_OK) return fail(HSDDP_ERR_DEVICE, std::string("advance: ") + hipGetErrorString(e));
+    }
+    static const char *msg = "a phase would carry more than HSDDP_MAX_TD touchdown constraints";
+    if (rc == HSDDP_OK) return overflow ? fail(HSDDP_ERR_UNSUPPORTED, msg) : HSDDP_OK;
+    if (overflow) fail(rc, std::string(hsddp_last_error()) + " (and " + msg + ")");
+    return rc;
 }
 
 extern "C" int hsddp_get_phase_info(hsddp_handle h, int *contacts, double *durations)

@@ -189,6 +189,21 @@ DEV double running_cost(const Params &p, const int *c, const double *x, const do
     return l;
 }
 
+// The step after the sweep / linear rollout of MultiPhaseDDP::solve (MultiPhaseDDP.cpp:331-343):
+// merit weight rho from the expected cost change (w1, w2) = (dV_1, dV_2), the merit, the values
+// the line search compares against, and the early termination before the line search.
+DEV void merit_step(const Params &p, ElemState &E, double w1, double w2)
+{
+    const double cost = E.cost, feas = E.feas;
+    const double dV_abs = fabs(w1 + 0.5 * w2);
+    const double rho = (feas > p.feas_thresh) ? dV_abs / ((1 - p.merit_scale) * feas) + p.merit_offset : 0;
+    const double merit = cost + rho * feas;
+    E.dV1 = w1; E.dV2 = w2; E.merit_rho = rho; E.merit = merit;
+    E.cost_prev = cost; E.merit_prev = merit; E.feas_prev = feas;
+    if (!p.no_early_exit && dV_abs < p.cost_thresh && feas <= p.feas_thresh) { E.inner_done = 1; E.ls_active = 0; }
+    else E.ls_active = 1;
+}
+
 // the legs of the phase's touchdown constraints (union of the slot masks; TD_PENDING slots are
 // resolved before any solve)
 DEV unsigned td_union(const int *mask)

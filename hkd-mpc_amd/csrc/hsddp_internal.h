@@ -107,6 +107,10 @@ struct Params {
     int elem_layout;  // 1: element b's layout is Bufs::lay[b] (N, s0, k0, ss above unused)
     int n_pairs;      // sweep waves: Bufs::pairs [n_pairs][2] (elem_layout), else ceil(B / 2)
     int store_value;  // the sweep writes G[0], H[0] of every phase (Bufs::value0)
+    // single shooting (HSDDP_OPTION::MS = false, MultiPhaseDDP.cpp:326-331; SinglePhase.cpp:211-220):
+    // no linear rollout, the sweep forms dV_1 / dV_2 (SinglePhase.cpp:359-362) and the merit, and the
+    // rollout simulates every phase from its first state (k_rollout_ss)
+    int ms0;
 };
 
 // one element deferred to the parallel retry: its index and the regularisation of its failed sweep
@@ -151,6 +155,7 @@ struct Bufs {
     int *retry_count, *retry_flag;
     void *retry_K;                         // real (fp64, or fp32 in the C5 mode) [..][KCW]
     double *retry_dU;                      // [..][24]
+    double *retry_dv;                      // [retry_cap][retry_m] the attempt's sum of Qu^T dU (single shooting)
     unsigned long long *dbg;               // [B][16] diagnostic builds only (in-kernel stamps)
     // get_solver_info buffers (MultiPhaseDDP.cpp:532-541): per element hcap entries of
     // (actual_cost, dynamics feasibility, max terminal violation, max path violation)

@@ -886,6 +886,101 @@ __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double ep
     }
 }
 
+// k_rollout_ss: one trial with single shooting (HSDDP_OPTION::MS = false).  SinglePhase::
+// hybrid_rollout (SinglePhase.cpp:181-233) then takes X[k+1] = Xsim[k+1] at every knot whatever
+// SS_set says (:214-220); only a phase's first state stays a shooting state when its set holds 0
+// (:187-193): X[0] = Xbar[0] + eps dX[0] (dX is not written without the linear rollout,
+// MultiPhaseDDP.cpp:326-329, so it keeps its last values), else X[0] = x_init.  So phases that start
+// from a shooting state are independent: one thread per (element, phase), 16 per element (four
+// elements per 64-thread block), each simulating its phase's knots one after another.  Then, after
+// the block's barrier, the phase-start Defects (Xsim[0] = x_init: x0 or the reset map of the
+// previous phase's X[N], MultiPhaseDDP.cpp:73-81) and the phases without shooting states (a new
+// last phase of <= 2 knots after a receding-horizon shift), which start from that reset map.
+template <bool EL>
+DEV void ss_phase(const Params &p, const Bufs &d, int b, int i, double eps, const double *x_init)
+{
+    const auto L = layout_of<EL>(d, b);
+    const size_t sb = (size_t)b * p.S, kb = (size_t)b * p.Kc;
+    const int nb = nom_buf(d, b);
+    const double *Xbar = d.Xb[nb], *Ubar = d.Ub[nb];
+    double *X = d.Xb[nb ^ 1], *U = d.Ub[nb ^ 1];
+    const int N = L.N(i), s0 = L.s0(i), k0 = L.k0(i);
+    int c[4], cn[4];
+    load_contacts(d, p, b, i, c, cn);
+    const double cd[4] = {(double)c[0], (double)c[1], (double)c[2], (double)c[3]};
+    double x[NX], xs[NX], u[NU];
+    if (x_init) {  // no shooting state: X[0] = x_init (Defect[0] = 0)
+        for (int j = 0; j < NX; ++j) x[j] = x_init[j];
+    } else {       // X[0] = Xbar[0] + eps dX[0] (k_rollout's expression)
+        const double *xb = Xbar + (sb + s0) * NX, *dx = d.dX + (sb + s0) * NX;
+        for (int j = 0; j < NX; ++j) x[j] = __builtin_fma(eps, dx[j], xb[j]);
+    }
+    for (int k = 0; k <= N; ++k) {
+        const int s = s0 + k;
+        double *xg = X + (sb + s) * NX;
+        if (k > 0)
+            for (int j = 0; j < NX; ++j) x[j] = xs[j];
+        for (int j = 0; j < NX; ++j) xg[j] = x[j];
+        if (k > 0 || x_init) finish_defect(p, d, b, s, k, x, k > 0 ? xs : x);
+        if (k == N) {
+            finish_terminal(p, d, b, s, i, c, cn, x);
+            break;
+        }
+        // U = Ubar + eps dU + K (X - Xbar) (SinglePhase.cpp:200), K from the 12 coupled gain rows
+        const int kc = k0 + k;
+        const double *xb = Xbar + (sb + s) * NX, *ub = Ubar + (kb + kc) * NU, *du = d.dU + (kb + kc) * NU;
+        double dx[NX];
+        for (int j = 0; j < NX; ++j) dx[j] = x[j] - xb[j];
+        for (int j = 0; j < NU; ++j) u[j] = 0.0;
+        for (int q = 0; q < 12; ++q) {
+            const size_t kr = ((kb + kc) * 12 + q) * NX;
+            double acc = 0.0;
+            for (int j = 0; j < NX; ++j) acc += (p.fp32 ? (double)d.K32[kr + j] : d.K[kr + j]) * dx[j];
+            u[c[q / 3] ? q : 12 + q] = acc;
+        }
+        double *ug = U + (kb + kc) * NU;
+        for (int j = 0; j < NU; ++j) { u[j] = ub[j] + eps * du[j] + u[j]; ug[j] = u[j]; }
+        finish_running(p, d, b, s, kc, c, x, u);
+        hkd_step(x, u, cd, p.dt, xs);
+    }
+}
+
+template <bool EL>
+__global__ __launch_bounds__(64) void k_rollout_ss(Params p, Bufs d, double eps, int init, int tix)
+{
+    if (ls_skip(d, tix)) return;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 4), i = threadIdx.x & 15;
+    bool mine = false, shoot = false;
+    if (b < p.B) {
+        const ElemState &E = d.el[b];
+        const auto L = layout_of<EL>(d, b);
+        mine = (init ? !E.done : E.ls_active != 0) && i < L.P();
+        shoot = mine && L.ss(i) > 0;
+    }
+    if (shoot) ss_phase<EL>(p, d, b, i, eps, nullptr);
+    __syncthreads();  // every phase's X[N] written (same block)
+    if (!mine) return;
+    const auto L = layout_of<EL>(d, b);
+    const size_t sb = (size_t)b * p.S;
+    const int nb = nom_buf(d, b), s0 = L.s0(i);
+    const double *X = d.Xb[nb ^ 1];
+    double xi[NX];
+    if (i == 0) {
+        for (int j = 0; j < NX; ++j) xi[j] = d.x0[(size_t)b * NX + j];
+    } else {
+        int cp_[4], cpn[4];
+        load_contacts(d, p, b, i - 1, cp_, cpn);
+        hkd_resetmap(X + (sb + s0 - 1) * NX, cp_, cpn, xi);
+    }
+    if (shoot) {
+        double x[NX];
+        for (int j = 0; j < NX; ++j) x[j] = X[(sb + s0) * NX + j];
+        finish_defect(p, d, b, s0, 0, x, xi);
+    } else {
+        ss_phase<EL>(p, d, b, i, eps, xi);
+    }
+}
+
 // k_decide: reductions of one trial + merit acceptance (MultiPhaseDDP.cpp:113-133) + the
 // later-termination test (:358).  16 lanes per element, one per phase: each lane sums its phase's
 // slots in order, and the phase sums are added in phase order — the reference's summation order
@@ -1416,10 +1511,14 @@ static inline unsigned blocks_for(long n, int bs) { return (unsigned)((n + bs - 
     } while (0)
 
 // small batches without non-shooting tails decide each trial in its rollout launch (k_rollout FUSE)
-static bool fused_decide(const Params &p) { return p.B <= 16 && !p.has_tail; }
+static bool fused_decide(const Params &p) { return p.B <= 16 && !p.has_tail && !p.ms0; }
 
 void launch_rollout(const Params &p, const Bufs &d, double eps, int last, int init, int tix, hipStream_t st)
 {
+    if (p.ms0) {  // single shooting: every knot simulated (k_rollout_ss)
+        LAUNCH_EL(k_rollout_ss, dim3((p.B + 3) / 4), dim3(64), st, p, d, eps, init, tix);
+        return;
+    }
     // slot waves, then the phase-boundary waves (k_rollout, rollout_boundary)
     const dim3 g(blocks_for((long)p.B * p.S, 64) + blocks_for((long)p.B * p.P, 64));
     if (fused_decide(p)) {

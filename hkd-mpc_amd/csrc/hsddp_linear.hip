@@ -560,16 +560,7 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
     __syncthreads();
     if (lane < 8) d.dbg[(size_t)__builtin_amdgcn_readfirstlane((int)eb[1]) * 16 + 8 + lane] += lin_stamps().st[lane];
 #endif
-    if (r == 0 && act) {
-        const double cost = E.cost, feas = E.feas, w1 = v1, w2 = v2;
-        const double dV_abs = fabs(w1 + 0.5 * w2);
-        const double rho = (feas > p.feas_thresh) ? dV_abs / ((1 - p.merit_scale) * feas) + p.merit_offset : 0;
-        const double merit = cost + rho * feas;
-        E.dV1 = w1; E.dV2 = w2; E.merit_rho = rho; E.merit = merit;
-        E.cost_prev = cost; E.merit_prev = merit; E.feas_prev = feas;
-        if (!p.no_early_exit && dV_abs < p.cost_thresh && feas <= p.feas_thresh) { E.inner_done = 1; E.ls_active = 0; }
-        else E.ls_active = 1;
-    }
+    if (r == 0 && act) merit_step(p, E, v1, v2);
 }
 
 void launch_lin_rollout(const Params &p, const Bufs &d, hipStream_t st)

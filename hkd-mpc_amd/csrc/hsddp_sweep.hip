@@ -27,8 +27,8 @@
 //   the next knot's images requested by LDS-DMA
 //   elimination on [Quu_cc | Qux_c | Qu_c] in LDL^T order (12 pivot steps, pivots by DPP
 //   broadcast, the next pivot's reciprocal threaded through the current step), back substitution
-//   K = -Quu_cc^-1 Qux_c, dU, G = Qx - Qux_c^T Quu_cc^-1 Qu_c  (the sweep's dV is not formed: the
-//   MS linear rollout replaces it, quirk A3)
+//   K = -Quu_cc^-1 Qux_c, dU, G = Qx - Qux_c^T Quu_cc^-1 Qu_c  (the sweep's dV is formed only with
+//   single shooting, DV: with MS the linear rollout replaces it, quirk A3)
 //   H = Qxx - Qux_c^T Quu_cc^-1 Qux_c by DPP broadcast of K from the lanes holding it
 //   (HSDDP_VALUE_MFMA = 1: on the matrix cores, v_mfma_f64_16x16x4_f64, symmetric tiles)
 //   K rows and dU stored after one wait for all vector memory operations (nothing waits on them)
@@ -352,12 +352,15 @@ DEV void eliminate(real (&w)[HC], real (&w2)[HC], unsigned long long &bad)
 // One knot of SinglePhase::backward_sweep for the wave's two items.  h / g: H[k+1] row pp and
 // G[k+1][pp] on entry, H[k], G[k] on exit.  live: this half's item is still sweeping (turns false
 // at a failed PSD test: nothing of this knot or below is written).  more: the next knot's images
-// are requested into S.img during the elimination (nrec*/ndef*).  The expected cost change of the
-// sweep (SinglePhase.cpp:357-358) is not formed: the MS linear rollout replaces it (quirk A3).
-template <typename real>
+// are requested into S.img during the elimination (nrec*/ndef*).  DV (single shooting only): the
+// knot's Qu^T dU (dV_k = -Qu^T dU, SinglePhase.cpp:359-362) is added to the lane's dvs — position 24
+// the coupled controls' part, positions < 12 one decoupled control each.  Without DV (multiple
+// shooting) it is not formed: the linear rollout replaces it (quirk A3), and that instantiation is
+// the one the metric runs.
+template <typename real, bool DV>
 DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &ph, const Item<real> &it, int kc,
               real (&h)[NX], real &g, bool &live, bool first, bool more, const real *nrec0, const real *ndef0,
-              const real *nrec1, const real *ndef1)
+              const real *nrec1, const real *ndef1, double &dvs)
 {
     typename Lds<real>::Item &I = S.it[L.e];
     const real *img = S.img[L.e];
@@ -486,10 +489,11 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     if (more) fetch(S, nrec0, ndef0, nrec1, ndef1, L.lane);
     STAMP(5);
     // ---- PSD test + Gauss-Jordan on [Quu_cc | Qux_c | Qu_c] --------------------------------------
-    // Qux_c column pp, kept for G and the value update (positions >= 24: zero, so their H row stays 0)
+    // Qux_c column pp, kept for G and the value update (positions >= 24: zero, so their H row stays 0;
+    // DV: position 24 keeps Qu_c for the knot's Qu_c^T dU_c, and its H row is cleared after the update)
     real quxs[HC];
 #pragma unroll
-    for (int q = 0; q < HC; ++q) quxs[q] = L.row ? w2[q] : (real)0;
+    for (int q = 0; q < HC; ++q) quxs[q] = (L.row || (DV && pp == NX)) ? w2[q] : (real)0;
     pin(quxs);
     unsigned long long bad = __builtin_amdgcn_ballot_w64(zl && !(qzz > (real)1e-9));
     // w2 becomes -Quu_cc^-1 [Qux_c | Qu_c] = [K_c | dU_c] (the reference's explicit inverse,
@@ -518,6 +522,13 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
 #pragma unroll
     for (int q = 0; q < HC; ++q) gq4[q & 3] = __builtin_fma(quxs[q], I.MI[NX * TS + q], gq4[q & 3]);
     const real gq = (gq4[0] + gq4[1]) + (gq4[2] + gq4[3]);
+    if constexpr (DV) {
+        real dq = 0;
+#pragma unroll
+        for (int q = 0; q < HC; ++q) dq = __builtin_fma(quxs[q], I.MI[NX * TS + q], dq);
+        const double v = pp == NX ? (double)dq : zl ? (double)quz * (double)I.du[du_z] : 0.0;
+        if (st) dvs += v;
+    }
     STAMP(7);
     // ---- H = Qxx - Qux_c^T Quu_cc^-1 Qux_c = Qxx + Qux_c^T K_c on the matrix cores ------------------
     // (tiles (0,0), (0,1), (1,1) of the symmetric 24 x 24 product, K = 12, for both items at once;
@@ -576,6 +587,12 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     real gq4[4] = {qx, 0, 0, 0};
     static_for<HC>([&](auto Q) { bfma<8>(gq4[Q & 3], kb[Q], quxs[Q]); });
     const real gq = (gq4[0] + gq4[1]) + (gq4[2] + gq4[3]);
+    if constexpr (DV) {  // position 24: Qu_c^T dU_c (dU_c by broadcast from position 24 = kb's position 8)
+        real dq = 0;
+        static_for<HC>([&](auto Q) { bfma<8>(dq, kb[Q], quxs[Q]); });
+        const double v = pp == NX ? (double)dq : zl ? (double)quz * (double)(-(quz / qzz)) : 0.0;
+        if (st) dvs += v;
+    }
     STAMP(7);
     // ---- H = Qxx - Qux_c^T Quu_cc^-1 Qux_c = Qxx + Qux_c^T K_c (SinglePhase.cpp:360): row pp,
     // K_c by DPP broadcast from the lanes that hold its columns
@@ -590,6 +607,10 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
                 bfma<c & 15>(h[c], kb[Q], quxs[Q]);
         });
     });
+    if constexpr (DV)
+        if (!L.row)
+#pragma unroll
+            for (int c = 0; c < NX; ++c) h[c] = 0;
     STAMP(8);
 #endif
     g = L.row ? gq : (real)0;
@@ -624,10 +645,13 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
 
 // MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229) for the wave's two items with their
 // own regularisation.  Returns, per half, -1 (success) or the control slot of the first knot whose
-// Quu fails the PSD test (that knot and the ones below it are not written).
-template <typename real, bool EL>
-DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, const Item<real> &it)
+// Quu fails the PSD test (that knot and the ones below it are not written).  DV: dv = the half's
+// sum over every knot of Qu^T dU (= dV_1 = -dV_2 of the sweep, SinglePhase.cpp:359-362,
+// MultiPhaseDDP.cpp:224-226), on every lane of the half.
+template <typename real, bool EL, bool DV>
+DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, const Item<real> &it, double &dv)
 {
+    double dvs = 0.0;
     const int pp = L.pp;
     const real *lqg = Prec<real>::lq(d), *defg = Prec<real>::def(d);
     // the other item of the wave (its element's records feed the DMA even when this half is idle)
@@ -709,8 +733,8 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
             const bool more = k > 0;
             const int kn = more ? k - 1 : 0;
             const bool was = live;
-            knot(p, S, L, ph, it, k0 + k, h, g, live, k == N - 1, more, recp(b0, kn), defp(b0, kn), recp(b1, kn),
-                 defp(b1, kn));
+            knot<real, DV>(p, S, L, ph, it, k0 + k, h, g, live, k == N - 1, more, recp(b0, kn), defp(b0, kn), recp(b1, kn),
+                           defp(b1, kn), dvs);
             if (was && !live) fail = k0 + k;
             if (!__builtin_amdgcn_ballot_w64(live)) break;
         }
@@ -731,6 +755,11 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
             V[pp] = (double)g;
         }
     }
+    if constexpr (DV) {
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) dvs += __shfl_xor(dvs, o);
+    }
+    dv = dvs;
     return it.act ? fail : -1;
 }
 
@@ -813,7 +842,7 @@ using namespace sweep;
 // the sweep with each element's mu, then (for an element whose first sweep fails and that the
 // parallel retry cannot take) mu = max(mu * update_regularization, 1e-3) until a sweep succeeds or
 // mu > 1e2, then mu / 20 (0 below 1e-6) as the next regularisation.
-template <typename real, bool EL>
+template <typename real, bool EL, bool DV>
 __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
 {
     __shared__ Lds<real> S;
@@ -853,14 +882,17 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
     it.K = Prec<real>::K(d) + (size_t)bv * p.Kc * KCW;
     it.dU = d.dU + (size_t)bv * p.Kc * NX;
     bool need = act, ok = false;
+    double dvk = 0.0;  // DV: Qu^T dU summed over the successful sweep
     for (int attempt = 0; __builtin_amdgcn_ballot_w64(need); ++attempt) {
         it.act = need;
         it.reg = (real)reg;
-        const int fk = sweep_pair<real, EL>(p, d, S, L, it);
+        double dv;
+        const int fk = sweep_pair<real, EL, DV>(p, d, S, L, it, dv);
         if (need) {
             if (fk < 0) {
                 ok = true;
                 need = false;
+                dvk = dv;
             } else {
                 bool deferred = false;
                 if (attempt == 0 && p.retry_cap > 0) {
@@ -895,6 +927,8 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
         E.iters += 1; E.cost = ecost; E.feas = efeas; E.accepted = 0;
         if (ok) E.reg = rn;
         else { E.reg = rn; E.status = 1; E.done = 1; E.ls_active = 0; }
+        // single shooting: merit and early exit from the sweep's dV (MultiPhaseDDP.cpp:326-343)
+        if (DV && ok) merit_step(p, E, dvk, -dvk);
     }
 }
 
@@ -902,7 +936,7 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
 // item (f, a) sweeps deferred element f with the a-th next mu of the schedule into its own scratch
 // rows, two items per wave.  Every attempt is the sweep the sequential loop would run with that mu,
 // so taking the first success (k_riccati_select) gives the loop's result.
-template <typename real, bool EL>
+template <typename real, bool EL, bool DV>
 __global__ __launch_bounds__(64, 2) void k_riccati_retry(Params p, Bufs d)
 {
     __shared__ Lds<real> S;
@@ -933,8 +967,10 @@ __global__ __launch_bounds__(64, 2) void k_riccati_retry(Params p, Bufs d)
     it.reg = (real)reg;
     it.K = (real *)d.retry_K + slot * p.Kc * KCW;
     it.dU = d.retry_dU + slot * p.Kc * NX;
-    const int fk = sweep_pair<real, EL>(p, d, S, L, it);
+    double dv;
+    const int fk = sweep_pair<real, EL, DV>(p, d, S, L, it, dv);
     if (act && L.pp == 0) *flag = fk < 0 ? 1 : -1 - fk;  // success, or -1 - (the failing control slot)
+    if (DV && act && L.pp == 0) d.retry_dv[slot] = dv;
 }
 
 // The outcome of backward_sweep_regularized for each deferred element: the first attempt that
@@ -989,6 +1025,10 @@ __global__ __launch_bounds__(64) void k_riccati_select(Params p, Bufs d)
         if (rn < 1e-06) rn = 0;
         E.reg = rn;
         if (!win) { E.status = 1; E.done = 1; E.ls_active = 0; }  // goto bad_solve
+        else if (p.ms0) {  // single shooting: merit from the winning attempt's dV (k_riccati's epilogue)
+            const double dv = d.retry_dv[(size_t)f * p.retry_m + (win - 1)];
+            merit_step(p, E, dv, -dv);
+        }
     }
 }
 
@@ -996,25 +1036,30 @@ void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
 {
     // (the retry list count is zeroed by the k_lq launch just before, in its first terminal task)
     const dim3 g1((unsigned)(p.elem_layout ? p.n_pairs : (p.B + 1) / 2));
-    if (p.fp32) {
-        if (p.elem_layout) hipLaunchKernelGGL((k_riccati<float, true>), g1, dim3(64), 0, st, p, d);
-        else hipLaunchKernelGGL((k_riccati<float, false>), g1, dim3(64), 0, st, p, d);
-    } else {
-        if (p.elem_layout) hipLaunchKernelGGL((k_riccati<double, true>), g1, dim3(64), 0, st, p, d);
-        else hipLaunchKernelGGL((k_riccati<double, false>), g1, dim3(64), 0, st, p, d);
-    }
+    // instantiations: precision x layout mode x single shooting (DV)
+#define HSDDP_RIC(kern, grid, real)                                                                          \
+    do {                                                                                                     \
+        if (p.ms0) {                                                                                         \
+            if (p.elem_layout) hipLaunchKernelGGL((kern<real, true, true>), grid, dim3(64), 0, st, p, d);      \
+            else hipLaunchKernelGGL((kern<real, false, true>), grid, dim3(64), 0, st, p, d);                   \
+        } else {                                                                                             \
+            if (p.elem_layout) hipLaunchKernelGGL((kern<real, true, false>), grid, dim3(64), 0, st, p, d);     \
+            else hipLaunchKernelGGL((kern<real, false, false>), grid, dim3(64), 0, st, p, d);                  \
+        }                                                                                                    \
+    } while (0)
+    if (p.fp32) HSDDP_RIC(k_riccati, g1, float);
+    else HSDDP_RIC(k_riccati, g1, double);
     if (p.retry_cap > 0) {
         const dim3 gr((unsigned)(p.retry_cap * (p.retry_m + (p.retry_m & 1)) / 2)), gs((unsigned)p.retry_cap);
         if (p.fp32) {
-            if (p.elem_layout) hipLaunchKernelGGL((k_riccati_retry<float, true>), gr, dim3(64), 0, st, p, d);
-            else hipLaunchKernelGGL((k_riccati_retry<float, false>), gr, dim3(64), 0, st, p, d);
+            HSDDP_RIC(k_riccati_retry, gr, float);
             hipLaunchKernelGGL(k_riccati_select<float>, gs, dim3(64), 0, st, p, d);
         } else {
-            if (p.elem_layout) hipLaunchKernelGGL((k_riccati_retry<double, true>), gr, dim3(64), 0, st, p, d);
-            else hipLaunchKernelGGL((k_riccati_retry<double, false>), gr, dim3(64), 0, st, p, d);
+            HSDDP_RIC(k_riccati_retry, gr, double);
             hipLaunchKernelGGL(k_riccati_select<double>, gs, dim3(64), 0, st, p, d);
         }
     }
+#undef HSDDP_RIC
 }
 
 }  // namespace hsddp

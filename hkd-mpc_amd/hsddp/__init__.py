@@ -261,10 +261,21 @@ class Solver:
         return out
 
     def upload_constraint_params(self, reb_delta=None, reb_eps=None, td_mask=None, al_sigma=None, al_lambda=None):
-        """hsddp_upload_constraint_params (None keeps a field)"""
-        arrs = [None if a is None else np.ascontiguousarray(a, dtype=t) for a, t in
-                ((reb_delta, np.float64), (reb_eps, np.float64), (td_mask, np.int32), (al_sigma, np.float64),
-                 (al_lambda, np.float64))]
+        """hsddp_upload_constraint_params (None keeps a field); shapes as constraint_params()'s.  The C
+        side reads B x Kc x 20 / B x P x MAX_TD (x 4) values from each pointer, so the shapes are
+        checked here (a [Kc][20] array for B > 1 would be read past its end)."""
+        B, P, Kc, T = self.B, self.P, self.Kc, self.MAX_TD
+        arrs = []
+        for name, a, t, shape in (("reb_delta", reb_delta, np.float64, (B, Kc, 20)),
+                                  ("reb_eps", reb_eps, np.float64, (B, Kc, 20)),
+                                  ("td_mask", td_mask, np.int32, (B, P, T)),
+                                  ("al_sigma", al_sigma, np.float64, (B, P, T, 4)),
+                                  ("al_lambda", al_lambda, np.float64, (B, P, T, 4))):
+            if a is not None:
+                a = np.ascontiguousarray(a, dtype=t)
+                if a.shape != shape:
+                    raise HSDDPError(f"{name}: shape {a.shape}, expected {shape}")
+            arrs.append(a)
         check(lib().hsddp_upload_constraint_params(self._h, *(None if a is None else a.ctypes.data for a in arrs)))
 
     def set_value_export(self, on: bool = True) -> None:
@@ -285,6 +296,7 @@ class Solver:
         out = np.zeros(self.B, dtype=MPC_COMMAND)
         dur = None if status_durations is None else np.ascontiguousarray(status_durations, dtype=np.float64)
         feet = None if foot_placements is None else np.ascontiguousarray(foot_placements, dtype=np.float32)
+        self._check_cmd_inputs(dur, feet)
         check(lib().hsddp_extract_commands(
             self._h, int(nsteps_between_mpc), float(mpc_time), float(dt_mpc),
             None if dur is None else dur.ctypes.data, int(dur is not None and dur.ndim == 3),
@@ -292,13 +304,20 @@ class Solver:
             float(solve_time), out.ctypes.data))
         return out
 
+    def _check_cmd_inputs(self, dur, feet):
+        """the C side reads [P][4] or [B][P][4] durations and [12] or [B][12] feet by the arrays' rank"""
+        if dur is not None and dur.shape not in ((self.P, 4), (self.B, self.P, 4)):
+            raise HSDDPError(f"status_durations: shape {dur.shape}, expected ({self.P}, 4) or ({self.B}, {self.P}, 4)")
+        if feet is not None and feet.shape not in ((12,), (self.B, 12)):
+            raise HSDDPError(f"foot_placements: shape {feet.shape}, expected (12,) or ({self.B}, 12)")
+
     def extract_commands_async(self, nsteps_between_mpc: int = 1, mpc_time: float = 0.0, dt_mpc: float = 0.01,
                                status_durations=None, foot_placements=None, solve_time: float = 0.0) -> int:
         """hsddp_extract_commands_async: the records cross PCIe on the handle's copy stream while the
         caller goes on (the next tick's advance / solve); returns the ticket for commands_wait."""
         dur = None if status_durations is None else np.ascontiguousarray(status_durations, dtype=np.float64)
         feet = None if foot_placements is None else np.ascontiguousarray(foot_placements, dtype=np.float32)
-        self._cmd_keep = (dur, feet)
+        self._check_cmd_inputs(dur, feet)
         t = C.c_int()
         check(lib().hsddp_extract_commands_async(
             self._h, int(nsteps_between_mpc), float(mpc_time), float(dt_mpc),
@@ -347,10 +366,11 @@ class Solver:
         """hsddp_shift_elements: contact_change [B][n_steps], each element's own flags; returns the
         per-element layouts afterwards (element_layouts)."""
         cc = np.ascontiguousarray(contact_change, dtype=np.int32).reshape(self.B, -1)
-        check(lib().hsddp_shift_elements(self._h, int(cc.shape[1]), ip(cc)))
+        rc = lib().hsddp_shift_elements(self._h, int(cc.shape[1]), ip(cc))
         lay = self.element_layouts()
         self.P = int(lay["n_phases"].max())
         self.S = self.Kc + self.P
+        check(rc)  # (a touchdown overflow is reported after the complete shift)
         return lay
 
     def _layout_arrays(self):
@@ -390,13 +410,15 @@ class Solver:
         """len(contact_change) simulation steps of HKDProblem::update on the device-held warm start;
         returns the new layout.  Call update_problem with inputs of that layout before solving."""
         cc = np.ascontiguousarray(np.asarray(contact_change, dtype=np.int32).reshape(-1))
-        check(lib().hsddp_shift(self._h, int(cc.size), ip(cc)))
+        rc = lib().hsddp_shift(self._h, int(cc.size), ip(cc))
         if self._follow_layout():  # per-element layouts
+            check(rc)
             return self.element_layouts()
         lay = self.layout()
         self.P = len(lay["horizons"])
         self.S = sum(n + 1 for n in lay["horizons"])
         self.Kc = sum(lay["horizons"])
+        check(rc)  # (a touchdown overflow is reported after the complete shift)
         return lay
 
     def update_problem(self, contacts, x0, ref_x=None, ref_u=None, ref_foot=None) -> None:
@@ -414,9 +436,12 @@ class Solver:
         new initial state (None: call update_problem(None, x0) next, e.g. with x0 formed from the
         new first phase's contact).  Returns the contact-change flag of every step."""
         flags = np.zeros(max(1, n_steps), np.int32)
-        check(lib().hsddp_advance(self._h, int(n_steps), float(plan_duration), float(dt_mpc),
-                                  None if x0 is None else dp(np.ascontiguousarray(x0, dtype=np.float64)), ip(flags)))
+        rc = lib().hsddp_advance(self._h, int(n_steps), float(plan_duration), float(dt_mpc),
+                                 None if x0 is None else dp(np.ascontiguousarray(x0, dtype=np.float64)), ip(flags))
+        # a touchdown overflow (HSDDP_ERR_UNSUPPORTED) is reported after a complete step: the layout
+        # is followed first
         self._follow_layout()
+        check(rc)
         return [int(f) for f in flags[:n_steps]]
 
     def phase_info(self) -> dict:

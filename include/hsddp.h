@@ -355,9 +355,15 @@ int hsddp_update_problem(hsddp_handle h, const int *contacts, const double *x0, 
  * (compute_hkd_state, HKDMPC.cpp:132-134) and call hsddp_update_problem(h, NULL, x0, NULL, NULL,
  * NULL), where NULL contacts are the ones derived here.  The caller's whole MPC tick is
  * hsddp_advance + hsddp_solve + hsddp_extract_commands (HKDMPCSolver::update, HKDMPC.cpp:96-165).
- * A phase that would carry more than HSDDP_MAX_TD touchdown constraints returns
- * HSDDP_ERR_UNSUPPORTED once the rest of the advance is done (the constraints past the limit are
- * not added), as hsddp_shift returns it after its shift. */
+ * A phase that would carry more than HSDDP_MAX_TD touchdown constraints keeps its first
+ * HSDDP_MAX_TD (the later ones are not registered) and the call returns HSDDP_ERR_UNSUPPORTED after
+ * the whole step, on either shift path: layout, references, contacts, x0, durations and clock are
+ * the new step's and the handle solves (hsddp_shift / hsddp_shift_elements return the same status
+ * after their shift).  The reference registers one constraint at every step a last phase has
+ * reached its end (HKDProblem.cpp:199-202); one step later the contact at the horizon end differs
+ * and a new phase starts, so with one reference sample per simulation step a phase carries at most
+ * two (its initial one and one on reaching its end) — the limit is only met by contact sequences
+ * that change faster than the simulation step (tests/test_gpu_td_overflow.py). */
 int hsddp_advance(hsddp_handle h, int n_steps, float plan_duration, float dt_mpc, const double *x0,
                   int *contact_change);
 /* The handle's phase bookkeeping: contacts [B][P+1][4] (row P: the last phase's next contact) and,
@@ -393,7 +399,8 @@ int hsddp_extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_ti
  * copy stream of their own, so the copy overlaps whatever the caller issues next (the next tick's
  * hsddp_advance / hsddp_solve).  ticket receives the buffer (0 or 1); hsddp_commands_wait(h,
  * ticket, &records) waits for that copy and points records at the buffer, which stays valid until
- * the extraction after next reuses it. */
+ * the extraction after next reuses it.  status_durations and foot_placements are read before the
+ * call returns (the caller may release them). */
 int hsddp_extract_commands_async(hsddp_handle h, int nsteps_between_mpc, double mpc_time, double dt_mpc,
                                  const double *status_durations, int durations_per_element,
                                  const float *foot_placements, int feet_per_element, float solve_time, int *ticket);

@@ -133,7 +133,8 @@ def td_bits(c, cn):
     return sum(1 << l for l in range(4) if c[l] == 0 and cn[l] == 1)
 
 
-def shift_constraints(horizons, reach_end, cons, contact_change, grf_delta, grf_eps, td_sigma, td_lambda):
+def shift_constraints(horizons, reach_end, cons, contact_change, grf_delta, grf_eps, td_sigma, td_lambda,
+                      cap=False):
     """HKDProblem::update (HKDProblem.cpp:117-222) on one element's constraint objects, which live on
     in the phases across MPC ticks (HKDProblem::update's reset_params is a no-op, ConstraintsBase.h:
     165-167, 341-348).  cons: reb_delta, reb_eps [Kc][20]; td_mask [P][MAX_TD]; al_sigma, al_lambda
@@ -143,13 +144,16 @@ def shift_constraints(horizons, reach_end, cons, contact_change, grf_delta, grf_
     from the initial ReB parameters and carries no touchdown constraint; at every step whose last
     phase has reached its end, add_tconstr_one_phase appends one more touchdown constraint with the
     initial AL parameters (HKDProblem.cpp:199-202) — its legs follow from the next contact rows
-    (TD_PENDING, resolve_td).  Returns the new cons."""
+    (TD_PENDING, resolve_td).  Returns the new cons.  cap: a phase holds at most MAX_TD constraints
+    and the later ones are not registered (the device's HSDDP_MAX_TD; "overflow" in the result says
+    whether one was dropped) — the reference's lists are unbounded, so without cap that is an error."""
     hz, re = list(horizons), list(reach_end)
     rd = split_phases(cons["reb_delta"], hz, False)
     rs = split_phases(cons["reb_eps"], hz, False)
     td = [list(zip([int(m) for m in cons["td_mask"][i]], [np.array(v) for v in cons["al_sigma"][i]],
                    [np.array(v) for v in cons["al_lambda"][i]])) for i in range(len(hz))]
     init_row = lambda v: np.full(20, v)  # noqa: E731
+    overflow = False
     for cc in contact_change:
         if hz[0] <= 1:
             for L in (hz, re, rd, rs, td):
@@ -169,13 +173,16 @@ def shift_constraints(horizons, reach_end, cons, contact_change, grf_delta, grf_
         if re[-1]:  # one more touchdown constraint on the last phase, in its first free slot
             slots = td[-1]
             j = next((q for q, s in enumerate(slots) if s[0] == 0), None)
+            if j is None and cap:
+                overflow = True
+                continue
             assert j is not None, "more than MAX_TD touchdown constraints on one phase"
             slots[j] = (TD_PENDING, np.full(4, td_sigma), np.full(4, td_lambda))
     flat = lambda L: np.array([r for ph in L for r in ph])  # noqa: E731
     return {"reb_delta": flat(rd), "reb_eps": flat(rs),
             "td_mask": np.array([[s[0] for s in ph] for ph in td], np.int32),
             "al_sigma": np.array([[s[1] for s in ph] for ph in td]),
-            "al_lambda": np.array([[s[2] for s in ph] for ph in td])}
+            "al_lambda": np.array([[s[2] for s in ph] for ph in td]), "overflow": overflow}
 
 
 def resolve_td(cons, contacts):

@@ -130,18 +130,20 @@ def test_shift_matches_oracle(steps):
     s.close()
 
 
-def test_mpc_loop_matches_oracle():
+@pytest.mark.parametrize("ms", [1, 0])
+def test_mpc_loop_matches_oracle(ms):
     """HKDMPCSolver::update's loop (HKDMPC.cpp:96-165): shift one step, new inputs with the warm
     start kept, re-solve with max_AL_iter = 2, max_DDP_iter = 1 (quirk A17) — including the
-    updates whose new last phase has no shooting states — against the oracle doing the same."""
+    updates whose new last phase has no shooting states — against the oracle doing the same; with
+    multiple (MS 1) and single (MS 0) shooting."""
     B, P, N = 8, 4, 5
     sc, prob = _scenario_batch(B, P, N)
-    s = hsddp.Solver(prob, hsddp.load_settings())
+    s = hsddp.Solver(prob, hsddp.load_settings(MS=ms))
     s.solve()
-    r = O.solve_batch(prob, O.default_options(), n_threads=8)
+    r = O.solve_batch(prob, O.default_options(MS=ms), n_threads=8)
     g = {**s.trajectory(), **s.working(), **s.element_info()}
     assert _rel(g["Xbar"], r["Xbar"]) < 1e-9
-    kw = dict(max_AL_iter=2, max_DDP_iter=1)
+    kw = dict(max_AL_iter=2, max_DDP_iter=1, MS=ms)
     s.set_options(hsddp.load_settings(**kw))
     tails = n_td = 0
     op, _ = O.default_problem(prob["horizons"], prob["dt"])  # the initial ReB / AL parameters

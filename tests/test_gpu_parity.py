@@ -221,14 +221,6 @@ def test_warm_start_round_trip():
     assert rel(g["Xbar"], r["Xbar"]) < 1e-9 and rel(g["K"], r["K"]) < 1e-9
 
 
-def test_single_shooting_rejected():
-    prob = syn.make_batch(2, 2, 5, "trot")
-    s = hsddp.Solver(prob, hsddp.load_settings(MS=0))
-    with pytest.raises(hsddp.HSDDPError, match="single shooting"):
-        s.solve()
-    s.close()
-
-
 def _stack(idx, P, N, gait):
     ps = [syn.make_batch(1, P, N, gait, first_element=i) for i in idx]
     q = dict(ps[0]); q["batch"] = len(idx)
