@@ -243,11 +243,11 @@ struct hsddp_handle_t {
     void *scratch = nullptr;    // device staging for the MPC-side calls (grown on demand)
     size_t scratch_bytes = 0;
     // receding-horizon state (HKDProblemData, HKDProblem.h:20-66): is_phase_reach_end per phase,
-    // state-slot capacity (a shift keeps Kc and may add phases), and the second Xbar / Ubar / K
-    // set the shift gathers into (allocated by the first shift)
+    // state-slot capacity (a shift keeps Kc and may add phases), and the second set of compact gain
+    // rows the shift gathers into (allocated by the first shift; the new Xbar / Ubar rows go to each
+    // element's third trajectory buffer)
     std::vector<int> reach_end;
     size_t S_cap = 0;
-    double *spare_Xbar = nullptr, *spare_Ubar = nullptr;
     void *spare_K = nullptr;
     // ... and of the constraint parameters the phases carry (ReB per knot, touchdown constraints)
     double *spare_reb_delta = nullptr, *spare_reb_eps = nullptr, *spare_al_sigma = nullptr, *spare_al_lambda = nullptr;
@@ -449,10 +449,11 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
     int *contacts; double *x0, *rx, *ru, *rf;
     int rc = 0;
     if ((rc = dalloc(h, contacts, B * (P + 1) * 4)) || (rc = dalloc(h, x0, B * NX)) || (rc = dalloc(h, rx, Br * S * NX)) ||
-        (rc = dalloc(h, ru, Br * S * NX)) || (rc = dalloc(h, rf, Br * S * 12)) || (rc = dalloc(h, d.Xb[0], B * S * NX)) ||
-        (rc = dalloc(h, d.Xb[1], B * S * NX)) || (rc = dalloc(h, d.Defect, B * S * NX)) || (rc = dalloc(h, d.sel, B)) ||
+        (rc = dalloc(h, ru, Br * S * NX)) || (rc = dalloc(h, rf, Br * S * 12)) || (rc = dalloc(h, d.X3, 3 * B * S * NX)) ||
+        (rc = dalloc(h, d.D3, 3 * B * S * NX)) || (rc = dalloc(h, d.U3, 3 * B * Kc * NX)) || (rc = dalloc(h, d.sel, B)) ||
+        (rc = dalloc(h, d.ovr_u, B * MOVR * 12)) ||
         (rc = dalloc(h, d.dX, B * S * NX)) ||
-        (rc = dalloc(h, d.Ub[0], B * Kc * NX)) || (rc = dalloc(h, d.Ub[1], B * Kc * NX)) || (rc = dalloc(h, d.dU, B * Kc * NX)) ||
+        (rc = dalloc(h, d.dU, B * Kc * NX)) ||
         (rc = dalloc(h, d.du, B * Kc * NX)) || (rc = dalloc(h, d.dbg, B * 16)) ||
         (p.fp32 ? ((rc = dalloc(h, d.K32, B * Kc * KCW)) || (rc = dalloc(h, d.lq32, B * Kc * LQW32)) ||
                    (rc = dalloc(h, d.def32, B * S * NX)))
@@ -468,6 +469,10 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         return rc;
     }
     d.contacts = contacts; d.x0 = x0; d.ref_x = rx; d.ref_u = ru; d.ref_foot = rf;
+    d.xs3 = B * S * NX;  // (S = S_cap here)
+    d.us3 = B * Kc * NX;
+    d.rows3 = (int)(B * S);
+    d.urows3 = (int)(B * Kc);
     {   // parallel regularisation retries: p.retry_m attempts for each of up to `cap` deferred elements
         // per launch (HSDDP_SEQUENTIAL_RETRY=1 keeps every retry inside k_riccati: a diagnostic for
         // tests).  Scratch per deferred element: M attempts x (Kc gain rows + Kc dU rows), 8.5 MB at the
@@ -724,9 +729,9 @@ extern "C" int hsddp_upload_problem(hsddp_handle h, const int *contacts, const d
     const size_t B = p.B, S = p.S, Br = h->Bref;
     // default warm start: Xbar = X = reference (HKDProblem.cpp:84-90), Ubar = U = 0, K = 0
     HIPCHK(hipMemsetAsync(h->d.sel, 0, B * sizeof(int), h->stream));  // nominal and working rows in buffer 0
-    if (Br == 1) launch_broadcast(h->d.Xb[0], h->d.ref_x, S * NX, B, h->stream);
-    else HIPCHK(hipMemcpyAsync(h->d.Xb[0], h->d.ref_x, B * S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
-    HIPCHK(hipMemsetAsync(h->d.Ub[0], 0, B * p.Kc * NX * sizeof(double), h->stream));
+    if (Br == 1) launch_broadcast(h->d.X3, h->d.ref_x, S * NX, B, h->stream);
+    else HIPCHK(hipMemcpyAsync(h->d.X3, h->d.ref_x, B * S * NX * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipMemsetAsync(h->d.U3, 0, B * p.Kc * NX * sizeof(double), h->stream));
     if (p.fp32) HIPCHK(hipMemsetAsync(h->d.K32, 0, B * p.Kc * KCW * sizeof(float), h->stream));
     else HIPCHK(hipMemsetAsync(h->d.K, 0, B * p.Kc * KCW * sizeof(double), h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -761,12 +766,10 @@ static int reset_working(hsddp_handle h, bool params)
     const Params &p = h->p;
     const size_t B = p.B, S = p.S, Kc = p.Kc;
     Bufs &d = h->d;
-    launch_normalize(p, d, h->stream);
-    HIPCHK(hipMemsetAsync(d.sel, 0, B * sizeof(int), h->stream));  // X = Xbar, U = Ubar: one buffer
+    launch_reset_working(p, d, h->stream);  // X = Xbar, U = Ubar (one buffer), Defect = 0
     HIPCHK(hipMemsetAsync(d.dX, 0, B * S * NX * sizeof(double), h->stream));
     HIPCHK(hipMemsetAsync(d.du, 0, B * Kc * NX * sizeof(double), h->stream));
     HIPCHK(hipMemsetAsync(d.dU, 0, B * Kc * NX * sizeof(double), h->stream));
-    HIPCHK(hipMemsetAsync(d.Defect, 0, B * S * NX * sizeof(double), h->stream));
     if (params) {
         launch_init_params(p, d, h->stream);
         h->reb_at_init = true;
@@ -790,8 +793,8 @@ extern "C" int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const
     Bufs &d = h->d;
     int rc;
     launch_normalize(p, d, h->stream);  // every element's nominal rows in buffer 0
-    if (Xbar && (rc = h2d(d.Xb[0], Xbar, B * S * NX * sizeof(double), h->stream))) return rc;
-    if (Ubar && (rc = h2d(d.Ub[0], Ubar, B * Kc * NX * sizeof(double), h->stream))) return rc;
+    if (Xbar && (rc = h2d(d.X3, Xbar, B * S * NX * sizeof(double), h->stream))) return rc;
+    if (Ubar && (rc = h2d(d.U3, Ubar, B * Kc * NX * sizeof(double), h->stream))) return rc;
     if (K) { // keep the 12 coupled rows of each knot's gain (KCW layout, hsddp_internal.h)
         std::vector<double> kc(B * Kc * KCW);
         for (size_t b = 0; b < B; ++b)
@@ -1218,7 +1221,7 @@ extern "C" int hsddp_download_trajectory(hsddp_handle h, double *Xbar, double *U
     int rc;
     launch_normalize(h->p, h->d, h->stream);  // nominal rows in buffer 0
     HIPCHK(hipStreamSynchronize(h->stream));
-    if ((rc = d2h(Xbar, h->d.Xb[0], B * S * NX * 8)) || (rc = d2h(Ubar, h->d.Ub[0], B * Kc * NX * 8)))
+    if ((rc = d2h(Xbar, h->d.X3, B * S * NX * 8)) || (rc = d2h(Ubar, h->d.U3, B * Kc * NX * 8)))
         return rc;
     if (K && h->need_inputs)
         return fail(HSDDP_ERR_ARG, "the layout changed (hsddp_shift): call hsddp_update_problem before downloading K");
@@ -1259,21 +1262,22 @@ extern "C" int hsddp_download_working(hsddp_handle h, double *X, double *U, doub
     HIPCHK(hipStreamSynchronize(h->stream));
     const size_t B = h->p.B, S = h->p.S, Kc = h->p.Kc;
     int rc;
-    if ((rc = d2h(Defect, h->d.Defect, B * S * NX * 8)) || (rc = d2h(dX, h->d.dX, B * S * NX * 8)) ||
-        (rc = d2h(dU, h->d.dU, B * Kc * NX * 8)))
+    if ((rc = d2h(dX, h->d.dX, B * S * NX * 8)) || (rc = d2h(dU, h->d.dU, B * Kc * NX * 8)))
         return rc;
-    if (X || U) {  // each element's working rows from the buffer sel names
+    if (X || U || Defect) {  // each element's working rows from the buffer sel names
         std::vector<int> sel(B);
         HIPCHK(hipMemcpy(sel.data(), h->d.sel, B * sizeof(int), hipMemcpyDeviceToHost));
-        for (int q = 0; q < 2; ++q) {
-            std::vector<double> xb(X ? B * S * NX : 0), ub(U ? B * Kc * NX : 0);
-            if ((rc = d2h(X ? xb.data() : nullptr, h->d.Xb[q], B * S * NX * 8)) ||
-                (rc = d2h(U ? ub.data() : nullptr, h->d.Ub[q], B * Kc * NX * 8)))
+        for (int q = 0; q < 3; ++q) {
+            std::vector<double> xb(X ? B * S * NX : 0), ub(U ? B * Kc * NX : 0), db(Defect ? B * S * NX : 0);
+            if ((rc = d2h(X ? xb.data() : nullptr, h->d.X3 + q * h->d.xs3, B * S * NX * 8)) ||
+                (rc = d2h(U ? ub.data() : nullptr, h->d.U3 + q * h->d.us3, B * Kc * NX * 8)) ||
+                (rc = d2h(Defect ? db.data() : nullptr, h->d.D3 + q * h->d.xs3, B * S * NX * 8)))
                 return rc;
             for (size_t b = 0; b < B; ++b) {
-                if (((sel[b] >> 1) & 1) != q) continue;
+                if (((sel[b] >> 2) & 3) != q) continue;
                 if (X) std::copy(xb.begin() + b * S * NX, xb.begin() + (b + 1) * S * NX, X + b * S * NX);
                 if (U) std::copy(ub.begin() + b * Kc * NX, ub.begin() + (b + 1) * Kc * NX, U + b * Kc * NX);
+                if (Defect) std::copy(db.begin() + b * S * NX, db.begin() + (b + 1) * S * NX, Defect + b * S * NX);
             }
         }
     }
@@ -1901,13 +1905,11 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     HIPCHK(hipSetDevice(h->desc.device));
     Bufs &d = h->d;
     int rc;
-    if (!h->spare_Xbar) {
-        double *sx, *su;
+    if (!h->spare_K) {  // (the new Xbar / Ubar rows go to each element's third buffer)
         void *sk;
-        if ((rc = dalloc(h, sx, B * h->S_cap * NX)) || (rc = dalloc(h, su, B * p.Kc * NX))) return rc;
         if (p.fp32) { float *k32; if ((rc = dalloc(h, k32, B * p.Kc * KCW))) return rc; sk = k32; }
         else { double *k64; if ((rc = dalloc(h, k64, B * p.Kc * KCW))) return rc; sk = k64; }
-        h->spare_Xbar = sx; h->spare_Ubar = su; h->spare_K = sk;
+        h->spare_K = sk;
     }
     if (!h->spare_reb_delta) {
         if ((rc = dalloc(h, h->spare_reb_delta, B * p.Kc * 20)) || (rc = dalloc(h, h->spare_reb_eps, B * p.Kc * 20)) ||
@@ -1945,21 +1947,18 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     a.map_id = nk > 1 ? did : nullptr;
     a.fp32 = p.fp32;
     a.zero_u0 = 1;  // trajectory_ptrs.front()->Ubar[0].setZero() (HKDProblem.cpp:219)
-    launch_shift_gather(p.B, a, d, h->spare_Xbar, h->spare_Ubar, h->spare_K, h->stream);
+    launch_shift_gather(p.B, a, d, h->spare_K, h->stream);  // (and sel: the third buffers)
     HIPCHK(hipGetLastError());
     // defer (hsddp_advance, one layout for the batch): the caller's host work runs under the gather;
     // everything after it is ordered on the handle's stream
     const bool async = defer && nk == 1;
     if (!async) HIPCHK(hipStreamSynchronize(h->stream));
-    std::swap(d.Xb[0], h->spare_Xbar);
-    std::swap(d.Ub[0], h->spare_Ubar);
     std::swap(d.reb_delta, h->spare_reb_delta);
     std::swap(d.reb_eps, h->spare_reb_eps);
     std::swap(d.al_sigma, h->spare_al_sigma);
     std::swap(d.al_lambda, h->spare_al_lambda);
     std::swap(d.td_mask, h->spare_td_mask);
     const bool td_overflow = !async && h->host_counter[6] != 0;
-    HIPCHK(hipMemsetAsync(d.sel, 0, B * sizeof(int), h->stream));  // the gathered warm start is buffer 0's
     if (p.fp32) { float *t = d.K32; d.K32 = (float *)h->spare_K; h->spare_K = t; }
     else { double *t = d.K; d.K = (double *)h->spare_K; h->spare_K = t; }
     // the new layouts

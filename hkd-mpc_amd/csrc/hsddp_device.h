@@ -81,9 +81,44 @@ DEV void knot_phase(const L_ &L, int kc, int &i, int &k)
     k = kc - L.k0(i);
 }
 
-// element b's nominal (Xbar / Ubar), working (X / U) and trial-target buffers (Bufs::sel)
-DEV int nom_buf(const Bufs &d, int b) { return d.sel[b] & 1; }
-DEV int work_buf(const Bufs &d, int b) { return (d.sel[b] >> 1) & 1; }
+// element b's nominal (Xbar / Ubar), working (X / U / Defect) and trial-target buffers (Bufs::sel)
+DEV int nom_buf(const Bufs &d, int b) { return d.sel[b] & 3; }
+DEV int work_buf(const Bufs &d, int b) { return (d.sel[b] >> 2) & 3; }
+DEV int trial_of(int nb, int wb) { return nb == wb ? (nb == 2 ? 0 : nb + 1) : 3 - nb - wb; }
+DEV int trial_buf(const Bufs &d, int b) { const int q = d.sel[b]; return trial_of(q & 3, (q >> 2) & 3); }
+DEV int sel_code(int nb, int wb) { return nb | (wb << 2); }
+// Bufs read in place from the kernel-argument segment, for kernels whose first two arguments are
+// (Params, Bufs): loads the compiler can repeat where a value is used, instead of keeping the
+// pointers live in scalar registers across the kernel (it spilled them to VGPR lanes)
+typedef const __attribute__((address_space(4))) Bufs KBufs;
+DEV KBufs *kbufs()
+{
+    constexpr size_t off = (sizeof(Params) + alignof(Bufs) - 1) / alignof(Bufs) * alignof(Bufs);
+    return (KBufs *)((const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr() + off);
+}
+DEV double *kxbuf(int q) { return kbufs()->X3 + (size_t)q * kbufs()->xs3; }
+DEV double *kdbuf(int q) { return kbufs()->D3 + (size_t)q * kbufs()->xs3; }
+DEV double *kubuf(int q) { return kbufs()->U3 + (size_t)q * kbufs()->us3; }
+
+// buffer q of the three-buffer sets (one allocation each: base + q x stride)
+DEV double *xbuf(const Bufs &d, int q) { return d.X3 + (size_t)q * d.xs3; }
+DEV double *dbuf(const Bufs &d, int q) { return d.D3 + (size_t)q * d.xs3; }
+DEV double *ubuf(const Bufs &d, int q) { return d.U3 + (size_t)q * d.us3; }
+
+// the control forces element b's stored GRF constraint values at control knot kc come from: the
+// older forces of an ElemState::ovr_kc entry (Bufs::ovr_u), or nullptr — the control row's own.
+// (A pointer, not a copy: the callers read a leg's three forces where they use them, so the
+// common case keeps no second force vector in registers.)
+DEV const double *constraint_forces(const Bufs &d, const ElemState &E, int b, int kc)
+{
+    const int n = E.ovr_n;
+    const double *o = nullptr;
+    for (int j = 0; j < n; ++j)
+        if (E.ovr_kc[j] == kc) o = d.ovr_u + ((size_t)b * MOVR + j) * 12;
+    return o;
+}
+// force a of leg lg for the GRF constraint rows: the control row's, or the older ones (ovr)
+DEV double grf_force(const double *u, const double *ovr, int i) { return ovr ? ovr[i] : u[i]; }
 
 DEV void load_contacts(const Bufs &d, const Params &p, int b, int i, int *c, int *cn)
 {
@@ -129,8 +164,10 @@ DEV double grf_value(double mu, int r, const double *f)
 
 // running cost l_k (tracking + foot regularisation + dt * ReB), and min(0, min g)
 DEV double running_cost(const Params &p, const int *c, const double *x, const double *u, const double *xr,
-                        const double *ur, const double *pf, const double *delta, const double *eps, double &viol)
+                        const double *ur, const double *pf, const double *delta, const double *eps, double &viol,
+                        const double *ovr = nullptr)
 {
+    // ovr: older control forces of the stored GRF constraint values (constraint_forces), else u's
     double lt = 0.0, lu = 0.0, lf = 0.0;
 #pragma unroll
     for (int j = 0; j < NX; ++j) { double e = x[j] - xr[j]; lt += e * q_diag(p, c, j) * e; }
@@ -159,9 +196,10 @@ DEV double running_cost(const Params &p, const int *c, const double *x, const do
             for (int lg = 0; lg < 4; ++lg) {
                 if (!c[lg]) continue;
                 double prod = 1.0, quad = 0.0;
+                const double f[3] = {grf_force(u, ovr, 3 * lg), grf_force(u, ovr, 3 * lg + 1), grf_force(u, ovr, 3 * lg + 2)};
 #pragma unroll
                 for (int r = 0; r < 5; ++r) {
-                    const double g = grf_value(p.mu, r, u + 3 * lg);
+                    const double g = grf_value(p.mu, r, f);
                     mk = fmin(mk, g);
                     const double t = (g - 2 * dl) * inv_dl;
                     prod *= g > dl ? g : 1.0;
@@ -173,9 +211,10 @@ DEV double running_cost(const Params &p, const int *c, const double *x, const do
 #pragma unroll
             for (int lg = 0; lg < 4; ++lg) {
                 if (!c[lg]) continue;
+                const double f[3] = {grf_force(u, ovr, 3 * lg), grf_force(u, ovr, 3 * lg + 1), grf_force(u, ovr, 3 * lg + 2)};
 #pragma unroll
                 for (int r = 0; r < 5; ++r) {
-                    double g = grf_value(p.mu, r, u + 3 * lg);
+                    double g = grf_value(p.mu, r, f);
                     mk = fmin(mk, g);
                     rc += eps[5 * lg + r] * reb_cost(g, delta[5 * lg + r], log(delta[5 * lg + r]));
                 }

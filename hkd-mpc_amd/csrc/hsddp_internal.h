@@ -1,8 +1,9 @@
 // hsddp_internal.h — device data layout and kernel interface of the batched HS-DDP solver.
 //
 // HBM layout (element-major, fp64; b = element, s = state slot, kc = control slot):
-//   Xb[2], Defect, dX                 [B][S][24]     Xb: the nominal Xbar and the working / trial X (sel)
-//   Ub[2], dU, du                     [B][Kc][24]     du = dU + K dX (linear-rollout control step)
+//   X3, D3 [3], dX                    [B][S][24]     X3: the nominal Xbar, the working X and the trial
+//                                                     rows (sel); D3: the Defect of each buffer's rows
+//   U3 [3], dU, du                    [B][Kc][24]     du = dU + K dX (linear-rollout control step)
 //   K                                 [B][Kc][12][24] row-major, coupled controls only (below)
 //   lq                                [B][Kc][LQW]    compact LQ model of one knot (below)
 //   term                              [B][P][TW]      Phix | Phixx | Px (reset-map Jacobian at X_i[N])
@@ -119,11 +120,21 @@ struct RetryEntry {
     double reg;
 };
 
+// Constraint values older than the working rows (a diverged trial, SinglePhase.cpp:205-208): the
+// rollout returns before compute_path_constraints at the knot whose simulated state breaks the
+// 1e6 bound, so the GRF constraint data of that knot keep the values of an earlier control row
+// while U[k] is the trial's.  Up to MOVR such knots per element, each with the control forces its
+// stored constraint values come from (Bufs::ovr_u); every later cost, LQ and ReB update there uses
+// them (ElemState::ovr_kc; ascending).  A rollout that passes a knot refreshes it.
+constexpr int MOVR = 8;
+
 struct ElemState {
     double cost, feas, merit, merit_rho, dV1, dV2, reg;
     double max_t, max_p, max_t_prev, max_p_prev, cost_prev, merit_prev, feas_prev;
     int done, inner_done, ls_active, accepted, status, iters, outer_iters, n_ls;
     int hist_n;  // entries pushed to the solver-info history (MultiPhaseDDP.cpp:277-280, 368-371)
+    int ovr_n;   // knots with older constraint values (MOVR)
+    int ovr_kc[MOVR];
 };
 
 struct Bufs {
@@ -131,11 +142,18 @@ struct Bufs {
     const double *x0;                      // [B][24]
     const double *ref_x, *ref_u, *ref_foot; // [Bref][S][24|24|12]
     // Trajectory::update_nominal_vals without copies: each element's nominal (Xbar, Ubar) and working
-    // (X, U) rows live in one of two buffers, sel[b] bit 0 = the nominal's, bit 1 = the working one's.
-    // A line-search trial writes the non-nominal buffer; accepting it flips both bits to it.
-    double *Xb[2], *Defect, *dX;
-    double *Ub[2], *dU, *du;
+    // (X, U, Defect) rows live in two of three buffers, sel[b] bits 0-1 = the nominal's index, bits
+    // 2-3 = the working one's.  A line-search trial writes the third (trial_buf: neither, so that a
+    // diverged trial can keep the working rows past its break); accepting it makes it the nominal
+    // and the working buffer, rejecting it the working one (quirk A2).
+    // One allocation per set, buffer q at q x the set's stride (xbuf / dbuf / ubuf): kernels hold one
+    // base pointer per set, not three.
+    double *X3, *D3, *dX;                  // X3, D3: [3][B][S_cap][24]
+    double *U3, *dU, *du;                  // U3: [3][B][Kc][24]
+    size_t xs3, us3;                       // set strides (doubles): B x S_cap x 24, B x Kc x 24
+    int rows3, urows3;                     // the same in rows: B x S_cap, B x Kc
     int *sel;                              // [B]
+    double *ovr_u;                         // [B][MOVR][12] control forces of ElemState::ovr_kc
     double *K, *lq, *term;
     double *reb_delta, *reb_eps, *al_sigma, *al_lambda, *term_h;
     int *td_mask;                          // [B][P][MTD] (0: no constraint in that slot)
@@ -172,6 +190,8 @@ void launch_rollout(const Params &p, const Bufs &d, double eps, int last, int in
 void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, int tix, hipStream_t st);
 // nominal rows of every element into buffer 0 (Bufs::sel bit 0 cleared), for host transfers
 void launch_normalize(const Params &p, const Bufs &d, hipStream_t st);
+// every element's working rows back at its nominal ones (sel), its Defect rows zero
+void launch_reset_working(const Params &p, const Bufs &d, hipStream_t st);
 void launch_lq(const Params &p, const Bufs &d, hipStream_t st);
 void launch_riccati(const Params &p, const Bufs &d, hipStream_t st);
 void launch_lin_rollout(const Params &p, const Bufs &d, hipStream_t st);

@@ -17,6 +17,8 @@
 //
 // Every element carries its own control-flow state (ElemState): regularisation retries, line-search
 // acceptance, early exits and AL/ReB updates are per-element masks, never lockstep.
+#include <cstdlib>
+
 #include "hsddp_device.h"
 
 namespace hsddp {
@@ -110,7 +112,7 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
     // X[N] and the terminal cost's other inputs, staged together (no memory round trip at the end)
     if (t < NX) {
-        sx[t] = d.Xb[work_buf(d, b)][((size_t)b * p.S + s) * NX + t];
+        sx[t] = xbuf(d, work_buf(d, b))[((size_t)b * p.S + s) * NX + t];
         sxr[t] = xr[t];
     }
     // the phase's touchdown constraints: AL parameters [slot][leg] (sigma, then lambda) and leg masks
@@ -276,9 +278,10 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
     }
 }
 
-// lu + ReB gradient / Hessian of one knot (SinglePhase.cpp:380-394)
-DEV void lq_lu_reb(const Params &p, const int *c, const double *u, const double *ur, const double *dl, const double *ep,
-                   double *lu, double *rb)
+// lu + ReB gradient / Hessian of one knot (SinglePhase.cpp:380-394); the GRF constraint values from
+// the control row's forces, or the older ones ovr (constraint_forces)
+DEV void lq_lu_reb(const Params &p, const int *c, const double *u, const double *ovr, const double *ur, const double *dl,
+                   const double *ep, double *lu, double *rb)
 {
 #pragma unroll
     for (int j = 0; j < NU; ++j) lu[j] = p.dt * r_diag(p, j) * (u[j] - ur[j]);
@@ -293,11 +296,12 @@ DEV void lq_lu_reb(const Params &p, const int *c, const double *u, const double 
         for (int lg = 0; lg < 4; ++lg) {
             if (!c[lg]) continue;
             double gu[3] = {0, 0, 0}, hu[6] = {0, 0, 0, 0, 0, 0};
+            const double f0 = grf_force(u, ovr, 3 * lg), f1 = grf_force(u, ovr, 3 * lg + 1), f2 = grf_force(u, ovr, 3 * lg + 2);
 #pragma unroll
             for (int r = 0; r < 5; ++r) {
                 double row[3], d1, d2;
                 grf_row(p.mu, r, row);
-                double g = row[0] * u[3 * lg] + row[1] * u[3 * lg + 1] + row[2] * u[3 * lg + 2];
+                double g = row[0] * f0 + row[1] * f1 + row[2] * f2;
                 const double dlr = U ? p.grf_delta : dl[5 * lg + r];
                 reb_derivs(g, dlr, U ? inv_du : 1.0 / dlr, d1, d2);
                 double e = U ? p.grf_eps : ep[5 * lg + r];
@@ -382,10 +386,10 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     load_contacts(d, p, b, i, c, cn);
     double x[NX];
     const int wb = work_buf(d, b);
-    const double *xg = d.Xb[wb] + ((size_t)b * p.S + s) * NX;
+    const double *xg = xbuf(d, wb) + ((size_t)b * p.S + s) * NX;
 #pragma unroll
     for (int j = 0; j < NX; ++j) x[j] = xg[j];
-    const double *dg = d.Defect + ((size_t)b * p.S + s) * NX;
+    const double *dg = dbuf(d, wb) + ((size_t)b * p.S + s) * NX;
     if (SLOTS) {  // |Defect|^2 (else the last rollout's, of this working trajectory)
         double fs = 0.0;
 #pragma unroll
@@ -402,14 +406,16 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     const int kc = L.k0(i) + k;
     sridx[w][lane] = (long)b * p.Kc + kc;
     double u[NU];
-    const double *ug = d.Ub[wb] + ((size_t)b * p.Kc + kc) * NU;
+    const double *ug = ubuf(d, wb) + ((size_t)b * p.Kc + kc) * NU;
 #pragma unroll
     for (int j = 0; j < NU; ++j) u[j] = ug[j];
+    // the forces of the knot's stored GRF constraint values (older ones after a diverged trial)
+    const double *ovr = constraint_forces(d, E, b, kc);
     const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
     const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
     if (SLOTS) {  // the running cost (else the last rollout's: same trajectory, same parameters)
         double viol;
-        d.slot_cost[(size_t)b * p.S + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
+        d.slot_cost[(size_t)b * p.S + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol, ovr);
     }
 
     // the record in the solver's Riccati precision (fp64, or fp32 in config C5's mode)
@@ -459,7 +465,7 @@ __global__ __launch_bounds__(256, FWD_MINB) void k_lq(Params p, Bufs d)
     }
     // lu + ReB gradient / Hessian (SinglePhase.cpp:380-394)
     double lu[NU], rb[24];
-    lq_lu_reb(p, c, u, ur, dl, ep, lu, rb);
+    lq_lu_reb(p, c, u, ovr, ur, dl, ep, lu, rb);
 #pragma unroll
     for (int j = 0; j < NU; ++j) put(LQ_LU + j, lu[j]);
 #pragma unroll
@@ -478,7 +484,7 @@ DEV void finish_defect(const Params &p, const Bufs &d, int b, int s, int k, cons
 {
     const size_t sb = (size_t)b * p.S;
     double nrm = 0.0, fs = 0.0;
-    double *Dg = d.Defect + (sb + s) * NX;
+    double *Dg = dbuf(d, trial_buf(d, b)) + (sb + s) * NX;
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
         nrm += xs[j] * xs[j];
@@ -552,10 +558,10 @@ constexpr int RW = 65;      // rows per wave: 64 slots and the one before
 
 // X_t = Xbar + eps dX for rows r0 .. r0 + RW - 1 of the [rows][24] state buffers into LDS; rows
 // of inactive elements are skipped, own rows (own(r)) are stored to the element's trial buffer
-// (buf[nom ^ 1], the nominal being buf[nom], nom = nomof(element))
-template <typename Act, typename Own, typename Nom>
-DEV void stage_trial(double *L, double *const *buf, const double *del, long r0, long nrows, int per, double eps,
-                     int lane, Act active, Own own, Nom nomof)
+// (selof(element): the element's Bufs::sel, nominal and working buffer indices)
+template <typename Act, typename Own, typename Sel>
+DEV void stage_trial(double *L, const Bufs &d, const double *del, long r0, long nrows, int per, double eps,
+                     int lane, Act active, Own own, Sel selof)
 {
     constexpr int CH = NX / 2;  // 16-byte chunks per row
 #pragma unroll 1
@@ -563,9 +569,9 @@ DEV void stage_trial(double *L, double *const *buf, const double *del, long r0, 
         const int row = f / CH, cc = 2 * (f % CH);
         const long r = r0 + row;
         if (r < 0 || r >= nrows || !active((int)(r / per))) continue;
-        const int nb = nomof((int)(r / per));
-        const double *bar = buf[nb];
-        double *out = buf[nb ^ 1];
+        const int q = selof((int)(r / per));
+        const double *bar = xbuf(d, q & 3);
+        double *out = xbuf(d, trial_of(q & 3, (q >> 2) & 3));
         typedef double d2 __attribute__((ext_vector_type(2)));
         const d2 xb = *(const d2 *)(bar + r * NX + cc), dx = *(const d2 *)(del + r * NX + cc);
         d2 v;
@@ -583,13 +589,13 @@ DEV void stage_trial(double *L, double *const *buf, const double *del, long r0, 
 // of an element starts from x0 or a reset map of its own rows), so it is skipped.  Rows of
 // inactive elements are read (in range, harmless) but neither staged nor stored.
 DEV void stage_trial2(double *L, const Bufs &d, long r0, long nrows, int per, double eps, int lane, long g0, int bA,
-                      bool aA, int nA, int bB, bool aB, int nB)
+                      bool aA, int nA, int tA, int bB, bool aB, int nB, int tB)
 {
     constexpr int CH = NX / 2, NIT = (RW * CH + 63) / 64;
     typedef double d2 __attribute__((ext_vector_type(2)));
-    // the two buffers by constant index (a runtime index into the kernel argument is a memory read)
-    const double *barA = nA ? d.Xb[1] : d.Xb[0], *barB = nB ? d.Xb[1] : d.Xb[0], *del = d.dX;
-    double *outA = nA ? d.Xb[0] : d.Xb[1], *outB = nB ? d.Xb[0] : d.Xb[1];
+    // the elements' nominal (read) and trial (written) buffers
+    const double *barA = kxbuf(nA), *barB = kxbuf(nB), *del = d.dX;
+    double *outA = kxbuf(tA), *outB = kxbuf(tB);
     d2 xb[NIT], dx[NIT];
     long rr[NIT];
     bool use[NIT];
@@ -603,8 +609,7 @@ DEV void stage_trial2(double *L, const Bufs &d, long r0, long nrows, int per, do
         const bool first = eb == bA;
         use[it] = in && (first ? aA : eb == bB && aB);
         rr[it] = rc;
-        const double *bar = first ? barA : barB;
-        xb[it] = *(const d2 *)(bar + rc * NX + cc);
+        xb[it] = *(const d2 *)((first ? barA : barB) + rc * NX + cc);
         dx[it] = *(const d2 *)(del + rc * NX + cc);
     }
 #pragma unroll
@@ -666,7 +671,7 @@ DEV void rollout_boundary(const Params &p, const Bufs &d, double eps, int init, 
     const auto L = layout_of<EL>(d, b);
     if (i >= L.P()) return;
     const int nb = nom_buf(d, b), s0 = L.s0(i), sN = s0 + L.N(i);
-    const double *Xbar = d.Xb[nb];
+    const double *Xbar = xbuf(d, nb);
     const size_t sb = (size_t)b * p.S;
     // trial rows X = Xbar + eps dX (the slot waves' expression: the same values)
     auto trial = [&](int s, double *x) {
@@ -690,7 +695,9 @@ DEV void rollout_boundary(const Params &p, const Bufs &d, double eps, int init, 
     finish_terminal(p, d, b, sN, i, c, cn, x);
 }
 
-template <bool EL>
+// WIDE: p.S >= RW (instantiated apart: a wave's 64 slots then belong to at most two elements, and
+// the kernel carries only that staging path)
+template <bool EL, bool WIDE>
 DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
 {
     __shared__ double Xt[RW * RS];
@@ -710,8 +717,11 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
     for (int b = bA + 1; b < bB && !any; ++b) any = act(b);
     if (!any) return;
     auto active = [&](int b) { return b == bA ? aA : b == bB ? aB : act(b); };
-    const int nA = nom_buf(d, bA), nB = nom_buf(d, bB);
-    auto nomof = [&](int b) { return b == bA ? nA : b == bB ? nB : nom_buf(d, b); };
+    const int qA = d.sel[bA], qB = d.sel[bB];
+    const int nA = qA & 3, nB = qB & 3, tA = trial_of(nA, (qA >> 2) & 3), tB = trial_of(nB, (qB >> 2) & 3);
+    auto selof = [&](int b) { return b == bA ? qA : b == bB ? qB : d.sel[b]; };
+    auto nomof = [&](int b) { return selof(b) & 3; };
+    auto trialof = [&](int b) { const int q = selof(b); return trial_of(q & 3, (q >> 2) & 3); };
     // the control row before the wave's first slot (that slot's u_prev; every other slot takes its
     // u_prev from the previous lane): lanes 0..11 load it with the state rows, stage it after them
     typedef double d2 __attribute__((ext_vector_type(2)));
@@ -726,15 +736,15 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
         up0 = aA && s0 < L0.S() && k0 > 0 && lane < NU / 2;
         if (up0) {
             const long r = (long)bA * p.Kc + s0 - i0 - 1;
-            ua = ((const d2 *)(d.Ub[nA] + r * NU))[lane];
+            ua = ((const d2 *)(kubuf(nA) + r * NU))[lane];
             ue = ((const d2 *)(d.du + r * NU))[lane];
         }
     }
     const long xr0 = g0 - 1;
-    if (p.S >= RW)
-        stage_trial2(Xt, d, xr0, total, p.S, eps, lane, g0, bA, aA, nA, bB, aB, nB);
+    if constexpr (WIDE)
+        stage_trial2(Xt, d, xr0, total, p.S, eps, lane, g0, bA, aA, nA, tA, bB, aB, nB, tB);
     else
-        stage_trial(Xt, d.Xb, d.dX, xr0, total, p.S, eps, lane, active, [&](long r) { return r >= g0; }, nomof);
+        stage_trial(Xt, d, d.dX, xr0, total, p.S, eps, lane, active, [&](long r) { return r >= g0; }, selof);
     if (up0) {
         Up0[2 * lane] = ua.x + eps * ue.x;
         Up0[2 * lane + 1] = ua.y + eps * ue.y;
@@ -751,15 +761,15 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     const double *x = Xt + (gc - xr0) * RS;
-    const int nb = nomof(b);
+    const int nb = nomof(b), tb = trialof(b);
     const long kq = (long)b * p.Kc + s - i;  // the slot's control row (k < N)
     const long kqmax = (long)p.B * p.Kc - 1;
     // the trial control row of the slot (k < N; the terminal slot's row index is clamped and unused)
     double u[NU];
-    trial_row(d, d.Ub[nb], kq < kqmax ? kq : kqmax, eps, u);
+    trial_row(d, kubuf(nb), kq < kqmax ? kq : kqmax, eps, u);
     // the running cost of a control slot (the terminal cost at k = N: the boundary waves)
     if (mine && k < L.N(i)) {
-        d2 *ug = (d2 *)(d.Ub[nb ^ 1] + kq * NU);
+        d2 *ug = (d2 *)(kubuf(tb) + kq * NU);
 #if HSDDP_RO_EXP == 2
         if (u[0] == 12345.678)
 #endif
@@ -806,6 +816,8 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
         wave_sync();
     }
     wflag[lane] = wr;
+    const int rsplit = (int)((long)bB * p.S - g0);  // (WIDE) rows from here on are element bB's
+    double *const DtA = kdbuf(tA), *const DtB = kdbuf(tB);
     wave_sync();
     typedef double d2 __attribute__((ext_vector_type(2)));
     constexpr int CH = NX / 2;
@@ -814,7 +826,12 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
         const int row = f / CH, cc = 2 * (f % CH);
         if (wflag[row]) {
             const double *src = Xt + (row + 1) * RS + cc;
-            *(d2 *)(d.Defect + (g0 + row) * NX + cc) = d2{src[0], src[1]};
+            // the row's element's trial buffer (bA below rsplit, bB from it; horizons shorter than a
+            // wave: the row's own element)
+            double *Dt;
+            if constexpr (WIDE) Dt = row >= rsplit ? DtB : DtA;
+            else Dt = kdbuf(trialof((int)((g0 + row) / p.S)));
+            *(d2 *)(Dt + (g0 + row) * NX + cc) = d2{src[0], src[1]};
         }
     }
 }
@@ -834,9 +851,9 @@ __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double ep
     if (!(init ? !E.done : E.ls_active != 0)) return;
     const size_t sb = (size_t)b * p.S, kb = (size_t)b * p.Kc;
     const auto L = layout_of<EL>(d, b);
-    const int nb = nom_buf(d, b);
-    const double *Xbar = d.Xb[nb], *Ubar = d.Ub[nb];
-    double *X = d.Xb[nb ^ 1], *U = d.Ub[nb ^ 1];  // the trial's rows (k_rollout wrote the shooting ones)
+    const int nb = nom_buf(d, b), tb = trial_buf(d, b);
+    const double *Xbar = xbuf(d, nb), *Ubar = ubuf(d, nb);
+    double *X = xbuf(d, tb), *U = ubuf(d, tb);  // the trial's rows (k_rollout wrote the shooting ones)
     for (int i = 0; i < L.P(); ++i) {
         const int N = L.N(i), ss = L.ss(i), s0 = L.s0(i), k0 = L.k0(i);
         if (ss >= N + 1) continue;
@@ -901,9 +918,9 @@ DEV void ss_phase(const Params &p, const Bufs &d, int b, int i, double eps, cons
 {
     const auto L = layout_of<EL>(d, b);
     const size_t sb = (size_t)b * p.S, kb = (size_t)b * p.Kc;
-    const int nb = nom_buf(d, b);
-    const double *Xbar = d.Xb[nb], *Ubar = d.Ub[nb];
-    double *X = d.Xb[nb ^ 1], *U = d.Ub[nb ^ 1];
+    const int nb = nom_buf(d, b), tb = trial_buf(d, b);
+    const double *Xbar = xbuf(d, nb), *Ubar = ubuf(d, nb);
+    double *X = xbuf(d, tb), *U = ubuf(d, tb);
     const int N = L.N(i), s0 = L.s0(i), k0 = L.k0(i);
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
@@ -962,8 +979,8 @@ __global__ __launch_bounds__(64) void k_rollout_ss(Params p, Bufs d, double eps,
     if (!mine) return;
     const auto L = layout_of<EL>(d, b);
     const size_t sb = (size_t)b * p.S;
-    const int nb = nom_buf(d, b), s0 = L.s0(i);
-    const double *X = d.Xb[nb ^ 1];
+    const int s0 = L.s0(i);
+    const double *X = xbuf(d, trial_buf(d, b));
     double xi[NX];
     if (i == 0) {
         for (int j = 0; j < NX; ++j) xi[j] = d.x0[(size_t)b * NX + j];
@@ -981,10 +998,98 @@ __global__ __launch_bounds__(64) void k_rollout_ss(Params p, Bufs d, double eps,
     }
 }
 
+// A trial whose rollout breaks the 1e6 bound (SinglePhase::hybrid_rollout, SinglePhase.cpp:205-208)
+// first at state slot sbrk (= s0_i + k + 1: the state simulated from knot k of phase i): the
+// reference returns there and skips every later phase (MultiPhaseDDP.cpp:83-87), so X past the
+// break state, U past knot k and the Defect of phase i on keep the working rows of before the
+// trial, the GRF constraint values of knot k stay those of its earlier control row, and the cost
+// and feasibility that follow (:116-117) are sums over those mixed rows.  The slot kernels computed
+// every slot; here the element's 16 lanes (g) copy the working rows the reference keeps into the
+// trial buffer, record the break knot's older constraint forces (ElemState::ovr_kc), and recompute
+// the slot outputs from the break knot on.  No cross-lane operation (the caller's lanes diverge).
+template <bool EL>
+DEV void diverged_fixup(const Params &p, const Bufs &d, const LayT<EL> &L, int b, int g, int sbrk)
+{
+    int i, ks;
+    slot_phase(L, sbrk, i, ks);
+    const int kb = ks - 1, s0 = L.s0(i), kcb = L.k0(i) + kb, sbb = s0 + kb, S = L.S();
+    const int q = d.sel[b], nb = q & 3, wb = (q >> 2) & 3, tb = trial_of(nb, wb);
+    const size_t sb = (size_t)b * p.S, kq = (size_t)b * p.Kc;
+    double *XT = xbuf(d, tb), *UT = ubuf(d, tb), *DT = dbuf(d, tb);
+    const double *XW = xbuf(d, wb), *UW = ubuf(d, wb), *DW = dbuf(d, wb);
+    for (long e = g; e < (long)(S - sbrk) * NX; e += 16) XT[(sb + sbrk) * NX + e] = XW[(sb + sbrk) * NX + e];
+    for (long e = g; e < (long)(p.Kc - kcb - 1) * NX; e += 16) UT[(kq + kcb + 1) * NX + e] = UW[(kq + kcb + 1) * NX + e];
+    for (long e = g; e < (long)(S - s0) * NX; e += 16) DT[(sb + s0) * NX + e] = DW[(sb + s0) * NX + e];
+    int c[4], cn[4];
+    load_contacts(d, p, b, i, c, cn);
+    ElemState &E = d.el[b];
+    if (g == 0) {
+        // knots before the break were passed (their constraint values are the trial's): dropped;
+        // the break knot keeps an entry it has, or gets one with its working control forces
+        int n = 0;
+        bool have = false;
+        for (int j = 0; j < E.ovr_n; ++j) {
+            const int kc = E.ovr_kc[j];
+            if (kc < kcb) continue;
+            have = have || kc == kcb;
+            if (n != j) {
+                E.ovr_kc[n] = kc;
+                for (int r = 0; r < 12; ++r) d.ovr_u[((size_t)b * MOVR + n) * 12 + r] = d.ovr_u[((size_t)b * MOVR + j) * 12 + r];
+            }
+            ++n;
+        }
+        if (!have && (c[0] + c[1] + c[2] + c[3]) > 0) {  // (a phase without stance legs has no GRF rows)
+            if (n == MOVR) {  // more knots with older constraint values than the table holds
+                E.status = 2; E.done = 1; E.ls_active = 0;
+            } else {
+                E.ovr_kc[n] = kcb;
+                for (int r = 0; r < 12; ++r) d.ovr_u[((size_t)b * MOVR + n) * 12 + r] = UW[(kq + kcb) * NX + r];
+                ++n;
+            }
+        }
+        E.ovr_n = n;
+    }
+    __threadfence();  // rows and table visible to the other lanes of the element
+    // slot outputs over the mixed rows: |Defect|^2 of phase i on, costs from the break knot on
+    int ip = i;
+#pragma unroll 1
+    for (int s = s0 + g; s < S; s += 16) {
+        while (ip + 1 < L.P() && s >= L.s0(ip + 1)) ++ip;
+        const int k = s - L.s0(ip);
+        const double *dr = DT + (sb + s) * NX;
+        double fs = 0.0;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) fs += dr[j] * dr[j];
+        d.slot_feas[sb + s] = fs;
+        d.slot_div[sb + s] = 0;
+        if (s < sbb) continue;
+        load_contacts(d, p, b, ip, c, cn);
+        // (rows read in place, not staged in registers: this rare path stays light on the decide
+        // kernel's registers; the arithmetic is the slot kernels')
+        const double *x = XT + (sb + s) * NX;
+        if (k == L.N(ip)) {
+            finish_terminal(p, d, b, s, ip, c, cn, x);
+            continue;
+        }
+        const int kc = L.k0(ip) + k;
+        const double *u = UT + (kq + kc) * NU;
+        const double *ovr = constraint_forces(d, E, b, kc);
+        const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
+        const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
+        const double *dl = d.reb_delta + (kq + kc) * 20, *ep = d.reb_eps + (kq + kc) * 20;
+        double viol;
+        d.slot_cost[sb + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol, ovr);
+        d.slot_viol[sb + s] = viol;
+    }
+}
+
 // k_decide: reductions of one trial + merit acceptance (MultiPhaseDDP.cpp:113-133) + the
 // later-termination test (:358).  16 lanes per element, one per phase: each lane sums its phase's
 // slots in order, and the phase sums are added in phase order — the reference's summation order
-// (compute_cost, MultiPhaseDDP.cpp:431-440; SinglePhase.cpp:235-262).
+// (compute_cost, MultiPhaseDDP.cpp:431-440; SinglePhase.cpp:235-262).  A trial whose rollout broke
+// the 1e6 bound (slot_div) is rejected after its rows and slot outputs are made the reference's
+// mixed ones (diverged_fixup); max_tconstr / max_pconstr then cover the phases before the break
+// only (MultiPhaseDDP.cpp:83-92).
 template <bool EL>
 DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int init, int tix, int group)
 {
@@ -995,9 +1100,12 @@ DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int 
     const bool act = valid && (init ? !Ep->done : Ep->ls_active);
     const auto L = layout_of<EL>(d, valid ? b : 0);
     const int P = L.P();
+    constexpr int NONE = 0x7fffffff;
     double ci = 0.0, fi = 0.0, pv = 0.0, tv = 0.0;
-    int div = 0;
-    if (act && g < P) {
+    int kd = NONE;  // first knot of the lane's phase whose simulated state breaks the bound
+    auto sums = [&]() {
+        ci = 0.0; fi = 0.0; pv = 0.0; tv = 0.0;
+        if (!(act && g < P)) return;
         const size_t sb = (size_t)b * p.S + L.s0(g);
         const int N = L.N(g);
         // one pass, unrolled so that the loads of several slots are in flight together (each sum
@@ -1007,27 +1115,44 @@ DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int 
             ci += d.slot_cost[sb + k];
             pv = fmin(pv, d.slot_viol[sb + k]);
             fi += d.slot_feas[sb + k];
-            div |= d.slot_div[sb + k];
+            kd = (d.slot_div[sb + k] && k < kd) ? k : kd;
         }
         ci += d.slot_cost[sb + N];
         fi += d.slot_feas[sb + N];
-        div |= d.slot_div[sb + N];
+        kd = (d.slot_div[sb + N] && N < kd) ? N : kd;
         tv = d.slot_viol[sb + N];
-    }
+    };
+    sums();
     double cost = 0.0, feas = 0.0, max_p = 0.0, max_t = 0.0;
-    int dv = 0;
+    int sbrk = NONE;  // the element's first breaking slot
+    for (int i = 0; i < p.P; ++i)
+        sbrk = min(sbrk, __shfl(kd < NONE && g < P ? L.s0(g) + kd : NONE, base + i));
+    const bool dvg = act && sbrk < NONE;
+    int ibrk = NONE;
+    if (__builtin_amdgcn_ballot_w64(dvg)) {  // (wave-uniform: the lanes of other elements repeat their sums)
+        if (dvg) diverged_fixup<EL>(p, d, L, b, g, sbrk);
+        __threadfence();
+        kd = NONE;
+        sums();
+        if (dvg) {
+            int ks;
+            slot_phase(L, sbrk, ibrk, ks);
+            if (g >= ibrk) { pv = 0.0; tv = 0.0; }  // phases from the break on: not reached
+        }
+    }
     for (int i = 0; i < p.P; ++i) {  // uniform bound (lanes g >= P add exact zeros)
         cost += __shfl(ci, base + i);
         feas += __shfl(fi, base + i);
         max_p = fmin(max_p, __shfl(pv, base + i));
         max_t = fmax(max_t, __shfl(tv, base + i));
-        dv |= __shfl(div, base + i);
     }
     if (!act || g != 0) return;
     ElemState &E = d.el[b];
     feas = sqrt(feas);
     E.max_p = max_p;
     E.max_t = max_t;
+    // a rollout that passed every knot refreshed every constraint value
+    if (!dvg && E.ovr_n) E.ovr_n = 0;
     // one entry of the solver-info buffers (cost_buffer, dyn_feas_buffer, eqn_feas_buffer,
     // ineq_feas_buffer; MultiPhaseDDP.cpp:277-280, 368-371), float as the reference's vectors
     auto push_info = [&]() {
@@ -1037,9 +1162,9 @@ DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int 
         }
         E.hist_n += 1;
     };
-    const int nb = d.sel[b] & 1;
+    const int q = d.sel[b], nb = q & 3, tb = trial_of(nb, (q >> 2) & 3);
     if (init) {  // the initial rollout is taken (update_nominal_trajectory, MultiPhaseDDP.cpp:258)
-        d.sel[b] = (nb ^ 1) * 3;
+        d.sel[b] = sel_code(tb, tb);
         E.cost = cost; E.feas = feas; E.accepted = 1;
         push_info();  // the initial information (:277-280)
         return;
@@ -1050,14 +1175,17 @@ DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int 
     const double exp_merit = exp_cost - eps * E.merit_rho * E.feas_prev;
     E.cost = cost; E.feas = feas; E.merit = merit;
     bool fin = false;
-    if ((merit <= E.merit_prev + p.gamma * exp_merit) && !dv) {
+    if ((merit <= E.merit_prev + p.gamma * exp_merit) && !dvg) {
         E.accepted = 1; E.ls_active = 0; fin = true;
-        d.sel[b] = (nb ^ 1) * 3;  // the trial becomes the nominal and the working trajectory
-    } else if (last) {
-        E.accepted = 0; E.ls_active = 0; E.cost = E.cost_prev; E.merit = E.merit_prev; fin = true;
-        d.sel[b] = nb | ((nb ^ 1) << 1);  // quirk A2: the last trial stays the working trajectory
+        d.sel[b] = sel_code(tb, tb);  // the trial becomes the nominal and the working trajectory
+    } else {
+        // the trial's rows are the working ones (the reference's X): the next trial writes the
+        // third buffer, and after the last one they stay (quirk A2)
+        d.sel[b] = sel_code(nb, tb);
+        if (last) { E.accepted = 0; E.ls_active = 0; E.cost = E.cost_prev; E.merit = E.merit_prev; fin = true; }
     }
-    if (!fin && tix >= 0 && tix < LS_LIVE) d.ls_live[tix] = 1;  // still searching (same value from every writer)
+    if (E.done) fin = false;  // (the constraint-value table overflowed: status 2)
+    if (!fin && !E.done && tix >= 0 && tix < LS_LIVE) d.ls_live[tix] = 1;  // still searching (same value from every writer)
     if (fin) {
         // the later-termination test breaks before the iteration's entry is buffered (:358-371)
         if (!p.no_early_exit && fabs((E.cost_prev - E.cost) / E.cost_prev) < p.cost_thresh && E.feas <= p.feas_thresh)
@@ -1067,8 +1195,10 @@ DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int 
     }
 }
 
+// (six waves per SIMD as before the divergence path: that rare path spills instead)
 template <bool EL>
-__global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int last, int init, int tix)
+__global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int last,
+                                                                                         int init, int tix)
 {
     if (ls_skip(d, tix)) return;
     decide_group<EL>(p, d, eps, last, init, tix, blockIdx.x);
@@ -1079,12 +1209,12 @@ __global__ __launch_bounds__(64) void k_decide(Params p, Bufs d, double eps, int
 // every block publishes its slot outputs (device-scope release) and takes a ticket; the block
 // holding the last ticket (acquire) runs k_decide's work for the batch, four elements at a time,
 // and resets the ticket counter.  One launch less per trial on the latency path of C1.
-template <bool EL, bool FUSE>
+template <bool EL, bool FUSE, bool WIDE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOUT_WAVES))) void k_rollout(
     Params p, Bufs d, double eps, int init, int tix, int last)
 {
     if (ls_skip(d, tix)) return;
-    rollout_block<EL>(p, d, eps, init);
+    rollout_block<EL, WIDE>(p, d, eps, init);
     if constexpr (FUSE) {
         __shared__ int ticket;
         __threadfence();
@@ -1101,32 +1231,51 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
 // Bufs::sel: the accepted trial's buffer becomes the nominal one, no rows are copied.  (Defect_bar
 // is never read by the solver, MultiPhaseDDP.cpp / SinglePhase.cpp, and is not kept.)
 
-// one element's nominal rows into buffer 0 (a swap of the two buffers where sel says buffer 1):
-// host downloads and uploads see Xbar / Ubar in buffer 0; sel is fixed up by k_normalize_sel
+// one element's nominal rows into buffer 0 (a swap of buffer 0 with the nominal's, rows of X, U and
+// Defect): host downloads and uploads see Xbar / Ubar in buffer 0; sel is fixed up by k_normalize_sel
 __global__ __launch_bounds__(256) void k_normalize(Params p, Bufs d)
 {
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long per = (long)p.S * (NX / 2);
     if (gid >= (long)p.B * per) return;
     const int b = (int)(gid / per);
-    if (!(d.sel[b] & 1)) return;
-    double2 *x0 = reinterpret_cast<double2 *>(d.Xb[0]), *x1 = reinterpret_cast<double2 *>(d.Xb[1]);
-    const double2 t = x0[gid];
-    x0[gid] = x1[gid];
-    x1[gid] = t;
+    const int nb = nom_buf(d, b);
+    if (nb == 0) return;
+    auto swap2 = [&](double *a0, double *a1, long at) {
+        double2 *x0 = reinterpret_cast<double2 *>(a0), *x1 = reinterpret_cast<double2 *>(a1);
+        const double2 t = x0[at];
+        x0[at] = x1[at];
+        x1[at] = t;
+    };
+    swap2(xbuf(d, 0), xbuf(d, nb), gid);
+    swap2(dbuf(d, 0), dbuf(d, nb), gid);
     const long r = gid % per;
-    if (r < (long)p.Kc * (NU / 2)) {
-        const long ug = (long)b * p.Kc * (NU / 2) + r;
-        double2 *u0 = reinterpret_cast<double2 *>(d.Ub[0]), *u1 = reinterpret_cast<double2 *>(d.Ub[1]);
-        const double2 v = u0[ug];
-        u0[ug] = u1[ug];
-        u1[ug] = v;
-    }
+    if (r < (long)p.Kc * (NU / 2)) swap2(ubuf(d, 0), ubuf(d, nb), (long)b * p.Kc * (NU / 2) + r);
 }
 __global__ void k_normalize_sel(Params p, Bufs d)
 {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < p.B && (d.sel[b] & 1)) d.sel[b] ^= 3;  // nominal now in 0, the working one moved with it
+    if (b >= p.B) return;
+    const int nb = nom_buf(d, b), wb = work_buf(d, b);
+    if (nb == 0) return;
+    // nominal now in 0; buffers 0 and nb traded their rows, the working index follows its rows
+    d.sel[b] = sel_code(0, wb == nb ? 0 : wb == 0 ? nb : wb);
+}
+
+// the working trajectory back at the nominal one (X = Xbar, U = Ubar) with a zero Defect, rows left
+// where they are: first the nominal buffer's Defect rows are zeroed (k_reset_defect), then the
+// working index follows the nominal (k_reset_sel)
+__global__ __launch_bounds__(256) void k_reset_defect(Params p, Bufs d)
+{
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long per = (long)p.S * (NX / 2);
+    if (gid >= (long)p.B * per) return;
+    reinterpret_cast<double2 *>(dbuf(d, nom_buf(d, (int)(gid / per))))[gid] = double2{0.0, 0.0};
+}
+__global__ void k_reset_sel(Params p, Bufs d)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < p.B) d.sel[b] = sel_code(nom_buf(d, b), nom_buf(d, b));
 }
 
 __global__ void k_outer_begin(Params p, Bufs d)
@@ -1156,12 +1305,17 @@ __global__ __launch_bounds__(256) void k_reb_update(Params p, Bufs d)
         if (kc >= L.k0(j)) i = j;
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
-    const double *u = d.Ub[work_buf(d, b)] + gid * NU;
+    const double *u = ubuf(d, work_buf(d, b)) + gid * NU;
+    // the knot's stored GRF constraint values: from the control row, or older forces
+    const double *ovr = constraint_forces(d, d.el[b], b, kc);
     double *dl = d.reb_delta + gid * 20, *ep = d.reb_eps + gid * 20;
+#pragma unroll
     for (int l = 0; l < 4; ++l) {
         if (!c[l]) continue;
+#pragma unroll
         for (int r = 0; r < 5; ++r) {
-            double g = grf_value(p.mu, r, u + 3 * l);
+            const double f[3] = {grf_force(u, ovr, 3 * l), grf_force(u, ovr, 3 * l + 1), grf_force(u, ovr, 3 * l + 2)};
+            double g = grf_value(p.mu, r, f);
             if (g > -p.pconstr_thresh) continue;
             ep[5 * l + r] *= p.update_ReB;
             dl[5 * l + r] *= p.update_relax;
@@ -1510,8 +1664,15 @@ static inline unsigned blocks_for(long n, int bs) { return (unsigned)((n + bs - 
         else hipLaunchKernelGGL(kern<false>, grid, block, 0, st, __VA_ARGS__);                      \
     } while (0)
 
-// small batches without non-shooting tails decide each trial in its rollout launch (k_rollout FUSE)
-static bool fused_decide(const Params &p) { return p.B <= 16 && !p.has_tail && !p.ms0; }
+// small batches without non-shooting tails decide each trial in its rollout launch (k_rollout FUSE);
+// HSDDP_NO_FUSED_DECIDE=1 (read at every launch: a test switches it in-process) keeps k_decide's
+// launch, for the equality test of the two paths
+static bool fused_decide(const Params &p)
+{
+    if (p.B > 16 || p.has_tail || p.ms0) return false;
+    const char *e = std::getenv("HSDDP_NO_FUSED_DECIDE");
+    return !(e && *e && *e != '0');
+}
 
 void launch_rollout(const Params &p, const Bufs &d, double eps, int last, int init, int tix, hipStream_t st)
 {
@@ -1521,13 +1682,24 @@ void launch_rollout(const Params &p, const Bufs &d, double eps, int last, int in
     }
     // slot waves, then the phase-boundary waves (k_rollout, rollout_boundary)
     const dim3 g(blocks_for((long)p.B * p.S, 64) + blocks_for((long)p.B * p.P, 64));
+    const bool wide = p.S >= RW;  // (rollout_block)
     if (fused_decide(p)) {
-        if (p.elem_layout) hipLaunchKernelGGL((k_rollout<true, true>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
-        else hipLaunchKernelGGL((k_rollout<false, true>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+        if (p.elem_layout) {
+            if (wide) hipLaunchKernelGGL((k_rollout<true, true, true>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+            else hipLaunchKernelGGL((k_rollout<true, true, false>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+        } else {
+            if (wide) hipLaunchKernelGGL((k_rollout<false, true, true>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+            else hipLaunchKernelGGL((k_rollout<false, true, false>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+        }
         return;
     }
-    if (p.elem_layout) hipLaunchKernelGGL((k_rollout<true, false>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
-    else hipLaunchKernelGGL((k_rollout<false, false>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+    if (p.elem_layout) {
+        if (wide) hipLaunchKernelGGL((k_rollout<true, false, true>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+        else hipLaunchKernelGGL((k_rollout<true, false, false>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+    } else {
+        if (wide) hipLaunchKernelGGL((k_rollout<false, false, true>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+        else hipLaunchKernelGGL((k_rollout<false, false, false>), g, dim3(64), 0, st, p, d, eps, init, tix, last);
+    }
     if (p.has_tail) LAUNCH_EL(k_rollout_tail, dim3((p.B + 63) / 64), dim3(64), st, p, d, eps, init, tix);
 }
 void launch_decide(const Params &p, const Bufs &d, double eps, int last, int init, int tix, hipStream_t st)
@@ -1595,6 +1767,11 @@ void launch_broadcast(double *dst, const double *src, size_t n, size_t copies, h
     if (total) hipLaunchKernelGGL(k_broadcast, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dst, src, n, total);
 }
 
+void launch_reset_working(const Params &p, const Bufs &d, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_reset_defect, dim3(blocks_for((long)p.B * p.S * (NX / 2), 256)), dim3(256), 0, st, p, d);
+    hipLaunchKernelGGL(k_reset_sel, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);
+}
 void launch_outer_begin(const Params &p, const Bufs &d, hipStream_t st)
 {
     hipLaunchKernelGGL(k_outer_begin, dim3(blocks_for(p.B, 256)), dim3(256), 0, st, p, d);

@@ -53,13 +53,13 @@ template <> struct Prec<double> {
     static constexpr int LQS = LQW;
     static DEV const double *lq(const Bufs &d) { return d.lq; }
     static DEV double *K(const Bufs &d) { return d.K; }
-    static DEV const double *def(const Bufs &d) { return d.Defect; }
+    static DEV const double *def(const Bufs &d, int b) { return kdbuf(work_buf(d, b)); }  // the working rows' Defect (kernel (Params, Bufs, ...))
 };
 template <> struct Prec<float> {
     static constexpr int LQS = LQW32;
     static DEV const float *lq(const Bufs &d) { return d.lq32; }
     static DEV float *K(const Bufs &d) { return d.K32; }
-    static DEV const float *def(const Bufs &d) { return d.def32; }
+    static DEV const float *def(const Bufs &d, int) { return d.def32; }  // (k_lq's copy of the working Defect)
 };
 
 // per-phase constants of one element
@@ -209,7 +209,7 @@ struct LinSrc {
                 const size_t kq = b[h] * pr.Kc + kc;
                 const char *base = o < I::LQ ? (const char *)(Prec<real>::K(d) + kq * KCW) - I::K
                                  : o < I::D  ? (const char *)(Prec<real>::lq(d) + kq * Prec<real>::LQS) - I::LQ
-                                 : o < I::DU ? (const char *)(Prec<real>::def(d) + (b[h] * pr.S + s + 1) * NX) - I::D
+                                 : o < I::DU ? (const char *)(Prec<real>::def(d, (int)b[h]) + (b[h] * pr.S + s + 1) * NX) - I::D
                                              : (const char *)(d.dU + kq * NX) - I::DU;
                 p[h][j] = base + o;
             }
@@ -494,7 +494,7 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
     if (!__builtin_amdgcn_ballot_w64(act)) return;
     const bool rowl = r < NX, st = rowl && act;
     const int rr = rowl ? r : 0;
-    const real *defg = Prec<real>::def(d);
+    const real *defg = Prec<real>::def(d, (int)b);
     S.zero[lane] = 0;
     S.dx[hf][r] = 0;
     S.du[hf][r] = 0;

@@ -26,8 +26,9 @@ struct ShiftArgs {
     const int *map_id;        // [B] map of each element (null: one map for the batch)
     int fp32, zero_u0;
 };
-void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, double *Xbar_new, double *Ubar_new, void *K_new,
-                         hipStream_t st);
+// the new Xbar / Ubar rows into every element's third buffer, which becomes its nominal and working
+// one; the new compact K rows into K_new
+void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, void *K_new, hipStream_t st);
 // constraint parameters through the shift: ReB rows by control-slot source (rmap: old slot, -1 =
 // initial), touchdown constraints by phase source (pmap: old phase, -1 = new) plus nadd appended
 // pending ones per new phase; overflow counts phases past MTD constraints

@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdA
     }
     __syncthreads();
     const int *cb = d.contacts + (size_t)b * (p.P + 1) * 4;
-    const double *Xbar = d.Xb[nom_buf(d, b)], *Ubar = d.Ub[nom_buf(d, b)];
+    const double *Xbar = xbuf(d, nom_buf(d, b)), *Ubar = ubuf(d, nom_buf(d, b));
     // controls, body states, feedback rows (zero past N_mpcsteps, as a fresh message)
     for (int e = t; e < HSDDP_CMD_STEPS * 24; e += blockDim.x) {
         const int k = e / 24, j = e % 24;
@@ -95,10 +95,10 @@ __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdA
 
 // One thread per 16 bytes (two doubles / four floats, never straddling a row: NX and KCW are
 // multiples of 4) of the new Xbar / Ubar rows and compact K rows of every element; gathered reads,
-// contiguous writes.
+// contiguous writes.  The new rows go to the element's third buffer (neither its nominal nor its
+// working one, which the gather reads); k_shift_sel then makes it both.
 template <typename KT>
-__global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, Bufs d, const KT *K, double *Xn, double *Un,
-                                                      KT *Kn)
+__global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, Bufs d, const KT *K, KT *Kn)
 {
     constexpr int KV = 16 / sizeof(KT);  // K values per thread
     const long nx = (long)a.S_new * NX / 2, nu = (long)a.Kc * NX / 2, nk = (long)a.Kc * KCW / KV, per = nx + nu + nk;
@@ -107,7 +107,9 @@ __global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, Bufs d
     const long b = gid / per;
     long e = gid % per;
     const int m = a.map_id ? a.map_id[b] : 0;
-    const double *Xbar = d.Xb[nom_buf(d, (int)b)], *X = d.Xb[work_buf(d, (int)b)], *Ubar = d.Ub[nom_buf(d, (int)b)];
+    const double *Xbar = xbuf(d, nom_buf(d, (int)b)), *X = xbuf(d, work_buf(d, (int)b)),
+                 *Ubar = ubuf(d, nom_buf(d, (int)b));
+    double *Xn = xbuf(d, trial_buf(d, (int)b)), *Un = ubuf(d, trial_buf(d, (int)b));
     const int *smap = a.smap + (size_t)m * a.S_new, *cmap = a.cmap + (size_t)m * a.Kc;
     if (e < nx) {
         const int s = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = smap[s];
@@ -132,19 +134,23 @@ __global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, Bufs d
     *(float4 *)&Kn[(b * nk + e) * KV] = v;
 }
 
-void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, double *Xbar_new, double *Ubar_new, void *K_new,
-                         hipStream_t st)
+__global__ void k_shift_sel(int B, Bufs d)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < B) d.sel[b] = sel_code(trial_buf(d, b), trial_buf(d, b));
+}
+
+void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, void *K_new, hipStream_t st)
 {
     static_assert(NX % 4 == 0 && KCW % 4 == 0, "16-byte pieces within rows");
     const int KV = a.fp32 ? 4 : 2;
     const long n = (long)B * ((long)a.S_new * NX / 2 + (long)a.Kc * NX / 2 + (long)a.Kc * KCW / KV);
     const dim3 g((unsigned)((n + 255) / 256));
     if (a.fp32)
-        hipLaunchKernelGGL(k_shift_gather<float>, g, dim3(256), 0, st, B, a, d, d.K32, Xbar_new, Ubar_new,
-                           (float *)K_new);
+        hipLaunchKernelGGL(k_shift_gather<float>, g, dim3(256), 0, st, B, a, d, d.K32, (float *)K_new);
     else
-        hipLaunchKernelGGL(k_shift_gather<double>, g, dim3(256), 0, st, B, a, d, d.K, Xbar_new, Ubar_new,
-                           (double *)K_new);
+        hipLaunchKernelGGL(k_shift_gather<double>, g, dim3(256), 0, st, B, a, d, d.K, (double *)K_new);
+    hipLaunchKernelGGL(k_shift_sel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, B, d);
 }
 
 // The constraint parameters the phases carry through HKDProblem::update (HKDProblem.cpp:117-222):

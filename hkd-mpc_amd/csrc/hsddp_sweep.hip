@@ -121,13 +121,13 @@ template <typename real> struct Prec;
 template <> struct Prec<double> {
     static DEV const double *lq(const Bufs &d) { return d.lq; }
     static DEV double *K(const Bufs &d) { return d.K; }
-    static DEV const double *def(const Bufs &d) { return d.Defect; }
+    static DEV const double *def(const Bufs &d, int b) { return kdbuf(work_buf(d, b)); }  // the working rows' Defect (kernel (Params, Bufs, ...))
     static constexpr int LQS = LQW;
 };
 template <> struct Prec<float> {
     static DEV const float *lq(const Bufs &d) { return d.lq32; }
     static DEV float *K(const Bufs &d) { return d.K32; }
-    static DEV const float *def(const Bufs &d) { return d.def32; }
+    static DEV const float *def(const Bufs &d, int) { return d.def32; }  // (k_lq's copy of the working Defect)
     static constexpr int LQS = LQW32;
 };
 
@@ -653,10 +653,12 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
 {
     double dvs = 0.0;
     const int pp = L.pp;
-    const real *lqg = Prec<real>::lq(d), *defg = Prec<real>::def(d);
+    const real *lqg = Prec<real>::lq(d);
     // the other item of the wave (its element's records feed the DMA even when this half is idle)
     const int b = it.b;
     const int b0 = __builtin_amdgcn_readlane(b, 0), b1 = __builtin_amdgcn_readlane(b, 32);  // wave-uniform (SGPRs)
+    // each item's working Defect rows (the buffer its working trajectory is in)
+    const real *defg0 = Prec<real>::def(d, b0), *defg1 = Prec<real>::def(d, b1);
     bool live = it.act;
     int fail = -1;
     real h[NX], g = 0;
@@ -725,23 +727,24 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
         }
         const int N = PL.N(i), s0 = PL.s0(i), k0 = PL.k0(i);
         auto recp = [&](int bb, int k) { return lqg + ((size_t)bb * p.Kc + k0 + k) * Prec<real>::LQS; };
-        auto defp = [&](int bb, int k) { return defg + ((size_t)bb * p.S + s0 + k + 1) * NX; };
-        fetch(S, recp(b0, N - 1), defp(b0, N - 1), recp(b1, N - 1), defp(b1, N - 1), L.lane);
+        auto defp0 = [&](int k) { return defg0 + ((size_t)b0 * p.S + s0 + k + 1) * NX; };
+        auto defp1 = [&](int k) { return defg1 + ((size_t)b1 * p.S + s0 + k + 1) * NX; };
+        fetch(S, recp(b0, N - 1), defp0(N - 1), recp(b1, N - 1), defp1(N - 1), L.lane);
         int k = N - 1;
 #pragma unroll 1
         for (; k >= 0; --k) {
             const bool more = k > 0;
             const int kn = more ? k - 1 : 0;
             const bool was = live;
-            knot<real, DV>(p, S, L, ph, it, k0 + k, h, g, live, k == N - 1, more, recp(b0, kn), defp(b0, kn), recp(b1, kn),
-                           defp(b1, kn), dvs);
+            knot<real, DV>(p, S, L, ph, it, k0 + k, h, g, live, k == N - 1, more, recp(b0, kn), defp0(kn), recp(b1, kn),
+                           defp1(kn), dvs);
             if (was && !live) fail = k0 + k;
             if (!__builtin_amdgcn_ballot_w64(live)) break;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA left in flight
         if (!__builtin_amdgcn_ballot_w64(live)) break;
         // G[0] += H[0] Defect[0] (SinglePhase.cpp:365)
-        const real *d0 = defg + ((size_t)b * p.S + s0) * NX;
+        const real *d0 = (L.e ? defg1 : defg0) + ((size_t)b * p.S + s0) * NX;
         real dc[2] = {d0[L.pos], L.pos < NX - 16 ? d0[16 + L.pos] : (real)0};
         real a = 0;
         static_for<NX>([&](auto Cc) { vfma<Cc>(a, dc, h[Cc]); });

@@ -98,3 +98,26 @@ def test_graph_mixed_layouts_equals_launches():
     prob = syn.make_layout_batch(lays)
     opt = hsddp.load_settings(max_AL_iter=3)
     _equal(_solve(prob, opt, True), _solve(prob, opt, False))
+
+
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("B,P,N,gait", [(1, 1, 50, "trot"), (5, 8, 25, "jump"), (16, 4, 20, "trot")])
+def test_fused_decide_equals_separate_launch(monkeypatch, B, P, N, gait, graph):
+    """Batches of <= 16 elements decide each line-search trial in the rollout launch (the last block
+    to finish, k_rollout FUSE, with a ticket counter it resets itself); HSDDP_NO_FUSED_DECIDE=1 keeps
+    the k_decide launch.  Both give the same solve bit for bit, over full solves with early exits
+    (graph-replayed and launch by launch) and across repeated solves on one handle (the ticket
+    counter must be back at 0 after every trial)."""
+    prob = syn.make_batch(B, P, N, gait)
+    prob2 = syn.make_batch(B, P, N, gait, seed=7)
+    opt = hsddp.load_settings()
+
+    def new_x0(s):
+        s.upload_problem(prob2["contacts"], prob2["x0"], prob2["ref_x"], prob2["ref_u"], prob2["ref_foot"])
+
+    monkeypatch.setenv("HSDDP_NO_FUSED_DECIDE", "0")
+    a = _solve(prob, opt, graph, changes=(new_x0, new_x0))
+    monkeypatch.setenv("HSDDP_NO_FUSED_DECIDE", "1")
+    b = _solve(prob, opt, graph, changes=(new_x0, new_x0))
+    _equal(a, b)
+    assert a[1][0]["n_ls_trials"].sum() > 0
