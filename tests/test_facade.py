@@ -17,13 +17,14 @@ PKG = os.path.join(ROOT, "hkd-mpc_amd")
 
 
 def _make():
-    r = subprocess.run(["make", "-C", os.path.join(PKG, "facade")], capture_output=True, text=True)
-    assert r.returncode == 0, r.stdout + r.stderr
+    for d in (os.path.join(PKG, "facade"), os.path.join(ROOT, "tests", "drivers")):
+        r = subprocess.run(["make", "-C", d], capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
 
 
 def test_facade_builds_and_checks():
     _make()
-    r = subprocess.run([os.path.join(PKG, "facade_check"), os.path.join(PKG, "settings", "ddp_setting.info")],
+    r = subprocess.run([os.path.join(ROOT, "tests", "drivers", "facade_check"), os.path.join(PKG, "settings", "ddp_setting.info")],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "facade_check ok" in r.stdout
@@ -34,7 +35,7 @@ def test_reference_plugin_api_compiles_and_works_on_the_host():
     (HKDCost.h:75-81, HKDConstraints.h:21-37) and a user SinglePhaseBase compile against the facade;
     the bases' ReB / AL helpers give their closed forms; a user cost is refused by solve()."""
     _make()
-    r = subprocess.run([os.path.join(PKG, "plugin_check")], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([os.path.join(ROOT, "tests", "drivers", "plugin_check")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "plugin_check ok" in r.stdout
 
@@ -44,7 +45,7 @@ def test_hkd_plugins_evaluate_on_the_device():
     """The facade's hkd:: plugins' virtuals (running_cost(_par), terminal_cost(_par),
     compute_violation / compute_partial) through the device primitives."""
     _make()
-    r = subprocess.run([os.path.join(PKG, "plugin_check"), "gpu"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([os.path.join(ROOT, "tests", "drivers", "plugin_check"), "gpu"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "plugin_check ok" in r.stdout
 

@@ -106,7 +106,7 @@ def test_describe_refuses_what_the_device_cannot_hold():
     """plugin_check covers user plugins; here: a registration whose dynamics is not the HKD model is
     refused by describe() before any device work (facade_check runs it)."""
     _make()
-    r = subprocess.run([os.path.join(PKG, "facade_check"), SETTINGS], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([os.path.join(ROOT, "tests", "drivers", "facade_check"), SETTINGS], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "facade_check ok" in r.stdout, r.stdout + r.stderr
 
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 measurement on the GPU box, in two calls (each well inside gpurun's 20-minute limit):
+# End-of-round measurement on the GPU box, in two calls (each well inside gpurun's 20-minute limit):
 #   a: metric bench (with the CPU baseline), rocprofv3 kernel trace, fp64 PMC passes, configs C2..C5
 #   b: fp32 PMC passes, C1 latency, the MPC tick (tools/mpc_round.sh)
 # Stops at the first failing step.
