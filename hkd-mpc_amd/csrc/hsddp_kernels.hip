@@ -740,6 +740,18 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
             ue = ((const d2 *)(d.du + r * NU))[lane];
         }
     }
+    // every lane stays active up to the u_prev exchange: lanes without a slot of their own work on a
+    // valid one (clamped) and write nothing
+    const long gc = gid < total ? gid : total - 1;
+    const int b = (int)(gc / p.S), s = (int)(gc % p.S);
+    const auto L = layout_of<EL>(d, b);
+    const bool mine = gid < total && active(b) && s < L.S();
+    int i, k;
+    slot_phase(L, s < L.S() ? s : L.S() - 1, i, k);
+    const int nb = nomof(b), tb = trialof(b);
+    const long kq = (long)b * p.Kc + s - i;  // the slot's control row (k < N)
+    const long kqmax = (long)p.B * p.Kc - 1;
+    const long kqr = kq < kqmax ? kq : kqmax;  // (the terminal slot's row index is clamped and unused)
     const long xr0 = g0 - 1;
     if constexpr (WIDE)
         stage_trial2(Xt, d, xr0, total, p.S, eps, lane, g0, bA, aA, nA, tA, bB, aB, nB, tB);
@@ -750,23 +762,12 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
         Up0[2 * lane + 1] = ua.y + eps * ue.y;
     }
     __syncthreads();
-    // every lane stays active up to the u_prev exchange: lanes without a slot of their own work on a
-    // valid one (clamped) and write nothing
-    const long gc = gid < total ? gid : total - 1;
-    const int b = (int)(gc / p.S), s = (int)(gc % p.S);
-    const auto L = layout_of<EL>(d, b);
-    const bool mine = gid < total && active(b) && s < L.S();
-    int i, k;
-    slot_phase(L, s < L.S() ? s : L.S() - 1, i, k);
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     const double *x = Xt + (gc - xr0) * RS;
-    const int nb = nomof(b), tb = trialof(b);
-    const long kq = (long)b * p.Kc + s - i;  // the slot's control row (k < N)
-    const long kqmax = (long)p.B * p.Kc - 1;
-    // the trial control row of the slot (k < N; the terminal slot's row index is clamped and unused)
+    // the trial control row of the slot, U = Ubar + eps du (k < N)
     double u[NU];
-    trial_row(d, kubuf(nb), kq < kqmax ? kq : kqmax, eps, u);
+    trial_row(d, kubuf(nb), kqr, eps, u);
     // the running cost of a control slot (the terminal cost at k = N: the boundary waves)
     if (mine && k < L.N(i)) {
         d2 *ug = (d2 *)(kubuf(tb) + kq * NU);

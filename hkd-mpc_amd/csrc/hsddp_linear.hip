@@ -17,7 +17,17 @@ constexpr int HC = 12;  // coupled controls per knot
 #define HSDDP_STAMPS 0
 #endif
 #ifndef HSDDP_LIN_EXP
-#define HSDDP_LIN_EXP 0  // timing experiments only (tools/lin_exp.sh): 1 no dX / du stores, 2 no arithmetic
+#define HSDDP_LIN_EXP 0  // timing experiments only: 1 no dX / du stores, 2 no arithmetic
+#endif
+// a knot's wait for its image leaves the previous knot's dX / du stores in flight (1), or waits for
+// them too (0: the round-4 kernel; A/B builds only)
+// the knot images requested with the non-temporal policy (the last read of K, the records, dU in
+// the iteration)
+#ifndef HSDDP_LIN_NT
+#define HSDDP_LIN_NT 1
+#endif
+#ifndef HSDDP_LIN_SLACK
+#define HSDDP_LIN_SLACK 1
 #endif
 // Diagnostic build (make stamps): s_memtime at the stage boundaries of a knot, differences summed
 // per stage into LDS and written to Bufs::dbg of the wave's second element (tools/stamps.py)
@@ -234,7 +244,10 @@ DEV void lin_fetch(LinBuf<real> &buf, const LinSrc<real> &src)
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int j = 0; j < LinImg<real>::NI; ++j) lds_dma16(src.p[h][j], (unsigned)(size_t)(buf.v[h] + 1024 * j));
+        for (int j = 0; j < LinImg<real>::NI; ++j) {
+            if (HSDDP_LIN_NT) lds_dma16_nt(src.p[h][j], (unsigned)(size_t)(buf.v[h] + 1024 * j));
+            else lds_dma16(src.p[h][j], (unsigned)(size_t)(buf.v[h] + 1024 * j));
+        }
 }
 
 template <int W>
@@ -318,6 +331,7 @@ struct LinOut {
     double *du, *dx;  // this lane's entries of the pending knot
     real vu, vx;      // the pending knot's values
     int n;            // pending knots (0 or 1)
+    int nprev;        // store instructions the previous knot issued after its image requests
 };
 
 template <typename real>
@@ -361,8 +375,12 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
         lin_fetch(nxt, src);
     }
     const int ns = lin_store_pending(pend, st, out);
-    // all but what was just issued: the 2 NI DMA of the next knot, the previous knot's stores
-    vm_wait_n<NI2>((more ? NI2 : 0) + ns);
+    // every vector memory operation up to this knot's image: all but the ones issued after it (the
+    // stores the previous knot issued behind this image's requests, the 2 NI DMA of the next knot and
+    // the stores just issued; operations complete in issue order, so a store waited for here would
+    // only delay the image).  The stores left in flight are older than the next knot's image.
+    vm_wait_n<NI2>((HSDDP_LIN_SLACK ? out.nprev : 0) + (more ? NI2 : 0) + ns);
+    out.nprev = ns;
     LSYNC();
     LSTAMP(1);
 #if HSDDP_LIN_EXP == 2
@@ -511,6 +529,7 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         LinSrc<real> src;
         src.init(p, d, eb, s0, k0, lane);
         lin_fetch(B0, src);  // the phase's first knot (its wait is in lin_knot)
+        out.nprev = 0;       // (the stores of earlier knots are older than this image)
         LinRow<real> R;
         load_phase(p, d, eb, hf, i, R.pc);
         if (i > 0) { // dx_init = Px dX_end

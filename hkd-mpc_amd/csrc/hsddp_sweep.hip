@@ -51,6 +51,10 @@ namespace sweep {
 #endif
 // value update on the matrix cores (1) or by DPP-broadcast multiply-adds from the lanes holding
 // K_c (0, no LDS round trip)
+// knot images requested with the non-temporal policy (A/B experiment)
+#ifndef HSDDP_SWEEP_NT
+#define HSDDP_SWEEP_NT 0
+#endif
 #ifndef HSDDP_VALUE_MFMA
 #define HSDDP_VALUE_MFMA 0
 #endif
@@ -108,6 +112,26 @@ struct alignas(16) Lds {
 };
 static_assert(sizeof(Lds<double>) <= 20480, "two waves per SIMD on 160 KB of LDS need <= 20 KB per wave");
 
+// The column split (k_riccati_cs, small batches): one element pair over the two waves of a
+// workgroup, which share this LDS.  Knot images double-buffered (a wave requests the next knot's
+// while the other may still read the current one); per item, two 25-row images that trade roles
+// from knot to knot: M rows, then (after the column reads) this knot's H exchange, while the other
+// holds the Z rows — so every image is rewritten only after a barrier both waves have passed since
+// its last read.
+template <typename real>
+struct alignas(16) LdsCS {
+    real img[2][2][VW];            // [buffer][item]
+    real zero[32];
+    struct alignas(16) Item {
+        real TI[24 * TS];          // T rows (columns: the controls of both waves)
+        real MZ[2][25 * MS];       // M rows -> H exchange | Z rows; W at phase ends (MZ[0])
+        real du[24];
+        real pc[8];
+    } it[2];
+    int fl[2];                     // the retry slot wave 0 took for each item
+};
+static_assert(sizeof(LdsCS<double>) <= 40960, "four split workgroups per CU on 160 KB of LDS need <= 40 KB each");
+
 // knot image pieces (16 bytes) of one item: the record's coefficient part, Defect[k+1], the rest
 template <typename real>
 struct Pieces {
@@ -156,8 +180,8 @@ struct Phase {
 // Phase layout entries with a runtime phase index, read from the kernel-argument segment (scalar
 // loads): indexing the by-value Params directly makes the compiler copy it to scratch.
 
-template <typename real>
-DEV void load_phase(const Params &p, const Bufs &d, typename Lds<real>::Item &I, int b, int i, int pp, Phase<real> &ph)
+template <typename real, typename ItemT>
+DEV void load_phase(const Params &p, const Bufs &d, ItemT &I, int b, int i, int pp, Phase<real> &ph)
 {
     const int *cs = d.contacts + ((size_t)b * (p.P + 1) + i) * 4;
     int c[4];
@@ -212,7 +236,8 @@ DEV void fetch(Lds<real> &S, const real *rec0, const real *def0, const real *rec
             const real *rec = e ? rec1 : rec0, *def = e ? def1 : def0;
             const real *src = q < PC::NA ? rec + PC::E * q : q < PC::NA + PC::ND ? def + PC::E * (q - PC::NA)
                                                                                  : rec + PC::E * (q - PC::ND);
-            lds_dma16(src, (unsigned)(size_t)(&S.img[0][0]) + 1024u * t);
+            if (HSDDP_SWEEP_NT) lds_dma16_nt(src, (unsigned)(size_t)(&S.img[0][0]) + 1024u * t);
+            else lds_dma16(src, (unsigned)(size_t)(&S.img[0][0]) + 1024u * t);
         }
     }
 }
@@ -232,18 +257,33 @@ struct Lane {
     int xc0, xkind;  // lxx cross terms of row pp: kind 1 (rows 3..5): columns xc0 + 3 t; kind 2 (rows >= 12): xc0
 };
 
+// Column split: wave W of k_riccati_cs forms the entries of M, Z, Qxx and H in the columns c with
+// cs_wave(c) == W.  The two sets of 12 balance the structural multiply-adds of M = H A (and of
+// S^T M) per column: 36 for wave 0, 33 for wave 1.
+constexpr unsigned CS_COLS1 = (1u << 0) | (1u << 3) | (1u << 4) | (1u << 5) | (1u << 8) | (1u << 9) | (1u << 10) |
+                              (1u << 11) | (1u << 18) | (1u << 19) | (1u << 21) | (1u << 22);
+DEV constexpr int cs_wave(int c) { return (int)((CS_COLS1 >> c) & 1u); }
+// column c is formed here (W < 0: the unsplit sweep forms every column)
+template <int W>
+DEV constexpr bool cs_mine(int c) { return W < 0 || cs_wave(c) == W; }
+
 // acc[c] += sum_j x[j] S[j][c] (S = A - I: rows 0..2 eul, 3..5 the dt entries, 6..8 omega) in
-// source order: consecutive multiply-adds feed different accumulators
-template <typename real>
+// source order: consecutive multiply-adds feed different accumulators; W >= 0: the columns of
+// wave W only
+template <int W = -1, typename real>
 DEV void emit_SA(real (&acc)[NX], const real (&x)[NX], const real (&cf)[8], real dt)
 {
     auto sw_row = [&](auto I) {
         constexpr int i = I;
-        static_for<17>([&](auto Q) { vfma<sw_at(i, Q)>(acc[sw_col(Q)], cf, x[6 + i]); });
+        static_for<17>([&](auto Q) {
+            if constexpr (cs_mine<W>(sw_col(Q))) vfma<sw_at(i, Q)>(acc[sw_col(Q)], cf, x[6 + i]);
+        });
     };
     auto se_row = [&](auto I) {
         constexpr int i = I;
-        static_for<5>([&](auto Q) { vfma<V_SE + 5 * i + Q>(acc[se_col(Q)], cf, x[i]); });
+        static_for<5>([&](auto Q) {
+            if constexpr (cs_mine<W>(se_col(Q))) vfma<V_SE + 5 * i + Q>(acc[se_col(Q)], cf, x[i]);
+        });
     };
     sw_row(std::integral_constant<int, 0>{});
     se_row(std::integral_constant<int, 0>{});
@@ -251,24 +291,25 @@ DEV void emit_SA(real (&acc)[NX], const real (&x)[NX], const real (&cf)[8], real
     se_row(std::integral_constant<int, 1>{});
     sw_row(std::integral_constant<int, 2>{});
     se_row(std::integral_constant<int, 2>{});
-#pragma unroll
-    for (int a = 0; a < 3; ++a) acc[9 + a] = __builtin_fma(x[3 + a], dt, acc[9 + a]);
+    static_for<3>([&](auto A) {
+        if constexpr (cs_mine<W>(9 + A)) acc[9 + A] = __builtin_fma(x[3 + A], dt, acc[9 + A]);
+    });
 }
 
 // acc[q] += (B_c^T y)[q] for the 12 coupled controls, y = (y6, y7, y8) on B's omega rows (BW, DPP
 // broadcast), y9[a] on row 9 + a (bv: dt c / m), y12[q] on row 12 + q (bq: dt (1 - c)); the
-// structurally absent half of the last two is an exact zero
-template <typename real>
+// structurally absent half of the last two is an exact zero.  Controls Q0 .. Q1 - 1 only.
+template <int Q0 = 0, int Q1 = HC, typename real>
 DEV void emit_Bc(real (&acc)[HC], real y6, real y7, real y8, const real *y9, const real *y12, const real (&bv)[4],
                  const real (&bq)[4], const real (&cf)[8])
 {
 #pragma unroll
-    for (int q = 0; q < HC; ++q) acc[q] = __builtin_fma(y12[q], bq[q / 3], acc[q]);
+    for (int q = Q0; q < Q1; ++q) acc[q] = __builtin_fma(y12[q], bq[q / 3], acc[q]);
 #pragma unroll
-    for (int q = 0; q < HC; ++q) acc[q] = __builtin_fma(y9[q % 3], bv[q / 3], acc[q]);
-    static_for<HC>([&](auto Q) { vfma<bw_at(0, Q)>(acc[Q], cf, y6); });
-    static_for<HC>([&](auto Q) { vfma<bw_at(1, Q)>(acc[Q], cf, y7); });
-    static_for<HC>([&](auto Q) { vfma<bw_at(2, Q)>(acc[Q], cf, y8); });
+    for (int q = Q0; q < Q1; ++q) acc[q] = __builtin_fma(y9[q % 3], bv[q / 3], acc[q]);
+    static_for<Q1 - Q0>([&](auto Q) { vfma<bw_at(0, Q0 + Q)>(acc[Q0 + Q], cf, y6); });
+    static_for<Q1 - Q0>([&](auto Q) { vfma<bw_at(1, Q0 + Q)>(acc[Q0 + Q], cf, y7); });
+    static_for<Q1 - Q0>([&](auto Q) { vfma<bw_at(2, Q0 + Q)>(acc[Q0 + Q], cf, y8); });
 }
 
 // Gaussian elimination without pivoting on the columns held in lanes, then back substitution:
@@ -643,14 +684,242 @@ DEV void knot(const Params &p, Lds<real> &S, const Lane &L, const Phase<real> &p
     STAMP(9);
 }
 
+// Workgroup barrier of the column split: this wave's LDS writes done, both waves here.  No wait
+// for vector memory (the knot images and the K / dU stores stay in flight: each wave waits for its
+// own requests with vmcnt before the barrier that publishes them).
+#define CSYNC()                                              \
+    do {                                                     \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
+        __builtin_amdgcn_s_barrier();                        \
+        asm volatile("" ::: "memory");                       \
+        __builtin_amdgcn_sched_barrier(0);                   \
+    } while (0)
+
+// fetch for the column split: wave W requests its half of the two items' pieces into image buffer q
+template <int W, typename real>
+DEV void fetch_cs(LdsCS<real> &S, int q, const real *rec0, const real *def0, const real *rec1, const real *def1,
+                  int lane)
+{
+    using PC = Pieces<real>;
+    constexpr int H = (PC::NI + 1) / 2;
+#pragma unroll
+    for (int u = 0; u < H; ++u) {
+        const int t = W * H + u;
+        const int n = 64 * t + lane;
+        if (t < PC::NI && n < 2 * PC::NP) {
+            const int e = n >= PC::NP, qq = n - e * PC::NP;
+            const real *rec = e ? rec1 : rec0, *def = e ? def1 : def0;
+            const real *src = qq < PC::NA ? rec + PC::E * qq : qq < PC::NA + PC::ND ? def + PC::E * (qq - PC::NA)
+                                                                                    : rec + PC::E * (qq - PC::ND);
+            lds_dma16(src, (unsigned)(size_t)(&S.img[q][0][0]) + 1024u * t);
+        }
+    }
+}
+
+// One knot of the sweep for wave W of the column split (k_riccati_cs): the knot() stages with the
+// column-parallel work halved — T's controls 6 W .. 6 W + 5, the columns cs_wave(c) == W of M, Z,
+// Qxx and H — and the per-element chain (Gn, Qux_c, the Quu_cc columns, the elimination, the K
+// broadcast, G) formed whole in both waves, so each wave holds everything it multiplies by.  Three
+// barriers: M / T rows written -> column reads; Z rows written -> Qxx reads; this wave's H columns
+// written (and its share of the next images landed) -> the other wave's H columns read.  ib: the
+// image buffer of this knot (the next knot's go to ib ^ 1); par: which MZ image holds M (the
+// other takes Z).  Both waves run the same branch decisions (live, the PSD test) on equal values.
+template <int W, typename real>
+DEV void knot_cs(const Params &p, LdsCS<real> &S, const Lane &L, const Phase<real> &ph, const Item<real> &it, int kc,
+                 real (&h)[NX], real &g, bool &live, bool first, bool more, int ib, int par, const real *nrec0,
+                 const real *ndef0, const real *nrec1, const real *ndef1)
+{
+    constexpr int Q0 = 6 * W, Q1 = Q0 + 6;
+    auto &I = S.it[L.e];
+    const real *img = S.img[ib][L.e];
+    real *const MA = I.MZ[par], *const ZA = I.MZ[par ^ 1];
+    const int pp = L.pp, pos = L.pos;
+    const real dt = (real)p.dt;
+    const real reg = it.reg;
+    if (first) {  // the phase's first images (each wave waits for its own requests, then both)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        CSYNC();
+    }
+    real cf[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cf[k] = img[16 * k + pos];
+    real bv[4], bq[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) { bv[l] = I.pc[l]; bq[l] = I.pc[4 + l]; }
+    // ---- Gn = G + H d, T = H B_c (this wave's controls), M = H A (this wave's columns) -------------
+    real t[HC], ga[4] = {g, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < HC; ++q) t[q] = 0;
+    emit_Bc<Q0, Q1>(t, h[6], h[7], h[8], h + 9, h + 12, bv, bq, cf);
+    static_for<NX>([&](auto C) { vfma<V_D + C>(ga[C & 3], cf, h[C]); });
+    const real gn = (ga[0] + ga[1]) + (ga[2] + ga[3]);
+    pin(t);
+    real h9[NX];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) h9[j] = h[j];
+#pragma unroll
+    for (int j = 9; j < NX; ++j) h9[j] = 0;
+    SSYNC();
+    real (&m)[NX] = h;
+    emit_SA<W>(m, h9, cf, dt);
+    pin(t);
+    pin(m);
+    if (L.row) {
+        static_for<NX>([&](auto C) {
+            if constexpr (cs_mine<W>(C)) MA[pp * MS + C] = m[C];
+        });
+        if (W == 0) MA[pp * MS + NX] = gn;
+#pragma unroll
+        for (int q = Q0; q < Q1; ++q) I.TI[pp * TS + q] = t[q];
+    }
+    CSYNC();
+    // ---- column pp of M (position 24: Gn); Z row (this wave's columns), Qux_c column, Qu_c ----------
+    const int pc = pp < MS - 1 ? pp : MS - 1;
+    real mc[NX];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) mc[j] = MA[j * MS + pc];
+    real w2[HC];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        const real *lcp = pp == NX ? img + V_LU + (((ph.cmask >> l) & 1) ? 3 * l : 12 + 3 * l) : S.zero;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) w2[3 * l + a] = lcp[a];
+    }
+    emit_SA<W>(m, mc, cf, dt);
+    emit_Bc(w2, mc[6], mc[7], mc[8], mc + 9, mc + 12, bv, bq, cf);
+    pin(m);
+    pin(w2);
+    // ---- Qxx = lxx + reg I + (Z + Z^T) / 2 on this wave's columns ----------------------------------
+    if (pp <= NX) {
+        static_for<NX>([&](auto C) {
+            if constexpr (cs_mine<W>(C)) ZA[pp * MS + C] = m[C];
+        });
+        if (W == 0) {
+            ZA[pp * MS + NX] = 0;
+            ZA[pp * MS + NX + 1] = 0;
+        }
+    }
+    SSYNC();
+    if (L.row) {  // lxx and reg I on the entries of this wave's columns (behind its own Z stores)
+        real *zr = ZA + pp * MS;
+        if (cs_wave(pp) == W) lds_add(zr + pp, ph.lxd + reg);
+#pragma unroll
+        for (int t2 = 0; t2 < 4; ++t2) {
+            const int xc = L.xkind == 1 ? L.xc0 + 3 * t2 : L.xc0;
+            if (((ph.xmask >> t2) & 1) && cs_wave(xc) == W) lds_add(zr + xc, -ph.xw);
+        }
+    }
+    CSYNC();
+    const real *zrow = L.row ? ZA + pp * MS : S.zero;
+    real qxx[NX], zc[NX];
+    static_for<NX>([&](auto C) {
+        if constexpr (cs_mine<W>(C)) {
+            qxx[C] = zrow[C];
+            zc[C] = ZA[C * MS + pc];
+        }
+    });
+    static_for<NX>([&](auto C) {
+        if constexpr (cs_mine<W>(C)) qxx[C] = __builtin_fma(zc[C], (real)0.5, qxx[C] * (real)0.5);
+    });
+    const real qx = img[V_LX + (L.row ? pp : 0)] + (gn + ZA[NX * MS + pc]);
+    // ---- Quu_cc column pos = luu + reg + B_c^T T[:, pos] -------------------------------------------
+    real tcol[18];
+#pragma unroll
+    for (int j = 0; j < 18; ++j) tcol[j] = I.TI[(6 + j) * TS + pos];
+    real lbr[3];
+    const int aq = pos % 3;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) lbr[a] = (L.qlane ? img + L.rb[a] : S.zero + a)[0] + (a == aq ? ph.dtr + reg : (real)0);
+    const int lq = pos / 3;
+    real w[HC];
+#pragma unroll
+    for (int q = 0; q < HC; ++q) w[q] = (L.qlane && lq == q / 3) ? lbr[q % 3] : (real)0;
+    emit_Bc(w, tcol[0], tcol[1], tcol[2], tcol + 3, tcol + 6, bv, bq, cf);
+    pin(w);
+    const bool zl = pp < HC;
+    const int du_z = ((ph.cmask >> ((zl ? pp : 0) / 3)) & 1) ? 12 + pp : pp;
+    const real quz = img[zl ? V_LU + du_z : V_LU];
+    const real qzz = ph.dtrz + reg;
+    // the next knot's images into the other buffer (read last in the previous knot, before its last
+    // barrier)
+    if (more) fetch_cs<W>(S, ib ^ 1, nrec0, ndef0, nrec1, ndef1, L.lane);
+    // ---- PSD test + elimination on [Quu_cc | Qux_c | Qu_c] (both waves) ------------------------------
+    real quxs[HC];
+#pragma unroll
+    for (int q = 0; q < HC; ++q) quxs[q] = L.row ? w2[q] : (real)0;
+    pin(quxs);
+    unsigned long long bad = __builtin_amdgcn_ballot_w64(zl && !(qzz > (real)1e-9));
+    eliminate(w, w2, bad);
+    const bool okh = L.e ? (bad >> 32) == 0 : (bad & 0xffffffffull) == 0;
+    live = live && okh;
+    const bool st = live;
+    // ---- dU through LDS (both waves write the same values) -------------------------------------------
+    if (pp == NX)
+#pragma unroll
+        for (int q = 0; q < HC; ++q) I.du[(((ph.cmask >> (q / 3)) & 1) ? 0 : 12) + q] = w2[q];
+    if (zl) I.du[du_z] = -(quz / qzz);
+    SSYNC();
+    real ka[HC], kb[HC];
+#pragma unroll
+    for (int q = 0; q < HC; ++q) row_pair_last(w2[q], ka[q], kb[q]);
+    real gq4[4] = {qx, 0, 0, 0};
+    static_for<HC>([&](auto Q) { bfma<8>(gq4[Q & 3], kb[Q], quxs[Q]); });
+    const real gq = (gq4[0] + gq4[1]) + (gq4[2] + gq4[3]);
+    // ---- H = Qxx + Qux_c^T K_c on this wave's columns ------------------------------------------------
+    static_for<NX>([&](auto C) {
+        if constexpr (cs_mine<W>(C)) h[C] = qxx[C];
+    });
+    static_for<HC>([&](auto Q) {
+        static_for<NX>([&](auto C) {
+            constexpr int c = C;
+            if constexpr (cs_mine<W>(c)) {
+                if constexpr (c < 16)
+                    bfma<c & 15>(h[c], ka[Q], quxs[Q]);
+                else
+                    bfma<c & 15>(h[c], kb[Q], quxs[Q]);
+            }
+        });
+    });
+    g = L.row ? gq : (real)0;
+    // this wave's H columns into the M image (its column reads ended before the last barrier)
+    if (L.row)
+        static_for<NX>([&](auto C) {
+            if constexpr (cs_mine<W>(C)) MA[pp * MS + C] = h[C];
+        });
+    // K_c rows and dU: wave 0 columns 0..15, wave 1 columns 16..23 and dU; issued after this wave's
+    // image requests are complete (the barrier below publishes them)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (st) {
+        real *Kg = it.K + (size_t)kc * KCW;
+        if (W == 0) {
+#pragma unroll
+            for (int q = 0; q < HC; ++q) Kg[q * NX + pos] = ka[q];
+        } else {
+            if (pos < NX - 16)
+#pragma unroll
+                for (int q = 0; q < HC; ++q) Kg[q * NX + 16 + pos] = kb[q];
+            if (L.row) it.dU[(size_t)kc * NX + pp] = I.du[pp];
+        }
+    }
+    CSYNC();
+    // the other wave's columns of row pp
+    static_for<NX>([&](auto C) {
+        if constexpr (!cs_mine<W>(C)) h[C] = L.row ? MA[pp * MS + C] : (real)0;
+    });
+    SSYNC();
+}
+
 // MultiPhaseDDP::backward_sweep (MultiPhaseDDP.cpp:190-229) for the wave's two items with their
 // own regularisation.  Returns, per half, -1 (success) or the control slot of the first knot whose
 // Quu fails the PSD test (that knot and the ones below it are not written).  DV: dv = the half's
 // sum over every knot of Qu^T dU (= dV_1 = -dV_2 of the sweep, SinglePhase.cpp:359-362,
 // MultiPhaseDDP.cpp:224-226), on every lane of the half.
-template <typename real, bool EL, bool DV>
-DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, const Item<real> &it, double &dv)
+template <typename real, bool EL, bool DV, int CSW = -1, typename LdsT = Lds<real>>
+DEV int sweep_pair(const Params &p, const Bufs &d, LdsT &S, const Lane &L, const Item<real> &it, double &dv)
 {
+    constexpr bool CS = CSW >= 0;  // wave CSW of the column split (k_riccati_cs)
+    static_assert(!(CS && DV), "the column split sweeps with multiple shooting");
+    int ib = 0, par = 0;           // (CS) image buffer, M / Z image roles
     double dvs = 0.0;
     const int pp = L.pp;
     const real *lqg = Prec<real>::lq(d);
@@ -676,7 +945,16 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
         } else {
             // impact-aware step G' = Phix + Px^T G0, H' = Phixx + Px^T H0 Px (MultiPhaseDDP.cpp:480-484):
             // W = H0 Px by rows (Px by DPP broadcast), then row pp of W^T Px from column pp of W
-            typename Lds<real>::Item &I = S.it[L.e];
+            auto &I = S.it[L.e];
+            // scratch rows: the item's M image (CS: both waves form the same values into it, each
+            // reading only what it wrote itself; barriers on both sides keep the knots' images apart)
+            real *WI;
+            if constexpr (CS) {
+                WI = I.MZ[0];
+                CSYNC();
+            } else {
+                WI = I.MI;
+            }
             const double *Px = rec + TM_PX;
             // W = H0 Px by rows: Px in three 8-row chunks of DPP-broadcast coefficients
             real wr[NX];
@@ -694,14 +972,14 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
             SSYNC();
             if (L.row) {
 #pragma unroll
-                for (int c = 0; c < NX; ++c) I.MI[pp * WS + c] = wr[c];
-                I.MI[pp * WS + NX] = g;  // column 24: G0
+                for (int c = 0; c < NX; ++c) WI[pp * WS + c] = wr[c];
+                WI[pp * WS + NX] = g;  // column 24: G0
             }
             SSYNC();
             const int pc = pp < NX ? pp : NX;
             real wc[NX];
 #pragma unroll
-            for (int j = 0; j < NX; ++j) wc[j] = I.MI[j * WS + pc];
+            for (int j = 0; j < NX; ++j) wc[j] = WI[j * WS + pc];
             real vr[NX];
 #pragma unroll
             for (int c = 0; c < NX; ++c) vr[c] = 0;
@@ -717,27 +995,36 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
             SSYNC();
             if (pp == NX)
 #pragma unroll
-                for (int c = 0; c < NX; ++c) I.MI[NX * WS + c] = vr[c];  // Px^T G0
+                for (int c = 0; c < NX; ++c) WI[NX * WS + c] = vr[c];  // Px^T G0
             SSYNC();
-            const real gp = I.MI[NX * WS + (L.row ? pp : 0)];
+            const real gp = WI[NX * WS + (L.row ? pp : 0)];
 #pragma unroll
             for (int c = 0; c < NX; ++c) h[c] = L.row ? (real)rec[TM_PHIXX + pp * NX + c] + vr[c] : (real)0;
             g = L.row ? (real)rec[TM_PHIX + pp] + gp : (real)0;
             SSYNC();
+            if constexpr (CS) CSYNC();
         }
         const int N = PL.N(i), s0 = PL.s0(i), k0 = PL.k0(i);
         auto recp = [&](int bb, int k) { return lqg + ((size_t)bb * p.Kc + k0 + k) * Prec<real>::LQS; };
         auto defp0 = [&](int k) { return defg0 + ((size_t)b0 * p.S + s0 + k + 1) * NX; };
         auto defp1 = [&](int k) { return defg1 + ((size_t)b1 * p.S + s0 + k + 1) * NX; };
-        fetch(S, recp(b0, N - 1), defp0(N - 1), recp(b1, N - 1), defp1(N - 1), L.lane);
+        if constexpr (CS) fetch_cs<CSW>(S, ib, recp(b0, N - 1), defp0(N - 1), recp(b1, N - 1), defp1(N - 1), L.lane);
+        else fetch(S, recp(b0, N - 1), defp0(N - 1), recp(b1, N - 1), defp1(N - 1), L.lane);
         int k = N - 1;
 #pragma unroll 1
         for (; k >= 0; --k) {
             const bool more = k > 0;
             const int kn = more ? k - 1 : 0;
             const bool was = live;
-            knot<real, DV>(p, S, L, ph, it, k0 + k, h, g, live, k == N - 1, more, recp(b0, kn), defp0(kn), recp(b1, kn),
-                           defp1(kn), dvs);
+            if constexpr (CS) {
+                knot_cs<CSW>(p, S, L, ph, it, k0 + k, h, g, live, k == N - 1, more, ib, par, recp(b0, kn), defp0(kn),
+                             recp(b1, kn), defp1(kn));
+                ib ^= more ? 1 : 0;
+                par ^= 1;
+            } else {
+                knot<real, DV>(p, S, L, ph, it, k0 + k, h, g, live, k == N - 1, more, recp(b0, kn), defp0(kn), recp(b1, kn),
+                               defp1(kn), dvs);
+            }
             if (was && !live) fail = k0 + k;
             if (!__builtin_amdgcn_ballot_w64(live)) break;
         }
@@ -751,7 +1038,7 @@ DEV int sweep_pair(const Params &p, const Bufs &d, Lds<real> &S, const Lane &L, 
         if (L.row) g += a;
         // SinglePhase::get_value_approx (G[0], H[0] of the phase, SinglePhase.cpp:365) for callers
         // that read the value function (hsddp_set_value_export)
-        if (p.store_value && live && L.row) {
+        if (p.store_value && live && L.row && CSW <= 0) {
             double *V = d.value0 + ((size_t)b * p.P + i) * (NX + NN);
 #pragma unroll
             for (int c = 0; c < NX; ++c) V[NX + pp * NX + c] = (double)h[c];
@@ -816,7 +1103,7 @@ DEV void element_cost(const Params &p, const Bufs &d, int b, int lane, double *s
 DEV Lane make_lane()
 {
     Lane L;
-    L.lane = threadIdx.x;
+    L.lane = threadIdx.x & 63;  // (k_riccati_cs: the lane within its wave)
     L.e = L.lane >> 5;
     L.pp = L.lane & 31;
     L.pos = L.lane & 15;
@@ -830,8 +1117,8 @@ DEV Lane make_lane()
     return L;
 }
 
-template <typename real>
-DEV void zero_init(Lds<real> &S, int lane)
+template <typename LdsT>
+DEV void zero_init(LdsT &S, int lane)
 {
     if (lane < 32) S.zero[lane] = 0;
     SSYNC();
@@ -935,6 +1222,96 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
     }
 }
 
+// k_riccati for small batches (column split, launch_riccati's choice): one element pair per
+// workgroup of two waves, wave W running sweep_pair with knot_cs<W> — the same sweeps, attempts and
+// outcomes as k_riccati (each wave computes the values the other multiplies by, so both take the
+// same branches); wave 0 alone writes the element state and the retry list.  fp64, multiple
+// shooting.  At small batches k_riccati runs one wave per SIMD and its knot is one dependent chain
+// of ~11 k cycles; split, each wave issues ~970 of the 1 197 VALU instructions of a knot (static
+// count of the knot loops) and the knot takes ~10 % less (sweep_split).
+template <bool EL, int W>
+DEV void riccati_cs_wave(const Params &p, const Bufs &d, LdsCS<double> &S)
+{
+    using real = double;
+    const Lane L = make_lane();
+    int b, bv;
+    bool valid;
+    if constexpr (EL) {
+        const int e0 = d.pairs[2 * blockIdx.x], e1 = d.pairs[2 * blockIdx.x + 1];
+        b = L.e ? e1 : e0;
+        valid = b >= 0;
+        bv = valid ? b : (L.e ? e0 : e1);
+    } else {
+        b = 2 * blockIdx.x + L.e;
+        valid = b < p.B;
+        bv = valid ? b : p.B - 1;
+    }
+    ElemState &E = d.el[bv];
+    bool act = valid && !E.done && !E.inner_done;
+    // (act is the same in both waves: both return here, or neither)
+    if (!__builtin_amdgcn_ballot_w64(act)) return;
+    double ecost = 0, efeas = 0;
+    if (W == 0) {
+        double *stg = 2 * (size_t)p.S * sizeof(double) <= sizeof(S.it[0]) ? reinterpret_cast<double *>(&S.it[L.e]) : nullptr;
+        element_cost<EL>(p, d, bv, L.lane, stg, ecost, efeas);
+    }
+    CSYNC();  // (the staging area is the item's images)
+    double reg = E.reg;
+    Item<real> it;
+    it.b = bv;
+    it.K = d.K + (size_t)bv * p.Kc * KCW;
+    it.dU = d.dU + (size_t)bv * p.Kc * NX;
+    bool need = act, ok = false;
+    for (int attempt = 0; __builtin_amdgcn_ballot_w64(need); ++attempt) {
+        it.act = need;
+        it.reg = (real)reg;
+        double dv;
+        const int fk = sweep_pair<real, EL, false, W>(p, d, S, L, it, dv);
+        if (attempt == 0 && p.retry_cap > 0) {  // wave 0 takes the retry slots, both read them
+            if (W == 0 && need && fk >= 0 && L.pp == 0) {
+                const int f = atomicAdd(d.retry_count, 1);
+                if (f < p.retry_cap) d.retry_list[f] = RetryEntry{bv, 0, reg};
+                S.fl[L.e] = f;
+            }
+            CSYNC();
+        }
+        if (need) {
+            if (fk < 0) {
+                ok = true;
+                need = false;
+            } else {
+                const bool deferred = attempt == 0 && p.retry_cap > 0 && S.fl[L.e] < p.retry_cap;
+                if (deferred) {
+                    need = false;
+                    if (W == 0 && L.pp == 0) { E.iters += 1; E.cost = ecost; E.feas = efeas; E.accepted = 0; }
+                    act = false;
+                } else {
+                    reg = fmax(reg * p.update_regularization, 1e-03);
+                    if (reg > 1e2 || attempt >= MAX_REG_ATTEMPTS) need = false;
+                }
+            }
+        }
+        CSYNC();  // (S.fl read by both before a later attempt could rewrite it)
+    }
+    if (W == 0 && act && L.pp == 0) {
+        double rn = reg / 20;
+        if (rn < 1e-06) rn = 0;
+        E.iters += 1; E.cost = ecost; E.feas = efeas; E.accepted = 0;
+        E.reg = rn;
+        if (!ok) { E.status = 1; E.done = 1; E.ls_active = 0; }
+    }
+}
+
+template <bool EL>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k_riccati_cs(Params p, Bufs d)
+{
+    __shared__ LdsCS<double> S;
+    zero_init(S, threadIdx.x & 63);
+    __syncthreads();
+    if (threadIdx.x < 64) riccati_cs_wave<EL, 0>(p, d, S);
+    else riccati_cs_wave<EL, 1>(p, d, S);
+}
+
 // The retries of backward_sweep_regularized for the elements k_riccati deferred, all at once:
 // item (f, a) sweeps deferred element f with the a-th next mu of the schedule into its own scratch
 // rows, two items per wave.  Every attempt is the sweep the sequential loop would run with that mu,
@@ -1035,6 +1412,20 @@ __global__ __launch_bounds__(64) void k_riccati_select(Params p, Bufs d)
     }
 }
 
+// the column split (k_riccati_cs) when its workgroups take at most one CU each (B <= 512) in fp64
+// with multiple shooting; HSDDP_SWEEP_SPLIT = 0 / 1 forces it off / on (tests, A/B).  Measured
+// (one box, sweep ms per step at B = 64 / 256 / 512 / 1024 / 2048): split 0.738 / 0.740 / 0.757 /
+// 1.075 / 1.343, one-wave 0.821 / 0.825 / 0.836 / 0.951 / 1.372 — from two workgroups per CU on,
+// the waves of one CU slow each other (the one-wave kernel too: 0.84 -> 0.95 ms from 256 to 512
+// waves at an unchanged 2.3 GHz clock), and the split's two waves per pair lose.
+static bool sweep_split(const Params &p)
+{
+    if (p.fp32 || p.ms0) return false;
+    const char *e = std::getenv("HSDDP_SWEEP_SPLIT");
+    if (e && *e) return *e != '0';
+    return (p.elem_layout ? p.n_pairs : (p.B + 1) / 2) <= 256;
+}
+
 void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
 {
     // (the retry list count is zeroed by the k_lq launch just before, in its first terminal task)
@@ -1051,7 +1442,10 @@ void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
         }                                                                                                    \
     } while (0)
     if (p.fp32) HSDDP_RIC(k_riccati, g1, float);
-    else HSDDP_RIC(k_riccati, g1, double);
+    else if (sweep_split(p)) {
+        if (p.elem_layout) hipLaunchKernelGGL(k_riccati_cs<true>, g1, dim3(128), 0, st, p, d);
+        else hipLaunchKernelGGL(k_riccati_cs<false>, g1, dim3(128), 0, st, p, d);
+    } else HSDDP_RIC(k_riccati, g1, double);
     if (p.retry_cap > 0) {
         const dim3 gr((unsigned)(p.retry_cap * (p.retry_m + (p.retry_m & 1)) / 2)), gs((unsigned)p.retry_cap);
         if (p.fp32) {
