@@ -627,6 +627,9 @@ DEV void stage_trial2(double *L, const Bufs &d, long r0, long nrows, int per, do
     }
 }
 
+#ifndef HSDDP_RO_BFIRST
+#define HSDDP_RO_BFIRST 0
+#endif
 #ifndef HSDDP_ROLLOUT_WAVES
 #define HSDDP_ROLLOUT_WAVES 2  // measured: 2 (256 VGPRs, no spills) 0.93 ms/step forward vs 3: 1.23, 4: 1.07
 #endif
@@ -703,12 +706,24 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
     __shared__ double Xt[RW * RS];
     const int lane = threadIdx.x;
     const long total = (long)p.B * p.S;
+#if HSDDP_RO_BFIRST
+    // the phase-boundary waves first: their threads' serial work (reset map, terminal cost) then
+    // overlaps the slot waves instead of trailing them
+    const long nbnd = ((long)p.B * p.P + 63) / 64;
+    if ((long)blockIdx.x < nbnd) {
+        rollout_boundary<EL>(p, d, eps, init, (long)blockIdx.x * 64 + lane);
+        return;
+    }
+    const long blk = (long)blockIdx.x - nbnd;
+#else
     const long nslot = (total + 63) / 64;
     if ((long)blockIdx.x >= nslot) {  // the phase-boundary waves (after the slot waves)
         rollout_boundary<EL>(p, d, eps, init, ((long)blockIdx.x - nslot) * 64 + lane);
         return;
     }
-    const long g0 = (long)blockIdx.x * 64, gid = g0 + lane;
+    const long blk = (long)blockIdx.x;
+#endif
+    const long g0 = blk * 64, gid = g0 + lane;
     const long gl = min(g0 + 63, total - 1);
     const int bA = (int)(g0 / p.S), bB = (int)(gl / p.S);
     auto act = [&](int b) { const ElemState &E = d.el[b]; return init ? !E.done : E.ls_active != 0; };

@@ -19,15 +19,11 @@ constexpr int HC = 12;  // coupled controls per knot
 #ifndef HSDDP_LIN_EXP
 #define HSDDP_LIN_EXP 0  // timing experiments only: 1 no dX / du stores, 2 no arithmetic
 #endif
-// a knot's wait for its image leaves the previous knot's dX / du stores in flight (1), or waits for
-// them too (0: the round-4 kernel; A/B builds only)
-// the knot images requested with the non-temporal policy (the last read of K, the records, dU in
-// the iteration)
+// the knot images requested with the non-temporal policy: the iteration's last read of K, the
+// records and dU (0.82 -> 0.73 ms on one box; the sweep's image requests, which the linear rollout
+// reads again, stay default: nt there cost the rollout 0.045 ms)
 #ifndef HSDDP_LIN_NT
 #define HSDDP_LIN_NT 1
-#endif
-#ifndef HSDDP_LIN_SLACK
-#define HSDDP_LIN_SLACK 1
 #endif
 // Diagnostic build (make stamps): s_memtime at the stage boundaries of a knot, differences summed
 // per stage into LDS and written to Bufs::dbg of the wave's second element (tools/stamps.py)
@@ -379,7 +375,7 @@ DEV void lin_knot(const Params &p, LinVec<real> &S, LinBuf<real> &cur, LinBuf<re
     // stores the previous knot issued behind this image's requests, the 2 NI DMA of the next knot and
     // the stores just issued; operations complete in issue order, so a store waited for here would
     // only delay the image).  The stores left in flight are older than the next knot's image.
-    vm_wait_n<NI2>((HSDDP_LIN_SLACK ? out.nprev : 0) + (more ? NI2 : 0) + ns);
+    vm_wait_n<NI2>(out.nprev + (more ? NI2 : 0) + ns);
     out.nprev = ns;
     LSYNC();
     LSTAMP(1);
