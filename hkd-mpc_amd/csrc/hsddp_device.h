@@ -167,18 +167,35 @@ DEV double running_cost(const Params &p, const int *c, const double *x, const do
                         const double *ur, const double *pf, const double *delta, const double *eps, double &viol,
                         const double *ovr = nullptr)
 {
-    // ovr: older control forces of the stored GRF constraint values (constraint_forces), else u's
+    // ovr: older control forces of the stored GRF constraint values (constraint_forces), else u's.
+    // The reference rows (16-byte aligned: rows of 24 / 12 doubles) as 16-byte loads, all issued
+    // before the first use (a lane reads its own slot's rows: each instruction touches up to 64
+    // lines, and the vector L1 serves the later pieces of a row — read past it (nt), the forward
+    // line search took twice as long)
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    double xrv[NX], urv[NU], pfv[12];
+#pragma unroll
+    for (int j = 0; j < NX / 2; ++j) {
+        const d2v a = ((const d2v *)xr)[j], b = ((const d2v *)ur)[j];
+        xrv[2 * j] = a.x; xrv[2 * j + 1] = a.y;
+        urv[2 * j] = b.x; urv[2 * j + 1] = b.y;
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const d2v a = ((const d2v *)pf)[j];
+        pfv[2 * j] = a.x; pfv[2 * j + 1] = a.y;
+    }
     double lt = 0.0, lu = 0.0, lf = 0.0;
 #pragma unroll
-    for (int j = 0; j < NX; ++j) { double e = x[j] - xr[j]; lt += e * q_diag(p, c, j) * e; }
+    for (int j = 0; j < NX; ++j) { double e = x[j] - xrv[j]; lt += e * q_diag(p, c, j) * e; }
     lt = 0.5 * lt;
 #pragma unroll
-    for (int j = 0; j < NX; ++j) { double e = u[j] - ur[j]; lu += e * r_diag(p, j) * e; }
+    for (int j = 0; j < NX; ++j) { double e = u[j] - urv[j]; lu += e * r_diag(p, j) * e; }
     lt += 0.5 * lu;
     lt *= p.dt;
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
-        double e = (x[12 + j] - x[3 + j % 3]) - (pf[j] - xr[3 + j % 3]);
+        double e = (x[12 + j] - x[3 + j % 3]) - (pfv[j] - xrv[3 + j % 3]);
         lf += e * foot_weight(p, c, j) * e;
     }
     lf = .5 * lf;

@@ -26,7 +26,29 @@ namespace hsddp {
 using namespace hkd;
 
 #ifndef HSDDP_RO_EXP
-#define HSDDP_RO_EXP 0  // timing experiments only: 1 no Defect row stores, 2 no trial U row stores (k_rollout)
+#define HSDDP_RO_EXP 0  // timing experiments only: 1 no Defect row stores, 2 no trial U row stores (k_rollout),
+                        // 3 no running cost, 4 running cost without reference loads
+#endif
+#ifndef HSDDP_STAMPS
+#define HSDDP_STAMPS 0
+#endif
+// Diagnostic build (make stamps): s_memtime at the stage boundaries of a k_rollout slot wave (each
+// after an LDS drain only: a stage's own loads are waited where they are used), the differences of
+// every full slot wave added into Bufs::dbg — element 0's slots 12 .. 15 and element 1's slots 0 .. 3
+// (the sweep and the linear rollout use the others) — tools/stamps.py
+#if HSDDP_STAMPS
+#define RSTAMP(n)                                                                             \
+    do {                                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        unsigned long long t_;                                                                \
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        rst[n] = t_;                                                                          \
+    } while (0)
+#else
+#define RSTAMP(n) \
+    do {          \
+    } while (0)
 #endif
 #ifndef HSDDP_LQ_EXP
 #define HSDDP_LQ_EXP 0  // timing experiment only: 1 no terminal tasks
@@ -518,8 +540,17 @@ DEV void finish_terminal(const Params &p, const Bufs &d, int b, int s, int i, co
 DEV void finish_running(const Params &p, const Bufs &d, int b, int s, int kc, const int *c, const double *x, const double *u)
 {
     const size_t sb = (size_t)b * p.S;
+#if HSDDP_RO_EXP == 3
+    d.slot_cost[sb + s] = x[0];  // timing only: no running cost
+    d.slot_viol[sb + s] = u[0];
+    return;
+#endif
+#if HSDDP_RO_EXP == 4
+    const double *xr = x, *pf = x + 12, *ur = u;  // timing only: the cost without its reference loads
+#else
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
     const double *ur = ref_ptr(p, d.ref_u, b, s, NU);
+#endif
     const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
     double viol;
     d.slot_cost[sb + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
@@ -627,9 +658,6 @@ DEV void stage_trial2(double *L, const Bufs &d, long r0, long nrows, int per, do
     }
 }
 
-#ifndef HSDDP_RO_BFIRST
-#define HSDDP_RO_BFIRST 0
-#endif
 #ifndef HSDDP_ROLLOUT_WAVES
 #define HSDDP_ROLLOUT_WAVES 2  // measured: 2 (256 VGPRs, no spills) 0.93 ms/step forward vs 3: 1.23, 4: 1.07
 #endif
@@ -706,23 +734,16 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
     __shared__ double Xt[RW * RS];
     const int lane = threadIdx.x;
     const long total = (long)p.B * p.S;
-#if HSDDP_RO_BFIRST
-    // the phase-boundary waves first: their threads' serial work (reset map, terminal cost) then
-    // overlaps the slot waves instead of trailing them
-    const long nbnd = ((long)p.B * p.P + 63) / 64;
-    if ((long)blockIdx.x < nbnd) {
-        rollout_boundary<EL>(p, d, eps, init, (long)blockIdx.x * 64 + lane);
-        return;
-    }
-    const long blk = (long)blockIdx.x - nbnd;
-#else
     const long nslot = (total + 63) / 64;
     if ((long)blockIdx.x >= nslot) {  // the phase-boundary waves (after the slot waves)
         rollout_boundary<EL>(p, d, eps, init, ((long)blockIdx.x - nslot) * 64 + lane);
         return;
     }
     const long blk = (long)blockIdx.x;
+#if HSDDP_STAMPS
+    unsigned long long rst[8];
 #endif
+    RSTAMP(0);
     const long g0 = blk * 64, gid = g0 + lane;
     const long gl = min(g0 + 63, total - 1);
     const int bA = (int)(g0 / p.S), bB = (int)(gl / p.S);
@@ -767,6 +788,7 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
     const long kq = (long)b * p.Kc + s - i;  // the slot's control row (k < N)
     const long kqmax = (long)p.B * p.Kc - 1;
     const long kqr = kq < kqmax ? kq : kqmax;  // (the terminal slot's row index is clamped and unused)
+    RSTAMP(1);
     const long xr0 = g0 - 1;
     if constexpr (WIDE)
         stage_trial2(Xt, d, xr0, total, p.S, eps, lane, g0, bA, aA, nA, tA, bB, aB, nB, tB);
@@ -777,12 +799,17 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
         Up0[2 * lane + 1] = ua.y + eps * ue.y;
     }
     __syncthreads();
+    RSTAMP(2);
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     const double *x = Xt + (gc - xr0) * RS;
     // the trial control row of the slot, U = Ubar + eps du (k < N)
     double u[NU];
     trial_row(d, kubuf(nb), kqr, eps, u);
+#if HSDDP_STAMPS
+    asm volatile("" : "+v"(u[0]), "+v"(u[NU - 1]));
+#endif
+    RSTAMP(3);
     // the running cost of a control slot (the terminal cost at k = N: the boundary waves)
     if (mine && k < L.N(i)) {
         d2 *ug = (d2 *)(kubuf(tb) + kq * NU);
@@ -793,6 +820,7 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
         for (int j = 0; j < NU / 2; ++j) ug[j] = d2{u[2 * j], u[2 * j + 1]};
         finish_running(p, d, b, s, L.k0(i) + k, c, x, u);
     }
+    RSTAMP(4);
     // u_prev: the previous slot's control row is the previous lane's (k > 0: slot s - 1 is a
     // control slot of the same phase), lane 0's was staged
     double up[NU];
@@ -831,6 +859,7 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
     } else {
         wave_sync();
     }
+    RSTAMP(5);
     wflag[lane] = wr;
     const int rsplit = (int)((long)bB * p.S - g0);  // (WIDE) rows from here on are element bB's
     double *const DtA = kdbuf(tA), *const DtB = kdbuf(tB);
@@ -850,6 +879,17 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
             *(d2 *)(Dt + (g0 + row) * NX + cc) = d2{src[0], src[1]};
         }
     }
+#if HSDDP_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    RSTAMP(6);
+    if (lane == 0) {
+        unsigned long long *acc = (unsigned long long *)d.dbg;
+        const int slot[7] = {12, 13, 14, 15, 16, 17, 18};  // element 0: 12 .. 15, element 1: 0 .. 2
+#pragma unroll
+        for (int n = 1; n <= 6; ++n) atomicAdd(acc + slot[n - 1], rst[n] - rst[n - 1]);
+        atomicAdd(acc + 19, 1ull);  // waves
+    }
+#endif
 }
 
 // k_rollout_tail: the non-shooting states of a phase (k >= ss; HKDProblem::update leaves a new

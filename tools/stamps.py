@@ -21,6 +21,9 @@ STAGES = ["wait DMA, coefficients", "Gn, T, M rows", "M columns, Z, Qux_c, Qu_c"
           "Quu_cc columns, DMA", "elimination (12 steps)", "dU, K broadcast, G", "value update (DPP)",
           "K / dU stores"]
 LIN_STAGES = ["DMA issue, stores, image wait", "K dX, du", "A - I, B rows (DPP)", "row tail, dV"]
+RO_STAGES = ["element state, layout, u_prev row", "state rows staged (loads, LDS, barrier)",
+             "contacts, trial control row", "running cost (references, ReB)", "dynamics, Defect, feasibility",
+             "U rows (earlier), Defect rows stored (drained)"]
 
 
 def main():
@@ -47,6 +50,15 @@ def main():
     for name, c in zip(LIN_STAGES, lc):
         print(f"{name:28s} {c / (3 * 200):10.0f} cycles/knot  {100 * c / max(lt, 1):5.1f} %")
     print(f"{'total':28s} {lt / (3 * 200):10.0f} cycles/knot")
+    # k_rollout slot waves (hsddp_kernels.hip RSTAMP): element 0's slots 12..15, element 1's 0..3
+    flat = out.reshape(-1)
+    rc = flat[12:19].astype(np.float64)
+    nw = max(float(flat[19]), 1.0)
+    rt = rc.sum()
+    print(f"k_rollout slot waves ({nw:.0f} stamped)")
+    for name, c in zip(RO_STAGES, rc):
+        print(f"{name:44s} {c / nw:10.0f} cycles/wave  {100 * c / max(rt, 1):5.1f} %")
+    print(f"{'total':44s} {rt / nw:10.0f} cycles/wave")
 
 
 if __name__ == "__main__":
