@@ -93,6 +93,42 @@ def cpu_baseline(args):
                       f"{threads} threads, {dt:.1f} s wall"}
 
 
+def full_solve_c5(prob, device) -> dict:
+    """Config C5's other half (BASELINE.json: "fp32 Riccati + ReB/AL outer loop, ... tolerance vs
+    fp64 reference reported"): one full MultiPhaseDDP::solve of the same batch with the shipped
+    settings (AL / ReB outer loop, early exits) in the fp32 Riccati mode and in fp64, each timed
+    (synchronised wall clock, after an untimed solve of the same handle from the same start), and
+    the fp32 result against
+    the fp64 one: status agreement, relative final-cost difference, max |Xbar| difference.  After the
+    timed region of the bench line; not part of its value."""
+    res = {}
+    for fp32 in (True, False):
+        s = hsddp.Solver(prob, hsddp.load_settings(), device=device, riccati_fp32=fp32)
+        s.solve()  # warm: graph capture, allocation
+        # the same start again (the constructor's): inputs, then the batch's warm start
+        s.upload_problem(prob["contacts"], prob["x0"], prob["ref_x"], prob["ref_u"], prob["ref_foot"])
+        s.warm_start(prob.get("Xbar"), prob.get("Ubar"), prob.get("K"))
+        s.synchronize(); torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s.solve()
+        s.synchronize(); torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3
+        info = s.element_info()
+        res[fp32] = {"ms": ms, "Xbar": s.trajectory()["Xbar"], "status": info["status"], "cost": info["cost"],
+                     "iters": info["iters"], "outer": info["outer_iters"]}
+        s.close()
+    a, b = res[False], res[True]
+    dc = np.abs(b["cost"] - a["cost"]) / np.maximum(np.abs(a["cost"]), 1e-30)
+    return {"settings": "ddp_setting.info (max_AL_iter 5, max_DDP_iter 10, early exits)",
+            "ms_fp32": b["ms"], "ms_fp64": a["ms"],
+            "mean_inner_iters_fp32": float(b["iters"].mean()), "mean_inner_iters_fp64": float(a["iters"].mean()),
+            "mean_outer_iters_fp32": float(b["outer"].mean()), "mean_outer_iters_fp64": float(a["outer"].mean()),
+            "status_agreement": float(np.mean(a["status"] == b["status"])),
+            "cost_rel_diff_median": float(np.median(dc)), "cost_rel_diff_max": float(np.max(dc)),
+            "xbar_abs_diff_max": float(np.max(np.abs(b["Xbar"] - a["Xbar"]))),
+            "all_finite": bool(np.isfinite(b["Xbar"]).all())}
+
+
 def latency_c1(args) -> None:
     """BASELINE config 1 (Mini Cheetah trot, 1 phase x 50 knots, batch = 1): the reference's own use
     of the solver — one robot, one full MultiPhaseDDP::solve with the shipped ddp_setting.info
@@ -321,6 +357,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline and not args.riccati_fp32 and not args.mixed:
             out["cpu_baseline"] = cpu_baseline(args)
+        if world == 1 and args.riccati_fp32:
+            out["extra"]["full_solve"] = full_solve_c5(prob, local)
         print(json.dumps(out), flush=True)
     solver.close()
     if distributed:

@@ -724,10 +724,10 @@ DEV void fetch_cs(LdsCS<real> &S, int q, const real *rec0, const real *def0, con
 // written (and its share of the next images landed) -> the other wave's H columns read.  ib: the
 // image buffer of this knot (the next knot's go to ib ^ 1); par: which MZ image holds M (the
 // other takes Z).  Both waves run the same branch decisions (live, the PSD test) on equal values.
-template <int W, typename real>
+template <int W, bool DV, typename real>
 DEV void knot_cs(const Params &p, LdsCS<real> &S, const Lane &L, const Phase<real> &ph, const Item<real> &it, int kc,
                  real (&h)[NX], real &g, bool &live, bool first, bool more, int ib, int par, const real *nrec0,
-                 const real *ndef0, const real *nrec1, const real *ndef1)
+                 const real *ndef0, const real *nrec1, const real *ndef1, double &dvs)
 {
     constexpr int Q0 = 6 * W, Q1 = Q0 + 6;
     auto &I = S.it[L.e];
@@ -846,7 +846,7 @@ DEV void knot_cs(const Params &p, LdsCS<real> &S, const Lane &L, const Phase<rea
     // ---- PSD test + elimination on [Quu_cc | Qux_c | Qu_c] (both waves) ------------------------------
     real quxs[HC];
 #pragma unroll
-    for (int q = 0; q < HC; ++q) quxs[q] = L.row ? w2[q] : (real)0;
+    for (int q = 0; q < HC; ++q) quxs[q] = (L.row || (DV && pp == NX)) ? w2[q] : (real)0;
     pin(quxs);
     unsigned long long bad = __builtin_amdgcn_ballot_w64(zl && !(qzz > (real)1e-9));
     eliminate(w, w2, bad);
@@ -865,6 +865,12 @@ DEV void knot_cs(const Params &p, LdsCS<real> &S, const Lane &L, const Phase<rea
     real gq4[4] = {qx, 0, 0, 0};
     static_for<HC>([&](auto Q) { bfma<8>(gq4[Q & 3], kb[Q], quxs[Q]); });
     const real gq = (gq4[0] + gq4[1]) + (gq4[2] + gq4[3]);
+    if constexpr (DV) {  // as knot(): Qu_c^T dU_c on position 24, the decoupled controls' on pp < 12
+        real dq = 0;
+        static_for<HC>([&](auto Q) { bfma<8>(dq, kb[Q], quxs[Q]); });
+        const double v = pp == NX ? (double)dq : zl ? (double)quz * (double)(-(quz / qzz)) : 0.0;
+        if (st) dvs += v;
+    }
     // ---- H = Qxx + Qux_c^T K_c on this wave's columns ------------------------------------------------
     static_for<NX>([&](auto C) {
         if constexpr (cs_mine<W>(C)) h[C] = qxx[C];
@@ -880,6 +886,11 @@ DEV void knot_cs(const Params &p, LdsCS<real> &S, const Lane &L, const Phase<rea
             }
         });
     });
+    if constexpr (DV)  // (position 24's row took Qu_c through the update: not a row of H)
+        if (!L.row)
+            static_for<NX>([&](auto C) {
+                if constexpr (cs_mine<W>(C)) h[C] = 0;
+            });
     g = L.row ? gq : (real)0;
     // this wave's H columns into the M image (its column reads ended before the last barrier)
     if (L.row)
@@ -918,7 +929,6 @@ template <typename real, bool EL, bool DV, int CSW = -1, typename LdsT = Lds<rea
 DEV int sweep_pair(const Params &p, const Bufs &d, LdsT &S, const Lane &L, const Item<real> &it, double &dv)
 {
     constexpr bool CS = CSW >= 0;  // wave CSW of the column split (k_riccati_cs)
-    static_assert(!(CS && DV), "the column split sweeps with multiple shooting");
     int ib = 0, par = 0;           // (CS) image buffer, M / Z image roles
     double dvs = 0.0;
     const int pp = L.pp;
@@ -1017,8 +1027,8 @@ DEV int sweep_pair(const Params &p, const Bufs &d, LdsT &S, const Lane &L, const
             const int kn = more ? k - 1 : 0;
             const bool was = live;
             if constexpr (CS) {
-                knot_cs<CSW>(p, S, L, ph, it, k0 + k, h, g, live, k == N - 1, more, ib, par, recp(b0, kn), defp0(kn),
-                             recp(b1, kn), defp1(kn));
+                knot_cs<CSW, DV>(p, S, L, ph, it, k0 + k, h, g, live, k == N - 1, more, ib, par, recp(b0, kn),
+                                 defp0(kn), recp(b1, kn), defp1(kn), dvs);
                 ib ^= more ? 1 : 0;
                 par ^= 1;
             } else {
@@ -1225,11 +1235,11 @@ __global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
 // k_riccati for small batches (column split, launch_riccati's choice): one element pair per
 // workgroup of two waves, wave W running sweep_pair with knot_cs<W> — the same sweeps, attempts and
 // outcomes as k_riccati (each wave computes the values the other multiplies by, so both take the
-// same branches); wave 0 alone writes the element state and the retry list.  fp64, multiple
-// shooting.  At small batches k_riccati runs one wave per SIMD and its knot is one dependent chain
+// same branches); wave 0 alone writes the element state and the retry list.  fp64; DV: single
+// shooting's dV from the sweep, as k_riccati.  At small batches k_riccati runs one wave per SIMD and its knot is one dependent chain
 // of ~11 k cycles; split, each wave issues ~970 of the 1 197 VALU instructions of a knot (static
 // count of the knot loops) and the knot takes ~10 % less (sweep_split).
-template <bool EL, int W>
+template <bool EL, bool DV, int W>
 DEV void riccati_cs_wave(const Params &p, const Bufs &d, LdsCS<double> &S)
 {
     using real = double;
@@ -1262,11 +1272,12 @@ DEV void riccati_cs_wave(const Params &p, const Bufs &d, LdsCS<double> &S)
     it.K = d.K + (size_t)bv * p.Kc * KCW;
     it.dU = d.dU + (size_t)bv * p.Kc * NX;
     bool need = act, ok = false;
+    double dvk = 0.0;  // DV: Qu^T dU summed over the successful sweep
     for (int attempt = 0; __builtin_amdgcn_ballot_w64(need); ++attempt) {
         it.act = need;
         it.reg = (real)reg;
         double dv;
-        const int fk = sweep_pair<real, EL, false, W>(p, d, S, L, it, dv);
+        const int fk = sweep_pair<real, EL, DV, W>(p, d, S, L, it, dv);
         if (attempt == 0 && p.retry_cap > 0) {  // wave 0 takes the retry slots, both read them
             if (W == 0 && need && fk >= 0 && L.pp == 0) {
                 const int f = atomicAdd(d.retry_count, 1);
@@ -1279,6 +1290,7 @@ DEV void riccati_cs_wave(const Params &p, const Bufs &d, LdsCS<double> &S)
             if (fk < 0) {
                 ok = true;
                 need = false;
+                dvk = dv;
             } else {
                 const bool deferred = attempt == 0 && p.retry_cap > 0 && S.fl[L.e] < p.retry_cap;
                 if (deferred) {
@@ -1299,17 +1311,18 @@ DEV void riccati_cs_wave(const Params &p, const Bufs &d, LdsCS<double> &S)
         E.iters += 1; E.cost = ecost; E.feas = efeas; E.accepted = 0;
         E.reg = rn;
         if (!ok) { E.status = 1; E.done = 1; E.ls_active = 0; }
+        if (DV && ok) merit_step(p, E, dvk, -dvk);  // single shooting (k_riccati's epilogue)
     }
 }
 
-template <bool EL>
+template <bool EL, bool DV>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k_riccati_cs(Params p, Bufs d)
 {
     __shared__ LdsCS<double> S;
     zero_init(S, threadIdx.x & 63);
     __syncthreads();
-    if (threadIdx.x < 64) riccati_cs_wave<EL, 0>(p, d, S);
-    else riccati_cs_wave<EL, 1>(p, d, S);
+    if (threadIdx.x < 64) riccati_cs_wave<EL, DV, 0>(p, d, S);
+    else riccati_cs_wave<EL, DV, 1>(p, d, S);
 }
 
 // The retries of backward_sweep_regularized for the elements k_riccati deferred, all at once:
@@ -1412,15 +1425,15 @@ __global__ __launch_bounds__(64) void k_riccati_select(Params p, Bufs d)
     }
 }
 
-// the column split (k_riccati_cs) when its workgroups take at most one CU each (B <= 512) in fp64
-// with multiple shooting; HSDDP_SWEEP_SPLIT = 0 / 1 forces it off / on (tests, A/B).  Measured
+// the column split (k_riccati_cs) when its workgroups take at most one CU each (B <= 512), in fp64
+// (multiple or single shooting); HSDDP_SWEEP_SPLIT = 0 / 1 forces it off / on (tests, A/B).  Measured
 // (one box, sweep ms per step at B = 64 / 256 / 512 / 1024 / 2048): split 0.738 / 0.740 / 0.757 /
 // 1.075 / 1.343, one-wave 0.821 / 0.825 / 0.836 / 0.951 / 1.372 — from two workgroups per CU on,
 // the waves of one CU slow each other (the one-wave kernel too: 0.84 -> 0.95 ms from 256 to 512
 // waves at an unchanged 2.3 GHz clock), and the split's two waves per pair lose.
 static bool sweep_split(const Params &p)
 {
-    if (p.fp32 || p.ms0) return false;
+    if (p.fp32) return false;
     const char *e = std::getenv("HSDDP_SWEEP_SPLIT");
     if (e && *e) return *e != '0';
     return (p.elem_layout ? p.n_pairs : (p.B + 1) / 2) <= 256;
@@ -1443,8 +1456,13 @@ void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
     } while (0)
     if (p.fp32) HSDDP_RIC(k_riccati, g1, float);
     else if (sweep_split(p)) {
-        if (p.elem_layout) hipLaunchKernelGGL(k_riccati_cs<true>, g1, dim3(128), 0, st, p, d);
-        else hipLaunchKernelGGL(k_riccati_cs<false>, g1, dim3(128), 0, st, p, d);
+        if (p.ms0) {
+            if (p.elem_layout) hipLaunchKernelGGL((k_riccati_cs<true, true>), g1, dim3(128), 0, st, p, d);
+            else hipLaunchKernelGGL((k_riccati_cs<false, true>), g1, dim3(128), 0, st, p, d);
+        } else {
+            if (p.elem_layout) hipLaunchKernelGGL((k_riccati_cs<true, false>), g1, dim3(128), 0, st, p, d);
+            else hipLaunchKernelGGL((k_riccati_cs<false, false>), g1, dim3(128), 0, st, p, d);
+        }
     } else HSDDP_RIC(k_riccati, g1, double);
     if (p.retry_cap > 0) {
         const dim3 gr((unsigned)(p.retry_cap * (p.retry_m + (p.retry_m & 1)) / 2)), gs((unsigned)p.retry_cap);

@@ -6,8 +6,8 @@ kernel (k_riccati) / the split.  Every entry is formed by the same multiply-adds
 same order either way, so the two must agree bit for bit: trajectories, gains, dU, branch
 decisions.  Batches: B in {1, 5, 1024} (SURVEY.md §8's C1 and C2 sizes — C2 forced: it runs the
 one-wave kernel by default — and a ragged batch with an inactive half), jump phases with resets (the impact-aware value transfer at phase ends), per-element
-layouts (Bufs::pairs), failing sweeps with the parallel retries and the in-kernel regularisation
-loop, and the oracle at the small sizes.
+layouts (Bufs::pairs), single shooting (the sweep's dV), failing sweeps with the parallel retries
+and the in-kernel regularisation loop, and the oracle at the small sizes.
 """
 import numpy as np
 import pytest
@@ -44,6 +44,13 @@ def test_split_equals_one_wave_sweep(monkeypatch, B, gait, P, N):
     """Full solves (AL / ReB outer loop, early exits, graph replay) with each kernel: bit-identical."""
     prob = syn.make_batch(B, P, N, gait)
     _same(_run(monkeypatch, "1", prob), _run(monkeypatch, "0", prob))
+
+
+@pytest.mark.parametrize("gait,P,N", [("trot", 4, 50), ("jump", 8, 25)])
+def test_split_single_shooting(monkeypatch, gait, P, N):
+    """MS 0 (the sweep's dV, k_riccati_cs<EL, true>): bit-identical to the one-wave DV sweep."""
+    prob = syn.make_batch(5, P, N, gait)
+    _same(_run(monkeypatch, "1", prob, MS=0), _run(monkeypatch, "0", prob, MS=0))
 
 
 def test_split_per_element_layouts(monkeypatch):
