@@ -27,7 +27,7 @@ using namespace hkd;
 
 #ifndef HSDDP_RO_EXP
 #define HSDDP_RO_EXP 0  // timing experiments only: 1 no Defect row stores, 2 no trial U row stores (k_rollout),
-                        // 3 no running cost, 4 running cost without reference loads
+                        // 3 no running cost, 4 running cost without reference loads, 5 no control-row loads or stores
 #endif
 #ifndef HSDDP_STAMPS
 #define HSDDP_STAMPS 0
@@ -805,7 +805,11 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
     const double *x = Xt + (gc - xr0) * RS;
     // the trial control row of the slot, U = Ubar + eps du (k < N)
     double u[NU];
+#if HSDDP_RO_EXP == 5
+    for (int j = 0; j < NU; ++j) u[j] = x[j] * eps;  // timing only: no control-row loads
+#else
     trial_row(d, kubuf(nb), kqr, eps, u);
+#endif
 #if HSDDP_STAMPS
     asm volatile("" : "+v"(u[0]), "+v"(u[NU - 1]));
 #endif
@@ -813,7 +817,7 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
     // the running cost of a control slot (the terminal cost at k = N: the boundary waves)
     if (mine && k < L.N(i)) {
         d2 *ug = (d2 *)(kubuf(tb) + kq * NU);
-#if HSDDP_RO_EXP == 2
+#if HSDDP_RO_EXP == 2 || HSDDP_RO_EXP == 5
         if (u[0] == 12345.678)
 #endif
 #pragma unroll
