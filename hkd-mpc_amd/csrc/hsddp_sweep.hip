@@ -317,7 +317,8 @@ DEV void emit_Bc(real (&acc)[HC], real y6, real y7, real y8, const real *y9, con
 // Forward step j takes column j from DPP position j and eliminates it from the rows below; pivot
 // rows are kept scaled by 1 / pivot and negated, so after the back substitution w2 =
 // -Quu_cc^-1 (rhs).  The next step's pivot chain (DPP broadcast, reciprocal, Newton steps, the two
-// factors) is threaded through this step's independent multiply-adds, its operand row first.  The
+// factors) is threaded through this step's independent multiply-adds, its operand row first (the
+// scalar steps are compiler builtins: the compiler places them and their wait states).  The
 // pivots are those of the LDL^T factorisation of Quu_cc; bad: ballot of pivots <= 1e-9 (PSD test).
 template <typename real>
 DEV void eliminate(real (&w)[HC], real (&w2)[HC], unsigned long long &bad)
@@ -329,7 +330,6 @@ DEV void eliminate(real (&w)[HC], real (&w2)[HC], unsigned long long &bad)
         const real piv = row_bcast<0>(w[0]);
         bad |= __builtin_amdgcn_ballot_w64(!(piv > (real)1e-9));
         asm_rcp(r, piv);
-        asm volatile("s_nop 1" ::: "memory");
         asm_nfma1(e, piv, r);
         asm_newton(r, e);
         if constexpr (F64) {
@@ -360,7 +360,6 @@ DEV void eliminate(real (&w)[HC], real (&w2)[HC], unsigned long long &bad)
             if constexpr (nx) {
                 if constexpr (t == 1) pivn = row_bcast<(nx ? jn : 0)>(w[jn]);
                 if constexpr (t == 3) asm_rcp(rn, pivn);
-                if constexpr (t == 4 && 2 * NO <= 4) asm volatile("s_nop 1" ::: "memory");
                 if constexpr (t == 5) asm_nfma1(en, pivn, rn);
                 if constexpr (t == 7) asm_newton(rn, en);
                 if constexpr (F64 && t == 9) asm_nfma1(en, pivn, rn);

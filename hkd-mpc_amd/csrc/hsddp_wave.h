@@ -206,20 +206,23 @@ DEV void lds_add(real *p, real v)
 
 namespace hsddp {
 
-// Scalar f64 / f32 VALU operations as inline asm: emitted exactly where written among the
-// (equally volatile) DPP multiply-adds, so a dependent chain can be threaded between independent
-// instructions by hand (the Gauss-Jordan pivot chain, hsddp_sweep.hip).
-DEV void asm_rcp(double &r, double x) { asm volatile("v_rcp_f64 %0, %1" : "=v"(r) : "v"(x)); }
-DEV void asm_rcp(float &r, float x) { asm volatile("v_rcp_f32 %0, %1" : "=v"(r) : "v"(x)); }
+// The pivot chain's scalar operations (hsddp_sweep.hip, eliminate): the hardware reciprocal, the
+// Newton step's two multiply-adds and the negated product.  Round 4 wrote them as inline asm, placed
+// by hand between the (volatile, inline-asm) DPP multiply-adds; as builtins the compiler schedules
+// them and, seeing what they are, inserts only the wait states they need (the knot's s_nop count
+// 145 -> 89): the same instructions and results, C1 16.19 -> 16.0 ms, the sweep at B = 256
+// 0.743 -> 0.724 ms, B = 4096 unchanged (A/B on one box, round 5).
+DEV void asm_rcp(double &r, double x) { r = __builtin_amdgcn_rcp(x); }
+DEV void asm_rcp(float &r, float x) { r = __builtin_amdgcn_rcpf(x); }
 // e = 1 - x r
-DEV void asm_nfma1(double &e, double x, double r) { asm volatile("v_fma_f64 %0, -%1, %2, 1.0" : "=v"(e) : "v"(x), "v"(r)); }
-DEV void asm_nfma1(float &e, float x, float r) { asm volatile("v_fma_f32 %0, -%1, %2, 1.0" : "=v"(e) : "v"(x), "v"(r)); }
+DEV void asm_nfma1(double &e, double x, double r) { e = __builtin_fma(-x, r, 1.0); }
+DEV void asm_nfma1(float &e, float x, float r) { e = __builtin_fmaf(-x, r, 1.0f); }
 // r = r + r e
-DEV void asm_newton(double &r, double e) { asm volatile("v_fma_f64 %0, %0, %1, %0" : "+v"(r) : "v"(e)); }
-DEV void asm_newton(float &r, float e) { asm volatile("v_fma_f32 %0, %0, %1, %0" : "+v"(r) : "v"(e)); }
+DEV void asm_newton(double &r, double e) { r = __builtin_fma(r, e, r); }
+DEV void asm_newton(float &r, float e) { r = __builtin_fmaf(r, e, r); }
 // y = -(a b)
-DEV void asm_nmul(double &y, double a, double b) { asm volatile("v_mul_f64 %0, -%1, %2" : "=v"(y) : "v"(a), "v"(b)); }
-DEV void asm_nmul(float &y, float a, float b) { asm volatile("v_mul_f32 %0, -%1, %2" : "=v"(y) : "v"(a), "v"(b)); }
+DEV void asm_nmul(double &y, double a, double b) { y = -(a * b); }
+DEV void asm_nmul(float &y, float a, float b) { y = -(a * b); }
 
 
 // The values of x on the two 16-lane DPP rows of this lane's half-wave, at this lane's DPP
