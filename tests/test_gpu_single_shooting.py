@@ -69,6 +69,23 @@ def test_fixed_iterations_match_oracle(gait, P, N, n_iter):
     assert np.all(g["dX"] == 0)
 
 
+def test_per_element_layouts_match_oracle():
+    """MS 0 on a mixed-gait batch (config C4's per-element layouts, jumps on 8 x 25 beside 4 x 50):
+    each element's own phase walk in the sweep (Bufs::pairs), in k_rollout_ss and in the decisions."""
+    prob = syn.make_batch(6, 4, 50, "trot", mixed=True)
+    rng = np.random.default_rng(11)
+    prob["Xbar"] = prob["Xbar"] + 0.01 * rng.standard_normal(prob["Xbar"].shape)
+    kw = dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=2)
+    g = _run(prob, **kw)
+    r = O.solve_batch(prob, O.default_options(MS=0, **kw), n_threads=6)
+    p2 = dict(prob); p2["x0"] = prob["x0"] * (1 + 1e-15)
+    r2 = O.solve_batch(p2, O.default_options(MS=0, **kw), n_threads=6)
+    for f in ("Xbar", "Ubar", "K", "X", "U", "dU", "cost", "feas"):
+        assert rel(g[f], r[f]) < max(1e-9, 10 * rel(r2[f], r[f])), f
+    for f in ("iters", "status", "n_ls_trials"):
+        assert np.array_equal(g[f], r[f]), f
+
+
 @pytest.mark.parametrize("gait,P,N", [("trot", 4, 50), ("jump", 8, 25)])
 def test_full_solve_matches_oracle(gait, P, N):
     """The shipped settings with MS 0: early exits, AL / ReB outer loop, graph-replayed iterations.
