@@ -1141,26 +1141,32 @@ using namespace sweep;
 // the sweep with each element's mu, then (for an element whose first sweep fails and that the
 // parallel retry cannot take) mu = max(mu * update_regularization, 1e-3) until a sweep succeeds or
 // mu > 1e2, then mu / 20 (0 below 1e-6) as the next regularisation.
-template <typename real, bool EL, bool DV>
-__global__ __launch_bounds__(64, 2) void k_riccati(Params p, Bufs d)
+template <typename real, bool EL, bool DV, int WPB>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2))) void k_riccati(Params p, Bufs d)
 {
-    __shared__ Lds<real> S;
+    // WPB independent waves per workgroup, each with its own LDS and element pair (no barrier couples
+    // them; sweep_wpb)
+    __shared__ Lds<real> SS[WPB];
+    const int wv = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+    Lds<real> &S = SS[wv];
+    const int pair = (int)blockIdx.x * WPB + wv;
     const Lane L = make_lane();
     zero_init(S, L.lane);
 #if HSDDP_STAMPS
     if (L.lane < 12) S.st[L.lane] = 0;
 #endif
-    // the wave's two elements: 2 blockIdx + e, or a pair of elements with one layout (Bufs::pairs);
+    // the wave's two elements: 2 pair + e, or a pair of elements with one layout (Bufs::pairs);
     // an empty half runs on the other half's element, inactive
     int b, bv;
     bool valid;
     if constexpr (EL) {
-        const int e0 = d.pairs[2 * blockIdx.x], e1 = d.pairs[2 * blockIdx.x + 1];
+        if (pair >= p.n_pairs) return;
+        const int e0 = d.pairs[2 * pair], e1 = d.pairs[2 * pair + 1];
         b = L.e ? e1 : e0;
         valid = b >= 0;
         bv = valid ? b : (L.e ? e0 : e1);
     } else {
-        b = 2 * blockIdx.x + L.e;
+        b = 2 * pair + L.e;
         valid = b < p.B;
         bv = valid ? b : p.B - 1;
     }
@@ -1438,6 +1444,21 @@ static bool sweep_split(const Params &p)
     return (p.elem_layout ? p.n_pairs : (p.B + 1) / 2) <= 256;
 }
 
+// waves (element pairs) per workgroup of the one-wave sweep k_riccati in fp64: 2 while the launch has
+// at most one wave per SIMD (257 .. 1024 pairs), 1 from two waves per SIMD on; HSDDP_SWEEP_WPB = 1 / 2
+// forces it (tests, A/B).  Measured (one box, split off, sweep ms per step at B = 512 / 1024 / 2048 /
+// 4096): two per workgroup 0.866 / 0.883 / 1.29 / 1.61, one 0.812 / 0.913 / 1.36 / 1.59 — a
+// workgroup's two waves go to different SIMDs of one CU, which the single-wave workgroups of a
+// half-full launch do not reliably do.
+static int sweep_wpb(const Params &p)
+{
+    if (p.fp32) return 1;
+    const char *e = std::getenv("HSDDP_SWEEP_WPB");
+    if (e && *e) return *e == '2' ? 2 : 1;
+    const int pairs = p.elem_layout ? p.n_pairs : (p.B + 1) / 2;
+    return pairs > 256 && pairs <= 1024 ? 2 : 1;
+}
+
 void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
 {
     // (the retry list count is zeroed by the k_lq launch just before, in its first terminal task)
@@ -1453,7 +1474,19 @@ void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
             else hipLaunchKernelGGL((kern<real, false, false>), grid, dim3(64), 0, st, p, d);                  \
         }                                                                                                    \
     } while (0)
-    if (p.fp32) HSDDP_RIC(k_riccati, g1, float);
+    const int wpb = sweep_wpb(p);
+    const dim3 gw((unsigned)(((p.elem_layout ? p.n_pairs : (p.B + 1) / 2) + wpb - 1) / wpb));
+#define HSDDP_RIC_W(real, W)                                                                                   \
+    do {                                                                                                       \
+        if (p.ms0) {                                                                                           \
+            if (p.elem_layout) hipLaunchKernelGGL((k_riccati<real, true, true, W>), gw, dim3(64 * W), 0, st, p, d);  \
+            else hipLaunchKernelGGL((k_riccati<real, false, true, W>), gw, dim3(64 * W), 0, st, p, d);               \
+        } else {                                                                                               \
+            if (p.elem_layout) hipLaunchKernelGGL((k_riccati<real, true, false, W>), gw, dim3(64 * W), 0, st, p, d); \
+            else hipLaunchKernelGGL((k_riccati<real, false, false, W>), gw, dim3(64 * W), 0, st, p, d);              \
+        }                                                                                                      \
+    } while (0)
+    if (p.fp32) HSDDP_RIC_W(float, 1);
     else if (sweep_split(p)) {
         if (p.ms0) {
             if (p.elem_layout) hipLaunchKernelGGL((k_riccati_cs<true, true>), g1, dim3(128), 0, st, p, d);
@@ -1462,7 +1495,9 @@ void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)
             if (p.elem_layout) hipLaunchKernelGGL((k_riccati_cs<true, false>), g1, dim3(128), 0, st, p, d);
             else hipLaunchKernelGGL((k_riccati_cs<false, false>), g1, dim3(128), 0, st, p, d);
         }
-    } else HSDDP_RIC(k_riccati, g1, double);
+    } else if (wpb == 2) HSDDP_RIC_W(double, 2);
+    else HSDDP_RIC_W(double, 1);
+#undef HSDDP_RIC_W
     if (p.retry_cap > 0) {
         const dim3 gr((unsigned)(p.retry_cap * (p.retry_m + (p.retry_m & 1)) / 2)), gs((unsigned)p.retry_cap);
         if (p.fp32) {

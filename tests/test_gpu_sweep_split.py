@@ -95,3 +95,18 @@ def test_split_matches_oracle(monkeypatch, B, gait, P, N):
         assert err < max(1e-9, 10 * env), f
     for f in ("iters", "status", "n_ls_trials"):
         assert np.array_equal(g[f], r[f]), f
+
+
+@pytest.mark.parametrize("B,gait,P,N,mixed,ms", [(5, "trot", 4, 50, False, 1), (1024, "trot", 4, 50, False, 1),
+                                                  (7, "trot", 4, 50, True, 1), (5, "jump", 8, 25, False, 0)])
+def test_two_waves_per_workgroup_equals_one(monkeypatch, B, gait, P, N, mixed, ms):
+    """The one-wave sweep at two element pairs per workgroup (k_riccati<..., 2>, launched for 257 ..
+    1024 pairs) against one pair per workgroup, split off: bit-identical, including a workgroup whose
+    second wave has no pair (an odd pair count) and per-element layouts (Bufs::pairs)."""
+    prob = syn.make_batch(B, P, N, gait, mixed=mixed) if mixed else syn.make_batch(B, P, N, gait)
+    kw = dict(MS=ms) if ms == 0 else {}
+    monkeypatch.setenv("HSDDP_SWEEP_WPB", "2")
+    a = _run(monkeypatch, "0", prob, **kw)
+    monkeypatch.setenv("HSDDP_SWEEP_WPB", "1")
+    b = _run(monkeypatch, "0", prob, **kw)
+    _same(a, b)
