@@ -69,19 +69,20 @@ DEV float recip(float x)
     return __builtin_fmaf(r, e, r);
 }
 
-// value held by the same lane of the other half-wave (call with all 64 lanes active)
+// value held by the same lane of the other half-wave (call with all 64 lanes active; any wave of
+// a multi-wave workgroup)
 DEV double other_half(double v)
 {
     const unsigned lo = __double2loint(v), hi = __double2hiint(v);
     const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
     const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-    return threadIdx.x < 32 ? __hiloint2double(b[1], a[1]) : __hiloint2double(b[0], a[0]);
+    return (threadIdx.x & 32) == 0 ? __hiloint2double(b[1], a[1]) : __hiloint2double(b[0], a[0]);
 }
 DEV float other_half(float v)
 {
     const unsigned u = __float_as_uint(v);
     const auto a = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-    return __uint_as_float(threadIdx.x < 32 ? a[1] : a[0]);
+    return __uint_as_float((threadIdx.x & 32) == 0 ? a[1] : a[0]);
 }
 
 // sum over the 32 lanes of this lane's half-wave (every lane of the half gets it)
