@@ -51,6 +51,11 @@ namespace sweep {
 #endif
 // value update on the matrix cores (1) or by DPP-broadcast multiply-adds from the lanes holding
 // K_c (0, no LDS round trip)
+// waves per SIMD the two-pair workgroups' register budget is sized for: 1 (their launches have at
+// most one wave per SIMD: the spills go to AGPRs, not scratch)
+#ifndef SWEEP_WPB2_WPE
+#define SWEEP_WPB2_WPE 1
+#endif
 // knot images requested with the non-temporal policy (A/B experiment)
 #ifndef HSDDP_SWEEP_NT
 #define HSDDP_SWEEP_NT 0
@@ -1142,7 +1147,7 @@ using namespace sweep;
 // parallel retry cannot take) mu = max(mu * update_regularization, 1e-3) until a sweep succeeds or
 // mu > 1e2, then mu / 20 (0 below 1e-6) as the next regularisation.
 template <typename real, bool EL, bool DV, int WPB>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2))) void k_riccati(Params p, Bufs d)
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WPB == 2 ? SWEEP_WPB2_WPE : 2))) void k_riccati(Params p, Bufs d)
 {
     // WPB independent waves per workgroup, each with its own LDS and element pair (no barrier couples
     // them; sweep_wpb)
