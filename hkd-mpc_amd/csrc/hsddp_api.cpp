@@ -252,6 +252,9 @@ struct hsddp_handle_t {
     // ... and of the constraint parameters the phases carry (ReB per knot, touchdown constraints)
     double *spare_reb_delta = nullptr, *spare_reb_eps = nullptr, *spare_al_sigma = nullptr, *spare_al_lambda = nullptr;
     int *spare_td_mask = nullptr;
+    double *spare_cf_u = nullptr;
+    int *spare_cf_flag = nullptr;
+    double *shift_stage = nullptr;  // [3][B][S_cap][24] (ShiftArgs::stage), at the first stride-changing shift
     bool need_inputs = false;   // a shift changed the layout: update_problem before solving
     double *ref_table = nullptr;  // reference samples [n][RT_W] (hsddp_set_reference_table)
     int ref_n = 0;
@@ -331,7 +334,14 @@ static int dalloc(hsddp_handle h, T *&ptr, size_t n)
     if (sz == 0) sz = 16;
     hipError_t e = hipMalloc(&p, sz);
     if (e != hipSuccess) return fail(HSDDP_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
-    hipMemset(p, 0, sz);
+    // zeroed on the handle's stream once it exists: the null stream is not ordered with a
+    // non-blocking stream, so a null-stream memset of a buffer allocated mid-solve (the shift's
+    // spares) could land after the kernel that fills it
+    if (h->stream) hipMemsetAsync(p, 0, sz, h->stream);
+    else {
+        hipMemset(p, 0, sz);
+        hipStreamSynchronize(nullptr);
+    }
     h->allocs.push_back(p);
     h->bytes += sz;
     ptr = (T *)p;
@@ -398,6 +408,7 @@ static int ensure_history(hsddp_handle h)
     float *nh = nullptr;
     HIPCHK(hipMalloc(&nh, (size_t)h->p.B * cap * 4 * sizeof(float)));
     HIPCHK(hipMemset(nh, 0, (size_t)h->p.B * cap * 4 * sizeof(float)));
+    HIPCHK(hipStreamSynchronize(nullptr));  // (null-stream work is not ordered with h->stream)
     if (h->hist) {
         HIPCHK(hipStreamSynchronize(h->stream));
         hipFree(h->hist);
@@ -451,7 +462,7 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
     if ((rc = dalloc(h, contacts, B * (P + 1) * 4)) || (rc = dalloc(h, x0, B * NX)) || (rc = dalloc(h, rx, Br * S * NX)) ||
         (rc = dalloc(h, ru, Br * S * NX)) || (rc = dalloc(h, rf, Br * S * 12)) || (rc = dalloc(h, d.X3, 3 * B * S * NX)) ||
         (rc = dalloc(h, d.D3, 3 * B * S * NX)) || (rc = dalloc(h, d.U3, 3 * B * Kc * NX)) || (rc = dalloc(h, d.sel, B)) ||
-        (rc = dalloc(h, d.ovr_u, B * MOVR * 12)) ||
+        (rc = dalloc(h, d.cf_u, B * Kc * 12)) || (rc = dalloc(h, d.cf_flag, B * Kc)) ||
         (rc = dalloc(h, d.dX, B * S * NX)) ||
         (rc = dalloc(h, d.dU, B * Kc * NX)) ||
         (rc = dalloc(h, d.du, B * Kc * NX)) || (rc = dalloc(h, d.dbg, B * 16)) ||
@@ -750,23 +761,25 @@ extern "C" int hsddp_update_problem(hsddp_handle h, const int *contacts, const d
     int rc = upload_inputs(h, contacts, x0, ref_x, ref_u, ref_foot);
     if (rc) return rc;
     h->need_inputs = false;
-    // keeps Xbar / Ubar / K and the constraint parameters (HKDProblem::update's reset_params is a
-    // no-op, ConstraintsBase.h:165-167,341-348: the ReB / AL parameters carry over to the next
-    // tick); resets X, U, dX and the per-element solver state; touchdown constraints added by the
-    // shift take their legs from the new contact rows
+    // keeps Xbar / Ubar / K, the working trajectory (X, U, Defect) and the constraint objects —
+    // their ReB / AL parameters (HKDProblem::update's reset_params is a no-op, ConstraintsBase.h:
+    // 165-167,341-348) and stored values — as the reference's objects live on into the next tick;
+    // resets dX, dU and the per-element solver state; touchdown constraints added by the shift take
+    // their legs from the new contact rows
     return reset_working(h, false);
 }
 
-// the working trajectory restarts at the warm start (X = Xbar, U = Ubar, dX = du = dU = Defect = 0,
-// per-element solver state cleared); params: the ReB / AL parameters and touchdown constraints
-// return to their initial values (a new problem) — else they are kept.  Pending touchdown masks
-// are resolved from the contact rows either way.
+// params (a new problem: hsddp_upload_warm_start): the working trajectory restarts at the warm
+// start (X = Xbar, U = Ubar, Defect = 0), the ReB / AL parameters and touchdown constraints return
+// to their initial values and the constraint values to zero — else all of them are kept.  Either
+// way dX = du = dU = 0 (the next initial rollout multiplies them by eps = 0), the per-element solver
+// state is cleared and pending touchdown masks are resolved from the contact rows.
 static int reset_working(hsddp_handle h, bool params)
 {
     const Params &p = h->p;
     const size_t B = p.B, S = p.S, Kc = p.Kc;
     Bufs &d = h->d;
-    launch_reset_working(p, d, h->stream);  // X = Xbar, U = Ubar (one buffer), Defect = 0
+    if (params) launch_reset_working(p, d, h->stream);  // X = Xbar, U = Ubar (one buffer), Defect = 0
     HIPCHK(hipMemsetAsync(d.dX, 0, B * S * NX * sizeof(double), h->stream));
     HIPCHK(hipMemsetAsync(d.du, 0, B * Kc * NX * sizeof(double), h->stream));
     HIPCHK(hipMemsetAsync(d.dU, 0, B * Kc * NX * sizeof(double), h->stream));
@@ -860,9 +873,71 @@ extern "C" int hsddp_download_constraint_params(hsddp_handle h, double *reb_delt
     const Bufs &d = h->d;
     if (reb_delta) HIPCHK(hipMemcpy(reb_delta, d.reb_delta, nr * sizeof(double), hipMemcpyDeviceToHost));
     if (reb_eps) HIPCHK(hipMemcpy(reb_eps, d.reb_eps, nr * sizeof(double), hipMemcpyDeviceToHost));
-    if (td_legs) HIPCHK(hipMemcpy(td_legs, d.td_mask, nt * sizeof(int), hipMemcpyDeviceToHost));
+    if (td_legs) {
+        HIPCHK(hipMemcpy(td_legs, d.td_mask, nt * sizeof(int), hipMemcpyDeviceToHost));
+        for (size_t q = 0; q < nt; ++q) td_legs[q] &= 15;  // (legs only: TD_STALE is the device's)
+    }
     if (al_sigma) HIPCHK(hipMemcpy(al_sigma, d.al_sigma, nt * 4 * sizeof(double), hipMemcpyDeviceToHost));
     if (al_lambda) HIPCHK(hipMemcpy(al_lambda, d.al_lambda, nt * 4 * sizeof(double), hipMemcpyDeviceToHost));
+    return HSDDP_OK;
+}
+
+// The stored constraint values, formed on the host from what the device keeps (hsddp_internal.h):
+// a knot's GRF values from its cf_u forces where cf_flag is set, else from its working control row;
+// a touchdown constraint's residual is 0 while TD_STALE, else its phase end's (term_h, written by
+// the last rollout or divergence fix-up from the working X_i[N]).
+extern "C" int hsddp_download_constraint_values(hsddp_handle h, double *grf_g, double *td_h)
+{
+    if (!h) return fail(HSDDP_ERR_ARG, "null handle");
+    if (!h->have_problem) return fail(HSDDP_ERR_ARG, "upload the problem first");
+    if (grf_g && !h->contacts_current) return fail(HSDDP_ERR_ARG, "no contacts of this layout on the handle");
+    const Params &p = h->p;
+    const size_t B = p.B, Kc = p.Kc, P = p.P;
+    int rc;
+    std::vector<ElemState> el(B);
+    HIPCHK(hipSetDevice(h->desc.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipMemcpy(el.data(), h->d.el, B * sizeof(ElemState), hipMemcpyDeviceToHost));
+    if (grf_g) {
+        std::vector<double> U(B * Kc * NX), cfu(B * Kc * 12);
+        std::vector<int> cff(B * Kc);
+        if ((rc = hsddp_download_working(h, nullptr, U.data(), nullptr, nullptr, nullptr))) return rc;
+        HIPCHK(hipMemcpy(cfu.data(), h->d.cf_u, cfu.size() * sizeof(double), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(cff.data(), h->d.cf_flag, cff.size() * sizeof(int), hipMemcpyDeviceToHost));
+        std::fill(grf_g, grf_g + B * Kc * 20, 0.0);
+        for (size_t b = 0; b < B; ++b) {
+            const Layout L = layout_of(h, b);
+            for (int i = 0; i < L.P; ++i)
+                for (int k = 0; k < L.N[i]; ++k) {
+                    const size_t q = b * Kc + L.k0[i] + k;
+                    const double *f = (el[b].ovr && cff[q]) ? &cfu[q * 12] : &U[q * NX];
+                    for (int l = 0; l < 4; ++l) {
+                        if (!h->contacts[(b * (P + 1) + i) * 4 + l]) continue;
+                        const double *fl = f + 3 * l;
+                        double *g = grf_g + q * 20 + 5 * l;  // GRFConstraint rows (HKDConstraints.cpp:15-22)
+                        g[0] = fl[2];
+                        g[1] = -fl[0] + p.mu * fl[2];
+                        g[2] = fl[0] + p.mu * fl[2];
+                        g[3] = -fl[1] + p.mu * fl[2];
+                        g[4] = fl[1] + p.mu * fl[2];
+                    }
+                }
+        }
+    }
+    if (td_h) {
+        std::vector<int> mask(B * P * MTD);
+        std::vector<double> th(B * P * 4);
+        HIPCHK(hipMemcpy(mask.data(), h->d.td_mask, mask.size() * sizeof(int), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(th.data(), h->d.term_h, th.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (size_t b = 0; b < B; ++b)
+            for (size_t i = 0; i < P; ++i)
+                for (int j = 0; j < MTD; ++j) {
+                    const int m = mask[(b * P + i) * MTD + j];
+                    for (int l = 0; l < 4; ++l)
+                        td_h[((b * P + i) * MTD + j) * 4 + l] =
+                            ((m >> l) & 1) && !(m & TD_STALE) ? th[(b * P + i) * 4 + l] : 0.0;
+                }
+    }
     return HSDDP_OK;
 }
 
@@ -1459,6 +1534,7 @@ extern "C" int hsddp_set_value_export(hsddp_handle h, int on)
         const size_t n = (size_t)h->p.B * HSDDP_MAX_PHASES * (NX + NN);
         HIPCHK(hipMalloc(&h->value0, n * sizeof(double)));
         HIPCHK(hipMemset(h->value0, 0, n * sizeof(double)));
+        HIPCHK(hipStreamSynchronize(nullptr));
         h->bytes += n * sizeof(double);
         h->d.value0 = h->value0;
     }
@@ -1915,7 +1991,8 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
         if ((rc = dalloc(h, h->spare_reb_delta, B * p.Kc * 20)) || (rc = dalloc(h, h->spare_reb_eps, B * p.Kc * 20)) ||
             (rc = dalloc(h, h->spare_al_sigma, B * HSDDP_MAX_PHASES * MTD * 4)) ||
             (rc = dalloc(h, h->spare_al_lambda, B * HSDDP_MAX_PHASES * MTD * 4)) ||
-            (rc = dalloc(h, h->spare_td_mask, B * HSDDP_MAX_PHASES * MTD)))
+            (rc = dalloc(h, h->spare_td_mask, B * HSDDP_MAX_PHASES * MTD)) ||
+            (rc = dalloc(h, h->spare_cf_u, B * p.Kc * 12)) || (rc = dalloc(h, h->spare_cf_flag, B * p.Kc)))
             return rc;
     }
     char *buf;
@@ -1933,13 +2010,16 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     // the constraint parameters first (they read the old layout's strides)
     ShiftParamArgs pa;
     pa.Kc = p.Kc; pa.P_old = p.P; pa.P_new = Pnew;
-    pa.rmap = drm; pa.pmap = dpm; pa.nadd = dna;
+    pa.rmap = drm; pa.cmap = dcm; pa.pmap = dpm; pa.nadd = dna;
     pa.map_id = nk > 1 ? did : nullptr;
     pa.reb_delta0 = p.grf_delta; pa.reb_eps0 = p.grf_eps; pa.td_sigma0 = p.td_sigma; pa.td_lambda0 = p.td_lambda;
     pa.overflow = d.counter + 6;
     HIPCHK(hipMemsetAsync(d.counter + 6, 0, sizeof(int), h->stream));
-    launch_shift_params(p.B, pa, d, h->spare_reb_delta, h->spare_reb_eps, h->spare_al_sigma, h->spare_al_lambda,
-                        h->spare_td_mask, h->stream);
+    ShiftParamOut po;
+    po.reb_delta = h->spare_reb_delta; po.reb_eps = h->spare_reb_eps; po.al_sigma = h->spare_al_sigma;
+    po.al_lambda = h->spare_al_lambda; po.td_mask = h->spare_td_mask; po.cf_u = h->spare_cf_u;
+    po.cf_flag = h->spare_cf_flag;
+    launch_shift_params(p.B, pa, d, po, h->stream);
     HIPCHK(hipMemcpyAsync(h->host_counter + 6, d.counter + 6, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     ShiftArgs a;
     a.S_old = p.S; a.S_new = Snew; a.Kc = p.Kc;
@@ -1947,7 +2027,12 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     a.map_id = nk > 1 ? did : nullptr;
     a.fp32 = p.fp32;
     a.zero_u0 = 1;  // trajectory_ptrs.front()->Ubar[0].setZero() (HKDProblem.cpp:219)
-    launch_shift_gather(p.B, a, d, h->spare_K, h->stream);  // (and sel: the third buffers)
+    a.stage = nullptr;
+    if (Snew != p.S) {
+        if (!h->shift_stage && (rc = dalloc(h, h->shift_stage, 3 * B * h->S_cap * NX))) return rc;
+        a.stage = h->shift_stage;
+    }
+    launch_shift_gather(p.B, a, d, h->spare_K, h->stream);  // (working rows and sel too)
     HIPCHK(hipGetLastError());
     // defer (hsddp_advance, one layout for the batch): the caller's host work runs under the gather;
     // everything after it is ordered on the handle's stream
@@ -1958,6 +2043,8 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     std::swap(d.al_sigma, h->spare_al_sigma);
     std::swap(d.al_lambda, h->spare_al_lambda);
     std::swap(d.td_mask, h->spare_td_mask);
+    std::swap(d.cf_u, h->spare_cf_u);
+    std::swap(d.cf_flag, h->spare_cf_flag);
     const bool td_overflow = !async && h->host_counter[6] != 0;
     if (p.fp32) { float *t = d.K32; d.K32 = (float *)h->spare_K; h->spare_K = t; }
     else { double *t = d.K; d.K = (double *)h->spare_K; h->spare_K = t; }

@@ -106,16 +106,14 @@ DEV double *dbuf(const Bufs &d, int q) { return d.D3 + (size_t)q * d.xs3; }
 DEV double *ubuf(const Bufs &d, int q) { return d.U3 + (size_t)q * d.us3; }
 
 // the control forces element b's stored GRF constraint values at control knot kc come from: the
-// older forces of an ElemState::ovr_kc entry (Bufs::ovr_u), or nullptr — the control row's own.
+// knot's own entry of Bufs::cf_u where its cf_flag is set, or nullptr — the working control row's.
 // (A pointer, not a copy: the callers read a leg's three forces where they use them, so the
 // common case keeps no second force vector in registers.)
 DEV const double *constraint_forces(const Bufs &d, const ElemState &E, int b, int kc)
 {
-    const int n = E.ovr_n;
-    const double *o = nullptr;
-    for (int j = 0; j < n; ++j)
-        if (E.ovr_kc[j] == kc) o = d.ovr_u + ((size_t)b * MOVR + j) * 12;
-    return o;
+    if (!E.ovr) return nullptr;
+    const size_t q = (size_t)b * kparams()->Kc + kc;
+    return d.cf_flag[q] ? d.cf_u + q * 12 : nullptr;
 }
 // force a of leg lg for the GRF constraint rows: the control row's, or the older ones (ovr)
 DEV double grf_force(const double *u, const double *ovr, int i) { return ovr ? ovr[i] : u[i]; }
@@ -261,7 +259,7 @@ DEV void merit_step(const Params &p, ElemState &E, double w1, double w2)
 }
 
 // the legs of the phase's touchdown constraints (union of the slot masks; TD_PENDING slots are
-// resolved before any solve)
+// resolved before any solve; TD_STALE is not a leg)
 DEV unsigned td_union(const int *mask)
 {
     unsigned u = 0;
@@ -282,8 +280,11 @@ DEV int td_bits(const int *c, const int *cn)
 // (hkd_foot_height_grad - ground; any value for other legs), and max |h|.  The AL terms are
 // summed per touchdown constraint (slot j: legs mask[j], parameters sig / lam [j][4]) and added
 // constraint by constraint, as update_terminal_cost_with_tconstr (SinglePhase.cpp:402-411).
+// stored: the constraints' stored residuals (a TD_STALE constraint's is 0), as compute_cost reads
+// them; else h as a rollout that completes the phase computes it for every constraint.
 DEV double terminal_cost_h(const Params &p, const int *c, const double *x, const double *xr, const double *pf,
-                           const int *mask, const double *sig, const double *lam, const double *hl, double &tviol)
+                           const int *mask, const double *sig, const double *lam, const double *hl, double &tviol,
+                           bool stored = true)
 {
     double phi = 0.0, fc = 0.0;
 #pragma unroll
@@ -301,12 +302,13 @@ DEV double terminal_cost_h(const Params &p, const int *c, const double *x, const
     double tv = 0.0;
     for (int q = 0; q < MTD; ++q) {
         const int m = mask[q];
-        if (!m) continue;
+        if (!(m & 15)) continue;
+        const bool zero = stored && (m & TD_STALE);
         double al = 0.0;
 #pragma unroll
         for (int l = 0; l < 4; ++l) {
             if (!((m >> l) & 1)) continue;
-            const double h = hl[l];
+            const double h = zero ? 0.0 : hl[l];
             tv = fmax(tv, fabs(h));
             al += 0.5 * sig[4 * q + l] * h * h;
             al += lam[4 * q + l] * h;
@@ -317,14 +319,16 @@ DEV double terminal_cost_h(const Params &p, const int *c, const double *x, const
     return phi;
 }
 
-// terminal cost Phi (tracking Qf + 10 * foot + AL), max |h| and h per constraint leg
+// terminal cost Phi (tracking Qf + 10 * foot + AL), max |h| and h per constraint leg (stored:
+// terminal_cost_h)
 DEV double terminal_cost(const Params &p, const int *c, const double *x, const double *xr, const double *pf,
-                         const int *mask, const double *sig, const double *lam, double &tviol, double *h_out)
+                         const int *mask, const double *sig, const double *lam, double &tviol, double *h_out,
+                         bool stored)
 {
     const unsigned u = td_union(mask);
 #pragma unroll
     for (int l = 0; l < 4; ++l) h_out[l] = ((u >> l) & 1) ? hkd_foot_height_grad(l, x, nullptr) - p.ground : 0.0;
-    return terminal_cost_h(p, c, x, xr, pf, mask, sig, lam, h_out, tviol);
+    return terminal_cost_h(p, c, x, xr, pf, mask, sig, lam, h_out, tviol, stored);
 }
 
 

@@ -8,7 +8,9 @@
 //   lq                                [B][Kc][LQW]    compact LQ model of one knot (below)
 //   term                              [B][P][TW]      Phix | Phixx | Px (reset-map Jacobian at X_i[N])
 //   reb_delta, reb_eps                [B][Kc][20]     ReB params, index leg*5 + row
-//   td_mask                           [B][P][MTD]     touchdown constraints of each phase (bit l = leg l)
+//   td_mask                           [B][P][MTD]     touchdown constraints of each phase (bit l = leg l;
+//                                                     TD_PENDING, TD_STALE below)
+//   cf_u, cf_flag                     [B][Kc][12], [B][Kc]  stored GRF values not from U (below)
 //   al_sigma, al_lambda               [B][P][MTD][4]  their AL parameters, per constraint and leg
 //   term_h                            [B][P][4]       foot heights at the phase end (constraint legs)
 //   slot_cost, slot_feas, slot_viol   [B][S]          per-slot partial sums for per-element reductions
@@ -120,21 +122,29 @@ struct RetryEntry {
     double reg;
 };
 
-// Constraint values older than the working rows (a diverged trial, SinglePhase.cpp:205-208): the
-// rollout returns before compute_path_constraints at the knot whose simulated state breaks the
-// 1e6 bound, so the GRF constraint data of that knot keep the values of an earlier control row
-// while U[k] is the trial's.  Up to MOVR such knots per element, each with the control forces its
-// stored constraint values come from (Bufs::ovr_u); every later cost, LQ and ReB update there uses
-// them (ElemState::ovr_kc; ascending).  A rollout that passes a knot refreshes it.
-constexpr int MOVR = 8;
+// The constraint objects' stored values (IneqConstrData::g, TConstrData::h; ConstraintsBase.h:
+// 12-55) live on from trial to trial and from solve to solve.  A rollout that returns at the knot
+// whose simulated state breaks the 1e6 bound (SinglePhase.cpp:205-208) computes no constraint
+// value from there on, and a new problem, a pushed-back knot and a new touchdown constraint start
+// from zero (create_data, PathConstraintBase::push_back).  Stored explicitly only where they are
+// not a function of the working rows:
+//  * GRF (g = A_leg f): Bufs::cf_flag[b][kc] = 1 when the stored values of control knot kc come
+//    from the forces Bufs::cf_u[b][kc] (the break knot's earlier control row; zeros for a new
+//    problem) rather than from the working control row U[kc];
+//  * touchdown (h = foot height at X_i[N] - ground): a constraint whose h was never computed since
+//    it was registered (0) carries TD_STALE in its td_mask entry; every other one's h is that of
+//    the working X_i[N] (the rollout that computes h also sets X_i[N], SinglePhase.cpp:196-227).
+// ElemState::ovr / td_stale: some flag of the element may be set (the kernels read the per-knot
+// flags only then); both survive k_reset_elements.  A rollout that passes knot kc / completes
+// phase i clears its flags (k_decide).
+constexpr int TD_STALE = 0x20;
 
 struct ElemState {
     double cost, feas, merit, merit_rho, dV1, dV2, reg;
     double max_t, max_p, max_t_prev, max_p_prev, cost_prev, merit_prev, feas_prev;
     int done, inner_done, ls_active, accepted, status, iters, outer_iters, n_ls;
     int hist_n;  // entries pushed to the solver-info history (MultiPhaseDDP.cpp:277-280, 368-371)
-    int ovr_n;   // knots with older constraint values (MOVR)
-    int ovr_kc[MOVR];
+    int ovr, td_stale;  // (above; persistent across solves)
 };
 
 struct Bufs {
@@ -153,7 +163,8 @@ struct Bufs {
     size_t xs3, us3;                       // set strides (doubles): B x S_cap x 24, B x Kc x 24
     int rows3, urows3;                     // the same in rows: B x S_cap, B x Kc
     int *sel;                              // [B]
-    double *ovr_u;                         // [B][MOVR][12] control forces of ElemState::ovr_kc
+    double *cf_u;                          // [B][Kc][12] forces of the stored GRF values where cf_flag
+    int *cf_flag;                          // [B][Kc] (above)
     double *K, *lq, *term;
     double *reb_delta, *reb_eps, *al_sigma, *al_lambda, *term_h;
     int *td_mask;                          // [B][P][MTD] (0: no constraint in that slot)

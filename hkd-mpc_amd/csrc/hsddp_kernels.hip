@@ -220,8 +220,9 @@ DEV void terminal_task(const Params &p, const Bufs &d, TermLds &S, int task, int
             for (int q = 0; q < MTD; ++q)
                 if ((smask[q] >> l) & 1) {
                     const double sg = ssl[4 * q + l], lm = ssl[MTD * 4 + 4 * q + l];
-                    c0 += sg * h + lm;
-                    c1 += sg * (1 + h) + lm;
+                    const double hq = (smask[q] & TD_STALE) ? 0.0 : h;  // the constraint's stored h
+                    c0 += sg * hq + lm;
+                    c1 += sg * (1 + hq) + lm;
                 }
         scoef[l][0] = c0;
         scoef[l][1] = c1;
@@ -522,15 +523,19 @@ DEV void finish_defect(const Params &p, const Bufs &d, int b, int s, int k, cons
     d.slot_div[sb + s] = (k > 0 && sqrt(nrm) > 1e6) ? 1 : 0;
 }
 
-// the terminal cost of phase i at its last slot s (x = X[N]) with its violation and touchdown residuals
-DEV void finish_terminal(const Params &p, const Bufs &d, int b, int s, int i, const int *c, const int *cn, const double *x)
+// the terminal cost of phase i at its last slot s (x = X[N]) with its violation and touchdown
+// residuals; stored: with the constraints' stored residuals (a phase the rollout did not complete),
+// else as a rollout completing the phase computes them
+DEV void finish_terminal(const Params &p, const Bufs &d, int b, int s, int i, const int *c, const int *cn, const double *x,
+                         bool stored = false)
 {
     const size_t sb = (size_t)b * p.S;
     const double *xr = ref_ptr(p, d.ref_x, b, s, NX), *pf = ref_ptr(p, d.ref_foot, b, s, 12);
     double tv, h[4];
     const size_t q = ((size_t)b * p.P + i) * MTD;
     (void)cn;
-    d.slot_cost[sb + s] = terminal_cost(p, c, x, xr, pf, d.td_mask + q, d.al_sigma + q * 4, d.al_lambda + q * 4, tv, h);
+    d.slot_cost[sb + s] = terminal_cost(p, c, x, xr, pf, d.td_mask + q, d.al_sigma + q * 4, d.al_lambda + q * 4, tv, h,
+                                        stored);
     d.slot_viol[sb + s] = tv;
 #pragma unroll
     for (int l = 0; l < 4; ++l) d.term_h[((size_t)b * p.P + i) * 4 + l] = h[l];
@@ -1065,8 +1070,10 @@ __global__ __launch_bounds__(64) void k_rollout_ss(Params p, Bufs d, double eps,
 // trial, the GRF constraint values of knot k stay those of its earlier control row, and the cost
 // and feasibility that follow (:116-117) are sums over those mixed rows.  The slot kernels computed
 // every slot; here the element's 16 lanes (g) copy the working rows the reference keeps into the
-// trial buffer, record the break knot's older constraint forces (ElemState::ovr_kc), and recompute
-// the slot outputs from the break knot on.  No cross-lane operation (the caller's lanes diverge).
+// trial buffer, update the stored GRF values' table (Bufs::cf_flag / cf_u: the knots before the
+// break now hold the trial's values, the break knot keeps its earlier ones, the later knots are
+// untouched) and recompute the slot outputs from the break knot on.  No cross-lane operation (the
+// caller's lanes diverge).
 template <bool EL>
 DEV void diverged_fixup(const Params &p, const Bufs &d, const LayT<EL> &L, int b, int g, int sbrk)
 {
@@ -1083,31 +1090,18 @@ DEV void diverged_fixup(const Params &p, const Bufs &d, const LayT<EL> &L, int b
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
     ElemState &E = d.el[b];
+    // the knots before the break were passed: their stored values are the trial's (flags cleared);
+    // the break knot's stay what they were — the forces of its entry if it has one, else those of
+    // its working control row (the one U[kcb] held before this trial), which becomes its entry
+    int *cf = d.cf_flag + kq;
+    if (E.ovr)
+        for (int kc = g; kc < kcb; kc += 16) cf[kc] = 0;
     if (g == 0) {
-        // knots before the break were passed (their constraint values are the trial's): dropped;
-        // the break knot keeps an entry it has, or gets one with its working control forces
-        int n = 0;
-        bool have = false;
-        for (int j = 0; j < E.ovr_n; ++j) {
-            const int kc = E.ovr_kc[j];
-            if (kc < kcb) continue;
-            have = have || kc == kcb;
-            if (n != j) {
-                E.ovr_kc[n] = kc;
-                for (int r = 0; r < 12; ++r) d.ovr_u[((size_t)b * MOVR + n) * 12 + r] = d.ovr_u[((size_t)b * MOVR + j) * 12 + r];
-            }
-            ++n;
+        if (!(E.ovr && cf[kcb])) {
+            for (int r = 0; r < 12; ++r) d.cf_u[(kq + kcb) * 12 + r] = UW[(kq + kcb) * NX + r];
+            cf[kcb] = 1;
         }
-        if (!have && (c[0] + c[1] + c[2] + c[3]) > 0) {  // (a phase without stance legs has no GRF rows)
-            if (n == MOVR) {  // more knots with older constraint values than the table holds
-                E.status = 2; E.done = 1; E.ls_active = 0;
-            } else {
-                E.ovr_kc[n] = kcb;
-                for (int r = 0; r < 12; ++r) d.ovr_u[((size_t)b * MOVR + n) * 12 + r] = UW[(kq + kcb) * NX + r];
-                ++n;
-            }
-        }
-        E.ovr_n = n;
+        E.ovr = 1;
     }
     __threadfence();  // rows and table visible to the other lanes of the element
     // slot outputs over the mixed rows: |Defect|^2 of phase i on, costs from the break knot on
@@ -1128,7 +1122,7 @@ DEV void diverged_fixup(const Params &p, const Bufs &d, const LayT<EL> &L, int b
         // kernel's registers; the arithmetic is the slot kernels')
         const double *x = XT + (sb + s) * NX;
         if (k == L.N(ip)) {
-            finish_terminal(p, d, b, s, ip, c, cn, x);
+            finish_terminal(p, d, b, s, ip, c, cn, x, true);
             continue;
         }
         const int kc = L.k0(ip) + k;
@@ -1200,6 +1194,15 @@ DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int 
             if (g >= ibrk) { pv = 0.0; tv = 0.0; }  // phases from the break on: not reached
         }
     }
+    if (act) {
+        const ElemState &Er = d.el[b];
+        // a rollout that passed every knot computed every stored GRF value from its rows
+        if (!dvg && Er.ovr)
+            for (int kc = g; kc < p.Kc; kc += 16) d.cf_flag[(size_t)b * p.Kc + kc] = 0;
+        // the phases it completed computed their touchdown residuals
+        if (Er.td_stale && g < P && g < ibrk)
+            for (int j = 0; j < MTD; ++j) d.td_mask[((size_t)b * p.P + g) * MTD + j] &= ~TD_STALE;
+    }
     for (int i = 0; i < p.P; ++i) {  // uniform bound (lanes g >= P add exact zeros)
         cost += __shfl(ci, base + i);
         feas += __shfl(fi, base + i);
@@ -1211,8 +1214,7 @@ DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int 
     feas = sqrt(feas);
     E.max_p = max_p;
     E.max_t = max_t;
-    // a rollout that passed every knot refreshed every constraint value
-    if (!dvg && E.ovr_n) E.ovr_n = 0;
+    if (!dvg) { E.ovr = 0; E.td_stale = 0; }  // (their flags cleared above)
     // one entry of the solver-info buffers (cost_buffer, dyn_feas_buffer, eqn_feas_buffer,
     // ineq_feas_buffer; MultiPhaseDDP.cpp:277-280, 368-371), float as the reference's vectors
     auto push_info = [&]() {
@@ -1244,8 +1246,7 @@ DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int 
         d.sel[b] = sel_code(nb, tb);
         if (last) { E.accepted = 0; E.ls_active = 0; E.cost = E.cost_prev; E.merit = E.merit_prev; fin = true; }
     }
-    if (E.done) fin = false;  // (the constraint-value table overflowed: status 2)
-    if (!fin && !E.done && tix >= 0 && tix < LS_LIVE) d.ls_live[tix] = 1;  // still searching (same value from every writer)
+    if (!fin && tix >= 0 && tix < LS_LIVE) d.ls_live[tix] = 1;  // still searching (same value from every writer)
     if (fin) {
         // the later-termination test breaks before the iteration's entry is buffered (:358-371)
         if (!p.no_early_exit && fabs((E.cost_prev - E.cost) / E.cost_prev) < p.cost_thresh && E.feas <= p.feas_thresh)
@@ -1401,7 +1402,8 @@ __global__ void k_outer_end(Params p, Bufs d)
                 const int m = d.td_mask[((size_t)b * p.P + i) * MTD + j];
                 for (int l = 0; l < 4; ++l) {
                     if (!((m >> l) & 1)) continue;
-                    const double h = d.term_h[((size_t)b * p.P + i) * 4 + l];
+                    // the constraint's stored h: 0 when never computed since it was registered
+                    const double h = (m & TD_STALE) ? 0.0 : d.term_h[((size_t)b * p.P + i) * 4 + l];
                     const size_t q = (((size_t)b * p.P + i) * MTD + j) * 4 + l;
                     if (fabs(h) < p.tconstr_thresh) continue;
                     if (fabs(h) > 0.005) {
@@ -1425,7 +1427,10 @@ __global__ void k_reset_elements(Params p, Bufs d)
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= p.B) return;
     ElemState &E = d.el[b];
+    const int ovr = E.ovr, tds = E.td_stale;  // (the constraint objects outlive the solve)
     E = ElemState{};
+    E.ovr = ovr;
+    E.td_stale = tds;
 }
 
 __global__ __launch_bounds__(256) void k_init_params(Params p, Bufs d)
@@ -1435,7 +1440,12 @@ __global__ __launch_bounds__(256) void k_init_params(Params p, Bufs d)
     if (gid < (long)p.B * p.P * MTD * 4) { d.al_sigma[gid] = p.td_sigma; d.al_lambda[gid] = p.td_lambda; }
     // one touchdown constraint per phase towards the next phase's contact (HKDProblem::
     // initialization's add_tconstr_one_phase, HKDProblem.cpp:104), resolved from the contact rows
-    if (gid < (long)p.B * p.P * MTD) d.td_mask[gid] = gid % MTD == 0 ? TD_PENDING : 0;
+    if (gid < (long)p.B * p.P * MTD) d.td_mask[gid] = gid % MTD == 0 ? TD_PENDING | TD_STALE : 0;
+    // a new problem's constraint values are zero (create_data, ConstraintsBase.h:26-34, 50-54):
+    // every knot's GRF values from zero forces, every touchdown h zero (TD_STALE above)
+    if (gid < (long)p.B * p.Kc * 12) d.cf_u[gid] = 0.0;
+    if (gid < (long)p.B * p.Kc) d.cf_flag[gid] = 1;
+    if (gid < (long)p.B) { d.el[gid].ovr = 1; d.el[gid].td_stale = 1; }
 }
 
 // Px rows 0 .. 11 of every terminal record slot (the allocation's B x MAXP, whatever the
@@ -1459,10 +1469,11 @@ __global__ __launch_bounds__(256) void k_resolve_td(Params p, Bufs d)
     const int b = (int)(gid / ((long)p.P * MTD)), i = (int)(gid / MTD % p.P);
     int &m = d.td_mask[gid];
     if (i >= layout_of<EL>(d, b).P()) { m = 0; return; }
-    if (m != TD_PENDING) return;
+    if (!(m & TD_PENDING)) return;
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
-    m = td_bits(c, cn);
+    const int legs = td_bits(c, cn);
+    m = legs ? legs | (m & TD_STALE) : 0;
 }
 
 // which: 0 = elements with ls_active, 1 = elements still iterating (!done && !inner_done), 2 = !done

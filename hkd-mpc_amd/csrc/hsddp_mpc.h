@@ -25,23 +25,35 @@ struct ShiftArgs {
     const int *smap, *cmap;   // [n_maps][S_new], [n_maps][Kc] device
     const int *map_id;        // [B] map of each element (null: one map for the batch)
     int fp32, zero_u0;
+    // [3][B][S_old][24] staging (the state rows' element stride changes, S_new != S_old): the
+    // nominal X, working X and working Defect rows are copied here first, and the gathers read them
+    // from here — written in place at the new stride, element b's rows would overlap the old rows
+    // of its neighbours in a buffer another element still reads (every element picks its own
+    // buffers); null: the strides agree and every element's rows stay inside its own region
+    double *stage;
 };
-// the new Xbar / Ubar rows into every element's third buffer, which becomes its nominal and working
-// one; the new compact K rows into K_new
+// the new Xbar / Ubar rows into every element's third buffer, which becomes its nominal one; the
+// working rows (X, U, Defect) follow into the same buffer when they are the nominal ones, else into
+// the old nominal buffer (read by then), which becomes the working one; the new compact K rows into K_new
 void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, void *K_new, hipStream_t st);
-// constraint parameters through the shift: ReB rows by control-slot source (rmap: old slot, -1 =
-// initial), touchdown constraints by phase source (pmap: old phase, -1 = new) plus nadd appended
-// pending ones per new phase; overflow counts phases past MTD constraints
+// constraint objects through the shift: ReB rows by control-slot source (rmap: old slot, -1 =
+// initial), the stored GRF values' table by control-slot source (cmap: old slot, -1 = a new knot,
+// whose zero values are its zero working row's), touchdown constraints by phase source (pmap: old
+// phase, -1 = new) plus nadd appended pending ones per new phase (zero residual: TD_STALE);
+// overflow counts phases past MTD constraints
 struct ShiftParamArgs {
     int Kc, P_old, P_new;
-    const int *rmap;          // [n_maps][Kc]
+    const int *rmap, *cmap;   // [n_maps][Kc]
     const int *pmap, *nadd;   // [n_maps][MAXP]
     const int *map_id;        // [B] (null: one map)
     double reb_delta0, reb_eps0, td_sigma0, td_lambda0;
     int *overflow;
 };
-void launch_shift_params(int B, const ShiftParamArgs &a, const Bufs &d, double *reb_delta, double *reb_eps,
-                         double *al_sigma, double *al_lambda, int *td_mask, hipStream_t st);
+struct ShiftParamOut {
+    double *reb_delta, *reb_eps, *al_sigma, *al_lambda, *cf_u;
+    int *td_mask, *cf_flag;
+};
+void launch_shift_params(int B, const ShiftParamArgs &a, const Bufs &d, const ShiftParamOut &o, hipStream_t st);
 
 // reference sample table on the device: [n][RT_W] doubles per sample
 constexpr int RT_BODY = 0, RT_QJ = 12, RT_QJD = 24, RT_FOOT = 36, RT_GRF = 48, RT_C = 60, RT_W = 64;

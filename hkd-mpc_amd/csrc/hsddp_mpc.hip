@@ -10,7 +10,8 @@
 //   k_shift_gather       HKDProblem::update's trajectory edits (HKDProblem.cpp:117-222): the
 //                        warm start (Xbar, Ubar, K) re-laid for the shifted phases — dropped
 //                        front knots / phases, pushed-back copies of X.back(), zero new phases —
-//                        as one gather over (element, new slot, entry) from host-built slot maps.
+//                        as one gather over (element, new slot, entry) from host-built slot maps;
+//                        k_shift_gather_work then the working rows (X, U, Defect) alike.
 #include "../../include/hsddp.h"
 #include "hsddp_device.h"
 #include "hsddp_mpc.h"
@@ -97,6 +98,29 @@ __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdA
 // multiples of 4) of the new Xbar / Ubar rows and compact K rows of every element; gathered reads,
 // contiguous writes.  The new rows go to the element's third buffer (neither its nominal nor its
 // working one, which the gather reads); k_shift_sel then makes it both.
+// element b's old state rows (stride S_old): nominal X (q = 0), working X (1), working Defect (2),
+// in place or from the staging copy
+DEV const double *old_rows(const ShiftArgs &a, const Bufs &d, long b, int q)
+{
+    if (a.stage) return a.stage + ((size_t)q * d.rows3 + b * a.S_old) * NX;
+    const int buf = q == 0 ? nom_buf(d, (int)b) : work_buf(d, (int)b);
+    return (q == 2 ? dbuf(d, buf) : xbuf(d, buf)) + b * a.S_old * NX;
+}
+
+// the staging copy (ShiftArgs::stage): one thread per 16 bytes of an element's old rows
+__global__ __launch_bounds__(256) void k_shift_stage(int B, ShiftArgs a, Bufs d)
+{
+    const long per = (long)a.S_old * NX / 2, gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= 3L * B * per) return;
+    const int q = (int)(gid / ((long)B * per));
+    const long r = gid % ((long)B * per), b = r / per;
+    const int nb = nom_buf(d, (int)b), wb = work_buf(d, (int)b);
+    if (q == 1 && nb == wb) return;  // (read from the nominal copy)
+    const double *src = (q == 2 ? dbuf(d, wb) : xbuf(d, q == 0 ? nb : wb)) + b * a.S_old * NX;
+    reinterpret_cast<double2 *>(a.stage + ((size_t)q * d.rows3 + b * a.S_old) * NX)[r % per] =
+        reinterpret_cast<const double2 *>(src)[r % per];
+}
+
 template <typename KT>
 __global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, Bufs d, const KT *K, KT *Kn)
 {
@@ -107,15 +131,16 @@ __global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, Bufs d
     const long b = gid / per;
     long e = gid % per;
     const int m = a.map_id ? a.map_id[b] : 0;
-    const double *Xbar = xbuf(d, nom_buf(d, (int)b)), *X = xbuf(d, work_buf(d, (int)b)),
+    const bool same = nom_buf(d, (int)b) == work_buf(d, (int)b);
+    const double *Xbar = old_rows(a, d, b, 0), *X = old_rows(a, d, b, same ? 0 : 1),
                  *Ubar = ubuf(d, nom_buf(d, (int)b));
     double *Xn = xbuf(d, trial_buf(d, (int)b)), *Un = ubuf(d, trial_buf(d, (int)b));
     const int *smap = a.smap + (size_t)m * a.S_new, *cmap = a.cmap + (size_t)m * a.Kc;
     if (e < nx) {
         const int s = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = smap[s];
         double2 v = {0.0, 0.0};
-        if (lab >= 0) v = *(const double2 *)&Xbar[(b * a.S_old + lab) * NX + j];
-        else if (lab <= -2) v = *(const double2 *)&X[(b * a.S_old + (-2 - lab)) * NX + j];
+        if (lab >= 0) v = *(const double2 *)&Xbar[lab * NX + j];
+        else if (lab <= -2) v = *(const double2 *)&X[(-2 - lab) * NX + j];
         *(double2 *)&Xn[(b * nx + e) * 2] = v;
         return;
     }
@@ -134,10 +159,55 @@ __global__ __launch_bounds__(256) void k_shift_gather(int B, ShiftArgs a, Bufs d
     *(float4 *)&Kn[(b * nk + e) * KV] = v;
 }
 
+// The working trajectory through the same update (Trajectory::pop_front / push_back_state,
+// TrajectoryManagement.cpp:118-207; a new phase's rows are zero): X rows by the state map (a
+// pushed-back state is X.back() either way), U rows by the control map (a new knot's are zero;
+// Ubar[0]'s zeroing is the nominal's only), Defect rows by the state map with a pushed-back state's
+// zero.  After k_shift_gather: an element whose working rows are its nominal ones (no failed last
+// line search, sel nominal == working) gathers only its Defect, into the third buffer beside the
+// new nominal rows; any other gathers X, U and Defect into its old nominal buffer, which
+// k_shift_gather has finished reading.
+__global__ __launch_bounds__(256) void k_shift_gather_work(int B, ShiftArgs a, Bufs d)
+{
+    const long nx = (long)a.S_new * NX / 2, nu = (long)a.Kc * NX / 2, per = 2 * nx + nu;
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)B * per) return;
+    const long b = gid / per;
+    long e = gid % per;
+    const int nb = nom_buf(d, (int)b), wb = work_buf(d, (int)b), same = nb == wb;
+    const int m = a.map_id ? a.map_id[b] : 0, dst = same ? trial_of(nb, wb) : nb;
+    const int *smap = a.smap + (size_t)m * a.S_new, *cmap = a.cmap + (size_t)m * a.Kc;
+    if (e < nx) {  // Defect
+        const int s = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = smap[s];
+        double2 v = {0.0, 0.0};
+        if (lab >= 0) v = *(const double2 *)&old_rows(a, d, b, 2)[lab * NX + j];
+        *(double2 *)&dbuf(d, dst)[(b * nx + e) * 2] = v;
+        return;
+    }
+    if (same) return;
+    e -= nx;
+    if (e < nx) {  // X
+        const int s = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = smap[s];
+        const int src = lab >= 0 ? lab : -2 - lab;
+        double2 v = {0.0, 0.0};
+        if (lab != -1) v = *(const double2 *)&old_rows(a, d, b, 1)[src * NX + j];
+        *(double2 *)&xbuf(d, dst)[(b * nx + e) * 2] = v;
+        return;
+    }
+    e -= nx;
+    const int k = (int)(2 * e / NX), j = (int)(2 * e % NX), lab = cmap[k];
+    double2 v = {0.0, 0.0};
+    if (lab >= 0) v = *(const double2 *)&ubuf(d, wb)[(b * a.Kc + lab) * NX + j];
+    *(double2 *)&ubuf(d, dst)[(b * nu + e) * 2] = v;
+}
+
+// new selection: nominal = the third buffer; working = the same, or the old nominal buffer
 __global__ void k_shift_sel(int B, Bufs d)
 {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < B) d.sel[b] = sel_code(trial_buf(d, b), trial_buf(d, b));
+    if (b >= B) return;
+    const int nb = nom_buf(d, b), wb = work_buf(d, b), t = trial_of(nb, wb);
+    d.sel[b] = sel_code(t, nb == wb ? t : nb);
 }
 
 void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, void *K_new, hipStream_t st)
@@ -146,30 +216,40 @@ void launch_shift_gather(int B, const ShiftArgs &a, const Bufs &d, void *K_new, 
     const int KV = a.fp32 ? 4 : 2;
     const long n = (long)B * ((long)a.S_new * NX / 2 + (long)a.Kc * NX / 2 + (long)a.Kc * KCW / KV);
     const dim3 g((unsigned)((n + 255) / 256));
+    if (a.stage) {
+        const long ns = 3L * B * a.S_old * NX / 2;
+        hipLaunchKernelGGL(k_shift_stage, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, B, a, d);
+    }
     if (a.fp32)
         hipLaunchKernelGGL(k_shift_gather<float>, g, dim3(256), 0, st, B, a, d, d.K32, (float *)K_new);
     else
         hipLaunchKernelGGL(k_shift_gather<double>, g, dim3(256), 0, st, B, a, d, d.K, (double *)K_new);
+    const long nw = (long)B * ((long)a.S_new * NX + (long)a.Kc * NX / 2);
+    hipLaunchKernelGGL(k_shift_gather_work, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, B, a, d);
     hipLaunchKernelGGL(k_shift_sel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, B, d);
 }
 
-// The constraint parameters the phases carry through HKDProblem::update (HKDProblem.cpp:117-222):
+// The constraint objects the phases carry through HKDProblem::update (HKDProblem.cpp:117-222):
 // per-knot ReB (delta, eps) follow their knots (PathConstraintBase::pop_front / push_back,
-// ConstraintsBase.h:147-158: a pushed knot copies the last one's; a new phase starts from the
-// initial values), and each phase keeps its touchdown constraints with their AL parameters; the
-// update's add_tconstr_one_phase appends one more (initial parameters, legs resolved from the next
-// contact rows: TD_PENDING) at every step its last phase has reached its end.  One thread per
-// (element, control slot, row) and per (element, new phase).
-__global__ __launch_bounds__(256) void k_shift_params(int B, ShiftParamArgs a, Bufs d, double *rd, double *re,
-                                                      double *sg, double *lm, int *mk)
+// ConstraintsBase.h:147-158, 271-291: a pushed knot copies the last one's; a new phase starts from
+// the initial values), and so do the stored GRF values (a pushed knot's are zero, as its working
+// control row: no table entry); each phase keeps its touchdown constraints with their AL
+// parameters and stored residuals; the update's add_tconstr_one_phase appends one more (initial
+// parameters, zero residual, legs resolved from the next contact rows: TD_PENDING | TD_STALE) at
+// every step its last phase has reached its end.  One thread per (element, control slot, row) and
+// per (element, new phase).
+__global__ __launch_bounds__(256) void k_shift_params(int B, ShiftParamArgs a, Bufs d, ShiftParamOut o)
 {
     const long nr = (long)B * a.Kc * 20, gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid < nr) {
         const long b = gid / ((long)a.Kc * 20);
         const int k = (int)(gid / 20 % a.Kc), r = (int)(gid % 20);
         const int m = a.map_id ? a.map_id[b] : 0, lab = a.rmap[(size_t)m * a.Kc + k];
-        rd[gid] = lab >= 0 ? d.reb_delta[(b * a.Kc + lab) * 20 + r] : a.reb_delta0;
-        re[gid] = lab >= 0 ? d.reb_eps[(b * a.Kc + lab) * 20 + r] : a.reb_eps0;
+        o.reb_delta[gid] = lab >= 0 ? d.reb_delta[(b * a.Kc + lab) * 20 + r] : a.reb_delta0;
+        o.reb_eps[gid] = lab >= 0 ? d.reb_eps[(b * a.Kc + lab) * 20 + r] : a.reb_eps0;
+        const int src = a.cmap[(size_t)m * a.Kc + k];
+        if (r < 12) o.cf_u[(b * a.Kc + k) * 12 + r] = src >= 0 ? d.cf_u[(b * a.Kc + src) * 12 + r] : 0.0;
+        if (r == 0) o.cf_flag[b * a.Kc + k] = src >= 0 ? d.cf_flag[b * a.Kc + src] : 0;
         return;
     }
     const long g = gid - nr;
@@ -177,13 +257,13 @@ __global__ __launch_bounds__(256) void k_shift_params(int B, ShiftParamArgs a, B
     const long b = g / a.P_new;
     const int i = (int)(g % a.P_new), m = a.map_id ? a.map_id[b] : 0;
     const int src = a.pmap[m * MAXP + i], add = a.nadd[m * MAXP + i];
-    const size_t o = ((size_t)b * a.P_new + i) * MTD, q = ((size_t)b * a.P_old + src) * MTD;
+    const size_t w = ((size_t)b * a.P_new + i) * MTD, q = ((size_t)b * a.P_old + src) * MTD;
     int mask[MTD];
     for (int j = 0; j < MTD; ++j) {
         mask[j] = src >= 0 ? d.td_mask[q + j] : 0;
         for (int l = 0; l < 4; ++l) {
-            sg[(o + j) * 4 + l] = src >= 0 ? d.al_sigma[(q + j) * 4 + l] : a.td_sigma0;
-            lm[(o + j) * 4 + l] = src >= 0 ? d.al_lambda[(q + j) * 4 + l] : a.td_lambda0;
+            o.al_sigma[(w + j) * 4 + l] = src >= 0 ? d.al_sigma[(q + j) * 4 + l] : a.td_sigma0;
+            o.al_lambda[(w + j) * 4 + l] = src >= 0 ? d.al_lambda[(q + j) * 4 + l] : a.td_lambda0;
         }
     }
     for (int n = 0; n < add; ++n) {  // appended constraints take the first free slots
@@ -193,20 +273,20 @@ __global__ __launch_bounds__(256) void k_shift_params(int B, ShiftParamArgs a, B
             atomicAdd(a.overflow, 1);
             break;
         }
-        mask[j] = TD_PENDING;
+        mask[j] = TD_PENDING | TD_STALE;
+        d.el[b].td_stale = 1;
         for (int l = 0; l < 4; ++l) {
-            sg[(o + j) * 4 + l] = a.td_sigma0;
-            lm[(o + j) * 4 + l] = a.td_lambda0;
+            o.al_sigma[(w + j) * 4 + l] = a.td_sigma0;
+            o.al_lambda[(w + j) * 4 + l] = a.td_lambda0;
         }
     }
-    for (int j = 0; j < MTD; ++j) mk[o + j] = mask[j];
+    for (int j = 0; j < MTD; ++j) o.td_mask[w + j] = mask[j];
 }
 
-void launch_shift_params(int B, const ShiftParamArgs &a, const Bufs &d, double *rd, double *re, double *sg, double *lm,
-                         int *mk, hipStream_t st)
+void launch_shift_params(int B, const ShiftParamArgs &a, const Bufs &d, const ShiftParamOut &o, hipStream_t st)
 {
     const long n = (long)B * a.Kc * 20 + (long)B * a.P_new;
-    hipLaunchKernelGGL(k_shift_params, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, B, a, d, rd, re, sg, lm, mk);
+    hipLaunchKernelGGL(k_shift_params, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, B, a, d, o);
 }
 
 // HKDSinglePhaseReference::get_reference_at_t (HKDReference.cpp:8-57) at state slot s of reference

@@ -260,6 +260,14 @@ class Solver:
                                                                ("reb_delta", "reb_eps", "td_mask", "al_sigma", "al_lambda"))))
         return out
 
+    def constraint_values(self) -> dict:
+        """The constraint objects' stored values after the last solve (hsddp_download_constraint_values):
+        grf_g [B][Kc][20] (GRF rows of the stance legs), td_h [B][P][MAX_TD][4] (touchdown residuals)."""
+        B, P, Kc, T = self.B, self.P, self.Kc, self.MAX_TD
+        out = {"grf_g": np.empty((B, Kc, 20)), "td_h": np.empty((B, P, T, 4))}
+        check(lib().hsddp_download_constraint_values(self._h, out["grf_g"].ctypes.data, out["td_h"].ctypes.data))
+        return out
+
     def upload_constraint_params(self, reb_delta=None, reb_eps=None, td_mask=None, al_sigma=None, al_lambda=None):
         """hsddp_upload_constraint_params (None keeps a field); shapes as constraint_params()'s.  The C
         side reads B x Kc x 20 / B x P x MAX_TD (x 4) values from each pointer, so the shapes are

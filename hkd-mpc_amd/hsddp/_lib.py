@@ -107,6 +107,7 @@ EXPORTS = [
     "hsddp_hkd_touchdown_constraint", "hsddp_set_element_layouts",
     "hsddp_shift_elements", "hsddp_get_element_layouts", "hsddp_extract_commands_device",
     "hsddp_set_layout", "hsddp_upload_constraint_params", "hsddp_download_constraint_params",
+    "hsddp_download_constraint_values",
     "hsddp_extract_commands_async", "hsddp_commands_wait",
 ]
 
@@ -184,6 +185,7 @@ def lib():
     L.hsddp_set_layout.argtypes = [V, C.c_int, IP, IP, IP]
     L.hsddp_upload_constraint_params.argtypes = [V] * 6
     L.hsddp_download_constraint_params.argtypes = [V] * 6
+    L.hsddp_download_constraint_values.argtypes = [V] * 3
     L.hsddp_extract_commands_async.argtypes = [V, C.c_int, C.c_double, C.c_double, V, C.c_int, V, C.c_int, C.c_float,
                                                C.POINTER(C.c_int)]
     L.hsddp_commands_wait.argtypes = [V, C.c_int, C.POINTER(C.c_void_p)]

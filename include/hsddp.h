@@ -88,6 +88,8 @@ enum {
 enum {
     HSDDP_STATUS_OK = 0,            /* finished: converged or iteration budget spent */
     HSDDP_STATUS_REG_OVERFLOW = 1,  /* regularization exceeded 1e2 (MultiPhaseDDP.cpp:162-167) */
+    /* (no other outcome: rollouts that break the 1e6 bound are the reference's rejected trials and
+       keep any number of older constraint values, hsddp_download_constraint_values) */
 };
 
 /* POD mirror of HSDDP_OPTION (HSDDP_CompoundTypes.h:18-60), same field names and meaning. */
@@ -189,9 +191,11 @@ int hsddp_upload_problem(hsddp_handle h, const int *contacts, const double *x0, 
                          const double *ref_u, const double *ref_foot);
 /* Xbar [B][S][24], Ubar [B][Kc][24], K [B][Kc][24][24]; NULL keeps the current value (initially
  * Xbar = ref_x, Ubar = 0, K = 0 as HKDProblem.cpp:84-90 / TrajectoryManagement.cpp:5-35).  Also
- * resets X = Xbar, U = Ubar, dX = 0 and the constraint parameters to those of a new problem: ReB
- * (delta, eps) = desc->cparams at every knot, one touchdown constraint per phase (the touchdown legs
- * from contact row i to row i + 1, none when there are none) with the initial AL parameters. */
+ * resets X = Xbar, U = Ubar, Defect = dX = 0 and the constraint objects to those of a new problem:
+ * ReB (delta, eps) = desc->cparams at every knot, one touchdown constraint per phase (the touchdown
+ * legs from contact row i to row i + 1, none when there are none) with the initial AL parameters,
+ * and zero stored constraint values (hsddp_download_constraint_values).  hsddp_update_problem, in
+ * contrast, keeps all of these, as the reference's objects persist from tick to tick. */
 int hsddp_upload_warm_start(hsddp_handle h, const double *Xbar, const double *Ubar, const double *K);
 /* The constraint parameters the solve reads and updates (its update_AL_params / update_REB_params,
  * ConstraintsBase.h:160-176, 354-372), for callers that keep their constraint objects themselves
@@ -205,6 +209,16 @@ int hsddp_upload_constraint_params(hsddp_handle h, const double *reb_delta, cons
                                    const double *al_sigma, const double *al_lambda);
 int hsddp_download_constraint_params(hsddp_handle h, double *reb_delta, double *reb_eps, int *td_legs,
                                      double *al_sigma, double *al_lambda);
+/* The constraint objects' stored values after the last solve (IneqConstrData::g and TConstrData::h,
+ * ConstraintsBase.h:12-55; GRFConstraint / TouchDownConstraint::compute_violation,
+ * HKDConstraints.cpp:36-53, 79-120), which — like the reference's objects — live on from trial to
+ * trial and from solve to solve: a rollout that returns at a diverging knot (SinglePhase.cpp:205-208)
+ * leaves them as they were from there on, and a new problem's, a pushed-back knot's and a newly
+ * registered touchdown constraint's are zero until a rollout computes them.  grf_g [B][Kc][20]:
+ * row 5 l + r of stance leg l (0 for swing legs); td_h [B][P][HSDDP_MAX_TD][4]: the residual of
+ * each touchdown constraint's legs (0 outside its mask).  Valid after hsddp_solve / solve_end,
+ * before the next hsddp_shift.  Either pointer may be NULL. */
+int hsddp_download_constraint_values(hsddp_handle h, double *grf_g, double *td_h);
 
 /* MultiPhaseDDP::solve (MultiPhaseDDP.cpp:232-428) for every element.  With early exits on, each
  * inner iteration is replayed from a cached hipGraph and stats carries ms_total but no per-phase
@@ -338,7 +352,10 @@ int hsddp_set_layout(hsddp_handle h, int n_phases, const int *horizons, const in
  * (ConstraintsBase.h:165-167, 341-348), so the per-knot ReB parameters and every touchdown
  * constraint's AL parameters carry over from the previous solve (shifted with their knots and phases
  * by hsddp_shift / hsddp_advance, which also append the touchdown constraints add_tconstr_one_phase
- * registers: their legs are the new contact rows' touchdown legs).  Resets X = Xbar, U = Ubar. */
+ * registers: their legs are the new contact rows' touchdown legs).  The working trajectory (X, U,
+ * Defect) and the constraint objects' stored values carry over too (shifted alike): a solve whose
+ * initial rollout diverges keeps them past its break, as the reference's objects do.  Resets
+ * dX = dU = 0 and the per-element solver state. */
 int hsddp_update_problem(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
                          const double *ref_u, const double *ref_foot);
 

@@ -87,6 +87,13 @@ typedef struct {
        199-202): legs (bit l = leg l, 0 = no constraint) and AL parameters per constraint and leg */
     double *al_sigma, *al_lambda;                /* [P][ORC_MAX_TD][4] */
     int *td_mask;                                /* [P][ORC_MAX_TD] */
+    /* the constraint objects' stored values (IneqConstrData::g, TConstrData::h, ConstraintsBase.h:
+       12-55), which live on in the objects from solve to solve: a rollout that returns at a knot
+       (SinglePhase.cpp:205-208) leaves them as they were from there on.  GRF values per control
+       slot and row [Kc][20]; touchdown residuals per constraint and leg [P][ORC_MAX_TD][4].  Zero
+       for a new problem and for knots / constraints the receding-horizon update adds (create_data,
+       PathConstraintBase::push_back).  NULL: zeros at the start of the solve. */
+    double *grf_g, *td_h;
     /* outputs */
     double cost, feas, merit, max_tconstr, max_pconstr;
     int iters, outer_iters, status, n_ls_trials;
@@ -94,6 +101,9 @@ typedef struct {
        (cost, feas, max_tconstr, max_pconstr) as float; NULL = not recorded.  hist_n: entries pushed */
     float *hist;
     int hist_cap, hist_n;
+    /* diagnostics: the initial rollout broke the 1e6 bound (SinglePhase.cpp:205-208); line-search
+       trials that broke it */
+    int diverged_init, n_diverged;
 } orc_element;
 
 void orc_default_options(orc_options *o);

@@ -74,8 +74,9 @@ typedef struct {
     double *Phi, *Phix, *Phixx;         /* per phase */
     double *G, *H;                      /* per state slot */
     double *Xsim;                       /* [S][NX] */
-    double *g;                          /* [Kc][20] */
-    double h[MAXP][4], hx[MAXP][4][NX];
+    double *g;                          /* [Kc][20] stored GRF constraint values (orc_element.grf_g) */
+    double *td_h;                       /* [P][ORC_MAX_TD][4] stored touchdown values (orc_element.td_h) */
+    double hx[MAXP][4][NX];
     double pviol[MAXP], tviol[MAXP];
     double phase_cost[MAXP], dV1p[MAXP], dV2p[MAXP];
     /* multi-phase scalars (MultiPhaseDDP.h:437-451) */
@@ -213,12 +214,19 @@ static int phase_hybrid_rollout(ctx_t *C, int i, double eps, const double *x_ini
     double tv = 0;
     const double *xN = X + (size_t)(s0 + N) * NX;
     const int tdu = td_legs(C->e, i);
+    double hl[4] = {0, 0, 0, 0};
     for (int l = 0; l < 4; ++l) {
         if (!((tdu >> l) & 1)) continue;
         double pf[3];
         orc_foot_position(l, xN + 3, xN, xN + 12 + 3 * l, pf);
-        C->h[i][l] = pf[2] - C->p->ground_height;
-        tv = fmax(tv, fabs(C->h[i][l]));
+        hl[l] = pf[2] - C->p->ground_height;
+        tv = fmax(tv, fabs(hl[l]));
+    }
+    /* each constraint's data[i].h for its impact feet */
+    for (int j = 0; j < ORC_MAX_TD; ++j) {
+        const int m = e->td_mask[i * ORC_MAX_TD + j];
+        for (int l = 0; l < 4; ++l)
+            if ((m >> l) & 1) C->td_h[(i * ORC_MAX_TD + j) * 4 + l] = hl[l];
     }
     C->tviol[i] = tv;
     /* compute_defect (TrajectoryManagement.cpp:210-217) */
@@ -299,7 +307,7 @@ static void phase_compute_cost(ctx_t *C, int i)
             for (int l = 0; l < 4; ++l) {
                 if (!((m >> l) & 1)) continue;
                 const int q = (i * ORC_MAX_TD + j) * 4 + l;
-                double sg = e->al_sigma[q], lm = e->al_lambda[q], hh = C->h[i][l];
+                double sg = e->al_sigma[q], lm = e->al_lambda[q], hh = C->td_h[q];
                 al += 0.5 * sg * hh * hh;
                 al += lm * hh;
             }
@@ -392,7 +400,7 @@ static void phase_LQ(ctx_t *C, int i)
                 if (!((m >> l) & 1)) continue;
                 const int q = (i * ORC_MAX_TD + j) * 4 + l;
                 const double *hxv = C->hx[i][l];
-                double sg = e->al_sigma[q], lm = e->al_lambda[q], hh = C->h[i][l];
+                double sg = e->al_sigma[q], lm = e->al_lambda[q], hh = C->td_h[q];
                 double a1 = sg * hh + lm, a2 = sg * (1 + hh) + lm; /* quirk A4 */
                 for (int a = 0; a < NX; ++a) {
                     grad[a] += a1 * hxv[a];
@@ -792,6 +800,7 @@ static int mp_line_search(ctx_t *C)
     while (eps > 1e-3) {
         int ok = mp_hybrid_rollout(C, eps);
         C->n_ls++;
+        C->e->n_diverged += !ok;
         mp_compute_cost(C);
         C->feas = mp_feas(C);
         C->merit = C->actual_cost + C->merit_rho * C->feas;
@@ -813,9 +822,9 @@ static void mp_update_AL(ctx_t *C)
             const int m = e->td_mask[i * ORC_MAX_TD + j];
             for (int l = 0; l < 4; ++l) {
                 if (!((m >> l) & 1)) continue;
-                double hh = C->h[i][l];
-                if (fabs(hh) < o->tconstr_thresh) continue;
                 const int q = (i * ORC_MAX_TD + j) * 4 + l;
+                double hh = C->td_h[q];
+                if (fabs(hh) < o->tconstr_thresh) continue;
                 double *sg = &e->al_sigma[q];
                 if (fabs(hh) > 0.005) { *sg *= o->update_penalty; *sg = fmin(*sg, C->p->td_sigma_max); }
                 else e->al_lambda[q] += hh * *sg;
@@ -847,6 +856,9 @@ void orc_init_element(const orc_problem *p, orc_element *e)
 {
     int P = p->n_phases, Kc = 0;
     for (int i = 0; i < P; ++i) Kc += p->horizons[i];
+    /* create_data: zero constraint values (ConstraintsBase.h:26-34, 50-54, 133-139, 318-320) */
+    if (e->grf_g) memset(e->grf_g, 0, sizeof(double) * (size_t)Kc * 20);
+    if (e->td_h) memset(e->td_h, 0, sizeof(double) * (size_t)P * ORC_MAX_TD * 4);
     for (int q = 0; q < Kc * 20; ++q) { e->reb_delta[q] = p->grf_delta; e->reb_eps[q] = p->grf_eps; }
     for (int q = 0; q < P * ORC_MAX_TD * 4; ++q) { e->al_sigma[q] = p->td_sigma; e->al_lambda[q] = p->td_lambda; }
     for (int i = 0; i < P; ++i)
@@ -895,7 +907,7 @@ void orc_knot_eval(const orc_problem *p, const orc_options *o, const int *c, con
     e.X = X; e.Xbar = Xbar; e.U = U; e.Ubar = Ubar; e.Defect = D; e.Defect_bar = Db; e.dX = dX; e.dU = dU; e.K = K;
     e.reb_delta = rd; e.reb_eps = re; e.al_sigma = as; e.al_lambda = al; e.td_mask = tdm;
     ctx_t *C = (ctx_t *)calloc(1, sizeof(ctx_t));
-    double *pool = (double *)calloc(8 * NN + 4 * NX + 64, sizeof(double));
+    double *pool = (double *)calloc(8 * NN + 4 * NX + 64 + ORC_MAX_TD * 4, sizeof(double));
     C->p = &p1; C->o = o; C->e = &e; C->P = 1; C->S = 2; C->Kc = 1;
     C->N[0] = 1; C->s0[0] = 0; C->k0[0] = 0;
     for (int l = 0; l < 4; ++l) { C->c[0][l] = c[l]; C->c[1][l] = cn[l]; }
@@ -904,13 +916,14 @@ void orc_knot_eval(const orc_problem *p, const orc_options *o, const int *c, con
     C->A = q; q += NN; C->B = q; q += NN; C->lxx = q; q += NN; C->luu = q; q += NN; C->lux = q; q += NN;
     C->l = q; q += 1; C->lx = q; q += NX; C->lu = q; q += NX;
     C->Phi = q; q += 1; C->Phix = q; q += NX; C->Phixx = q; q += NN; C->g = q; q += 20;
+    C->td_h = q; q += ORC_MAX_TD * 4;
     for (int l = 0; l < 4; ++l)
         if (c[l]) grf_rows(p1.mu_fric, u + 3 * l, C->g + 5 * l);
     for (int l = 0; l < 4; ++l) {
         if (!(c[l] == 0 && cn[l] == 1)) continue;
         double pfz[3];
         orc_foot_position(l, x_end + 3, x_end, x_end + 12 + 3 * l, pfz);
-        C->h[0][l] = pfz[2] - p1.ground_height;
+        C->td_h[l] = pfz[2] - p1.ground_height;  /* constraint slot 0 */
     }
     phase_compute_cost(C, 0);
     phase_LQ(C, 0);
@@ -957,7 +970,8 @@ int orc_solve(const orc_problem *p, const orc_options *o, orc_element *e)
     setup_costs(C);
     size_t Kc = (size_t)C->Kc, S = (size_t)C->S;
     double *pool = (double *)calloc(Kc * NN * 5 + Kc * (1 + 2 * NX) + (size_t)C->P * (1 + NX + NN) +
-                                        S * (NX + NN) + S * NX + Kc * 20, sizeof(double));
+                                        S * (NX + NN) + S * NX + Kc * 20 + (size_t)C->P * ORC_MAX_TD * 4,
+                                    sizeof(double));
     if (!pool) { free(C); return -1; }
     double *q = pool;
     C->A = q; q += Kc * NN; C->B = q; q += Kc * NN;
@@ -965,12 +979,17 @@ int orc_solve(const orc_problem *p, const orc_options *o, orc_element *e)
     C->l = q; q += Kc; C->lx = q; q += Kc * NX; C->lu = q; q += Kc * NX;
     C->Phi = q; q += C->P; C->Phix = q; q += (size_t)C->P * NX; C->Phixx = q; q += (size_t)C->P * NN;
     C->G = q; q += S * NX; C->H = q; q += S * NN; C->Xsim = q; q += S * NX; C->g = q; q += Kc * 20;
+    C->td_h = q; q += (size_t)C->P * ORC_MAX_TD * 4;
+    /* the constraint objects' data persists across solves (orc_element.grf_g / td_h) */
+    if (e->grf_g) C->g = e->grf_g;
+    if (e->td_h) C->td_h = e->td_h;
 
     int iter = 0, iter_ou = 0, iter_in = 0, success = 1;
     double cost_prev = 0, merit_prev = 0;
     e->status = 0;
 
-    mp_hybrid_rollout(C, 0);
+    e->n_diverged = 0;
+    e->diverged_init = !mp_hybrid_rollout(C, 0);
     mp_update_nominal(C);
     mp_compute_cost(C);
     C->feas = mp_feas(C);

@@ -123,6 +123,39 @@ def shift(horizons, shooting, reach_end, Xbar, X, Ubar, K, contact_change):
     return hz, ss, re, flat(xb), flat(ub), flat(kk)
 
 
+def shift_working(horizons, reach_end, X, U, Defect, contact_change):
+    """The same update on one element's working trajectory, which the reference keeps from tick to
+    tick beside the nominal one (a solve whose last line search failed leaves X, U != Xbar, Ubar,
+    quirk A2; a later initial rollout that breaks keeps them past the break): Trajectory::pop_front
+    drops the front rows of X, U and Defect (TrajectoryManagement.cpp:118-145), push_back_state
+    appends X.back() to X, a zero U row and a zero Defect row (:179-207), a new phase starts from
+    zeros (Trajectory::create_data).  Returns (X, U, Defect) in the flat slot layout."""
+    hz, re = list(horizons), list(reach_end)
+    xw, dw, uw = split_phases(X, hz, True), split_phases(Defect, hz, True), split_phases(U, hz, False)
+    for cc in contact_change:
+        if hz[0] <= 1:
+            for L in (hz, re, xw, dw, uw):
+                L.pop(0)
+        else:
+            for L in (xw[0], dw[0], uw[0]):
+                L.pop(0)
+            hz[0] -= 1
+        if cc and re[-1]:
+            hz.append(1); re.append(0)
+            xw.append([np.zeros_like(X[0]) for _ in range(2)])
+            dw.append([np.zeros_like(X[0]) for _ in range(2)])
+            uw.append([np.zeros_like(U[0])])
+        else:
+            xw[-1].append(np.array(xw[-1][-1], copy=True))
+            dw[-1].append(np.zeros_like(X[0]))
+            uw[-1].append(np.zeros_like(U[0]))
+            hz[-1] += 1
+            if cc:
+                re[-1] = 1
+    flat = lambda L: np.array([r for ph in L for r in ph])  # noqa: E731
+    return flat(xw), flat(uw), flat(dw)
+
+
 # ---- the constraint objects through the receding-horizon update --------------------------------
 MAX_TD = 4          # touchdown constraints per phase (HSDDP_MAX_TD)
 TD_PENDING = 0x10   # a constraint registered by the update whose legs come from the next contact rows
@@ -144,29 +177,38 @@ def shift_constraints(horizons, reach_end, cons, contact_change, grf_delta, grf_
     from the initial ReB parameters and carries no touchdown constraint; at every step whose last
     phase has reached its end, add_tconstr_one_phase appends one more touchdown constraint with the
     initial AL parameters (HKDProblem.cpp:199-202) — its legs follow from the next contact rows
-    (TD_PENDING, resolve_td).  Returns the new cons.  cap: a phase holds at most MAX_TD constraints
+    (TD_PENDING, resolve_td).  With "grf_g" / "td_h" in cons, the constraint objects' stored values
+    follow too (zero for pushed knots, new phases and new constraints: create_data,
+    PathConstraintBase::push_back).  Returns the new cons.  cap: a phase holds at most MAX_TD constraints
     and the later ones are not registered (the device's HSDDP_MAX_TD; "overflow" in the result says
     whether one was dropped) — the reference's lists are unbounded, so without cap that is an error."""
     hz, re = list(horizons), list(reach_end)
     rd = split_phases(cons["reb_delta"], hz, False)
     rs = split_phases(cons["reb_eps"], hz, False)
+    # the stored constraint values (optional): GRF g per knot [Kc][20], touchdown h per constraint [P][MAX_TD][4]
+    vals = "grf_g" in cons
+    gg = split_phases(cons["grf_g"], hz, False) if vals else [[] for _ in hz]
+    th = cons["td_h"] if vals else np.zeros((len(hz), MAX_TD, 4))
     td = [list(zip([int(m) for m in cons["td_mask"][i]], [np.array(v) for v in cons["al_sigma"][i]],
-                   [np.array(v) for v in cons["al_lambda"][i]])) for i in range(len(hz))]
+                   [np.array(v) for v in cons["al_lambda"][i]], [np.array(v) for v in th[i]])) for i in range(len(hz))]
     init_row = lambda v: np.full(20, v)  # noqa: E731
     overflow = False
     for cc in contact_change:
         if hz[0] <= 1:
-            for L in (hz, re, rd, rs, td):
+            for L in (hz, re, rd, rs, gg, td):
                 L.pop(0)
         else:
             rd[0].pop(0); rs[0].pop(0)
+            if vals:
+                gg[0].pop(0)
             hz[0] -= 1
         if cc and re[-1]:
             hz.append(1); re.append(0)
-            rd.append([init_row(grf_delta)]); rs.append([init_row(grf_eps)])
-            td.append([(0, np.full(4, td_sigma), np.full(4, td_lambda)) for _ in range(MAX_TD)])
+            rd.append([init_row(grf_delta)]); rs.append([init_row(grf_eps)]); gg.append([np.zeros(20)])
+            td.append([(0, np.full(4, td_sigma), np.full(4, td_lambda), np.zeros(4)) for _ in range(MAX_TD)])
         else:
-            rd[-1].append(np.array(rd[-1][-1])); rs[-1].append(np.array(rs[-1][-1]))
+            # PathConstraintBase::push_back: a zero data row, the last knot's ReB parameters
+            rd[-1].append(np.array(rd[-1][-1])); rs[-1].append(np.array(rs[-1][-1])); gg[-1].append(np.zeros(20))
             hz[-1] += 1
             if cc:
                 re[-1] = 1
@@ -177,12 +219,16 @@ def shift_constraints(horizons, reach_end, cons, contact_change, grf_delta, grf_
                 overflow = True
                 continue
             assert j is not None, "more than MAX_TD touchdown constraints on one phase"
-            slots[j] = (TD_PENDING, np.full(4, td_sigma), np.full(4, td_lambda))
+            slots[j] = (TD_PENDING, np.full(4, td_sigma), np.full(4, td_lambda), np.zeros(4))
     flat = lambda L: np.array([r for ph in L for r in ph])  # noqa: E731
-    return {"reb_delta": flat(rd), "reb_eps": flat(rs),
-            "td_mask": np.array([[s[0] for s in ph] for ph in td], np.int32),
-            "al_sigma": np.array([[s[1] for s in ph] for ph in td]),
-            "al_lambda": np.array([[s[2] for s in ph] for ph in td]), "overflow": overflow}
+    out = {"reb_delta": flat(rd), "reb_eps": flat(rs),
+           "td_mask": np.array([[s[0] for s in ph] for ph in td], np.int32),
+           "al_sigma": np.array([[s[1] for s in ph] for ph in td]),
+           "al_lambda": np.array([[s[2] for s in ph] for ph in td]), "overflow": overflow}
+    if vals:
+        out["grf_g"] = flat(gg)
+        out["td_h"] = np.array([[s[3] for s in ph] for ph in td])
+    return out
 
 
 def resolve_td(cons, contacts):

@@ -51,11 +51,12 @@ class OrcElement(C.Structure):
                 ("Xbar", DP), ("X", DP), ("Defect", DP), ("Defect_bar", DP), ("dX", DP),
                 ("Ubar", DP), ("U", DP), ("dU", DP), ("K", DP),
                 ("reb_delta", DP), ("reb_eps", DP), ("al_sigma", DP), ("al_lambda", DP), ("td_mask", IP),
+                ("grf_g", DP), ("td_h", DP),
                 ("cost", C.c_double), ("feas", C.c_double), ("merit", C.c_double),
                 ("max_tconstr", C.c_double), ("max_pconstr", C.c_double),
                 ("iters", C.c_int), ("outer_iters", C.c_int), ("status", C.c_int),
                 ("n_ls_trials", C.c_int), ("hist", C.POINTER(C.c_float)), ("hist_cap", C.c_int),
-                ("hist_n", C.c_int)]
+                ("hist_n", C.c_int), ("diverged_init", C.c_int), ("n_diverged", C.c_int)]
 
 
 def build(quiet: bool = True) -> None:
@@ -204,15 +205,22 @@ def riccati_lq(N, A, B, lxx, luu, lx=None, lu=None, Phix=None, Phixx=None, reg=0
 # ---- solver -----------------------------------------------------------------------------------
 MAX_TD = 4  # ORC_MAX_TD / HSDDP_MAX_TD
 CONSTRAINT_FIELDS = ("reb_delta", "reb_eps", "al_sigma", "al_lambda", "td_mask")
+# what else lives on from solve to solve in the reference's objects: the working trajectory (X, U,
+# Defect: Trajectory, TrajectoryManagement.cpp) and the constraint objects' stored values (GRF g per
+# knot and row, touchdown h per constraint and leg: ConstraintsBase.h:12-55)
+STATE_FIELDS = ("X", "U", "Defect", "grf_g", "td_h")
 
 
 def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 1,
-                elements=None, weights: dict | None = None, constraints: dict | None = None) -> dict:
+                elements=None, weights: dict | None = None, constraints: dict | None = None,
+                state: dict | None = None) -> dict:
     """Run the oracle solve on (a subset of) a synthetic batch; returns per-element outputs.
     weights: HKD cost-weight overrides by field name (e.g. {"r_qJd": -0.5}).
     constraints: the elements' constraint parameters (CONSTRAINT_FIELDS, [B] leading axis) to start
     from instead of a new problem's (orc_init_element) — an MPC tick's carried-over ReB / AL
-    parameters and touchdown constraints; the outputs carry them after the solve."""
+    parameters and touchdown constraints; the outputs carry them after the solve.
+    state: STATE_FIELDS ([B] leading axis) to start from instead of a new problem's (X = Xbar,
+    U = Ubar, Defect = 0, zero constraint values) — the previous tick's, shifted (mpc_oracle)."""
     options = options or default_options()
     B = prob["batch"]
     idx = list(range(B)) if elements is None else list(elements)
@@ -235,6 +243,7 @@ def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 
         "reb_delta": np.zeros((n, Kc, 20)), "reb_eps": np.zeros((n, Kc, 20)),
         "al_sigma": np.zeros((n, P, MAX_TD, 4)), "al_lambda": np.zeros((n, P, MAX_TD, 4)),
         "td_mask": np.zeros((n, P, MAX_TD), np.int32),
+        "grf_g": np.zeros((n, Kc, 20)), "td_h": np.zeros((n, P, MAX_TD, 4)),
     }
     contacts = np.ascontiguousarray(prob["contacts"][idx])
     x0 = np.ascontiguousarray(prob["x0"][idx])
@@ -256,6 +265,9 @@ def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 
         if constraints is not None:
             for k in CONSTRAINT_FIELDS:
                 st[k][j] = constraints[k][b]
+        if state is not None:
+            for k in STATE_FIELDS:
+                st[k][j] = state[k][b]
     hcap = 1 + options.max_AL_iter * options.max_DDP_iter
     hist = np.zeros((n, hcap, 4), np.float32)
     for j in range(n):
@@ -264,7 +276,7 @@ def solve_batch(prob: dict, options: OrcOptions | None = None, n_threads: int = 
     lib().orc_solve_batch(C.byref(p), C.byref(options), elems, n, n_threads)
     out = dict(st)
     for f in ("cost", "feas", "merit", "max_tconstr", "max_pconstr", "iters", "outer_iters", "status",
-              "n_ls_trials"):
+              "n_ls_trials", "diverged_init", "n_diverged"):
         out[f] = np.array([getattr(elems[j], f) for j in range(n)])
     # get_solver_info buffers per element: [n_j][4] (cost, dyn_feas, eqn_feas, ineq_feas)
     out["solver_info"] = [hist[j, :min(elems[j].hist_n, hcap)].copy() for j in range(n)]

@@ -110,3 +110,96 @@ def test_divergence_full_solve_matches_oracle():
     err, tol = _close(DC.untranslate(g["Xbar"], T, es)[ok], DC.untranslate(r["Xbar"], T, es)[ok],
                       DC.untranslate(r2["Xbar"], T, es)[ok], 1e-7)
     assert err <= tol, (err, tol)
+
+
+# ---- rollouts that break before any trial ----------------------------------------------------
+def _values_close(g, r, r2, fields=("grf_g", "td_h")):
+    for f in fields:
+        err, tol = _close(g[f], r[f], r2[f])
+        assert err <= tol, (f, err, tol)
+
+
+@pytest.mark.parametrize("kw", [dict(no_early_exit=1, max_AL_iter=1, max_DDP_iter=1),
+                                dict(no_early_exit=1, max_AL_iter=2, max_DDP_iter=3), {}])
+def test_new_problem_initial_rollout_diverges(kw):
+    """A new problem's constraint values are zero (create_data, ConstraintsBase.h:26-34, 50-54):
+    when its first rollout breaks at knot k (SinglePhase.cpp:205-208), every GRF value from k on
+    and every touchdown residual from the break phase on stay zero — here ~24 knots of an element
+    whose every later trial breaks too, far more knots with older values than round 5's 8-entry
+    table held — and the cost, the LQ model and the ReB / AL updates read them; X past the break is
+    the warm start's.  Fixed iterations and the shipped settings, against the oracle."""
+    prob, breaks, T, es = DC.make_init("trot", 4, 12, 8)
+    s = hsddp.Solver(prob, hsddp.load_settings(**kw))
+    s.solve()
+    g = {**s.trajectory(), **s.working(), **s.element_info(), **s.constraint_values(), **s.constraint_params()}
+    s.close()
+    r = O.solve_batch(prob, O.default_options(**kw), n_threads=8)
+    p2 = dict(prob); p2["x0"] = prob["x0"] * (1 + 1e-15)
+    r2 = O.solve_batch(p2, O.default_options(**kw), n_threads=8)
+    for b, j in enumerate(breaks):
+        assert r["diverged_init"][b] == (j >= 0), b
+    most = max(len(DC.stale_knots(prob, r["U"], r["grf_g"], b)) for b in range(8))
+    assert most > 8, most
+    for f in ("iters", "outer_iters", "status", "n_ls_trials"):
+        assert np.array_equal(g[f], r[f]), f
+    for f in ("Xbar", "X"):
+        err, tol = _close(DC.untranslate(g[f], T, es), DC.untranslate(r[f], T, es), DC.untranslate(r2[f], T, es))
+        assert err <= tol, (f, err, tol)
+    for f in ("Ubar", "U", "K", "dU", "cost", "feas", "merit", "max_tconstr", "max_pconstr",
+              "reb_delta", "reb_eps", "al_sigma", "al_lambda"):
+        err, tol = _close(g[f], r[f], r2[f])
+        assert err <= tol, (f, err, tol)
+    _values_close(g, r, r2)
+    # the device's own account of the older values agrees knot for knot
+    for b in range(8):
+        assert DC.stale_knots(prob, g["U"], g["grf_g"], b) == DC.stale_knots(prob, r["U"], r["grf_g"], b), b
+
+
+# pronk element 3 of the receding-horizon batch (B, P, N = 8, 4, 5), translated so that the bound
+# falls between the initial rollout's largest simulated-state norms of ticks 1 and 2: the window
+# (found by bisection over oracle loops) is [447213.5389, 447213.58); its middle
+MPC_T3 = 447213.56
+
+
+def test_mpc_tick_initial_rollout_diverges():
+    """HKDMPCSolver::update's loop (shift, new inputs, re-solve with max_AL_iter = 2, max_DDP_iter = 1)
+    on a batch whose element 3 is translated until, from tick 2 on, the initial rollout of every
+    solve breaks (SinglePhase.cpp:205-208).  The reference's objects live on from tick to tick:
+    past the break the solve keeps the working trajectory of the previous tick (shifted, quirk A2
+    included) and the constraint objects' stored values (shifted with their knots; zero for pushed
+    knots and new touchdown constraints), and the tick's cost, LQ model and merit read them.  Every
+    tick against the oracle doing the same (mpc_oracle.shift_working / shift_constraints)."""
+    B, P, N, ticks = 8, 4, 5, 8
+    T = np.zeros(B); T[3] = MPC_T3
+    prob, r0, out = DC.mpc_loop_oracle(B, P, N, T, ticks)
+    _, r0p, outp = DC.mpc_loop_oracle(B, P, N, T, ticks, perturb=1e-15)
+    div = [t["r"]["diverged_init"][3] for t in out]
+    assert r0["diverged_init"][3] == 0 and div[0] == 0 and all(div[1:]), div
+    assert all(t["r"]["diverged_init"][b] == 0 for t in out for b in range(B) if b != 3)
+    s = hsddp.Solver(prob, hsddp.load_settings())
+    s.solve()
+    g = {**s.trajectory(), **s.element_info()}
+    for f in ("n_ls_trials", "status"):
+        assert np.array_equal(g[f], r0[f]), f
+    s.set_options(hsddp.load_settings(max_AL_iter=2, max_DDP_iter=1))
+    for it, (t, tp) in enumerate(zip(out, outp)):
+        s.shift(t["flags"])
+        inp = t["inp"]
+        s.update_problem(inp["contacts"], inp["x0"], inp["ref_x"], inp["ref_u"], inp["ref_foot"])
+        s.solve()
+        g = {**s.trajectory(), **s.working(), **s.element_info(), **s.constraint_values(), **s.constraint_params()}
+        r, r2 = t["r"], tp["r"]
+        hz = t["prob"]["horizons"]
+        es = np.stack([DC.direction_of(inp["contacts"][b], hz) for b in range(B)])
+        for f in ("iters", "status", "n_ls_trials"):
+            assert np.array_equal(g[f], r[f]), (it, f)
+        assert np.array_equal(g["td_mask"], r["td_mask"]), it
+        for f in ("Xbar", "X"):
+            err, tol = _close(DC.untranslate(g[f], T, es), DC.untranslate(r[f], T, es), DC.untranslate(r2[f], T, es))
+            assert err <= tol, (it, f, err, tol)
+        for f in ("Ubar", "U", "K", "cost", "feas", "merit", "max_tconstr", "max_pconstr",
+                  "reb_delta", "reb_eps", "al_sigma", "al_lambda", "grf_g", "td_h"):
+            err, tol = _close(g[f], r[f], r2[f])
+            assert err <= tol, (it, f, err, tol)
+        assert DC.stale_knots(t["prob"], g["U"], g["grf_g"], 3) == DC.stale_knots(t["prob"], r["U"], r["grf_g"], 3), it
+    s.close()

@@ -65,3 +65,40 @@ def test_foot_placement_search_rules():
     assert np.array_equal(pf[0:3], Xbar[s0[2]][12:15].astype(np.float32))
     assert np.array_equal(pf[3:6], cur[3:6]) and np.array_equal(pf[6:9], cur[6:9])
     assert np.array_equal(pf[9:12], Xbar[s0[5]][21:24].astype(np.float32))
+
+
+def test_shift_working_follows_the_trajectory_edits():
+    """mpc_oracle.shift_working (Trajectory::pop_front / push_back_state, TrajectoryManagement.cpp:
+    118-207): the working X moves like the nominal (X.back() pushed), U and Defect get zero rows,
+    a new phase is zero; with X = Xbar it reproduces shift()'s Xbar."""
+    horizons, reach = [3, 2, 4], [0, 0, 0]
+    X, U, _ = _traj(horizons, 2)
+    D = np.random.default_rng(3).standard_normal(X.shape)
+    flags = [1, 1, 0]  # mark the end, then a new phase, then grow it
+    hz, ss, re, Xb, Ub, _ = M.shift(horizons, [n + 1 for n in horizons], reach, X, X, U, np.zeros((9, 24, 24)), flags)
+    Xw, Uw, Dw = M.shift_working(horizons, reach, X, U, D, flags)
+    # [3, 2, 4] -> pop, push (end reached) [2, 2, 5] -> pop, new phase [1, 2, 5, 1] -> phase 0 gone, push [2, 5, 2]
+    assert hz == [2, 5, 2] and np.array_equal(Xw, Xb)
+    assert np.array_equal(Uw[0], U[3]) and not Ub[0].any()            # Ubar[0] zeroed, U[0] kept
+    assert np.array_equal(Uw[:6], U[3:9]) and not Uw[6:].any()         # pushed knot and new phase: zero
+    assert np.array_equal(Dw[:8], D[4:12]) and not Dw[8:].any()        # pushed state and new phase: zero
+
+
+def test_shift_constraints_carries_stored_values():
+    """The constraint objects' stored values follow their knots and constraints (PathConstraintBase::
+    pop_front / push_back, ConstraintsBase.h:271-291): a pushed knot's GRF row and a new phase's are
+    zero, a newly registered touchdown constraint's residual is zero, the others move unchanged."""
+    horizons, reach = [3, 2, 4], [0, 0, 0]
+    rng = np.random.default_rng(5)
+    cons = {"reb_delta": rng.random((9, 20)), "reb_eps": rng.random((9, 20)),
+            "td_mask": np.array([[3, 0, 0, 0], [0, 0, 0, 0], [12, 0, 0, 0]], np.int32),
+            "al_sigma": rng.random((3, 4, 4)), "al_lambda": rng.random((3, 4, 4)),
+            "grf_g": rng.random((9, 20)), "td_h": rng.random((3, 4, 4)) * (np.arange(4) == 0)[None, :, None]}
+    out = M.shift_constraints(horizons, reach, cons, [1, 0], 0.1, 0.1, 50.0, 0.0)
+    # step 1: pop knot 0, push a zero knot on the last phase, mark its end -> a pending constraint
+    # step 2: pop knot 1 (phase 0 keeps knot 2), push another zero knot, one more pending constraint
+    assert np.array_equal(out["grf_g"][:7], cons["grf_g"][2:9])
+    assert not out["grf_g"][7:].any()
+    assert np.array_equal(out["td_h"][:, 0], cons["td_h"][:, 0])
+    assert list(out["td_mask"][2]) == [12, M.TD_PENDING, M.TD_PENDING, 0]
+    assert not out["td_h"][2, 1:].any()

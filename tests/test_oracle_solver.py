@@ -60,3 +60,21 @@ def test_converged_elements_meet_reference_tests():
         if r["outer_iters"][b] < o.max_AL_iter:  # stopped by a test, not by the budget
             assert r["feas"][b] <= o.dynamics_feas_thresh
     assert np.all(r["status"] == 0)
+
+
+def test_new_problem_rollout_break_keeps_zero_constraint_values():
+    """Oracle restatement of a new problem's first rollout breaking at knot k (SinglePhase.cpp:
+    205-208): the GRF values of the knots from k on stay zero (create_data) while the trial's
+    control rows there are the warm start's, so the stored values differ from A U exactly there."""
+    import divergence_case as DC
+    prob, breaks, T, es = DC.make_init("trot", 2, 12, 4)
+    r = O.solve_batch(prob, O.default_options(no_early_exit=1, max_AL_iter=1, max_DDP_iter=0), n_threads=4)
+    for b, j in enumerate(breaks):
+        assert r["diverged_init"][b] == (j >= 0)
+        stale = DC.stale_knots(prob, r["U"], r["grf_g"], b)
+        if j < 0:
+            assert stale == []
+            continue
+        # the initial rollout only: the break knot (state slot j + 1's control) and every later
+        # stance knot keep zero values
+        assert len(stale) > 8 and stale[0] == j and all(not r["grf_g"][b, kc].any() for kc in stale)
