@@ -280,6 +280,8 @@ struct hsddp_handle_t {
     hsddp_mpc_command *cmd_dev[2] = {nullptr, nullptr}, *cmd_host[2] = {nullptr, nullptr};
     hipStream_t copy_stream = nullptr;
     hipEvent_t cmd_ready[2] = {nullptr, nullptr}, cmd_copied[2] = {nullptr, nullptr};
+    char *cmd_in_host[2] = {nullptr, nullptr};  // pinned staging of each ticket's durations / feet
+    size_t cmd_in_bytes[2] = {0, 0};
     int cmd_next = 0;
 };
 
@@ -554,6 +556,7 @@ extern "C" int hsddp_destroy(hsddp_handle h)
         if (h->cmd_host[q]) hipHostFree(h->cmd_host[q]);
         if (h->cmd_ready[q]) hipEventDestroy(h->cmd_ready[q]);
         if (h->cmd_copied[q]) hipEventDestroy(h->cmd_copied[q]);
+        if (h->cmd_in_host[q]) hipHostFree(h->cmd_in_host[q]);
     }
     if (h->copy_stream) hipStreamDestroy(h->copy_stream);
     for (hipEvent_t e : h->events) hipEventDestroy(e);
@@ -764,8 +767,8 @@ extern "C" int hsddp_update_problem(hsddp_handle h, const int *contacts, const d
     // keeps Xbar / Ubar / K, the working trajectory (X, U, Defect) and the constraint objects —
     // their ReB / AL parameters (HKDProblem::update's reset_params is a no-op, ConstraintsBase.h:
     // 165-167,341-348) and stored values — as the reference's objects live on into the next tick;
-    // resets dX, dU and the per-element solver state; touchdown constraints added by the shift take
-    // their legs from the new contact rows
+    // resets the per-element solver state; touchdown constraints added by the shift take their legs
+    // from the new contact rows
     return reset_working(h, false);
 }
 
@@ -780,9 +783,16 @@ static int reset_working(hsddp_handle h, bool params)
     const size_t B = p.B, S = p.S, Kc = p.Kc;
     Bufs &d = h->d;
     if (params) launch_reset_working(p, d, h->stream);  // X = Xbar, U = Ubar (one buffer), Defect = 0
-    HIPCHK(hipMemsetAsync(d.dX, 0, B * S * NX * sizeof(double), h->stream));
-    HIPCHK(hipMemsetAsync(d.du, 0, B * Kc * NX * sizeof(double), h->stream));
-    HIPCHK(hipMemsetAsync(d.dU, 0, B * Kc * NX * sizeof(double), h->stream));
+    // dX, du, dU: a new problem's are zero.  Between solves the initial rollout (eps = 0) does not
+    // read them (fma_step / add_step) and the sweep and linear rollout rewrite them before any
+    // trial, so an update keeps them (474 MB of memsets at B = 4096 saved per MPC tick) — except dX
+    // with single shooting, which no linear rollout writes: the trials read it (zero, as in a
+    // problem that never ran multiple shooting; the reference's is never written there either)
+    if (params || p.ms0) HIPCHK(hipMemsetAsync(d.dX, 0, B * S * NX * sizeof(double), h->stream));
+    if (params) {
+        HIPCHK(hipMemsetAsync(d.du, 0, B * Kc * NX * sizeof(double), h->stream));
+        HIPCHK(hipMemsetAsync(d.dU, 0, B * Kc * NX * sizeof(double), h->stream));
+    }
     if (params) {
         launch_init_params(p, d, h->stream);
         h->reb_at_init = true;
@@ -1755,19 +1765,36 @@ static int extract_commands(hsddp_handle h, int nsteps_between_mpc, double mpc_t
     int rc;
     if ((rc = scratch(h, cmd_bytes + dur_bytes + feet_bytes, &buf))) return rc;
     hsddp_mpc_command *dcmd = ticket >= 0 ? h->cmd_dev[ticket] : out_on_device ? out : (hsddp_mpc_command *)buf;
+    const size_t dur_len = (a.dur_per_elem ? B : 1) * p.P * 4 * sizeof(double);
+    const void *dur_src = status_durations, *feet_src = foot_placements;
+    if (ticket >= 0 && (status_durations || foot_placements)) {
+        // the call returns before the kernel runs and the caller may release its (pageable) inputs:
+        // they are copied into this ticket's pinned staging first, and the H2D copies read from
+        // there — nothing waits for the handle's stream.  The staging's previous copies (two
+        // extractions ago) finished before that extraction's kernel, whose event is long past.
+        char *&pin = h->cmd_in_host[ticket];
+        if (h->cmd_in_bytes[ticket] < dur_bytes + feet_bytes) {
+            HIPCHK(hipEventSynchronize(h->cmd_ready[ticket]));
+            if (pin) hipHostFree(pin);
+            pin = nullptr;
+            h->cmd_in_bytes[ticket] = 0;
+            HIPCHK(hipHostMalloc((void **)&pin, dur_bytes + feet_bytes, 0));
+            h->cmd_in_bytes[ticket] = dur_bytes + feet_bytes;
+        } else {
+            HIPCHK(hipEventSynchronize(h->cmd_ready[ticket]));
+        }
+        if (status_durations) std::memcpy(pin, status_durations, dur_len);
+        if (foot_placements) std::memcpy(pin + dur_bytes, foot_placements, feet_bytes);
+        dur_src = pin;
+        feet_src = pin + dur_bytes;
+    }
     if (status_durations) {
         a.durations = (const double *)(buf + cmd_bytes);
-        if ((rc = h2d((void *)a.durations, status_durations, (a.dur_per_elem ? B : 1) * p.P * 4 * sizeof(double), h->stream))) return rc;
+        if ((rc = h2d((void *)a.durations, dur_src, dur_len, h->stream))) return rc;
     }
     if (foot_placements) {
         a.feet = (const float *)(buf + cmd_bytes + dur_bytes);
-        if ((rc = h2d((void *)a.feet, foot_placements, feet_bytes, h->stream))) return rc;
-    }
-    if (ticket >= 0 && (status_durations || foot_placements)) {
-        // the caller's inputs are pageable host memory and the call returns before the kernel runs:
-        // wait for their two small copies (a few microseconds) so the caller may release them
-        HIPCHK(hipEventRecord(h->cmd_ready[ticket], h->stream));
-        HIPCHK(hipEventSynchronize(h->cmd_ready[ticket]));
+        if ((rc = h2d((void *)a.feet, feet_src, feet_bytes, h->stream))) return rc;
     }
     if (ticket >= 0)  // the buffer's previous copy (two extractions ago) has left it
         HIPCHK(hipStreamWaitEvent(h->stream, h->cmd_copied[ticket], 0));

@@ -134,9 +134,10 @@ struct RetryEntry {
 //  * touchdown (h = foot height at X_i[N] - ground): a constraint whose h was never computed since
 //    it was registered (0) carries TD_STALE in its td_mask entry; every other one's h is that of
 //    the working X_i[N] (the rollout that computes h also sets X_i[N], SinglePhase.cpp:196-227).
-// ElemState::ovr / td_stale: some flag of the element may be set (the kernels read the per-knot
-// flags only then); both survive k_reset_elements.  A rollout that passes knot kc / completes
-// phase i clears its flags (k_decide).
+// ElemState::ovr / td_stale: some flag of the element may be set; both survive k_reset_elements.
+// The per-knot GRF flags are read only while ovr is 1 (their contents are arbitrary while it is 0:
+// the fix-up that sets it clears them first, and the shift carries them only then).  A rollout
+// that passes every knot resets ovr; one that completes phase i clears its TD_STALE bits (k_decide).
 constexpr int TD_STALE = 0x20;
 
 struct ElemState {

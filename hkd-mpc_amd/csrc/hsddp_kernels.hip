@@ -590,6 +590,12 @@ DEV bool ls_skip(const Bufs &d, int tix)
 // are formed with coalesced 16-byte loads (lanes over row entries, not rows) into LDS — the output
 // X rows are stored from the same pass — and each lane then reads its rows from LDS.
 constexpr int RS = NX + 1;  // LDS row stride (doubles): conflict-free row-per-lane reads
+
+// The trial's steps b + eps v.  The initial rollout (eps = 0) takes the nominal rows as they are,
+// without reading its (finite or not) step rows into them: dX, du and dU are not reset between
+// solves (hsddp_update_problem), as the reference keeps its own (shifted) from tick to tick.
+DEV double fma_step(double eps, double v, double b) { return eps == 0.0 ? b : __builtin_fma(eps, v, b); }
+DEV double add_step(double b, double eps, double v) { return eps == 0.0 ? b : b + eps * v; }
 constexpr int RW = 65;      // rows per wave: 64 slots and the one before
 
 // X_t = Xbar + eps dX for rows r0 .. r0 + RW - 1 of the [rows][24] state buffers into LDS; rows
@@ -611,8 +617,8 @@ DEV void stage_trial(double *L, const Bufs &d, const double *del, long r0, long 
         typedef double d2 __attribute__((ext_vector_type(2)));
         const d2 xb = *(const d2 *)(bar + r * NX + cc), dx = *(const d2 *)(del + r * NX + cc);
         d2 v;
-        v.x = __builtin_fma(eps, dx.x, xb.x);
-        v.y = __builtin_fma(eps, dx.y, xb.y);
+        v.x = fma_step(eps, dx.x, xb.x);
+        v.y = fma_step(eps, dx.y, xb.y);
         L[row * RS + cc] = v.x;
         L[row * RS + cc + 1] = v.y;
         if (own(r)) *(d2 *)(out + r * NX + cc) = v;
@@ -654,8 +660,8 @@ DEV void stage_trial2(double *L, const Bufs &d, long r0, long nrows, int per, do
         const int f = lane + 64 * it, row = f / CH, cc = 2 * (f % CH);
         const long r = rr[it];
         d2 v;  // Xbar + eps dX as one rounding (rollout_boundary forms the same rows)
-        v.x = __builtin_fma(eps, dx[it].x, xb[it].x);
-        v.y = __builtin_fma(eps, dx[it].y, xb[it].y);
+        v.x = fma_step(eps, dx[it].x, xb[it].x);
+        v.y = fma_step(eps, dx[it].y, xb[it].y);
         L[row * RS + cc] = v.x;
         L[row * RS + cc + 1] = v.y;
         const bool first = r / per == bA;
@@ -676,8 +682,8 @@ DEV void trial_row(const Bufs &d, const double *Ubar, long r, double eps, double
 #pragma unroll
     for (int j = 0; j < NU / 2; ++j) {
         const d2 a = ub[j], e = du[j];
-        u[2 * j] = a.x + eps * e.x;
-        u[2 * j + 1] = a.y + eps * e.y;
+        u[2 * j] = add_step(a.x, eps, e.x);
+        u[2 * j + 1] = add_step(a.y, eps, e.y);
     }
 }
 
@@ -713,7 +719,7 @@ DEV void rollout_boundary(const Params &p, const Bufs &d, double eps, int init, 
     auto trial = [&](int s, double *x) {
         const double *xb = Xbar + (sb + s) * NX, *dx = d.dX + (sb + s) * NX;
 #pragma unroll
-        for (int j = 0; j < NX; ++j) x[j] = __builtin_fma(eps, dx[j], xb[j]);
+        for (int j = 0; j < NX; ++j) x[j] = fma_step(eps, dx[j], xb[j]);
     };
     int c[4], cn[4];
     load_contacts(d, p, b, i, c, cn);
@@ -800,8 +806,8 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
     else
         stage_trial(Xt, d, d.dX, xr0, total, p.S, eps, lane, active, [&](long r) { return r >= g0; }, selof);
     if (up0) {
-        Up0[2 * lane] = ua.x + eps * ue.x;
-        Up0[2 * lane + 1] = ua.y + eps * ue.y;
+        Up0[2 * lane] = add_step(ua.x, eps, ue.x);
+        Up0[2 * lane + 1] = add_step(ua.y, eps, ue.y);
     }
     __syncthreads();
     RSTAMP(2);
@@ -959,7 +965,7 @@ __global__ __launch_bounds__(64) void k_rollout_tail(Params p, Bufs d, double ep
                     u[c[q / 3] ? q : 12 + q] = acc;
                 }
                 double *ug = U + (kb + kc) * NU;
-                for (int j = 0; j < NU; ++j) { u[j] = ub[j] + eps * du[j] + u[j]; ug[j] = u[j]; }
+                for (int j = 0; j < NU; ++j) { u[j] = add_step(ub[j], eps, du[j]) + u[j]; ug[j] = u[j]; }
                 up = u;
             }
             finish_slot(p, d, L, b, s, i, k, c, cn, x, xs, up);
@@ -995,7 +1001,7 @@ DEV void ss_phase(const Params &p, const Bufs &d, int b, int i, double eps, cons
         for (int j = 0; j < NX; ++j) x[j] = x_init[j];
     } else {       // X[0] = Xbar[0] + eps dX[0] (k_rollout's expression)
         const double *xb = Xbar + (sb + s0) * NX, *dx = d.dX + (sb + s0) * NX;
-        for (int j = 0; j < NX; ++j) x[j] = __builtin_fma(eps, dx[j], xb[j]);
+        for (int j = 0; j < NX; ++j) x[j] = fma_step(eps, dx[j], xb[j]);
     }
     for (int k = 0; k <= N; ++k) {
         const int s = s0 + k;
@@ -1021,7 +1027,7 @@ DEV void ss_phase(const Params &p, const Bufs &d, int b, int i, double eps, cons
             u[c[q / 3] ? q : 12 + q] = acc;
         }
         double *ug = U + (kb + kc) * NU;
-        for (int j = 0; j < NU; ++j) { u[j] = ub[j] + eps * du[j] + u[j]; ug[j] = u[j]; }
+        for (int j = 0; j < NU; ++j) { u[j] = add_step(ub[j], eps, du[j]) + u[j]; ug[j] = u[j]; }
         finish_running(p, d, b, s, kc, c, x, u);
         hkd_step(x, u, cd, p.dt, xs);
     }
@@ -1094,8 +1100,9 @@ DEV void diverged_fixup(const Params &p, const Bufs &d, const LayT<EL> &L, int b
     // the break knot's stay what they were — the forces of its entry if it has one, else those of
     // its working control row (the one U[kcb] held before this trial), which becomes its entry
     int *cf = d.cf_flag + kq;
-    if (E.ovr)
-        for (int kc = g; kc < kcb; kc += 16) cf[kc] = 0;
+    // (while E.ovr is 0 the flags are not read and their contents are arbitrary: cleared here first)
+    for (int kc = g; kc < (E.ovr ? kcb : p.Kc); kc += 16)
+        if (kc != kcb) cf[kc] = 0;  // (lane 0 writes the break knot's)
     if (g == 0) {
         if (!(E.ovr && cf[kcb])) {
             for (int r = 0; r < 12; ++r) d.cf_u[(kq + kcb) * 12 + r] = UW[(kq + kcb) * NX + r];
@@ -1196,9 +1203,8 @@ DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int 
     }
     if (act) {
         const ElemState &Er = d.el[b];
-        // a rollout that passed every knot computed every stored GRF value from its rows
-        if (!dvg && Er.ovr)
-            for (int kc = g; kc < p.Kc; kc += 16) d.cf_flag[(size_t)b * p.Kc + kc] = 0;
+        // (a rollout that passed every knot computed every stored GRF value from its rows: E.ovr = 0
+        // below, and the per-knot flags are not read until a fix-up sets it again)
         // the phases it completed computed their touchdown residuals
         if (Er.td_stale && g < P && g < ibrk)
             for (int j = 0; j < MTD; ++j) d.td_mask[((size_t)b * p.P + g) * MTD + j] &= ~TD_STALE;
@@ -1214,7 +1220,7 @@ DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int 
     feas = sqrt(feas);
     E.max_p = max_p;
     E.max_t = max_t;
-    if (!dvg) { E.ovr = 0; E.td_stale = 0; }  // (their flags cleared above)
+    if (!dvg) { E.ovr = 0; E.td_stale = 0; }  // (the stale bits cleared above)
     // one entry of the solver-info buffers (cost_buffer, dyn_feas_buffer, eqn_feas_buffer,
     // ineq_feas_buffer; MultiPhaseDDP.cpp:277-280, 368-371), float as the reference's vectors
     auto push_info = [&]() {

@@ -247,9 +247,11 @@ __global__ __launch_bounds__(256) void k_shift_params(int B, ShiftParamArgs a, B
         const int m = a.map_id ? a.map_id[b] : 0, lab = a.rmap[(size_t)m * a.Kc + k];
         o.reb_delta[gid] = lab >= 0 ? d.reb_delta[(b * a.Kc + lab) * 20 + r] : a.reb_delta0;
         o.reb_eps[gid] = lab >= 0 ? d.reb_eps[(b * a.Kc + lab) * 20 + r] : a.reb_eps0;
-        const int src = a.cmap[(size_t)m * a.Kc + k];
-        if (r < 12) o.cf_u[(b * a.Kc + k) * 12 + r] = src >= 0 ? d.cf_u[(b * a.Kc + src) * 12 + r] : 0.0;
-        if (r == 0) o.cf_flag[b * a.Kc + k] = src >= 0 ? d.cf_flag[b * a.Kc + src] : 0;
+        if (d.el[b].ovr && r < 12) {  // (an element's table is read only while its ovr is set)
+            const int src = a.cmap[(size_t)m * a.Kc + k];
+            o.cf_u[(b * a.Kc + k) * 12 + r] = src >= 0 ? d.cf_u[(b * a.Kc + src) * 12 + r] : 0.0;
+            if (r == 0) o.cf_flag[b * a.Kc + k] = src >= 0 ? d.cf_flag[b * a.Kc + src] : 0;
+        }
         return;
     }
     const long g = gid - nr;

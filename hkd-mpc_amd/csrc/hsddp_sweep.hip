@@ -1441,12 +1441,28 @@ __global__ __launch_bounds__(64) void k_riccati_select(Params p, Bufs d)
 // 1.075 / 1.343, one-wave 0.821 / 0.825 / 0.836 / 0.951 / 1.372 — from two workgroups per CU on,
 // the waves of one CU slow each other (the one-wave kernel too: 0.84 -> 0.95 ms from 256 to 512
 // waves at an unchanged 2.3 GHz clock), and the split's two waves per pair lose.
+// The thresholds below scale with the current device's CU count (256 on an MI355X: the
+// measurements above), so a partitioned or smaller device keeps the same placement rules.
+static int device_cus()
+{
+    static int cus[64] = {0};
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
 static bool sweep_split(const Params &p)
 {
     if (p.fp32) return false;
     const char *e = std::getenv("HSDDP_SWEEP_SPLIT");
     if (e && *e) return *e != '0';
-    return (p.elem_layout ? p.n_pairs : (p.B + 1) / 2) <= 256;
+    return (p.elem_layout ? p.n_pairs : (p.B + 1) / 2) <= device_cus();  // one workgroup per CU
 }
 
 // waves (element pairs) per workgroup of the one-wave sweep k_riccati in fp64: 2 while the launch has
@@ -1460,8 +1476,8 @@ static int sweep_wpb(const Params &p)
     if (p.fp32) return 1;
     const char *e = std::getenv("HSDDP_SWEEP_WPB");
     if (e && *e) return *e == '2' ? 2 : 1;
-    const int pairs = p.elem_layout ? p.n_pairs : (p.B + 1) / 2;
-    return pairs > 256 && pairs <= 1024 ? 2 : 1;
+    const int pairs = p.elem_layout ? p.n_pairs : (p.B + 1) / 2, cus = device_cus();
+    return pairs > cus && pairs <= 4 * cus ? 2 : 1;  // at most one wave per SIMD (4 per CU)
 }
 
 void launch_riccati(const Params &p, const Bufs &d, hipStream_t st)

@@ -354,8 +354,9 @@ int hsddp_set_layout(hsddp_handle h, int n_phases, const int *horizons, const in
  * by hsddp_shift / hsddp_advance, which also append the touchdown constraints add_tconstr_one_phase
  * registers: their legs are the new contact rows' touchdown legs).  The working trajectory (X, U,
  * Defect) and the constraint objects' stored values carry over too (shifted alike): a solve whose
- * initial rollout diverges keeps them past its break, as the reference's objects do.  Resets
- * dX = dU = 0 and the per-element solver state. */
+ * initial rollout diverges keeps them past its break, as the reference's objects do.  Resets the
+ * per-element solver state (dX, dU and du keep their values: the next solve rewrites them before
+ * any line-search trial reads them; with MS false dX is reset to 0). */
 int hsddp_update_problem(hsddp_handle h, const int *contacts, const double *x0, const double *ref_x,
                          const double *ref_u, const double *ref_foot);
 
