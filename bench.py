@@ -115,16 +115,38 @@ def full_solve_c5(prob, device) -> dict:
         ms = (time.perf_counter() - t0) * 1e3
         info = s.element_info()
         res[fp32] = {"ms": ms, "Xbar": s.trajectory()["Xbar"], "status": info["status"], "cost": info["cost"],
-                     "iters": info["iters"], "outer": info["outer_iters"]}
+                     "iters": info["iters"], "outer": info["outer_iters"], "n_ls": info["n_ls_trials"],
+                     "hist": s.solver_info()["cost"]}
         s.close()
     a, b = res[False], res[True]
     dc = np.abs(b["cost"] - a["cost"]) / np.maximum(np.abs(a["cost"]), 1e-30)
+    same_path = (a["iters"] == b["iters"]) & (a["outer"] == b["outer"]) & (a["n_ls"] == b["n_ls"])
+    w = int(np.argmax(dc))
+
+    def parting(ha, hb, tol):
+        """first solver-info entry (the initial one is 0) whose costs differ by more than tol, relative"""
+        n = min(len(ha), len(hb))
+        for j in range(n):
+            if abs(float(hb[j]) - float(ha[j])) > tol * max(abs(float(ha[j])), 1e-30):
+                return j
+        return None if len(ha) == len(hb) else n
     return {"settings": "ddp_setting.info (max_AL_iter 5, max_DDP_iter 10, early exits)",
             "ms_fp32": b["ms"], "ms_fp64": a["ms"],
             "mean_inner_iters_fp32": float(b["iters"].mean()), "mean_inner_iters_fp64": float(a["iters"].mean()),
             "mean_outer_iters_fp32": float(b["outer"].mean()), "mean_outer_iters_fp64": float(a["outer"].mean()),
             "status_agreement": float(np.mean(a["status"] == b["status"])),
             "cost_rel_diff_median": float(np.median(dc)), "cost_rel_diff_max": float(np.max(dc)),
+            # the tail: how many elements part from the fp64 solve, and where the worst one does
+            "n_cost_rel_diff_gt_1e-6": int(np.sum(dc > 1e-6)), "n_cost_rel_diff_gt_1e-3": int(np.sum(dc > 1e-3)),
+            "frac_same_decisions": float(np.mean(same_path)),  # equal inner / outer iterations and trial counts
+            "cost_rel_diff_max_same_decisions": float(np.max(dc[same_path])) if same_path.any() else None,
+            "worst": {"element": w, "cost_fp64": float(a["cost"][w]), "cost_fp32": float(b["cost"][w]),
+                      "iters": [int(a["iters"][w]), int(b["iters"][w])], "outer": [int(a["outer"][w]), int(b["outer"][w])],
+                      "ls_trials": [int(a["n_ls"][w]), int(b["n_ls"][w])],
+                      "first_info_entry_parting_1e-6": parting(a["hist"][w], b["hist"][w], 1e-6),
+                      "first_info_entry_parting_1e-3": parting(a["hist"][w], b["hist"][w], 1e-3),
+                      "cost_history_fp64": [float(v) for v in a["hist"][w]],
+                      "cost_history_fp32": [float(v) for v in b["hist"][w]]},
             "xbar_abs_diff_max": float(np.max(np.abs(b["Xbar"] - a["Xbar"]))),
             "all_finite": bool(np.isfinite(b["Xbar"]).all())}
 

@@ -358,6 +358,10 @@ static void fill_params(hsddp_handle h)
     const hsddp_options &o = h->opt;
     p.dt = ds.dt;
     p.dt_m = ds.dt / hkd::kMass;
+    {
+        const char *tr = std::getenv("HSDDP_TRACE");
+        p.trace = (tr && tr[0] == '1') ? 1 : 0;
+    }
     p.mu = ds.cparams.mu_fric;
     p.grf_delta = ds.cparams.grf_delta; p.grf_delta_min = ds.cparams.grf_delta_min; p.grf_eps = ds.cparams.grf_eps;
     p.td_sigma = ds.cparams.td_sigma; p.td_sigma_max = ds.cparams.td_sigma_max; p.td_lambda = ds.cparams.td_lambda;
@@ -1042,6 +1046,7 @@ static std::vector<double> ls_steps(double alpha)
 
 static void begin_launches(hsddp_handle h)
 {
+    if (h->p.trace) hipMemsetAsync(h->d.dbg, 0, (size_t)h->p.B * 16 * sizeof(unsigned long long), h->stream);
     launch_reset_elements(h->p, h->d, h->stream);
     launch_rollout(h->p, h->d, 0.0, 0, 1, -1, h->stream);
     launch_decide(h->p, h->d, 0.0, 0, 1, -1, h->stream);

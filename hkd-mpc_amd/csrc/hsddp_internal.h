@@ -114,6 +114,9 @@ struct Params {
     // no linear rollout, the sweep forms dV_1 / dV_2 (SinglePhase.cpp:359-362) and the merit, and the
     // rollout simulates every phase from its first state (k_rollout_ss)
     int ms0;
+    // diagnostic (HSDDP_TRACE=1, read at create / option changes): every finished line search records
+    // (trials, accepted, the sweep's regularisation) of its inner iteration in Bufs::dbg (k_decide)
+    int trace;
 };
 
 // one element deferred to the parallel retry: its index and the regularisation of its failed sweep

@@ -1253,6 +1253,15 @@ DEV void decide_group(const Params &p, const Bufs &d, double eps, int last, int 
         if (last) { E.accepted = 0; E.ls_active = 0; E.cost = E.cost_prev; E.merit = E.merit_prev; fin = true; }
     }
     if (!fin && tix >= 0 && tix < LS_LIVE) d.ls_live[tix] = 1;  // still searching (same value from every writer)
+    if (fin && p.trace && E.iters >= 1 && E.iters <= 64) {
+        // diagnostic trace (HSDDP_TRACE): 16 bits per inner iteration — trials (bits 0..2), accepted
+        // (3), the sweep's regularisation as round(log2 mu) + 64 (bits 4..15; 0: mu = 0)
+        const double mu = E.reg * 20;  // (k_riccati leaves mu / 20, or 0 below 1e-6 / 20)
+        const int code = mu > 0 ? min(4095, max(1, (int)rint(log2(mu)) + 64)) : 0;
+        const unsigned long long v = (unsigned long long)((tix + 1) | (E.accepted << 3) | (code << 4)) & 0xffffull;
+        const int it = E.iters - 1;
+        d.dbg[(size_t)b * 16 + it / 4] |= v << (16 * (it % 4));
+    }
     if (fin) {
         // the later-termination test breaks before the iteration's entry is buffered (:358-371)
         if (!p.no_early_exit && fabs((E.cost_prev - E.cost) / E.cost_prev) < p.cost_thresh && E.feas <= p.feas_thresh)
