@@ -591,11 +591,12 @@ DEV bool ls_skip(const Bufs &d, int tix)
 // X rows are stored from the same pass — and each lane then reads its rows from LDS.
 constexpr int RS = NX + 1;  // LDS row stride (doubles): conflict-free row-per-lane reads
 
-// The trial's steps b + eps v.  The initial rollout (eps = 0) takes the nominal rows as they are,
-// without reading its (finite or not) step rows into them: dX, du and dU are not reset between
-// solves (hsddp_update_problem), as the reference keeps its own (shifted) from tick to tick.
-DEV double fma_step(double eps, double v, double b) { return eps == 0.0 ? b : __builtin_fma(eps, v, b); }
-DEV double add_step(double b, double eps, double v) { return eps == 0.0 ? b : b + eps * v; }
+// The trial's steps b + eps v.  dX, du and dU are not reset between solves (hsddp_update_problem),
+// as the reference keeps its own from tick to tick: the initial rollout (eps = 0) multiplies them
+// by 0 as the reference does (SinglePhase.cpp:189, 200, 216).  (A select that skipped them at
+// eps = 0 cost the metric's trials 7 %: k_rollout 148.8 -> 159.7 us.)
+DEV double fma_step(double eps, double v, double b) { return __builtin_fma(eps, v, b); }
+DEV double add_step(double b, double eps, double v) { return b + eps * v; }
 constexpr int RW = 65;      // rows per wave: 64 slots and the one before
 
 // X_t = Xbar + eps dX for rows r0 .. r0 + RW - 1 of the [rows][24] state buffers into LDS; rows

@@ -17,7 +17,7 @@ constexpr int HC = 12;  // coupled controls per knot
 #define HSDDP_STAMPS 0
 #endif
 #ifndef HSDDP_LIN_EXP
-#define HSDDP_LIN_EXP 0  // timing experiments only: 1 no dX / du stores, 2 no arithmetic
+#define HSDDP_LIN_EXP 0  // timing experiments only: 1 no dX / du stores, 2 no arithmetic, 3 no decoupled du stores
 #endif
 // the knot images requested with the non-temporal policy: the iteration's last read of K, the
 // records and dU (0.82 -> 0.73 ms on one box; the sweep's image requests, which the linear rollout
@@ -328,6 +328,7 @@ struct LinOut {
     real vu, vx;      // the pending knot's values
     int n;            // pending knots (0 or 1)
     int nprev;        // store instructions the previous knot issued after its image requests
+    bool ust;         // this lane stores its du entry
 };
 
 template <typename real>
@@ -348,7 +349,7 @@ DEV int lin_store_pending(bool go, bool st, LinOut<real> &out)
     if (!go || out.n == 0) return 0;
     out.n = 0;
     if (st) {
-        *out.du = (double)out.vu;
+        if (out.ust) *out.du = (double)out.vu;
         *out.dx = (double)out.vx;
     }
     out.du += NX;
@@ -550,6 +551,7 @@ __global__ __launch_bounds__(64, 2) void k_lin_rollout(Params p, Bufs d)
         R.cpl = rowl && (rr < HC ? stl : !stl);
         R.krow0 = (rr % HC) * NX;
         lin_row(p, R, r);
+        out.ust = HSDDP_LIN_EXP == 3 ? R.cpl : true;  // (3: timing only, the decoupled du entries not stored)
         out.du = d.du + (b * p.Kc + k0) * NX + rr;
         out.dx = d.dX + (b * p.S + s0 + 1) * NX + rr;
         real q1s = 0, q2s = 0;
