@@ -158,30 +158,33 @@ def test_new_problem_initial_rollout_diverges(kw):
 # pronk element 3 of the receding-horizon batch (B, P, N = 8, 4, 5), translated so that the bound
 # falls between the initial rollout's largest simulated-state norms of ticks 1 and 2: the window
 # (found by bisection over oracle loops) is [447213.5389, 447213.58); its middle
-MPC_T3 = 447213.56
+MPC_T3 = {1: (447213.56, 1), 0: (447213.58, 4)}  # ms -> (translation of element 3, first tick that breaks)
 
 
-def test_mpc_tick_initial_rollout_diverges():
+@pytest.mark.parametrize("ms", [1, 0])
+def test_mpc_tick_initial_rollout_diverges(ms):
     """HKDMPCSolver::update's loop (shift, new inputs, re-solve with max_AL_iter = 2, max_DDP_iter = 1)
-    on a batch whose element 3 is translated until, from tick 2 on, the initial rollout of every
-    solve breaks (SinglePhase.cpp:205-208).  The reference's objects live on from tick to tick:
+    on a batch whose element 3 is translated until, from a later tick on, the initial rollout of
+    every solve breaks (SinglePhase.cpp:205-208): from the 2nd tick on with multiple shooting, from
+    the 5th on in single shooting (MS false; T chosen where the oracle's decisions hold over
+    T +- 1e-5 and under a 1e-15 perturbation, the earlier ticks' line searches diverging too).  The reference's objects live on from tick to tick:
     past the break the solve keeps the working trajectory of the previous tick (shifted, quirk A2
     included) and the constraint objects' stored values (shifted with their knots; zero for pushed
     knots and new touchdown constraints), and the tick's cost, LQ model and merit read them.  Every
     tick against the oracle doing the same (mpc_oracle.shift_working / shift_constraints)."""
     B, P, N, ticks = 8, 4, 5, 8
-    T = np.zeros(B); T[3] = MPC_T3
-    prob, r0, out = DC.mpc_loop_oracle(B, P, N, T, ticks)
-    _, r0p, outp = DC.mpc_loop_oracle(B, P, N, T, ticks, perturb=1e-15)
+    T = np.zeros(B); T[3], first = MPC_T3[ms]
+    prob, r0, out = DC.mpc_loop_oracle(B, P, N, T, ticks, ms=ms)
+    _, r0p, outp = DC.mpc_loop_oracle(B, P, N, T, ticks, ms=ms, perturb=1e-15)
     div = [t["r"]["diverged_init"][3] for t in out]
-    assert r0["diverged_init"][3] == 0 and div[0] == 0 and all(div[1:]), div
+    assert r0["diverged_init"][3] == 0 and not any(div[:first]) and all(div[first:]), div
     assert all(t["r"]["diverged_init"][b] == 0 for t in out for b in range(B) if b != 3)
-    s = hsddp.Solver(prob, hsddp.load_settings())
+    s = hsddp.Solver(prob, hsddp.load_settings(MS=ms))
     s.solve()
     g = {**s.trajectory(), **s.element_info()}
     for f in ("n_ls_trials", "status"):
         assert np.array_equal(g[f], r0[f]), f
-    s.set_options(hsddp.load_settings(max_AL_iter=2, max_DDP_iter=1))
+    s.set_options(hsddp.load_settings(max_AL_iter=2, max_DDP_iter=1, MS=ms))
     for it, (t, tp) in enumerate(zip(out, outp)):
         s.shift(t["flags"])
         inp = t["inp"]
