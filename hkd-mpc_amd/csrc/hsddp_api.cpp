@@ -260,6 +260,7 @@ struct hsddp_handle_t {
     int ref_n = 0;
     float ref_dt = 0;
     bool refs_on_device = false;  // references built by hsddp_build_references for this layout
+    bool ref_cols_stale = true;   // Bufs::ref_t behind the reference rows (refreshed by begin_launches)
     // reference-driven MPC state (hsddp_advance): the table's samples on the host (contacts and
     // durations are read there), each reference element's window start, the window length and
     // the simulation step of the last hsddp_build_references, QuadReference::t_cur, and the
@@ -466,7 +467,8 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
     int *contacts; double *x0, *rx, *ru, *rf;
     int rc = 0;
     if ((rc = dalloc(h, contacts, B * (P + 1) * 4)) || (rc = dalloc(h, x0, B * NX)) || (rc = dalloc(h, rx, Br * S * NX)) ||
-        (rc = dalloc(h, ru, Br * S * NX)) || (rc = dalloc(h, rf, Br * S * 12)) || (rc = dalloc(h, d.X3, 3 * B * S * NX)) ||
+        (rc = dalloc(h, ru, Br * S * NX)) || (rc = dalloc(h, rf, Br * S * 12)) || (rc = dalloc(h, d.ref_t, REF_COLS * Br * S)) ||
+        (rc = dalloc(h, d.X3, 3 * B * S * NX)) ||
         (rc = dalloc(h, d.D3, 3 * B * S * NX)) || (rc = dalloc(h, d.U3, 3 * B * Kc * NX)) || (rc = dalloc(h, d.sel, B)) ||
         (rc = dalloc(h, d.cf_u, B * Kc * 12)) || (rc = dalloc(h, d.cf_flag, B * Kc)) ||
         (rc = dalloc(h, d.dX, B * S * NX)) ||
@@ -486,6 +488,7 @@ extern "C" int hsddp_create(const hsddp_problem_desc *desc, hsddp_handle *out)
         return rc;
     }
     d.contacts = contacts; d.x0 = x0; d.ref_x = rx; d.ref_u = ru; d.ref_foot = rf;
+    d.ref_tw = Br * S;
     d.xs3 = B * S * NX;  // (S = S_cap here)
     d.us3 = B * Kc * NX;
     d.rows3 = (int)(B * S);
@@ -672,6 +675,7 @@ extern "C" int hsddp_set_element_layouts(hsddp_handle h, const int *n_phases, co
     h->have_problem = false;  // inputs of the new layouts next (hsddp_upload_problem)
     h->contacts_current = false;
     h->refs_on_device = false;
+    h->ref_cols_stale = true;
     return HSDDP_OK;
 }
 
@@ -732,7 +736,10 @@ static int upload_inputs(hsddp_handle h, const int *contacts, const double *x0, 
          (rc = h2d((void *)h->d.ref_u, ref_u, Br * S * NX * sizeof(double), h->stream)) ||
          (rc = h2d((void *)h->d.ref_foot, ref_foot, Br * S * 12 * sizeof(double), h->stream))))
         return rc;
-    if (!keep_refs) h->refs_on_device = false;
+    if (!keep_refs) {
+        h->refs_on_device = false;
+        h->ref_cols_stale = true;
+    }
     h->contacts.assign(contacts, contacts + B * (P + 1) * 4);
     h->contacts_current = true;
     return HSDDP_OK;
@@ -1047,6 +1054,10 @@ static std::vector<double> ls_steps(double alpha)
 static void begin_launches(hsddp_handle h)
 {
     if (h->p.trace) hipMemsetAsync(h->d.dbg, 0, (size_t)h->p.B * 16 * sizeof(unsigned long long), h->stream);
+    if (h->ref_cols_stale) {
+        launch_ref_columns(h->p, h->d, h->Bref, h->stream);
+        h->ref_cols_stale = false;
+    }
     launch_reset_elements(h->p, h->d, h->stream);
     launch_rollout(h->p, h->d, 0.0, 0, 1, -1, h->stream);
     launch_decide(h->p, h->d, 0.0, 0, 1, -1, h->stream);
@@ -2108,6 +2119,7 @@ static int shift_impl(hsddp_handle h, int n_steps, const int *cc, size_t bstride
     }
     h->need_inputs = true;
     h->refs_on_device = false;  // built for the old layout
+    h->ref_cols_stale = true;
     h->contacts_current = false;
     if (async) {
         h->shift_overflow_pending = true;
@@ -2195,6 +2207,7 @@ extern "C" int hsddp_set_layout(hsddp_handle h, int n_phases, const int *horizon
     h->need_inputs = false;
     h->contacts_current = false;
     h->refs_on_device = false;
+    h->ref_cols_stale = true;
     return HSDDP_OK;
 }
 
@@ -2312,6 +2325,7 @@ static int build_refs(hsddp_handle h, const int *window_start, int window_len, c
         return rc;
     RefArgs a{h->ref_table, h->ref_n, dstart, didx, elem ? dmap : nullptr};
     launch_build_refs(p, h->d, Br, a, h->stream);
+    h->ref_cols_stale = false;  // (k_build_refs writes the entry-major copy too)
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(h->stream));
     h->refs_on_device = true;

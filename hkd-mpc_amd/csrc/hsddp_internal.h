@@ -155,6 +155,12 @@ struct Bufs {
     const int *contacts;                   // [B][P+1][4]
     const double *x0;                      // [B][24]
     const double *ref_x, *ref_u, *ref_foot; // [Bref][S][24|24|12]
+    // the same references entry-major, for kernels with one slot per lane (a lane's entry j is next to
+    // its neighbours': one contiguous piece per wave instead of 64 rows): [REF_COLS][ref_tw], column
+    // r = (ref_per_element ? b : 0) S + s, entries ref_x 0 .. 23, ref_u 24 .. 47, ref_foot 48 .. 59.
+    // Refreshed from the rows by launch_ref_columns whenever the rows change (hsddp_api.cpp)
+    double *ref_t;
+    size_t ref_tw;
     // Trajectory::update_nominal_vals without copies: each element's nominal (Xbar, Ubar) and working
     // (X, U, Defect) rows live in two of three buffers, sel[b] bits 0-1 = the nominal's index, bits
     // 2-3 = the working one's.  A line-search trial writes the third (trial_buf: neither, so that a
@@ -217,6 +223,9 @@ void launch_reset_elements(const Params &p, const Bufs &d, hipStream_t st);
 void launch_init_params(const Params &p, const Bufs &d, hipStream_t st);
 // TD_PENDING touchdown masks resolved from the contact rows (after new contacts are uploaded)
 void launch_resolve_td(const Params &p, const Bufs &d, hipStream_t st);
+// Bufs::ref_t from the reference rows (Bref x S columns)
+constexpr int REF_COLS = 24 + 24 + 12;  // (ref_x, ref_u, ref_foot widths)
+void launch_ref_columns(const Params &p, const Bufs &d, int Bref, hipStream_t st);
 void launch_count(const Params &p, const Bufs &d, int which, hipStream_t st);
 void launch_stat_sums(const Params &p, const Bufs &d, hipStream_t st);
 // dst[c][n] = src[n] for c < copies

@@ -541,9 +541,31 @@ DEV void finish_terminal(const Params &p, const Bufs &d, int b, int s, int i, co
     for (int l = 0; l < 4; ++l) d.term_h[((size_t)b * p.P + i) * 4 + l] = h[l];
 }
 
-// the running cost of control slot kc = k0(i) + k at state slot s
+// the running cost of control slot kc = k0(i) + k at state slot s; COLS: the reference from the
+// entry-major copy (Bufs::ref_t: lanes on consecutive slots read contiguous pieces)
+template <bool COLS = false>
 DEV void finish_running(const Params &p, const Bufs &d, int b, int s, int kc, const int *c, const double *x, const double *u)
 {
+    if constexpr (COLS) {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        const size_t r = (size_t)(p.ref_per_element ? b : 0) * p.S + s, w = d.ref_tw;
+        const d2 *col = (const d2 *)d.ref_t + r;
+        alignas(16) double xr[NX], ur[NU], pf[12];
+        d2 v[REF_COLS / 2];
+#pragma unroll
+        for (int j = 0; j < REF_COLS / 2; ++j) v[j] = col[j * w];
+#pragma unroll
+        for (int j = 0; j < NX / 2; ++j) { xr[2 * j] = v[j].x; xr[2 * j + 1] = v[j].y; }
+#pragma unroll
+        for (int j = 0; j < NU / 2; ++j) { ur[2 * j] = v[NX / 2 + j].x; ur[2 * j + 1] = v[NX / 2 + j].y; }
+#pragma unroll
+        for (int j = 0; j < 6; ++j) { pf[2 * j] = v[(NX + NU) / 2 + j].x; pf[2 * j + 1] = v[(NX + NU) / 2 + j].y; }
+        const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
+        double viol;
+        d.slot_cost[(size_t)b * p.S + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
+        d.slot_viol[(size_t)b * p.S + s] = viol;
+        return;
+    }
     const size_t sb = (size_t)b * p.S;
 #if HSDDP_RO_EXP == 3
     d.slot_cost[sb + s] = x[0];  // timing only: no running cost
@@ -669,6 +691,10 @@ DEV void stage_trial2(double *L, const Bufs &d, long r0, long nrows, int per, do
         if (r >= g0) *(d2 *)((first ? outA : outB) + r * NX + cc) = v;
     }
 }
+
+#ifndef HSDDP_RO_COLS
+#define HSDDP_RO_COLS 1  // the slot waves' reference reads from Bufs::ref_t (0: from the rows)
+#endif
 
 #ifndef HSDDP_ROLLOUT_WAVES
 #define HSDDP_ROLLOUT_WAVES 2  // measured: 2 (256 VGPRs, no spills) 0.93 ms/step forward vs 3: 1.23, 4: 1.07
@@ -834,7 +860,7 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
 #endif
 #pragma unroll
         for (int j = 0; j < NU / 2; ++j) ug[j] = d2{u[2 * j], u[2 * j + 1]};
-        finish_running(p, d, b, s, L.k0(i) + k, c, x, u);
+        finish_running<HSDDP_RO_COLS>(p, d, b, s, L.k0(i) + k, c, x, u);
     }
     RSTAMP(4);
     // u_prev: the previous slot's control row is the previous lane's (k > 0: slot s - 1 is a
@@ -1490,6 +1516,23 @@ __global__ __launch_bounds__(256) void k_resolve_td(Params p, Bufs d)
     load_contacts(d, p, b, i, c, cn);
     const int legs = td_bits(c, cn);
     m = legs ? legs | (m & TD_STALE) : 0;
+}
+
+// Bufs::ref_t: one thread per (entry j, column r), j-major so that the column stores are contiguous
+__global__ __launch_bounds__(256) void k_ref_columns(Bufs d, long ncol)
+{
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= ncol * REF_COLS) return;
+    const int j = (int)(gid / ncol);
+    const long r = gid % ncol;
+    const double v = j < NX ? d.ref_x[r * NX + j] : j < NX + NU ? d.ref_u[r * NU + j - NX] : d.ref_foot[r * 12 + j - NX - NU];
+    d.ref_t[((size_t)(j >> 1) * d.ref_tw + r) * 2 + (j & 1)] = v;
+}
+
+void launch_ref_columns(const Params &p, const Bufs &d, int Bref, hipStream_t st)
+{
+    const long ncol = (long)Bref * p.S, n = ncol * REF_COLS;
+    hipLaunchKernelGGL(k_ref_columns, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, ncol);
 }
 
 // which: 0 = elements with ls_active, 1 = elements still iterating (!done && !inner_done), 2 = !done

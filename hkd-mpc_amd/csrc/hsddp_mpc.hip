@@ -312,6 +312,12 @@ __global__ __launch_bounds__(256) void k_build_refs(Params p, Bufs d, int Bref, 
         ru[12 + j] = q[RT_QJD + j];
         rf[j] = q[RT_FOOT + j];
     }
+    // the entry-major copy (Bufs::ref_t, column gid) from the rows just written: no separate pass
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    d2 *col = (d2 *)d.ref_t + gid;
+    for (int j = 0; j < NX / 2; ++j) col[(size_t)j * d.ref_tw] = d2{rx[2 * j], rx[2 * j + 1]};
+    for (int j = 0; j < NU / 2; ++j) col[(size_t)(NX / 2 + j) * d.ref_tw] = d2{ru[2 * j], ru[2 * j + 1]};
+    for (int j = 0; j < 6; ++j) col[(size_t)((NX + NU) / 2 + j) * d.ref_tw] = d2{rf[2 * j], rf[2 * j + 1]};
 }
 
 void launch_build_refs(const Params &p, const Bufs &d, int Bref, const RefArgs &a, hipStream_t st)
