@@ -141,7 +141,8 @@ def test_shift_elements_equals_uniform_shifts():
     gaits = ["trot"] * B
     Pm, Sm = m.P, m.S
     c, rx, ru, rf = _inputs(gaits, hzs, 1, Pm, Sm, B)
-    # the warm start right after the shift (before new inputs: X = Xbar is reset by update_problem)
+    # the warm start right after the shift and the new inputs (update_problem keeps Xbar / Ubar / K
+    # and the working rows, as the reference's objects live on into the next tick)
     m.update_problem(c, prob["x0"], rx, ru, rf)
     wm = m.trajectory()
     m.solve()
