@@ -130,6 +130,25 @@ DEV const double *ref_ptr(const Params &p, const double *base, int b, int s, int
     return base + ((size_t)(p.ref_per_element ? b : 0) * p.S + s) * width;
 }
 
+// The reference of state slot s from the entry-major copy (Bufs::ref_t) into rows xr[24], ur[24],
+// pf[12]: 30 16-byte loads in flight at once, and lanes on consecutive slots read one contiguous
+// piece per entry pair (the rows would be 64 lines per load instruction)
+DEV void ref_from_cols(const Params &p, const Bufs &d, int b, int s, double *xr, double *ur, double *pf)
+{
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const size_t r = (size_t)(p.ref_per_element ? b : 0) * p.S + s, w = d.ref_tw;
+    const d2 *col = (const d2 *)d.ref_t + r;
+    d2 v[REF_COLS / 2];
+#pragma unroll
+    for (int j = 0; j < REF_COLS / 2; ++j) v[j] = col[j * w];
+#pragma unroll
+    for (int j = 0; j < NX / 2; ++j) { xr[2 * j] = v[j].x; xr[2 * j + 1] = v[j].y; }
+#pragma unroll
+    for (int j = 0; j < NU / 2; ++j) { ur[2 * j] = v[NX / 2 + j].x; ur[2 * j + 1] = v[NX / 2 + j].y; }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) { pf[2 * j] = v[(NX + NU) / 2 + j].x; pf[2 * j + 1] = v[(NX + NU) / 2 + j].y; }
+}
+
 // ReB barrier (ConstraintsBase.h:204-263)
 DEV double reb_cost(double g, double delta, double log_delta)
 {

@@ -547,19 +547,8 @@ template <bool COLS = false>
 DEV void finish_running(const Params &p, const Bufs &d, int b, int s, int kc, const int *c, const double *x, const double *u)
 {
     if constexpr (COLS) {
-        typedef double d2 __attribute__((ext_vector_type(2)));
-        const size_t r = (size_t)(p.ref_per_element ? b : 0) * p.S + s, w = d.ref_tw;
-        const d2 *col = (const d2 *)d.ref_t + r;
         alignas(16) double xr[NX], ur[NU], pf[12];
-        d2 v[REF_COLS / 2];
-#pragma unroll
-        for (int j = 0; j < REF_COLS / 2; ++j) v[j] = col[j * w];
-#pragma unroll
-        for (int j = 0; j < NX / 2; ++j) { xr[2 * j] = v[j].x; xr[2 * j + 1] = v[j].y; }
-#pragma unroll
-        for (int j = 0; j < NU / 2; ++j) { ur[2 * j] = v[NX / 2 + j].x; ur[2 * j + 1] = v[NX / 2 + j].y; }
-#pragma unroll
-        for (int j = 0; j < 6; ++j) { pf[2 * j] = v[(NX + NU) / 2 + j].x; pf[2 * j + 1] = v[(NX + NU) / 2 + j].y; }
+        ref_from_cols(p, d, b, s, xr, ur, pf);
         const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
         double viol;
         d.slot_cost[(size_t)b * p.S + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
