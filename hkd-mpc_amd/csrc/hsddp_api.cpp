@@ -1051,13 +1051,19 @@ static std::vector<double> ls_steps(double alpha)
     return trials;
 }
 
+// Bufs::ref_t refreshed from the reference rows if an upload changed them since (before any
+// launch that reads the references; never inside a graph capture)
+static void sync_ref_columns(hsddp_handle h)
+{
+    if (!h->ref_cols_stale) return;
+    launch_ref_columns(h->p, h->d, h->Bref, h->stream);
+    h->ref_cols_stale = false;
+}
+
 static void begin_launches(hsddp_handle h)
 {
     if (h->p.trace) hipMemsetAsync(h->d.dbg, 0, (size_t)h->p.B * 16 * sizeof(unsigned long long), h->stream);
-    if (h->ref_cols_stale) {
-        launch_ref_columns(h->p, h->d, h->Bref, h->stream);
-        h->ref_cols_stale = false;
-    }
+    sync_ref_columns(h);
     launch_reset_elements(h->p, h->d, h->stream);
     launch_rollout(h->p, h->d, 0.0, 0, 1, -1, h->stream);
     launch_decide(h->p, h->d, 0.0, 0, 1, -1, h->stream);
@@ -1291,6 +1297,7 @@ extern "C" int hsddp_iterate(hsddp_handle h, int n, hsddp_stats *stats)
     Timer tm{h->stream, stats != nullptr, &h->events};
     hipEvent_t e0 = start_stats(h, stats);
     const std::vector<double> trials = ls_steps(h->opt.alpha);
+    sync_ref_columns(h);  // (references uploaded after hsddp_solve_begin)
     for (int i = 0; i < n; ++i) iteration_launches(h, trials, tm);
     return finish_stats(h, tm, e0, stats, n, 0, n);
 }
