@@ -179,46 +179,40 @@ DEV double grf_value(double mu, int r, const double *f)
     return row[0] * f[0] + row[1] * f[1] + row[2] * f[2];
 }
 
-// running cost l_k (tracking + foot regularisation + dt * ReB), and min(0, min g)
-DEV double running_cost(const Params &p, const int *c, const double *x, const double *u, const double *xr,
-                        const double *ur, const double *pf, const double *delta, const double *eps, double &viol,
-                        const double *ovr = nullptr)
+// The running cost's terms (running_cost below): the tracking, control and foot sums over their
+// entries in order, the dt * ReB sum with min(0, min g), and their combination.  Split so that a
+// caller can bring the reference in pieces (k_rollout's slot waves), every term computed as
+// running_cost computes it.
+DEV double cost_tracking(const Params &p, const int *c, const double *x, const double *xrv)
 {
-    // ovr: older control forces of the stored GRF constraint values (constraint_forces), else u's.
-    // The reference rows (16-byte aligned: rows of 24 / 12 doubles) as 16-byte loads, all issued
-    // before the first use (a lane reads its own slot's rows: each instruction touches up to 64
-    // lines, and the vector L1 serves the later pieces of a row — read past it (nt), the forward
-    // line search took twice as long)
-    typedef double d2v __attribute__((ext_vector_type(2)));
-    double xrv[NX], urv[NU], pfv[12];
-#pragma unroll
-    for (int j = 0; j < NX / 2; ++j) {
-        const d2v a = ((const d2v *)xr)[j], b = ((const d2v *)ur)[j];
-        xrv[2 * j] = a.x; xrv[2 * j + 1] = a.y;
-        urv[2 * j] = b.x; urv[2 * j + 1] = b.y;
-    }
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        const d2v a = ((const d2v *)pf)[j];
-        pfv[2 * j] = a.x; pfv[2 * j + 1] = a.y;
-    }
-    double lt = 0.0, lu = 0.0, lf = 0.0;
+    double lt = 0.0;
 #pragma unroll
     for (int j = 0; j < NX; ++j) { double e = x[j] - xrv[j]; lt += e * q_diag(p, c, j) * e; }
-    lt = 0.5 * lt;
+    return lt;
+}
+DEV double cost_control(const Params &p, const double *u, const double *urv)
+{
+    double lu = 0.0;
 #pragma unroll
     for (int j = 0; j < NX; ++j) { double e = u[j] - urv[j]; lu += e * r_diag(p, j) * e; }
-    lt += 0.5 * lu;
-    lt *= p.dt;
+    return lu;
+}
+DEV double cost_foot(const Params &p, const int *c, const double *x, const double *xrv, const double *pfv)
+{
+    double lf = 0.0;
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
         double e = (x[12 + j] - x[3 + j % 3]) - (pfv[j] - xrv[3 + j % 3]);
         lf += e * foot_weight(p, c, j) * e;
     }
-    lf = .5 * lf;
-    lf *= p.dt;
-    double l = lt + lf;
-    double rc = 0.0, mk = 0.0;
+    return lf;
+}
+// ovr: older control forces of the stored GRF constraint values (constraint_forces), else u's
+DEV double cost_reb(const Params &p, const int *c, const double *u, const double *delta, const double *eps, double &mk,
+                    const double *ovr)
+{
+    double rc = 0.0;
+    mk = 0.0;
     // unrolled: a runtime leg index into u would put the control vector in scratch.  Uniform ReB
     // parameters (the default schedule): one log(delta) for the 20 rows, the value each would compute
     auto reb_sum = [&](auto uniform) {
@@ -257,9 +251,47 @@ DEV double running_cost(const Params &p, const int *c, const double *x, const do
     };
     if (p.reb_uniform) reb_sum(std::true_type{});
     else reb_sum(std::false_type{});
+    return rc;
+}
+DEV double cost_combine(const Params &p, const int *c, double lt, double lu, double lf, double rc)
+{
+    lt = 0.5 * lt;
+    lt += 0.5 * lu;
+    lt *= p.dt;
+    lf = .5 * lf;
+    lf *= p.dt;
+    double l = lt + lf;
     if (p.ReB_active && (c[0] + c[1] + c[2] + c[3]) > 0) l += p.dt * rc;
-    viol = mk;
     return l;
+}
+
+// running cost l_k (tracking + foot regularisation + dt * ReB), and min(0, min g)
+DEV double running_cost(const Params &p, const int *c, const double *x, const double *u, const double *xr,
+                        const double *ur, const double *pf, const double *delta, const double *eps, double &viol,
+                        const double *ovr = nullptr)
+{
+    // The reference rows (16-byte aligned: rows of 24 / 12 doubles) as 16-byte loads, all issued
+    // before the first use (a lane reads its own slot's rows: each instruction touches up to 64
+    // lines, and the vector L1 serves the later pieces of a row — read past it (nt), the forward
+    // line search took twice as long)
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    double xrv[NX], urv[NU], pfv[12];
+#pragma unroll
+    for (int j = 0; j < NX / 2; ++j) {
+        const d2v a = ((const d2v *)xr)[j], b = ((const d2v *)ur)[j];
+        xrv[2 * j] = a.x; xrv[2 * j + 1] = a.y;
+        urv[2 * j] = b.x; urv[2 * j + 1] = b.y;
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const d2v a = ((const d2v *)pf)[j];
+        pfv[2 * j] = a.x; pfv[2 * j + 1] = a.y;
+    }
+    const double lt = cost_tracking(p, c, x, xrv), lu = cost_control(p, u, urv), lf = cost_foot(p, c, x, xrv, pfv);
+    double mk;
+    const double rc = cost_reb(p, c, u, delta, eps, mk, ovr);
+    viol = mk;
+    return cost_combine(p, c, lt, lu, lf, rc);
 }
 
 // The step after the sweep / linear rollout of MultiPhaseDDP::solve (MultiPhaseDDP.cpp:331-343):

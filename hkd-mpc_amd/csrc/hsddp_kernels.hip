@@ -547,12 +547,50 @@ template <bool COLS = false>
 DEV void finish_running(const Params &p, const Bufs &d, int b, int s, int kc, const int *c, const double *x, const double *u)
 {
     if constexpr (COLS) {
+        const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
+#if HSDDP_RO_STAGED
+        // the reference in two pieces, so that the 60 values are never live at once: the control
+        // reference first (the ReB term, which needs none, covers its loads), then the state and
+        // foot references
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        const size_t r = (size_t)(p.ref_per_element ? b : 0) * p.S + s, w = d.ref_tw;
+        const d2 *col = (const d2 *)d.ref_t + r;
+        double lu, mk, rc;
+        {
+            d2 v[NU / 2];
+#pragma unroll
+            for (int j = 0; j < NU / 2; ++j) v[j] = col[(NX / 2 + j) * w];
+            rc = cost_reb(p, c, u, dl, ep, mk, nullptr);
+            double urv[NU];
+#pragma unroll
+            for (int j = 0; j < NU / 2; ++j) { urv[2 * j] = v[j].x; urv[2 * j + 1] = v[j].y; }
+            lu = cost_control(p, u, urv);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        double lt, lf;
+        {
+            d2 v[(NX + 12) / 2];
+#pragma unroll
+            for (int j = 0; j < NX / 2; ++j) v[j] = col[j * w];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) v[NX / 2 + j] = col[((NX + NU) / 2 + j) * w];
+            double xrv[NX], pfv[12];
+#pragma unroll
+            for (int j = 0; j < NX / 2; ++j) { xrv[2 * j] = v[j].x; xrv[2 * j + 1] = v[j].y; }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) { pfv[2 * j] = v[NX / 2 + j].x; pfv[2 * j + 1] = v[NX / 2 + j].y; }
+            lt = cost_tracking(p, c, x, xrv);
+            lf = cost_foot(p, c, x, xrv, pfv);
+        }
+        d.slot_cost[(size_t)b * p.S + s] = cost_combine(p, c, lt, lu, lf, rc);
+        d.slot_viol[(size_t)b * p.S + s] = mk;
+#else
         alignas(16) double xr[NX], ur[NU], pf[12];
         ref_from_cols(p, d, b, s, xr, ur, pf);
-        const double *dl = d.reb_delta + ((size_t)b * p.Kc + kc) * 20, *ep = d.reb_eps + ((size_t)b * p.Kc + kc) * 20;
         double viol;
         d.slot_cost[(size_t)b * p.S + s] = running_cost(p, c, x, u, xr, ur, pf, dl, ep, viol);
         d.slot_viol[(size_t)b * p.S + s] = viol;
+#endif
         return;
     }
     const size_t sb = (size_t)b * p.S;
@@ -681,6 +719,9 @@ DEV void stage_trial2(double *L, const Bufs &d, long r0, long nrows, int per, do
     }
 }
 
+#ifndef HSDDP_RO_STAGED
+#define HSDDP_RO_STAGED 1  // the slot waves' reference loaded in two pieces (0: all 30 pairs at once)
+#endif
 #ifndef HSDDP_RO_COLS
 #define HSDDP_RO_COLS 1  // the slot waves' reference reads from Bufs::ref_t (0: from the rows)
 #endif
