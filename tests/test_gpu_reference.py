@@ -266,3 +266,30 @@ def test_advance_loop_matches_oracle():
         assert np.array_equal(g["n_ls_trials"], r["n_ls_trials"]), it
     assert n_td >= 2
     dev.close()
+
+
+def test_references_uploaded_after_begin_reach_the_line_search():
+    """The line search reads the references from an entry-major copy (Bufs::ref_t), refreshed
+    from the uploaded rows before the next launches that read them — also when new references
+    arrive between hsddp_solve_begin and hsddp_iterate.  A handle that began with other references
+    and then took the new ones must iterate exactly as one that had the new ones from the start
+    (the trials' running costs decide acceptance, so stale columns would part them)."""
+    from hsddp import synthetic as syn
+    prob = syn.make_batch(64, 4, 50, "trot")
+    rx2 = prob["ref_x"].copy()
+    rx2[..., 5] += 0.03   # a higher body (and the foot references with it: a different running cost)
+    rx2[..., 3] += 0.02
+    prob1 = dict(prob)
+    prob2 = dict(prob, ref_x=rx2)
+    opts = hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=3)
+    out = []
+    for p in (prob1, prob2):
+        s = hsddp.Solver(p, opts)
+        s.begin()
+        s.update_problem(prob["contacts"], prob["x0"], rx2, prob["ref_u"], prob["ref_foot"])
+        s.iterate(3)
+        out.append({**s.trajectory(), **s.element_info()})
+        s.close()
+    a, b = out
+    for f in ("Xbar", "Ubar", "K", "cost", "n_ls_trials", "status"):
+        assert np.array_equal(a[f], b[f]), f
