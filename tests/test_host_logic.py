@@ -119,3 +119,36 @@ def test_validate_options_refuses_unending_regularisation_schedule():
     assert L.hsddp_validate_options(C.byref(o)) == 0
     o = hsddp.default_options(alpha=1.0)
     assert L.hsddp_validate_options(C.byref(o)) == -1
+
+
+def test_every_handle_entry_point_refuses_a_null_handle():
+    """Every C-ABI function that takes a handle returns HSDDP_ERR_ARG for a NULL handle (NULL
+    pointers and zeros elsewhere) without touching a device; hsddp_destroy(NULL) is a no-op and
+    hsddp_device_bytes(NULL) is 0 (include/hsddp.h)."""
+    hdr = open(os.path.join(ROOT, "include", "hsddp.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    hdr = re.sub(r"//[^\n]*", "", hdr)
+    L = C.CDLL(_lib.LIB_PATH)
+    err_arg = int(re.search(r"HSDDP_ERR_ARG\s*=\s*(-?\d+)", open(os.path.join(ROOT, "include", "hsddp.h")).read()).group(1))
+    seen = 0
+    for ret, name, args in re.findall(r"\b([a-z_0-9 ]+?\**)\s*\b(hsddp_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", hdr):
+        params = [a.strip() for a in args.split(",") if a.strip()]
+        if not params or not params[0].startswith("hsddp_handle"):
+            continue
+        vals = []
+        for a in params:
+            if "*" in a or a.startswith("hsddp_handle"):
+                vals.append(None)
+            elif a.startswith("double"):
+                vals.append(C.c_double(0))
+            elif a.startswith("float"):
+                vals.append(C.c_float(0))
+            else:
+                vals.append(C.c_int(0))
+        f = getattr(L, name)
+        f.restype = C.c_size_t if "size_t" in ret else C.c_int
+        rc = f(*vals)
+        want = 0 if name in ("hsddp_destroy", "hsddp_device_bytes") else err_arg
+        assert rc == want, (name, rc)
+        seen += 1
+    assert seen >= 30
