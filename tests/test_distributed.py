@@ -1,4 +1,4 @@
-"""Multi-process path on CPU (gloo, world_size 2): the batch shards by element with no exchange
+"""Multi-process path on CPU (gloo, world_size 2 and 4): the batch shards by element with no exchange
 during the solve; only a final gather of per-element summaries.  The HIP solve is
 replaced here by the oracle because this container has no GPU; bench.py runs the same sharding
 with the HIP path and RCCL on the GPU box."""
@@ -63,9 +63,10 @@ def _worker(rank, world, port, B, out_dir):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_shards_and_gather(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_rank_shards_and_gather(tmp_path, world):
     import oracle_lib as O
-    world, B = 2, 3
+    B = 3
     mp.spawn(_worker, args=(world, _free_port(), B, str(tmp_path)), nprocs=world, join=True)
     full = syn.make_batch(world * B, 2, 8, "trot")
     assert np.array_equal(np.load(tmp_path / "x0.npy"), full["x0"])  # disjoint, reproducible shards
