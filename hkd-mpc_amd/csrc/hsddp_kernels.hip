@@ -719,6 +719,9 @@ DEV void stage_trial2(double *L, const Bufs &d, long r0, long nrows, int per, do
     }
 }
 
+#ifndef HSDDP_RO_REVERSE
+#define HSDDP_RO_REVERSE 1
+#endif
 #ifndef HSDDP_RO_STAGED
 #define HSDDP_RO_STAGED 1  // the slot waves' reference loaded in two pieces (0: all 30 pairs at once)
 #endif
@@ -797,7 +800,7 @@ DEV void rollout_boundary(const Params &p, const Bufs &d, double eps, int init, 
 // WIDE: p.S >= RW (instantiated apart: a wave's 64 slots then belong to at most two elements, and
 // the kernel carries only that staging path)
 template <bool EL, bool WIDE>
-DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
+DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init, int tix)
 {
     __shared__ double Xt[RW * RS];
     const int lane = threadIdx.x;
@@ -807,7 +810,9 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init)
         rollout_boundary<EL>(p, d, eps, init, ((long)blockIdx.x - nslot) * 64 + lane);
         return;
     }
-    const long blk = (long)blockIdx.x;
+    // (HSDDP_RO_REVERSE: the second trial walks the slot blocks from the batch's end, where the
+    // first trial's last reads may still sit in the memory-side cache)
+    const long blk = (HSDDP_RO_REVERSE && tix == 1) ? nslot - 1 - (long)blockIdx.x : (long)blockIdx.x;
 #if HSDDP_STAMPS
     unsigned long long rst[8];
 #endif
@@ -1347,7 +1352,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HSDDP_ROLLOU
     Params p, Bufs d, double eps, int init, int tix, int last)
 {
     if (ls_skip(d, tix)) return;
-    rollout_block<EL, WIDE>(p, d, eps, init);
+    rollout_block<EL, WIDE>(p, d, eps, init, tix);
     if constexpr (FUSE) {
         __shared__ int ticket;
         __threadfence();
