@@ -12,6 +12,7 @@
 //                        front knots / phases, pushed-back copies of X.back(), zero new phases —
 //                        as one gather over (element, new slot, entry) from host-built slot maps;
 //                        k_shift_gather_work then the working rows (X, U, Defect) alike.
+#include <cstddef>
 #include "../../include/hsddp.h"
 #include "hsddp_device.h"
 #include "hsddp_mpc.h"
@@ -92,6 +93,13 @@ __global__ __launch_bounds__(256) void k_extract_commands(Params p, Bufs d, CmdA
         o.N_mpcsteps = a.n;
         o.solve_time = a.solve_time;
     }
+    // the struct's padding bytes (after N_mpcsteps, after solve_time) zero too: a record is the same
+    // bytes wherever it is extracted (device buffers are not cleared; the multi-GPU gather sends bytes)
+    constexpr size_t p0 = offsetof(hsddp_mpc_command, N_mpcsteps) + sizeof(int), p1 = offsetof(hsddp_mpc_command, mpc_times);
+    constexpr size_t p2 = offsetof(hsddp_mpc_command, solve_time) + sizeof(float), p3 = sizeof(hsddp_mpc_command);
+    char *ob = reinterpret_cast<char *>(&o);
+    if (t < (int)(p1 - p0)) ob[p0 + t] = 0;
+    if (t < (int)(p3 - p2)) ob[p2 + t] = 0;
 }
 
 // One thread per 16 bytes (two doubles / four floats, never straddling a row: NX and KCW are

@@ -182,3 +182,25 @@ def test_mpc_loop_matches_oracle(ms):
     assert tails >= 2  # the loop passed through last phases without shooting states
     assert n_td >= 1   # (phases carrying two touchdown constraints: test_gpu_reference.py's file-driven loop)
     s.close()
+
+
+def test_command_records_are_the_same_bytes_wherever_extracted():
+    """hsddp_mpc_command has padding (after N_mpcsteps and after solve_time).  The extraction
+    kernel writes every byte of a record, so records extracted into buffers that held different
+    bytes — device memory from any allocator, the handle's scratch for the host path — compare
+    equal byte for byte (the multi-GPU gather sends the records as bytes)."""
+    import torch
+    from hsddp import shard
+    prob = syn.make_batch(8, 4, 20, "trot", mixed=True)
+    s = hsddp.Solver(prob, hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=2))
+    s.solve()
+    n = prob["batch"] * hsddp.MPC_COMMAND.itemsize
+    out = []
+    for fill in (0xAB, 0x11):
+        buf = torch.full((n,), fill, dtype=torch.uint8, device="cuda:0")
+        s.extract_commands_device(buf.data_ptr())
+        out.append(buf.cpu().numpy())
+    host = shard.command_bytes(s.extract_commands())
+    s.close()
+    assert np.array_equal(out[0], out[1])
+    assert np.array_equal(out[0], host)
