@@ -810,9 +810,9 @@ DEV void rollout_block(const Params &p, const Bufs &d, double eps, int init, int
         rollout_boundary<EL>(p, d, eps, init, ((long)blockIdx.x - nslot) * 64 + lane);
         return;
     }
-    // (HSDDP_RO_REVERSE: the second trial walks the slot blocks from the batch's end, where the
-    // first trial's last reads may still sit in the memory-side cache)
-    const long blk = (HSDDP_RO_REVERSE && tix == 1) ? nslot - 1 - (long)blockIdx.x : (long)blockIdx.x;
+    // (HSDDP_RO_REVERSE: every second trial walks the slot blocks from the batch's end, where the
+    // trial before's last reads of the same rows may still sit in the memory-side cache)
+    const long blk = (HSDDP_RO_REVERSE && tix > 0 && (tix & 1)) ? nslot - 1 - (long)blockIdx.x : (long)blockIdx.x;
 #if HSDDP_STAMPS
     unsigned long long rst[8];
 #endif
