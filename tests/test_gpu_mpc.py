@@ -188,19 +188,26 @@ def test_command_records_are_the_same_bytes_wherever_extracted():
     """hsddp_mpc_command has padding (after N_mpcsteps and after solve_time).  The extraction
     kernel writes every byte of a record, so records extracted into buffers that held different
     bytes — device memory from any allocator, the handle's scratch for the host path — compare
-    equal byte for byte (the multi-GPU gather sends the records as bytes)."""
-    import torch
+    equal byte for byte (the multi-GPU gather sends the records as bytes).  Device buffers come
+    from the HIP runtime the library uses (no torch: this module may load before it)."""
+    import ctypes as C
     from hsddp import shard
+    hip = C.CDLL("libamdhip64.so")
     prob = syn.make_batch(8, 4, 20, "trot", mixed=True)
     s = hsddp.Solver(prob, hsddp.load_settings(no_early_exit=1, max_AL_iter=1, max_DDP_iter=2))
     s.solve()
     n = prob["batch"] * hsddp.MPC_COMMAND.itemsize
     out = []
     for fill in (0xAB, 0x11):
-        buf = torch.full((n,), fill, dtype=torch.uint8, device="cuda:0")
-        s.extract_commands_device(buf.data_ptr())
-        out.append(buf.cpu().numpy())
-    host = shard.command_bytes(s.extract_commands())
+        ptr = C.c_void_p()
+        assert hip.hipMalloc(C.byref(ptr), C.c_size_t(n)) == 0
+        assert hip.hipMemset(ptr, C.c_int(fill), C.c_size_t(n)) == 0
+        s.extract_commands_device(ptr.value)
+        host = np.empty(n, np.uint8)
+        assert hip.hipMemcpy(C.c_void_p(host.ctypes.data), ptr, C.c_size_t(n), C.c_int(2)) == 0  # device to host
+        assert hip.hipFree(ptr) == 0
+        out.append(host)
+    ref = shard.command_bytes(s.extract_commands())
     s.close()
     assert np.array_equal(out[0], out[1])
-    assert np.array_equal(out[0], host)
+    assert np.array_equal(out[0], ref)
